@@ -1,0 +1,105 @@
+"""Synthetic input streams for the FFV1 encode path.
+
+* D1 -- the reference's own benchmark/FATE source clip (tests/videogen.c),
+  re-derived in csrc/synth.c and widened to 10/12/16 bit the way the
+  reference's swscale limited-range path does (``v << (depth - 8)``).
+* D2 -- the seeded LSB-active stress clip of SURVEY.md 8d (numpy PCG64).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import _paths
+
+_lib = None
+
+
+def _synth():
+    global _lib
+    if _lib is None:
+        path = _paths.synth_lib()
+        L = ctypes.CDLL(path)
+        L.ffv1syn_clip_new.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.ffv1syn_clip_new.restype = ctypes.c_void_p
+        L.ffv1syn_clip_free.argtypes = [ctypes.c_void_p]
+        L.ffv1syn_clip_next.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8)]
+        L.ffv1syn_clip_next.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+class VideogenClip:
+    """Frame iterator over the D1 clip at any even WxH (yuv420p, u8)."""
+
+    def __init__(self, width: int, height: int):
+        self.w, self.h = width, height
+        self._h = _synth().ffv1syn_clip_new(width, height)
+        if not self._h:
+            raise ValueError("videogen needs even dimensions")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _synth().ffv1syn_clip_free(self._h)
+            self._h = None
+
+    def next_yuv420p(self):
+        n = self.w * self.h
+        buf = np.empty(n * 3 // 2, np.uint8)
+        _synth().ffv1syn_clip_next(self._h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+        y = buf[:n].reshape(self.h, self.w)
+        u = buf[n:n + n // 4].reshape(self.h // 2, self.w // 2)
+        v = buf[n + n // 4:].reshape(self.h // 2, self.w // 2)
+        return [y, u, v]
+
+
+def widen(planes, depth: int):
+    """u8 planes -> u16 planes holding v << (depth - 8) (swscale shiftonly)."""
+    return [np.ascontiguousarray(p.astype(np.uint16) << (depth - 8)) for p in planes]
+
+
+def upsample_444(planes):
+    """yuv420p -> yuv444p by sample repetition (nearest neighbour)."""
+    y, u, v = planes
+    h, w = y.shape
+    up = lambda c: np.ascontiguousarray(np.repeat(np.repeat(c, 2, 0), 2, 1)[:h, :w])
+    return [y, up(u), up(v)]
+
+
+def videogen_frames(width: int, height: int, n: int, depth: int = 8, chroma444: bool = False):
+    clip = VideogenClip(width, height)
+    for _ in range(n):
+        f = clip.next_yuv420p()
+        if chroma444:
+            f = upsample_444(f)
+        if depth > 8:
+            f = widen(f, depth)
+        yield [np.ascontiguousarray(p) for p in f]
+
+
+def d2_frames(width: int, height: int, n: int, depth: int = 10, chroma444: bool = False,
+              seed: int = 20261015):
+    """SURVEY.md 8d "D2": smooth moving field + uniform noise, LSB-active.
+
+    Y = clip(512 + 300 sin((x+8t)/97) cos((y-5t)/61) + U{-8..8}, 0, 1023)
+    cb = 512 + 200 sin((x2+4t)/53); U = clip(cb + U{-4..4}); V = clip(1023-cb+U{-4..4})
+    Amplitudes scale by 2^(depth-10); samples are u16 (LSB aligned).
+    """
+    rng = np.random.Generator(np.random.PCG64(seed))
+    scale = 2.0 ** (depth - 10)
+    maxv = (1 << depth) - 1
+    cw = width if chroma444 else (width + 1) // 2
+    chh = height if chroma444 else (height + 1) // 2
+    ys = np.arange(height, dtype=np.float64)[:, None]
+    xs = np.arange(width, dtype=np.float64)[None, :]
+    xc = np.arange(cw, dtype=np.float64)[None, :]
+    for t in range(n):
+        base = 512 + 300 * np.sin((xs + 8 * t) / 97) * np.cos((ys - 5 * t) / 61)
+        Y = np.rint(base * scale) + rng.integers(-8, 9, size=(height, width)) * scale
+        cb = (512 + 200 * np.sin((xc + 4 * t) / 53)) * scale
+        cb = np.broadcast_to(cb, (chh, cw))
+        U = np.rint(cb) + rng.integers(-4, 5, size=(chh, cw)) * scale
+        V = np.rint(maxv - cb) + rng.integers(-4, 5, size=(chh, cw)) * scale
+        yield [np.ascontiguousarray(np.clip(p, 0, maxv).astype(np.uint16)) for p in (Y, U, V)]

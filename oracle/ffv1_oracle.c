@@ -1,0 +1,1505 @@
+/*
+ * ffv1_oracle.c -- CPU restatement of the reference FFV1 encoder + decoder.
+ *
+ * TEST INFRASTRUCTURE ONLY (see ffv1_oracle.h).  Written from the behaviour
+ * of the reference (FFmpeg libavcodec 57.51.100); every block cites the
+ * reference file:line whose semantics it restates.  Nothing here is linked
+ * into, or called by, the MI355X product path.
+ *
+ * Parity pins: tests/golden/known_answers.json (SURVEY.md 8c MD5s of the
+ * reference encoder's packets) and the FATE goldens tests/ref/vsynth/.
+ */
+#include "ffv1_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+#define AVERR_INVALIDDATA (-1094995529)
+#define AVERR_EINVAL (-22)
+#define AVERR_ENOSYS (-38)
+#define AVERR_ENOMEM (-12)
+
+/* ------------------------------------------------------------------------ */
+/* small helpers                                                            */
+
+static int ilog2u(unsigned v) /* av_log2 (libavutil/intmath.h:55-83) */
+{
+    int n = 0;
+    while (v >> 1) { v >>= 1; n++; }
+    return n;
+}
+
+static int median3(int a, int b, int c) /* mid_pred (mathops.h:95-120) */
+{
+    int lo = a < b ? a : b, hi = a < b ? b : a;
+    return c < lo ? lo : (c > hi ? hi : c);
+}
+
+static int ceil_rshift(int a, int s) { return -((-a) >> s); }
+
+/* fold() ffv1.h:148-159: wrap a residual into the signed range of `bits`. */
+static int fold_residual(int d, int bits)
+{
+    if (bits == 8)
+        return (int8_t)d;
+    {
+        unsigned half = 1u << (bits - 1);
+        unsigned m = ((unsigned)d + half) & ((half << 1) - 1);
+        return (int)m - (int)half;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* CRC-32/MPEG-2 style: MSB first, poly 0x04C11DB7, init 0, no xorout.      */
+/* The reference keeps its table byte-swapped and stores the result with   */
+/* AV_WL32 (crc.c:310-380, ffv1enc.c:1349-1350); net effect on the wire is  */
+/* the plain MSB-first CRC written big-endian.                             */
+
+static uint32_t crc_tab[256];
+static int crc_ready;
+
+static void crc_init(void)
+{
+    for (unsigned i = 0; i < 256; i++) {
+        uint32_t r = i << 24;
+        for (int k = 0; k < 8; k++)
+            r = (r & 0x80000000u) ? (r << 1) ^ 0x04C11DB7u : (r << 1);
+        crc_tab[i] = r;
+    }
+    crc_ready = 1;
+}
+
+uint32_t ffv1o_crc32(uint32_t crc, const uint8_t *buf, int64_t len)
+{
+    if (!crc_ready)
+        crc_init();
+    for (int64_t i = 0; i < len; i++)
+        crc = (crc << 8) ^ crc_tab[(crc >> 24) ^ buf[i]];
+    return crc;
+}
+
+static void put_be32(uint8_t *p, uint32_t v)
+{
+    p[0] = v >> 24; p[1] = v >> 16; p[2] = v >> 8; p[3] = v;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Adaptive binary range coder (rangecoder.h:35-102, rangecoder.c:42-116)   */
+
+typedef struct rc_tables {
+    uint8_t to0[256];  /* state after coding a 0 ("zero_state") */
+    uint8_t to1[256];  /* state after coding a 1 ("one_state")  */
+} rc_tables;
+
+typedef struct rc_enc {
+    int low, range;
+    int carry_run;      /* outstanding_count */
+    int pending;        /* outstanding_byte, -1 = none yet */
+    uint8_t *base, *ptr, *end;
+    int overflow;
+    const rc_tables *t;
+} rc_enc;
+
+/* ff_build_rac_states(c, 0.05*2^32, 256-8) (rangecoder.c:63-101). */
+static void rc_default_tables(rc_tables *t)
+{
+    const int64_t ONE = (int64_t)1 << 32;
+    const int factor = (int)(0.05 * (double)((int64_t)1 << 32));
+    const int max_p = 256 - 8;
+    int64_t p = ONE / 2;
+    int prev = 0;
+
+    memset(t, 0, sizeof(*t));
+    for (int i = 0; i < 128; i++) {
+        int p8 = (int)((256 * p + ONE / 2) >> 32);
+        if (p8 <= prev)
+            p8 = prev + 1;
+        if (prev && prev < 256 && p8 <= max_p)
+            t->to1[prev] = p8;
+        p += ((ONE - p) * factor + ONE / 2) >> 32;
+        prev = p8;
+    }
+    for (int i = 256 - max_p; i <= max_p; i++) {
+        if (t->to1[i])
+            continue;
+        p = ((int64_t)i * ONE + 128) >> 8;
+        p += ((ONE - p) * factor + ONE / 2) >> 32;
+        int p8 = (int)((256 * p + ONE / 2) >> 32);
+        if (p8 <= i)
+            p8 = i + 1;
+        if (p8 > max_p)
+            p8 = max_p;
+        t->to1[i] = p8;
+    }
+    for (int i = 1; i < 255; i++)
+        t->to0[i] = 256 - t->to1[256 - i];
+}
+
+/* Custom transition install (ffv1.c:95-101, ffv1enc.c:1309-1315). */
+static void rc_custom_tables(rc_tables *t, const rc_tables *dflt,
+                             const uint8_t stt[256])
+{
+    *t = *dflt;
+    for (int i = 1; i < 256; i++) {
+        t->to1[i] = stt[i];
+        t->to0[256 - i] = 256 - stt[i];
+    }
+}
+
+static void rc_enc_init(rc_enc *c, uint8_t *buf, int64_t size,
+                        const rc_tables *t)
+{
+    c->low = 0;
+    c->range = 0xFF00;
+    c->carry_run = 0;
+    c->pending = -1;
+    c->base = c->ptr = buf;
+    c->end = buf + size;
+    c->overflow = 0;
+    c->t = t;
+}
+
+static void rc_emit(rc_enc *c, int byte)
+{
+    if (c->ptr < c->end)
+        *c->ptr = (uint8_t)byte;
+    else
+        c->overflow = 1;
+    c->ptr++;
+}
+
+/* renorm_encoder (rangecoder.h:52-75): shift out whole bytes while the
+ * interval is narrower than 2^8; a byte can still be bumped by a carry, so
+ * it is held back ("pending") together with a run of 0xFF bytes. */
+static void rc_renorm(rc_enc *c)
+{
+    while (c->range < 0x100) {
+        if (c->pending < 0) {
+            c->pending = c->low >> 8;
+        } else if (c->low <= 0xFF00) {
+            rc_emit(c, c->pending);
+            for (; c->carry_run; c->carry_run--)
+                rc_emit(c, 0xFF);
+            c->pending = c->low >> 8;
+        } else if (c->low >= 0x10000) {
+            rc_emit(c, c->pending + 1);
+            for (; c->carry_run; c->carry_run--)
+                rc_emit(c, 0x00);
+            c->pending = (c->low >> 8) & 0xFF;
+        } else {
+            c->carry_run++;
+        }
+        c->low = (c->low & 0xFF) << 8;
+        c->range <<= 8;
+    }
+}
+
+/* put_rac (rangecoder.h:85-102) */
+static void rc_put(rc_enc *c, uint8_t *st, int bit)
+{
+    int r1 = (c->range * *st) >> 8;
+    if (bit) {
+        c->low += c->range - r1;
+        c->range = r1;
+        *st = c->t->to1[*st];
+    } else {
+        c->range -= r1;
+        *st = c->t->to0[*st];
+    }
+    rc_renorm(c);
+}
+
+/* ff_rac_terminate (rangecoder.c:104-116) */
+static int64_t rc_finish(rc_enc *c)
+{
+    c->range = 0xFF;
+    c->low += 0xFF;
+    rc_renorm(c);
+    c->range = 0xFF;
+    rc_renorm(c);
+    return c->ptr - c->base;
+}
+
+/* put_symbol_inline (ffv1enc.c:185-231): zero flag, unary exponent,
+ * mantissa MSB->LSB, then sign, each in its own adaptive slot. */
+static void rc_put_symbol(rc_enc *c, uint8_t st[32], int v, int is_signed)
+{
+    if (v == 0) {
+        rc_put(c, &st[0], 1);
+        return;
+    }
+    unsigned a = v < 0 ? -(unsigned)v : (unsigned)v;
+    int e = ilog2u(a);
+    rc_put(c, &st[0], 0);
+    for (int i = 0; i < e; i++)
+        rc_put(c, &st[1 + (i < 9 ? i : 9)], 1);
+    rc_put(c, &st[1 + (e < 9 ? e : 9)], 0);
+    for (int i = e - 1; i >= 0; i--)
+        rc_put(c, &st[22 + (i < 9 ? i : 9)], (a >> i) & 1);
+    if (is_signed)
+        rc_put(c, &st[11 + (e < 10 ? e : 10)], v < 0);
+}
+
+/* ---- decoder side (rangecoder.h:104-147, ffv1dec.c:42-66) ---- */
+
+typedef struct rc_dec {
+    int low, range;
+    const uint8_t *base, *ptr, *end;
+    const rc_tables *t;
+} rc_dec;
+
+static void rc_dec_init(rc_dec *c, const uint8_t *buf, int64_t size,
+                        const rc_tables *t)
+{
+    c->base = buf;
+    c->end = buf + size;
+    c->range = 0xFF00;
+    c->low = (buf[0] << 8) | buf[1];
+    c->ptr = buf + 2;
+    c->t = t;
+}
+
+static int rc_get(rc_dec *c, uint8_t *st)
+{
+    int r1 = (c->range * *st) >> 8;
+    int bit;
+    c->range -= r1;
+    if (c->low < c->range) {
+        *st = c->t->to0[*st];
+        bit = 0;
+    } else {
+        c->low -= c->range;
+        c->range = r1;
+        *st = c->t->to1[*st];
+        bit = 1;
+    }
+    if (c->range < 0x100) {
+        c->range <<= 8;
+        c->low <<= 8;
+        if (c->ptr < c->end)
+            c->low += *c->ptr;
+        c->ptr++;
+    }
+    return bit;
+}
+
+static int rc_get_symbol(rc_dec *c, uint8_t st[32], int is_signed)
+{
+    if (rc_get(c, &st[0]))
+        return 0;
+    int e = 0;
+    while (rc_get(c, &st[1 + (e < 9 ? e : 9)])) {
+        if (++e > 31)
+            return 0;
+    }
+    int a = 1;
+    for (int i = e - 1; i >= 0; i--)
+        a = 2 * a + rc_get(c, &st[22 + (i < 9 ? i : 9)]);
+    if (is_signed && rc_get(c, &st[11 + (e < 10 ? e : 10)]))
+        return -a;
+    return a;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Golomb-Rice side (golomb.h:508-563, put_bits.h:35-190, ffv1.h:192-224)   */
+
+typedef struct bitw {
+    uint8_t *base, *end;
+    int64_t nbits;
+    int overflow;
+} bitw;
+
+static void bw_init(bitw *b, uint8_t *buf, int64_t size)
+{
+    b->base = buf;
+    b->end = buf + (size > 0 ? size : 0);
+    b->nbits = 0;
+    b->overflow = 0;
+}
+
+/* MSB-first bit append; equivalent on the wire to put_bits + flush. */
+static void bw_put(bitw *b, int n, uint32_t v)
+{
+    for (int i = n - 1; i >= 0; i--) {
+        int64_t byte = b->nbits >> 3;
+        int sh = 7 - (int)(b->nbits & 7);
+        if (b->base + byte >= b->end) {
+            b->overflow = 1;
+        } else {
+            if (sh == 7)
+                b->base[byte] = 0;
+            b->base[byte] |= ((v >> i) & 1) << sh;
+        }
+        b->nbits++;
+    }
+}
+
+static int64_t bw_bytes(const bitw *b) { return (b->nbits + 7) >> 3; }
+
+typedef struct bitr {
+    const uint8_t *base;
+    int64_t pos, nbits;
+} bitr;
+
+static int br_get(bitr *b, int n)
+{
+    int v = 0;
+    for (int i = 0; i < n; i++) {
+        int bit = 0;
+        if (b->pos < b->nbits)
+            bit = (b->base[b->pos >> 3] >> (7 - (b->pos & 7))) & 1;
+        b->pos++;
+        v = (v << 1) | bit;
+    }
+    return v;
+}
+
+typedef struct vlc_ctx {
+    int drift, error_sum, bias, count;
+} vlc_ctx;
+
+static void vlc_reset(vlc_ctx *s)
+{
+    s->drift = 0;
+    s->error_sum = 4;
+    s->bias = 0;
+    s->count = 1;
+}
+
+/* update_vlc_state (ffv1.h:192-224) */
+static void vlc_adapt(vlc_ctx *s, int v)
+{
+    int drift = s->drift, count = s->count;
+    s->error_sum = (uint16_t)(s->error_sum + (v < 0 ? -v : v));
+    drift += v;
+    if (count == 128) {
+        count >>= 1;
+        drift >>= 1;
+        s->error_sum >>= 1;
+    }
+    count++;
+    if (drift <= -count) {
+        if (s->bias > -128)
+            s->bias--;
+        drift += count;
+        if (drift <= -count)
+            drift = -count + 1;
+    } else if (drift > 0) {
+        if (s->bias < 127)
+            s->bias++;
+        drift -= count;
+        if (drift > 0)
+            drift = 0;
+    }
+    s->drift = (int16_t)drift;
+    s->count = count;
+}
+
+static int vlc_k(const vlc_ctx *s)
+{
+    int k = 0, i = s->count;
+    while (i < s->error_sum) {
+        k++;
+        i += i;
+    }
+    return k;
+}
+
+/* put_vlc_symbol (ffv1enc.c:240-269) + set_sr_golomb/set_ur_golomb. */
+static void vlc_put(bitw *b, vlc_ctx *s, int v, int bits)
+{
+    v = fold_residual(v - s->bias, bits);
+    int k = vlc_k(s);
+    int code = v ^ ((2 * s->drift + s->count) >> 31);
+    unsigned u = code >= 0 ? 2u * (unsigned)code : (unsigned)(-2 * code - 1);
+    unsigned q = u >> k;
+    if (q < 12) {
+        bw_put(b, (int)q + k + 1, (1u << k) + (u & ((1u << k) - 1)));
+    } else {
+        bw_put(b, 12 + bits, u - 12 + 1);
+    }
+    vlc_adapt(s, v);
+}
+
+static int vlc_get(bitr *b, vlc_ctx *s, int bits)
+{
+    int k = vlc_k(s);
+    /* get_sr_golomb(gb, k, 12, bits) */
+    int q = 0;
+    while (q < 12 && br_get(b, 1) == 0)
+        q++;
+    unsigned u;
+    if (q < 12) {
+        u = ((unsigned)q << k) | (unsigned)br_get(b, k);
+    } else {
+        u = (unsigned)br_get(b, bits) + 11;
+    }
+    int v = (u & 1) ? -(int)((u + 1) >> 1) : (int)(u >> 1);
+    v ^= ((2 * s->drift + s->count) >> 31);
+    int ret = fold_residual(v + s->bias, bits);
+    vlc_adapt(s, v);
+    return ret;
+}
+
+static const uint8_t log2_run[41] = { /* ff_log2_run, bitstream.c:40-46 */
+    0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3,
+    4, 4, 5, 5, 6, 6, 7, 7, 8, 9, 10, 11, 12, 13, 14, 15,
+    16, 17, 18, 19, 20, 21, 22, 23, 24,
+};
+
+/* ------------------------------------------------------------------------ */
+/* Quantisation tables (ffv1enc.c:44-118, setup 846-879).                   */
+/* Each table is given by the first index of every step on [0,127]; the     */
+/* negative half mirrors it and index 128 copies -q[127] (the same rule     */
+/* read_quant_table applies, ffv1dec.c:475-498).                           */
+
+static void build_quant(int16_t q[256], const int *steps, int nsteps, int scale)
+{
+    int v = 0;
+    for (int i = 0; i < 128; i++) {
+        while (v < nsteps && i >= steps[v])
+            v++;
+        q[i] = (int16_t)(scale * v);
+    }
+    for (int i = 1; i < 128; i++)
+        q[256 - i] = -q[i];
+    q[128] = -q[127];
+}
+
+static const int Q11_STEPS[] = {1, 2, 5, 12, 35};        /* quant11      */
+static const int Q5_STEPS[] = {1, 4};                    /* quant5       */
+static const int Q9_10_STEPS[] = {5, 13, 27, 56};        /* quant9_10bit */
+static const int Q5_10_STEPS[] = {11, 50};               /* quant5_10bit */
+
+/* quant_tables[context_model] for the given depth */
+static void build_quant_set(int16_t qt[5][256], int model, int bits)
+{
+    const int *qa, *qb;
+    int na, nb;
+    if (bits <= 8) {
+        qa = Q11_STEPS; na = 5; qb = Q5_STEPS; nb = 2;
+    } else {
+        qa = Q9_10_STEPS; na = 4; qb = Q5_10_STEPS; nb = 2;
+    }
+    memset(qt, 0, 5 * 256 * sizeof(int16_t));
+    build_quant(qt[0], qa, na, 1);
+    build_quant(qt[1], qa, na, 11);
+    if (model == 0) {
+        build_quant(qt[2], qa, na, 121);
+    } else {
+        build_quant(qt[2], qb, nb, 121);
+        build_quant(qt[3], qb, nb, 605);
+        build_quant(qt[4], qb, nb, 3025);
+    }
+}
+
+static int context_count_of(int model)
+{
+    return model ? (11 * 11 * 5 * 5 * 5 + 1) / 2 : (11 * 11 * 11 + 1) / 2;
+}
+
+/* ver2_state (ffv1enc.c:120-137): the custom state-transition table the
+ * encoder installs for coder=1 ("range_tab"); format data of FFV1 v2+. */
+static const uint8_t CUSTOM_STT[256] = {
+    0, 10, 10, 10, 10, 16, 16, 16, 28, 16, 16, 29, 42, 49, 20, 49,
+    59, 25, 26, 26, 27, 31, 33, 33, 33, 34, 34, 37, 67, 38, 39, 39,
+    40, 40, 41, 79, 43, 44, 45, 45, 48, 48, 64, 50, 51, 52, 88, 52,
+    53, 74, 55, 57, 58, 58, 74, 60, 101, 61, 62, 84, 66, 66, 68, 69,
+    87, 82, 71, 97, 73, 73, 82, 75, 111, 77, 94, 78, 87, 81, 83, 97,
+    85, 83, 94, 86, 99, 89, 90, 99, 111, 92, 93, 134, 95, 98, 105, 98,
+    105, 110, 102, 108, 102, 118, 103, 106, 106, 113, 109, 112, 114, 112, 116, 125,
+    115, 116, 117, 117, 126, 119, 125, 121, 121, 123, 145, 124, 126, 131, 127, 129,
+    165, 130, 132, 138, 133, 135, 145, 136, 137, 139, 146, 141, 143, 142, 144, 148,
+    147, 155, 151, 149, 151, 150, 152, 157, 153, 154, 156, 168, 158, 162, 161, 160,
+    172, 163, 169, 164, 166, 184, 167, 170, 177, 174, 171, 173, 182, 176, 180, 178,
+    175, 189, 179, 181, 186, 183, 192, 185, 200, 187, 191, 188, 190, 197, 193, 196,
+    197, 194, 195, 196, 198, 202, 199, 201, 210, 203, 207, 204, 205, 206, 208, 214,
+    209, 211, 221, 212, 213, 215, 224, 216, 217, 218, 219, 220, 222, 228, 223, 225,
+    226, 224, 227, 229, 240, 230, 231, 232, 233, 234, 235, 236, 238, 239, 237, 242,
+    241, 243, 242, 244, 245, 246, 247, 248, 249, 250, 251, 252, 252, 253, 254, 255,
+};
+
+/* ------------------------------------------------------------------------ */
+/* encode_init parameter contract (ffv1enc.c:669-1029)                      */
+
+typedef struct pixfmt_info {
+    const char *name;
+    int planes;        /* 1 gray, 3 yuv */
+    int hs, vs;
+    int depth;         /* nominal depth of the storage format */
+    int family;        /* 9, 10, 16 or 8: which switch group it enters */
+} pixfmt_info;
+
+static const pixfmt_info PIXFMTS[] = {
+    {"yuv420p", 3, 1, 1, 8, 8},   {"yuv422p", 3, 1, 0, 8, 8},
+    {"yuv444p", 3, 0, 0, 8, 8},   {"yuv440p", 3, 0, 1, 8, 8},
+    {"yuv411p", 3, 2, 0, 8, 8},   {"yuv410p", 3, 2, 2, 8, 8},
+    {"gray", 1, 0, 0, 8, 8},
+    {"yuv420p9", 3, 1, 1, 9, 9},  {"yuv422p9", 3, 1, 0, 9, 9},
+    {"yuv444p9", 3, 0, 0, 9, 9},
+    {"yuv420p10", 3, 1, 1, 10, 10}, {"yuv422p10", 3, 1, 0, 10, 10},
+    {"yuv444p10", 3, 0, 0, 10, 10},
+    {"yuv420p16", 3, 1, 1, 16, 16}, {"yuv422p16", 3, 1, 0, 16, 16},
+    {"yuv444p16", 3, 0, 0, 16, 16}, {"gray16", 1, 0, 0, 16, 16},
+};
+
+int ffv1o_configure(ffv1o_config *cfg, int width, int height,
+                    const char *pix_fmt, int slices, int level, int coder,
+                    int context, int gop_size, int bits_per_raw_sample,
+                    int slicecrc)
+{
+    const pixfmt_info *pf = NULL;
+    for (size_t i = 0; i < sizeof(PIXFMTS) / sizeof(PIXFMTS[0]); i++)
+        if (!strcmp(PIXFMTS[i].name, pix_fmt))
+            pf = &PIXFMTS[i];
+    if (!pf || width <= 0 || height <= 0)
+        return pf ? AVERR_INVALIDDATA : AVERR_ENOSYS;
+
+    memset(cfg, 0, sizeof(*cfg));
+    cfg->width = width;
+    cfg->height = height;
+    cfg->gop_size = gop_size;
+    cfg->sar_num = 0;
+    cfg->sar_den = 1;
+
+    /* version selection, ffv1enc.c:678-697 */
+    int version = 0;
+    if (slices > 1)
+        version = 2;
+    if (slices == 0 && level < 0 && width * height > 720 * 576)
+        version = 2;
+    if (level <= 0 && version == 2)
+        version = 3;
+    if (level >= 0 && level <= 4) {
+        if (level < version)
+            return AVERR_EINVAL;
+        version = level;
+    }
+    int ec = slicecrc;
+    if (ec < 0)
+        ec = version >= 3;
+    if (version == 2 || version > 3) /* needs -strict experimental (:703) */
+        return AVERR_INVALIDDATA;
+
+    /* coder, ffv1enc.c:708-718 (coder -1 keeps the private default 0) */
+    int ac = 0;
+    if (coder != -1)
+        ac = coder > 0 ? 2 : 0;
+    if (ac == 1)
+        ac = 2;
+    else if (ac == -2)
+        ac = 1;
+    if (coder == -2)
+        ac = 1;
+
+    /* pix_fmt switch, ffv1enc.c:720-820 */
+    int bits = 0, packed = 0;
+    if (pf->family == 9 && !bits_per_raw_sample)
+        bits = 9;
+    if (pf->family == 9 || pf->family == 10) {
+        packed = 1;
+        if (!bits_per_raw_sample && !bits)
+            bits = 10;
+    }
+    if (pf->family >= 9) {
+        if (!bits_per_raw_sample && !bits)
+            bits = 16;
+        else if (!bits)
+            bits = bits_per_raw_sample;
+        if (bits <= 8)
+            return AVERR_INVALIDDATA;
+        if (ac == 0)
+            ac = 2;
+        if (version < 1)
+            version = 1;
+    }
+    if (!bits)
+        bits = 8;
+    if (context < 0 || context > 1)
+        return AVERR_EINVAL;
+
+    cfg->chroma_planes = pf->planes == 3;
+    cfg->chroma_h_shift = pf->planes == 3 ? pf->hs : 0;
+    cfg->chroma_v_shift = pf->planes == 3 ? pf->vs : 0;
+    cfg->transparency = 0;
+    cfg->bits_per_raw_sample = bits;
+    cfg->packed_at_lsb = packed;
+    cfg->sample_bytes = pf->depth > 8 ? 2 : 1;
+    cfg->version = version;
+    cfg->ac = ac;
+    cfg->ec = ec;
+    cfg->context_model = context;
+    cfg->num_h_slices = 1;
+    cfg->num_v_slices = 1;
+
+    /* slice grid search, ffv1enc.c:988-1000 */
+    if (version > 1) {
+        int nv = (width > 352 || height > 288 || !slices) ? 2 : 1;
+        for (; nv < 9; nv++)
+            for (int nh = nv; nh < 2 * nv; nh++)
+                if ((slices == nh * nv && slices <= 64) || !slices) {
+                    cfg->num_h_slices = nh;
+                    cfg->num_v_slices = nv;
+                    return 0;
+                }
+        return AVERR_ENOSYS;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Encoder state                                                            */
+
+typedef struct plane_state {
+    uint8_t *rac;       /* [contexts][32]   */
+    vlc_ctx *vlc;       /* [contexts]       */
+} plane_state;
+
+typedef struct slice_ctx {
+    int x0, y0, w, h;   /* luma rectangle, ffv1.c:117-145 */
+    plane_state ps[2];  /* plane_count == 2 (no alpha), ffv1enc.c:890-891 */
+    uint8_t *buf;
+    int64_t cap;
+    int64_t bytes;
+    int error;
+} slice_ctx;
+
+struct ffv1o_enc {
+    ffv1o_config cfg;
+    int16_t qt[5][256];
+    int contexts;
+    int coded_bits;     /* "bits" argument of encode_line */
+    rc_tables dflt, frame_tab;
+    uint8_t stt[256];
+    int nslices;
+    slice_ctx *sl;
+    int64_t picture_number;
+    int16_t *scratch;   /* one slice plane of samples */
+};
+
+static void slice_rects(const ffv1o_config *cfg, int i, int *x0, int *y0,
+                        int *w, int *h)
+{
+    int nh = cfg->num_h_slices, nv = cfg->num_v_slices;
+    int sx = i % nh, sy = i / nh;
+    int xs = (int)((int64_t)cfg->width * sx / nh);
+    int xe = (int)((int64_t)cfg->width * (sx + 1) / nh);
+    int ys = (int)((int64_t)cfg->height * sy / nv);
+    int ye = (int)((int64_t)cfg->height * (sy + 1) / nv);
+    *x0 = xs; *y0 = ys; *w = xe - xs; *h = ye - ys;
+}
+
+ffv1o_enc *ffv1o_enc_new(const ffv1o_config *cfg)
+{
+    if (cfg->transparency || cfg->num_h_slices * cfg->num_v_slices > 256)
+        return NULL;
+    ffv1o_enc *e = calloc(1, sizeof(*e));
+    if (!e)
+        return NULL;
+    e->cfg = *cfg;
+    build_quant_set(e->qt, cfg->context_model, cfg->bits_per_raw_sample);
+    e->contexts = context_count_of(cfg->context_model);
+    e->coded_bits = cfg->bits_per_raw_sample <= 8 ? 8 : cfg->bits_per_raw_sample;
+    rc_default_tables(&e->dflt);
+    if (cfg->ac == 2) {
+        memcpy(e->stt, CUSTOM_STT, 256);
+        rc_custom_tables(&e->frame_tab, &e->dflt, e->stt);
+    } else {
+        memcpy(e->stt, e->dflt.to1, 256);
+        e->frame_tab = e->dflt;
+    }
+    e->nslices = cfg->num_h_slices * cfg->num_v_slices;
+    e->sl = calloc(e->nslices, sizeof(slice_ctx));
+    int64_t maxw = 0;
+    for (int i = 0; i < e->nslices; i++) {
+        slice_ctx *s = &e->sl[i];
+        slice_rects(cfg, i, &s->x0, &s->y0, &s->w, &s->h);
+        if ((int64_t)s->w * s->h > maxw)
+            maxw = (int64_t)s->w * s->h;
+        /* generous per-slice budget: header + <=35 bytes per sample line */
+        s->cap = 4096 + (int64_t)s->w * s->h * 6 + (int64_t)s->w * 35 * 2;
+        s->buf = malloc(s->cap);
+        for (int p = 0; p < 2; p++) {
+            s->ps[p].rac = malloc((size_t)e->contexts * 32);
+            s->ps[p].vlc = malloc((size_t)e->contexts * sizeof(vlc_ctx));
+        }
+    }
+    e->scratch = malloc((size_t)maxw * sizeof(int16_t) + 16);
+    return e;
+}
+
+void ffv1o_enc_free(ffv1o_enc *e)
+{
+    if (!e)
+        return;
+    for (int i = 0; i < e->nslices; i++) {
+        free(e->sl[i].buf);
+        for (int p = 0; p < 2; p++) {
+            free(e->sl[i].ps[p].rac);
+            free(e->sl[i].ps[p].vlc);
+        }
+    }
+    free(e->sl);
+    free(e->scratch);
+    free(e);
+}
+
+/* write_quant_table(s) (ffv1enc.c:475-496): run lengths of each step. */
+static void put_quant_tables(rc_enc *c, int16_t qt[5][256])
+{
+    for (int t = 0; t < 5; t++) {
+        uint8_t st[32];
+        memset(st, 128, 32);
+        int last = 0, i;
+        for (i = 1; i < 128; i++)
+            if (qt[t][i] != qt[t][i - 1]) {
+                rc_put_symbol(c, st, i - last - 1, 0);
+                last = i;
+            }
+        rc_put_symbol(c, st, i - last - 1, 0);
+    }
+}
+
+/* write_extradata (ffv1enc.c:545-619) */
+int ffv1o_enc_extradata(ffv1o_enc *e, uint8_t *buf, int cap)
+{
+    const ffv1o_config *cfg = &e->cfg;
+    if (cfg->version < 2)
+        return 0;
+    rc_enc c;
+    uint8_t st[32];
+    memset(st, 128, 32);
+    rc_enc_init(&c, buf, cap - 4, &e->dflt);
+
+    rc_put_symbol(&c, st, cfg->version, 0);
+    if (cfg->version > 2)
+        rc_put_symbol(&c, st, cfg->version == 3 ? 4 : 2, 0);
+    rc_put_symbol(&c, st, cfg->ac, 0);
+    if (cfg->ac == 2)
+        for (int i = 1; i < 256; i++)
+            rc_put_symbol(&c, st, e->stt[i] - e->dflt.to1[i], 1);
+    rc_put_symbol(&c, st, 0, 0); /* colorspace YUV */
+    rc_put_symbol(&c, st, cfg->bits_per_raw_sample, 0);
+    rc_put(&c, &st[0], cfg->chroma_planes);
+    rc_put_symbol(&c, st, cfg->chroma_h_shift, 0);
+    rc_put_symbol(&c, st, cfg->chroma_v_shift, 0);
+    rc_put(&c, &st[0], cfg->transparency);
+    rc_put_symbol(&c, st, cfg->num_h_slices - 1, 0);
+    rc_put_symbol(&c, st, cfg->num_v_slices - 1, 0);
+
+    /* quant_table_count is always 2 (ffv1enc.c:847) */
+    rc_put_symbol(&c, st, 2, 0);
+    for (int set = 0; set < 2; set++) {
+        int16_t qt[5][256];
+        build_quant_set(qt, set, cfg->bits_per_raw_sample);
+        put_quant_tables(&c, qt);
+    }
+    for (int set = 0; set < 2; set++)
+        rc_put(&c, &st[0], 0); /* initial states are all 128 */
+    if (cfg->version > 2) {
+        rc_put_symbol(&c, st, cfg->ec, 0);
+        rc_put_symbol(&c, st, cfg->gop_size < 2, 0);
+    }
+    int64_t n = rc_finish(&c);
+    if (c.overflow)
+        return AVERR_ENOMEM;
+    put_be32(buf + n, ffv1o_crc32(0, buf, n));
+    return (int)(n + 4);
+}
+
+/* write_header for v<2 keyframes (ffv1enc.c:498-522) */
+static void put_v01_header(const ffv1o_enc *e, rc_enc *c)
+{
+    const ffv1o_config *cfg = &e->cfg;
+    uint8_t st[32];
+    memset(st, 128, 32);
+    rc_put_symbol(c, st, cfg->version, 0);
+    rc_put_symbol(c, st, cfg->ac, 0);
+    if (cfg->ac == 2)
+        for (int i = 1; i < 256; i++)
+            rc_put_symbol(c, st, e->stt[i] - c->t->to1[i], 1);
+    rc_put_symbol(c, st, 0, 0);
+    if (cfg->version > 0)
+        rc_put_symbol(c, st, cfg->bits_per_raw_sample, 0);
+    rc_put(c, &st[0], cfg->chroma_planes);
+    rc_put_symbol(c, st, cfg->chroma_h_shift, 0);
+    rc_put_symbol(c, st, cfg->chroma_v_shift, 0);
+    rc_put(c, &st[0], cfg->transparency);
+    put_quant_tables(c, (int16_t(*)[256])e->qt);
+}
+
+/* encode_slice_header (ffv1enc.c:1031-1062) */
+static void put_slice_header(const ffv1o_enc *e, const slice_ctx *s, rc_enc *c)
+{
+    const ffv1o_config *cfg = &e->cfg;
+    uint8_t st[32];
+    memset(st, 128, 32);
+    int nh = cfg->num_h_slices, nv = cfg->num_v_slices;
+    rc_put_symbol(c, st, (int)((int64_t)(s->x0 + 1) * nh / cfg->width), 0);
+    rc_put_symbol(c, st, (int)((int64_t)(s->y0 + 1) * nv / cfg->height), 0);
+    rc_put_symbol(c, st, (int)((int64_t)(s->w + 1) * nh / cfg->width) - 1, 0);
+    rc_put_symbol(c, st, (int)((int64_t)(s->h + 1) * nv / cfg->height) - 1, 0);
+    for (int j = 0; j < 2; j++)
+        rc_put_symbol(c, st, cfg->context_model, 0);
+    rc_put_symbol(c, st, 3, 0); /* progressive picture structure */
+    rc_put_symbol(c, st, cfg->sar_num, 0);
+    rc_put_symbol(c, st, cfg->sar_den, 0);
+}
+
+/* Load one slice plane into int16 storage, as encode_plane does
+ * (ffv1enc.c:390-407): 8-bit, LSB-packed u16, or MSB-aligned u16 >> shift. */
+static void load_plane(const ffv1o_config *cfg, const uint8_t *src,
+                       int stride, int x0, int y0, int w, int h, int16_t *dst)
+{
+    for (int y = 0; y < h; y++) {
+        const uint8_t *row = src + (int64_t)(y0 + y) * stride;
+        for (int x = 0; x < w; x++) {
+            int v;
+            if (cfg->sample_bytes == 1) {
+                v = row[x0 + x];
+            } else {
+                v = row[2 * (x0 + x)] | (row[2 * (x0 + x) + 1] << 8);
+                if (!cfg->packed_at_lsb)
+                    v >>= 16 - cfg->bits_per_raw_sample;
+            }
+            dst[(int64_t)y * w + x] = (int16_t)v;
+        }
+    }
+}
+
+/* Neighbourhood of sample (x,y) inside one slice plane P (w x h), exactly as
+ * the reference's zeroed ring buffer exposes it (ffv1enc.c:381-388):
+ * rows above the slice are 0, L at x=0 is T, LT at x=0 is the sample two
+ * rows up in column 0, RT past the right edge is T, LL at x=0 is 0 and at
+ * x=1 is T(0). */
+typedef struct taps {
+    int X, L, T, LT, RT, LL, TT;
+} taps;
+
+static void get_taps(const int16_t *P, int w, int x, int y, taps *t)
+{
+    const int16_t *cur = P + (int64_t)y * w;
+    const int16_t *up = y >= 1 ? cur - w : NULL;
+    const int16_t *up2 = y >= 2 ? cur - 2 * w : NULL;
+    t->X = cur[x];
+    t->T = up ? up[x] : 0;
+    int T0 = up ? up[0] : 0;
+    t->L = x ? cur[x - 1] : T0;
+    if (x)
+        t->LT = up ? up[x - 1] : 0;
+    else
+        t->LT = up2 ? up2[0] : 0;
+    t->RT = (x + 1 < w) ? (up ? up[x + 1] : 0) : t->T;
+    t->LL = x >= 2 ? cur[x - 2] : (x == 1 ? T0 : 0);
+    t->TT = up2 ? up2[x] : 0;
+}
+
+/* get_context + predict + sign normalisation + fold (ffv1.h:161-190,
+ * ffv1enc.c:306-317). */
+static void sample_symbol(const int16_t qt[5][256], int model1, int bits,
+                          const taps *t, int *ctx_out, int *diff_out)
+{
+    int ctx = qt[0][(t->L - t->LT) & 0xFF] + qt[1][(t->LT - t->T) & 0xFF] +
+              qt[2][(t->T - t->RT) & 0xFF];
+    if (model1)
+        ctx += qt[3][(t->LL - t->L) & 0xFF] + qt[4][(t->TT - t->T) & 0xFF];
+    int pred = median3(t->L, t->L + t->T - t->LT, t->T);
+    int diff = t->X - pred;
+    if (ctx < 0) {
+        ctx = -ctx;
+        diff = -diff;
+    }
+    *ctx_out = ctx;
+    *diff_out = fold_residual(diff, bits);
+}
+
+/* encode_plane/encode_line for the range coder */
+static void code_plane_rac(ffv1o_enc *e, rc_enc *c, plane_state *ps,
+                           const int16_t *P, int w, int h)
+{
+    int model1 = e->cfg.context_model;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            taps t;
+            int ctx, diff;
+            get_taps(P, w, x, y, &t);
+            sample_symbol(e->qt, model1, e->coded_bits, &t, &ctx, &diff);
+            rc_put_symbol(c, ps->rac + (int64_t)ctx * 32, diff, 1);
+        }
+}
+
+/* encode_plane/encode_line for Golomb-Rice incl. run mode
+ * (ffv1enc.c:306-370) */
+static void code_plane_golomb(ffv1o_enc *e, bitw *b, plane_state *ps,
+                              const int16_t *P, int w, int h)
+{
+    int model1 = e->cfg.context_model;
+    int bits = e->coded_bits;
+    int run_index = 0;
+    for (int y = 0; y < h; y++) {
+        int run_count = 0, run_mode = 0;
+        for (int x = 0; x < w; x++) {
+            taps t;
+            int ctx, diff;
+            get_taps(P, w, x, y, &t);
+            sample_symbol(e->qt, model1, bits, &t, &ctx, &diff);
+            if (ctx == 0)
+                run_mode = 1;
+            if (run_mode) {
+                if (diff) {
+                    while (run_count >= 1 << log2_run[run_index]) {
+                        run_count -= 1 << log2_run[run_index];
+                        run_index++;
+                        bw_put(b, 1, 1);
+                    }
+                    bw_put(b, 1 + log2_run[run_index], run_count);
+                    if (run_index)
+                        run_index--;
+                    run_count = 0;
+                    run_mode = 0;
+                    if (diff > 0)
+                        diff--;
+                } else {
+                    run_count++;
+                }
+            }
+            if (!run_mode)
+                vlc_put(b, &ps->vlc[ctx], diff, bits);
+        }
+        if (run_mode) {
+            while (run_count >= 1 << log2_run[run_index]) {
+                run_count -= 1 << log2_run[run_index];
+                run_index++;
+                bw_put(b, 1, 1);
+            }
+            if (run_count)
+                bw_put(b, 1, 1);
+        }
+    }
+}
+
+static void reset_slice_states(ffv1o_enc *e, slice_ctx *s)
+{
+    for (int p = 0; p < 2; p++) {
+        memset(s->ps[p].rac, 128, (size_t)e->contexts * 32);
+        for (int j = 0; j < e->contexts; j++)
+            vlc_reset(&s->ps[p].vlc[j]);
+    }
+}
+
+/* Planes of one slice in coding order: Y (plane context 0) then Cb, Cr
+ * (both plane context 1), ffv1enc.c:1185-1196. */
+typedef void (*plane_fn)(ffv1o_enc *, void *, plane_state *, const int16_t *,
+                         int, int);
+
+static void for_each_plane(ffv1o_enc *e, slice_ctx *s,
+                           const uint8_t *const planes[3], const int strides[3],
+                           void *coder, int golomb)
+{
+    const ffv1o_config *cfg = &e->cfg;
+    int np = cfg->chroma_planes ? 3 : 1;
+    for (int p = 0; p < np; p++) {
+        int x0 = s->x0, y0 = s->y0, w = s->w, h = s->h;
+        if (p) {
+            w = ceil_rshift(s->w, cfg->chroma_h_shift);
+            h = ceil_rshift(s->h, cfg->chroma_v_shift);
+            x0 = s->x0 >> cfg->chroma_h_shift;
+            y0 = s->y0 >> cfg->chroma_v_shift;
+        }
+        load_plane(cfg, planes[p], strides[p], x0, y0, w, h, e->scratch);
+        plane_state *ps = &s->ps[p ? 1 : 0];
+        if (golomb)
+            code_plane_golomb(e, (bitw *)coder, ps, e->scratch, w, h);
+        else
+            code_plane_rac(e, (rc_enc *)coder, ps, e->scratch, w, h);
+    }
+}
+
+int64_t ffv1o_enc_frame(ffv1o_enc *e, const uint8_t *const planes[3],
+                        const int strides[3], uint8_t *out, int64_t cap,
+                        int *key_out)
+{
+    const ffv1o_config *cfg = &e->cfg;
+    int key = cfg->gop_size == 0 || e->picture_number % cfg->gop_size == 0;
+
+    for (int i = 0; i < e->nslices; i++) {
+        slice_ctx *s = &e->sl[i];
+        rc_enc c;
+        s->error = 0;
+        /* slice 0 continues the packet-level coder that carries the key bit
+         * (+ the v0/v1 header) coded with the default table, ffv1enc.c:1287-1315 */
+        rc_enc_init(&c, s->buf, s->cap, &e->frame_tab);
+        if (i == 0) {
+            uint8_t ks = 128;
+            c.t = &e->dflt;
+            rc_put(&c, &ks, key);
+            if (key && cfg->version < 2)
+                put_v01_header(e, &c);
+            c.t = &e->frame_tab;
+        }
+        if (key)
+            reset_slice_states(e, s);
+        if (cfg->version > 2)
+            put_slice_header(e, s, &c);
+
+        if (cfg->ac == 0) {
+            bitw b;
+            int64_t ac_bytes = 0;
+            if (cfg->version > 2) {
+                uint8_t st = 129;
+                rc_put(&c, &st, 0);
+            }
+            if (cfg->version > 2 || (s->x0 == 0 && s->y0 == 0))
+                ac_bytes = rc_finish(&c);
+            bw_init(&b, s->buf + ac_bytes, s->cap - ac_bytes);
+            for_each_plane(e, s, planes, strides, &b, 1);
+            s->bytes = ac_bytes + bw_bytes(&b);
+            s->error = b.overflow || c.overflow;
+        } else {
+            for_each_plane(e, s, planes, strides, &c, 0);
+            uint8_t st = 129;
+            rc_put(&c, &st, 0);
+            s->bytes = rc_finish(&c);
+            s->error = c.overflow;
+        }
+        if (s->error)
+            return AVERR_INVALIDDATA;
+    }
+
+    /* packet assembly, ffv1enc.c:1326-1354 */
+    int64_t pos = 0;
+    for (int i = 0; i < e->nslices; i++) {
+        slice_ctx *s = &e->sl[i];
+        int64_t n = s->bytes;
+        int64_t need = n + 3 + 5;
+        if (pos + need > cap)
+            return AVERR_ENOMEM;
+        memcpy(out + pos, s->buf, n);
+        if (i > 0 || cfg->version > 2) {
+            out[pos + n] = (uint8_t)(n >> 16);
+            out[pos + n + 1] = (uint8_t)(n >> 8);
+            out[pos + n + 2] = (uint8_t)n;
+            n += 3;
+        }
+        if (cfg->ec) {
+            out[pos + n++] = 0;
+            put_be32(out + pos + n, ffv1o_crc32(0, out + pos, n));
+            n += 4;
+        }
+        pos += n;
+    }
+    e->picture_number++;
+    if (key_out)
+        *key_out = key;
+    return pos;
+}
+
+int ffv1o_enc_last_slice_bytes(const ffv1o_enc *e, int *bytes, int n)
+{
+    for (int i = 0; i < n && i < e->nslices; i++)
+        bytes[i] = (int)e->sl[i].bytes;
+    return e->nslices;
+}
+
+int64_t ffv1o_slice_symbols(const ffv1o_config *cfg,
+                            const uint8_t *const planes[3],
+                            const int strides[3], int slice, int32_t *out,
+                            int64_t cap)
+{
+    int16_t qt[5][256];
+    build_quant_set(qt, cfg->context_model, cfg->bits_per_raw_sample);
+    int bits = cfg->bits_per_raw_sample <= 8 ? 8 : cfg->bits_per_raw_sample;
+    int x0, y0, w, h;
+    slice_rects(cfg, slice, &x0, &y0, &w, &h);
+    int np = cfg->chroma_planes ? 3 : 1;
+    int64_t n = 0;
+    int16_t *P = malloc((size_t)w * h * sizeof(int16_t) + 16);
+    for (int p = 0; p < np; p++) {
+        int px = x0, py = y0, pw = w, ph = h;
+        if (p) {
+            pw = ceil_rshift(w, cfg->chroma_h_shift);
+            ph = ceil_rshift(h, cfg->chroma_v_shift);
+            px = x0 >> cfg->chroma_h_shift;
+            py = y0 >> cfg->chroma_v_shift;
+        }
+        load_plane(cfg, planes[p], strides[p], px, py, pw, ph, P);
+        for (int y = 0; y < ph; y++)
+            for (int x = 0; x < pw; x++) {
+                taps t;
+                int ctx, diff;
+                get_taps(P, pw, x, y, &t);
+                sample_symbol((const int16_t(*)[256])qt, cfg->context_model,
+                              bits, &t, &ctx, &diff);
+                if (n < cap)
+                    out[n] = (int32_t)(((uint32_t)ctx << 16) | (uint16_t)diff);
+                n++;
+            }
+    }
+    free(P);
+    return n;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Decoder (ffv1dec.c) -- used only for lossless round-trip checks          */
+
+typedef struct dslice {
+    int x0, y0, w, h;
+    plane_state ps[2];
+} dslice;
+
+struct ffv1o_dec {
+    ffv1o_config cfg;
+    int version, micro_version, ac, ec, bits, chroma_planes, hs, vs;
+    int num_h, num_v;
+    int16_t qsets[2][5][256];
+    int ctx_count[2];
+    int16_t qt[5][256];     /* v0/v1 in-band tables */
+    int contexts;
+    rc_tables dflt, frame_tab;
+    uint8_t stt[256];
+    int nslices;
+    dslice *sl;
+    int key_ok;
+    int16_t *scratch;
+};
+
+/* read_quant_table(s), ffv1dec.c:475-515 */
+static int get_quant_tables(rc_dec *c, int16_t qt[5][256])
+{
+    int count = 1;
+    for (int t = 0; t < 5; t++) {
+        uint8_t st[32];
+        memset(st, 128, 32);
+        int i = 0, v;
+        for (v = 0; i < 128; v++) {
+            unsigned len = (unsigned)rc_get_symbol(c, st, 0) + 1;
+            if (len > (unsigned)(128 - i) || !len)
+                return -1;
+            while (len--)
+                qt[t][i++] = (int16_t)(count * v);
+        }
+        for (i = 1; i < 128; i++)
+            qt[t][256 - i] = -qt[t][i];
+        qt[t][128] = -qt[t][127];
+        count *= 2 * v - 1;
+        if (count > 32768)
+            return -1;
+    }
+    return (count + 1) / 2;
+}
+
+static void dec_alloc_slices(ffv1o_dec *d)
+{
+    d->nslices = d->num_h * d->num_v;
+    d->sl = calloc(d->nslices, sizeof(dslice));
+    int maxctx = 7563;
+    for (int i = 0; i < d->nslices; i++) {
+        slice_rects(&d->cfg, i, &d->sl[i].x0, &d->sl[i].y0, &d->sl[i].w,
+                    &d->sl[i].h);
+        for (int p = 0; p < 2; p++) {
+            d->sl[i].ps[p].rac = malloc((size_t)maxctx * 32);
+            d->sl[i].ps[p].vlc = malloc((size_t)maxctx * sizeof(vlc_ctx));
+        }
+    }
+}
+
+ffv1o_dec *ffv1o_dec_new(const ffv1o_config *cfg, const uint8_t *ex, int exn)
+{
+    ffv1o_dec *d = calloc(1, sizeof(*d));
+    d->cfg = *cfg;
+    rc_default_tables(&d->dflt);
+    d->frame_tab = d->dflt;
+    d->version = cfg->version;
+    d->num_h = d->num_v = 1;
+    d->scratch = malloc((size_t)cfg->width * cfg->height * sizeof(int16_t) + 16);
+    if (exn > 0) { /* read_extra_header, ffv1dec.c:517-636 */
+        if (ffv1o_crc32(0, ex, exn) != 0)
+            goto fail;
+        rc_dec c;
+        uint8_t st[32];
+        memset(st, 128, 32);
+        rc_dec_init(&c, ex, exn - 4, &d->dflt);
+        d->version = rc_get_symbol(&c, st, 0);
+        if (d->version > 2)
+            d->micro_version = rc_get_symbol(&c, st, 0);
+        d->ac = rc_get_symbol(&c, st, 0);
+        if (d->ac == 2) {
+            for (int i = 1; i < 256; i++)
+                d->stt[i] = (uint8_t)(rc_get_symbol(&c, st, 1) + d->dflt.to1[i]);
+            rc_custom_tables(&d->frame_tab, &d->dflt, d->stt);
+        }
+        if (rc_get_symbol(&c, st, 0) != 0) /* colorspace */
+            goto fail;
+        d->bits = rc_get_symbol(&c, st, 0);
+        d->chroma_planes = rc_get(&c, &st[0]);
+        d->hs = rc_get_symbol(&c, st, 0);
+        d->vs = rc_get_symbol(&c, st, 0);
+        if (rc_get(&c, &st[0])) /* transparency */
+            goto fail;
+        d->num_h = 1 + rc_get_symbol(&c, st, 0);
+        d->num_v = 1 + rc_get_symbol(&c, st, 0);
+        int nq = rc_get_symbol(&c, st, 0);
+        if (nq < 1 || nq > 2)
+            goto fail;
+        for (int i = 0; i < nq; i++) {
+            d->ctx_count[i] = get_quant_tables(&c, d->qsets[i]);
+            if (d->ctx_count[i] < 0)
+                goto fail;
+        }
+        for (int i = 0; i < nq; i++)
+            if (rc_get(&c, &st[0])) /* non-default initial states unsupported */
+                goto fail;
+        if (d->version > 2) {
+            d->ec = rc_get_symbol(&c, st, 0);
+            if (d->micro_version > 2)
+                (void)rc_get_symbol(&c, st, 0);
+        }
+        d->cfg.num_h_slices = d->num_h;
+        d->cfg.num_v_slices = d->num_v;
+    }
+    dec_alloc_slices(d);
+    return d;
+fail:
+    free(d->scratch);
+    free(d);
+    return NULL;
+}
+
+void ffv1o_dec_free(ffv1o_dec *d)
+{
+    if (!d)
+        return;
+    for (int i = 0; i < d->nslices; i++)
+        for (int p = 0; p < 2; p++) {
+            free(d->sl[i].ps[p].rac);
+            free(d->sl[i].ps[p].vlc);
+        }
+    free(d->sl);
+    free(d->scratch);
+    free(d);
+}
+
+/* decode_plane/decode_line (ffv1dec.c:100-231): reconstruct into P, then
+ * store with the pixel format's alignment. */
+static void decode_plane_any(ffv1o_dec *d, void *coder, int golomb,
+                             plane_state *ps, const int16_t qt[5][256],
+                             int model1, int w, int h, uint8_t *dst,
+                             int stride, int x0, int y0)
+{
+    int bits = d->bits <= 8 ? 8 : d->bits;
+    int16_t *P = d->scratch;
+    int run_index = 0;
+    for (int y = 0; y < h; y++) {
+        int run_count = 0, run_mode = 0;
+        for (int x = 0; x < w; x++) {
+            taps t;
+            P[(int64_t)y * w + x] = 0;
+            get_taps(P, w, x, y, &t);
+            int ctx = qt[0][(t.L - t.LT) & 0xFF] + qt[1][(t.LT - t.T) & 0xFF] +
+                      qt[2][(t.T - t.RT) & 0xFF];
+            if (model1)
+                ctx += qt[3][(t.LL - t.L) & 0xFF] + qt[4][(t.TT - t.T) & 0xFF];
+            int sign = ctx < 0, diff;
+            if (sign)
+                ctx = -ctx;
+            if (!golomb) {
+                diff = rc_get_symbol((rc_dec *)coder, ps->rac + (int64_t)ctx * 32, 1);
+            } else {
+                bitr *b = (bitr *)coder;
+                if (ctx == 0 && run_mode == 0)
+                    run_mode = 1;
+                if (run_mode) {
+                    if (run_count == 0 && run_mode == 1) {
+                        if (br_get(b, 1)) {
+                            run_count = 1 << log2_run[run_index];
+                            if (x + run_count <= w)
+                                run_index++;
+                        } else {
+                            run_count = log2_run[run_index]
+                                            ? br_get(b, log2_run[run_index]) : 0;
+                            if (run_index)
+                                run_index--;
+                            run_mode = 2;
+                        }
+                    }
+                    run_count--;
+                    if (run_count < 0) {
+                        run_mode = 0;
+                        run_count = 0;
+                        diff = vlc_get(b, &ps->vlc[ctx], bits);
+                        if (diff >= 0)
+                            diff++;
+                    } else {
+                        diff = 0;
+                    }
+                } else {
+                    diff = vlc_get(b, &ps->vlc[ctx], bits);
+                }
+            }
+            if (sign)
+                diff = -diff;
+            int pred = median3(t.L, t.L + t.T - t.LT, t.T);
+            P[(int64_t)y * w + x] = (int16_t)((unsigned)(pred + diff) & ((1u << bits) - 1));
+        }
+    }
+    for (int y = 0; y < h; y++) {
+        uint8_t *row = dst + (int64_t)(y0 + y) * stride;
+        for (int x = 0; x < w; x++) {
+            unsigned v = (uint16_t)P[(int64_t)y * w + x];
+            if (d->cfg.sample_bytes == 1) {
+                row[x0 + x] = (uint8_t)v;
+            } else {
+                if (!d->cfg.packed_at_lsb)
+                    v = (v << (16 - d->bits)) & 0xFFFF;
+                row[2 * (x0 + x)] = (uint8_t)v;
+                row[2 * (x0 + x) + 1] = (uint8_t)(v >> 8);
+            }
+        }
+    }
+}
+
+int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
+                    uint8_t *const planes[3], const int strides[3], int *key_out)
+{
+    rc_dec c0;
+    uint8_t ks = 128;
+    rc_dec_init(&c0, pkt, size, &d->dflt);
+    int key = rc_get(&c0, &ks);
+    if (key) {
+        if (d->version < 2) { /* read_header v0/v1, ffv1dec.c:646-700 */
+            uint8_t st[32];
+            memset(st, 128, 32);
+            d->version = rc_get_symbol(&c0, st, 0);
+            d->ac = rc_get_symbol(&c0, st, 0);
+            if (d->ac == 2) {
+                for (int i = 1; i < 256; i++)
+                    d->stt[i] = (uint8_t)(rc_get_symbol(&c0, st, 1) + d->dflt.to1[i]);
+                rc_custom_tables(&d->frame_tab, &d->dflt, d->stt);
+            } else {
+                d->frame_tab = d->dflt;
+            }
+            (void)rc_get_symbol(&c0, st, 0);
+            d->bits = d->version > 0 ? rc_get_symbol(&c0, st, 0) : 8;
+            d->chroma_planes = rc_get(&c0, &st[0]);
+            d->hs = rc_get_symbol(&c0, st, 0);
+            d->vs = rc_get_symbol(&c0, st, 0);
+            (void)rc_get(&c0, &st[0]);
+            d->contexts = get_quant_tables(&c0, d->qt);
+            if (d->contexts < 0)
+                return -1;
+        }
+        d->key_ok = 1;
+    } else if (!d->key_ok) {
+        return -3;
+    }
+    if (d->version == 0 && d->bits == 0)
+        d->bits = 8;
+
+    /* slice chain from the end of the packet, ffv1dec.c:948-989 */
+    int trailer = 3 + (d->ec ? 5 : 0);
+    int64_t starts[256], lens[256];
+    int n = d->nslices;
+    const uint8_t *p = pkt + size;
+    if (d->version > 2) { /* count slices (read_header :805-818) */
+        int cnt = 0;
+        const uint8_t *q = pkt + size;
+        while (cnt < 256 && q - pkt > 3) {
+            int64_t sz = (q[-trailer] << 16) | (q[-trailer + 1] << 8) | q[-trailer + 2];
+            if (sz + trailer > q - pkt)
+                break;
+            q -= sz + trailer;
+            cnt++;
+        }
+        if (cnt != n)
+            return -1;
+    }
+    for (int i = n - 1; i >= 0; i--) {
+        int64_t v;
+        if (i || d->version > 2)
+            v = ((p[-trailer] << 16) | (p[-trailer + 1] << 8) | p[-trailer + 2]) + trailer;
+        else
+            v = p - pkt;
+        if (p - pkt < v)
+            return -1;
+        p -= v;
+        if (d->ec && ffv1o_crc32(0, p, v) != 0)
+            return -2;
+        starts[i] = p - pkt;
+        lens[i] = v;
+    }
+
+    for (int i = 0; i < n; i++) {
+        dslice *s = &d->sl[i];
+        rc_dec c;
+        if (i == 0) {
+            c = c0;
+            c.end = pkt + starts[0] + lens[0];
+        } else {
+            rc_dec_init(&c, pkt + starts[i], lens[i], &d->frame_tab);
+        }
+        c.t = &d->frame_tab;
+        const int16_t(*qt)[256] = (const int16_t(*)[256])d->qt;
+        int model1 = 0;
+        int contexts = d->contexts;
+        if (d->version > 2) { /* decode_slice_header, ffv1dec.c:282-359 */
+            uint8_t st[32];
+            memset(st, 128, 32);
+            int sx = rc_get_symbol(&c, st, 0), sy = rc_get_symbol(&c, st, 0);
+            int sw = rc_get_symbol(&c, st, 0), sh = rc_get_symbol(&c, st, 0);
+            int x0 = sx * d->cfg.width / d->num_h;
+            int y0 = sy * d->cfg.height / d->num_v;
+            int x1 = (sx + sw + 1) * d->cfg.width / d->num_h;
+            int y1 = (sy + sh + 1) * d->cfg.height / d->num_v;
+            s->x0 = x0; s->y0 = y0; s->w = x1 - x0; s->h = y1 - y0;
+            int qi = 0;
+            for (int j = 0; j < 2; j++)
+                qi = rc_get_symbol(&c, st, 0);
+            if (qi > 1)
+                return -1;
+            (void)rc_get_symbol(&c, st, 0); /* picture structure */
+            (void)rc_get_symbol(&c, st, 0);
+            (void)rc_get_symbol(&c, st, 0);
+            qt = (const int16_t(*)[256])d->qsets[qi];
+            model1 = qi;
+            contexts = d->ctx_count[qi];
+        }
+        if (key)
+            for (int pp = 0; pp < 2; pp++) {
+                memset(s->ps[pp].rac, 128, (size_t)contexts * 32);
+                for (int j = 0; j < contexts; j++)
+                    vlc_reset(&s->ps[pp].vlc[j]);
+            }
+        bitr b;
+        void *coder = &c;
+        int golomb = d->ac == 0;
+        if (golomb) {
+            int64_t acb = 0;
+            if (d->version > 2) {
+                uint8_t st = 129;
+                (void)rc_get(&c, &st);
+            }
+            if (d->version > 2 || (s->x0 == 0 && s->y0 == 0))
+                acb = (c.ptr - c.base) - 1;
+            int64_t blen = (i == 0 ? lens[0] : lens[i]) - acb;
+            b.base = c.base + acb;
+            b.pos = 0;
+            b.nbits = blen * 8;
+            coder = &b;
+        }
+        int np = d->chroma_planes ? 3 : 1;
+        for (int pl = 0; pl < np; pl++) {
+            int x0 = s->x0, y0 = s->y0, w = s->w, h = s->h;
+            if (pl) {
+                w = ceil_rshift(s->w, d->hs);
+                h = ceil_rshift(s->h, d->vs);
+                x0 = s->x0 >> d->hs;
+                y0 = s->y0 >> d->vs;
+            }
+            decode_plane_any(d, coder, golomb, &s->ps[pl ? 1 : 0], qt, model1,
+                             w, h, planes[pl], strides[pl], x0, y0);
+        }
+    }
+    if (key_out)
+        *key_out = key;
+    return 0;
+}
