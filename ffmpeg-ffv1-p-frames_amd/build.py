@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Builds the in-tree native libraries of the MI355X FFV1 encoder.
+
+  lib/libffv1hip.so    HIP kernels (gfx950) + the C-ABI of include/ffv1hip.h
+  lib/libffv1synth.so  synthetic input clips (host C)
+
+Everything is built in-tree so the .so files travel with the repo snapshot to
+the GPU box (they are git-ignored, not gpurun-ignored).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "lib")
+INCLUDE = os.path.join(os.path.dirname(HERE), "include")
+ARCH = os.environ.get("FFV1HIP_ARCH", "gfx950")
+
+
+def _stale(target, sources):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in sources)
+
+
+def _run(cmd):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+
+
+def build_synth(force=False):
+    os.makedirs(LIB, exist_ok=True)
+    out = os.path.join(LIB, "libffv1synth.so")
+    src = [os.path.join(CSRC, "synth.c")]
+    if force or _stale(out, src):
+        _run(["gcc", "-O2", "-std=c11", "-Wall", "-fPIC", "-shared", "-o", out] + src)
+    return out
+
+
+def hipcc():
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found")
+
+
+def build_hip(force=False, extra=()):
+    os.makedirs(LIB, exist_ok=True)
+    out = os.path.join(LIB, "libffv1hip.so")
+    srcs = [os.path.join(CSRC, "ffv1_kernels.hip"), os.path.join(CSRC, "ffv1_host.cpp")]
+    deps = srcs + [os.path.join(CSRC, "ffv1_internal.h"), os.path.join(INCLUDE, "ffv1hip.h")]
+    if force or _stale(out, deps):
+        _run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+              "-Wall", "-Wno-unused-function", "-I", INCLUDE, "-o", out, *extra] + srcs)
+    return out
+
+
+def build_all(force=False):
+    return build_synth(force), build_hip(force)
+
+
+if __name__ == "__main__":
+    force = "--force" in sys.argv
+    for p in build_all(force):
+        print(p)

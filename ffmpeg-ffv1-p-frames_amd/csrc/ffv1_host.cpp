@@ -1,0 +1,722 @@
+// ffv1_host.cpp -- host side of the MI355X FFV1 encoder: the C-ABI of
+// include/ffv1hip.h, encode_init's parameter contract, the (init-time)
+// extradata writer, the per-slice header op lists and HBM buffer management.
+// The per-sample work runs in ffv1_kernels.hip; nothing here touches pixels.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ffv1hip.h"
+#include "ffv1_internal.h"
+
+using namespace ffv1hip;
+
+namespace {
+
+thread_local char g_err[512];
+
+int set_err(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define HIP_TRY(expr)                                                         \
+  do {                                                                        \
+    hipError_t e_ = (expr);                                                   \
+    if (e_ != hipSuccess)                                                     \
+      return set_err(-5, "%s failed: %s", #expr, hipGetErrorString(e_));      \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// Transition tables.  Default: ff_build_rac_states(c, 0.05*2^32, 256-8)
+// (rangecoder.c:63-101); custom: the FFV1 v2+ table (ffv1enc.c:120-137)
+// installed as in ffv1.c:95-101.
+struct Tables {
+  uint8_t to0[256], to1[256];
+};
+
+Tables default_tables() {
+  Tables t;
+  std::memset(&t, 0, sizeof(t));
+  const int64_t one = int64_t(1) << 32;
+  const int factor = int(0.05 * double(int64_t(1) << 32));
+  const int max_p = 248;
+  int64_t p = one / 2;
+  int last = 0;
+  for (int i = 0; i < 128; i++) {
+    int p8 = int((256 * p + one / 2) >> 32);
+    if (p8 <= last) p8 = last + 1;
+    if (last && last < 256 && p8 <= max_p) t.to1[last] = uint8_t(p8);
+    p += ((one - p) * factor + one / 2) >> 32;
+    last = p8;
+  }
+  for (int i = 256 - max_p; i <= max_p; i++) {
+    if (t.to1[i]) continue;
+    int64_t q = (int64_t(i) * one + 128) >> 8;
+    q += ((one - q) * factor + one / 2) >> 32;
+    int p8 = int((256 * q + one / 2) >> 32);
+    if (p8 <= i) p8 = i + 1;
+    if (p8 > max_p) p8 = max_p;
+    t.to1[i] = uint8_t(p8);
+  }
+  for (int i = 1; i < 255; i++) t.to0[i] = uint8_t(256 - t.to1[256 - i]);
+  return t;
+}
+
+const uint8_t kCustomStt[256] = {
+    0,   10,  10,  10,  10,  16,  16,  16,  28,  16,  16,  29,  42,  49,  20,  49,
+    59,  25,  26,  26,  27,  31,  33,  33,  33,  34,  34,  37,  67,  38,  39,  39,
+    40,  40,  41,  79,  43,  44,  45,  45,  48,  48,  64,  50,  51,  52,  88,  52,
+    53,  74,  55,  57,  58,  58,  74,  60,  101, 61,  62,  84,  66,  66,  68,  69,
+    87,  82,  71,  97,  73,  73,  82,  75,  111, 77,  94,  78,  87,  81,  83,  97,
+    85,  83,  94,  86,  99,  89,  90,  99,  111, 92,  93,  134, 95,  98,  105, 98,
+    105, 110, 102, 108, 102, 118, 103, 106, 106, 113, 109, 112, 114, 112, 116, 125,
+    115, 116, 117, 117, 126, 119, 125, 121, 121, 123, 145, 124, 126, 131, 127, 129,
+    165, 130, 132, 138, 133, 135, 145, 136, 137, 139, 146, 141, 143, 142, 144, 148,
+    147, 155, 151, 149, 151, 150, 152, 157, 153, 154, 156, 168, 158, 162, 161, 160,
+    172, 163, 169, 164, 166, 184, 167, 170, 177, 174, 171, 173, 182, 176, 180, 178,
+    175, 189, 179, 181, 186, 183, 192, 185, 200, 187, 191, 188, 190, 197, 193, 196,
+    197, 194, 195, 196, 198, 202, 199, 201, 210, 203, 207, 204, 205, 206, 208, 214,
+    209, 211, 221, 212, 213, 215, 224, 216, 217, 218, 219, 220, 222, 228, 223, 225,
+    226, 224, 227, 229, 240, 230, 231, 232, 233, 234, 235, 236, 238, 239, 237, 242,
+    241, 243, 242, 244, 245, 246, 247, 248, 249, 250, 251, 252, 252, 253, 254, 255,
+};
+
+Tables custom_tables(const Tables& dflt) {
+  Tables t = dflt;
+  for (int i = 1; i < 256; i++) {
+    t.to1[i] = kCustomStt[i];
+    t.to0[256 - i] = uint8_t(256 - kCustomStt[i]);
+  }
+  return t;
+}
+
+// ---------------------------------------------------------------------------
+// Quantisation tables (ffv1enc.c:44-118, 846-879), expressed by the first
+// index of each quantiser step on [0,127]; the negative half mirrors.
+void quant_table(int16_t* q, std::initializer_list<int> steps, int scale) {
+  int level = 0;
+  auto it = steps.begin();
+  for (int i = 0; i < 128; i++) {
+    while (it != steps.end() && i >= *it) { ++level; ++it; }
+    q[i] = int16_t(scale * level);
+  }
+  for (int i = 1; i < 128; i++) q[256 - i] = int16_t(-q[i]);
+  q[128] = int16_t(-q[127]);
+}
+
+void quant_set(int16_t qt[5][256], int model, int bits) {
+  std::memset(qt, 0, sizeof(int16_t) * 5 * 256);
+  const bool hi = bits > 8;
+  auto A = hi ? std::initializer_list<int>{5, 13, 27, 56} : std::initializer_list<int>{1, 2, 5, 12, 35};
+  auto B = hi ? std::initializer_list<int>{11, 50} : std::initializer_list<int>{1, 4};
+  quant_table(qt[0], A, 1);
+  quant_table(qt[1], A, 11);
+  if (model == 0) {
+    quant_table(qt[2], A, 121);
+  } else {
+    quant_table(qt[2], B, 121);
+    quant_table(qt[3], B, 605);
+    quant_table(qt[4], B, 3025);
+  }
+}
+
+int contexts_of(int model) { return model ? (11 * 11 * 5 * 5 * 5 + 1) / 2 : (11 * 11 * 11 + 1) / 2; }
+
+// ---------------------------------------------------------------------------
+// Host range coder: only for the init-time extradata (write_extradata is
+// host work in the reference too, ffv1enc.c:545-619).
+struct HostRac {
+  int low = 0, range = 0xFF00, pending = -1, run = 0;
+  std::vector<uint8_t> out;
+  const Tables* t;
+  explicit HostRac(const Tables* tab) : t(tab) {}
+  void shift() {
+    while (range < 0x100) {
+      if (pending < 0) {
+        pending = low >> 8;
+      } else if (low <= 0xFF00) {
+        out.push_back(uint8_t(pending));
+        for (; run; run--) out.push_back(0xFF);
+        pending = low >> 8;
+      } else if (low >= 0x10000) {
+        out.push_back(uint8_t(pending + 1));
+        for (; run; run--) out.push_back(0x00);
+        pending = (low >> 8) & 0xFF;
+      } else {
+        run++;
+      }
+      low = (low & 0xFF) << 8;
+      range <<= 8;
+    }
+  }
+  void put(uint8_t* st, int bit) {
+    int r1 = (range * *st) >> 8;
+    if (bit) { low += range - r1; range = r1; *st = t->to1[*st]; }
+    else { range -= r1; *st = t->to0[*st]; }
+    shift();
+  }
+  void symbol(uint8_t* st, int v, bool sgn) {
+    if (!v) { put(st, 1); return; }
+    unsigned a = v < 0 ? 0u - unsigned(v) : unsigned(v);
+    int e = 31 - __builtin_clz(a);
+    put(st, 0);
+    for (int i = 0; i < e; i++) put(st + 1 + std::min(i, 9), 1);
+    put(st + 1 + std::min(e, 9), 0);
+    for (int i = e - 1; i >= 0; i--) put(st + 22 + std::min(i, 9), (a >> i) & 1);
+    if (sgn) put(st + 11 + std::min(e, 10), v < 0);
+  }
+  void finish() {
+    range = 0xFF; low += 0xFF; shift();
+    range = 0xFF; shift();
+  }
+};
+
+uint32_t crc32_msb(const uint8_t* p, size_t n) {
+  uint32_t crc = 0;
+  for (size_t i = 0; i < n; i++) {
+    crc ^= uint32_t(p[i]) << 24;
+    for (int k = 0; k < 8; k++) crc = (crc & 0x80000000u) ? (crc << 1) ^ 0x04C11DB7u : (crc << 1);
+  }
+  return crc;
+}
+
+// Recorder used to turn a header writer into an op list for the device.
+struct OpList {
+  std::vector<Op> ops;
+  void sym(int set, int tab, int v, bool sgn) { ops.push_back(Op{int16_t(sgn ? kOpSymS : kOpSymU), uint8_t(set), uint8_t(tab), v}); }
+  void bit(int set, int tab, int v) { ops.push_back(Op{int16_t(kOpBit), uint8_t(set), uint8_t(tab), v}); }
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+struct ffv1hip_ctx {
+  ffv1hip_params P{};
+  int device = 0;
+  int max_batch = 0;
+  int nslices = 0;
+  int contexts = 0;
+  Tables dflt{}, frame{};
+  int16_t qt[5][256]{};
+  std::vector<uint8_t> extradata;
+  std::vector<Op> ops;     // [key][slice][kMaxOps]
+  std::vector<int> nops;   // [key][slice]
+  int64_t slice_cap = 0;
+  int64_t packet_stride = 0;
+  int64_t frame_bytes = 0;  // host-layout batch buffer stride
+  int64_t plane_bytes[3]{};
+  int64_t picture_number = 0;
+  bool have_states = false;  // persistent states valid (a frame was coded)
+  int row_len = 0;
+  // device buffers
+  uint8_t* d_frames = nullptr;
+  int16_t* d_qt = nullptr;
+  uint8_t* d_tabs = nullptr;
+  Op* d_ops = nullptr;
+  int* d_nops = nullptr;
+  Segment* d_segs = nullptr;
+  uint8_t* d_keys = nullptr;
+  uint8_t* d_slice_out = nullptr;
+  int64_t* d_slice_bytes = nullptr;
+  uint8_t* d_packets = nullptr;
+  int64_t* d_packet_size = nullptr;
+  uint8_t* d_persist = nullptr;
+  uint8_t* d_gstates = nullptr;
+  int* d_status = nullptr;
+  hipStream_t stream = nullptr;
+  int last_n = 0;
+  std::vector<int> last_keys;
+};
+
+extern "C" {
+
+const char* ffv1hip_last_error(void) { return g_err; }
+int ffv1hip_abi_version(void) { return FFV1HIP_ABI_VERSION; }
+
+int ffv1hip_configure(ffv1hip_params* out, const ffv1hip_options* o) {
+  if (!out || !o || !o->pix_fmt || o->width <= 0 || o->height <= 0)
+    return set_err(-22, "invalid arguments");
+  struct Fmt { const char* name; int planes, hs, vs, depth; };
+  static const Fmt fmts[] = {
+      {"yuv420p", 3, 1, 1, 8},    {"yuv422p", 3, 1, 0, 8},    {"yuv444p", 3, 0, 0, 8},
+      {"yuv440p", 3, 0, 1, 8},    {"yuv411p", 3, 2, 0, 8},    {"yuv410p", 3, 2, 2, 8},
+      {"gray", 1, 0, 0, 8},       {"yuv420p9", 3, 1, 1, 9},   {"yuv422p9", 3, 1, 0, 9},
+      {"yuv444p9", 3, 0, 0, 9},   {"yuv420p10", 3, 1, 1, 10}, {"yuv422p10", 3, 1, 0, 10},
+      {"yuv444p10", 3, 0, 0, 10}, {"yuv420p16", 3, 1, 1, 16}, {"yuv422p16", 3, 1, 0, 16},
+      {"yuv444p16", 3, 0, 0, 16}, {"gray16", 1, 0, 0, 16},
+  };
+  const Fmt* f = nullptr;
+  for (const Fmt& c : fmts)
+    if (!std::strcmp(c.name, o->pix_fmt)) f = &c;
+  if (!f) return set_err(-38, "pix_fmt %s not supported", o->pix_fmt);
+
+  ffv1hip_params p{};
+  p.width = o->width;
+  p.height = o->height;
+  p.gop_size = o->gop_size;
+  p.sar_num = 0;
+  p.sar_den = 1;
+  // version (ffv1enc.c:678-706)
+  int version = 0;
+  if (o->slices > 1) version = 2;
+  if (o->slices == 0 && o->level < 0 && int64_t(o->width) * o->height > 720 * 576) version = 2;
+  if (o->level <= 0 && version == 2) version = 3;
+  if (o->level >= 0 && o->level <= 4) {
+    if (o->level < version) return set_err(-22, "version %d needed, level %d requested", version, o->level);
+    version = o->level;
+  }
+  p.ec = o->slicecrc < 0 ? (version >= 3) : o->slicecrc;
+  if (version == 2 || version > 3)
+    return set_err(FFV1HIP_AVERROR_INVALIDDATA, "version %d is experimental in the reference", version);
+  // coder (ffv1enc.c:708-718)
+  int ac = 0;
+  if (o->coder != -1) ac = o->coder > 0 ? 2 : 0;
+  if (o->coder == -2) ac = 1;
+  // sample format (ffv1enc.c:720-820)
+  int bits = 0, packed = 0;
+  if (f->depth > 8) {
+    if (f->depth == 9 && !o->bits_per_raw_sample) bits = 9;
+    if (f->depth <= 10) {
+      packed = 1;
+      if (!o->bits_per_raw_sample && !bits) bits = 10;
+    }
+    if (!o->bits_per_raw_sample && !bits) bits = 16;
+    else if (!bits) bits = o->bits_per_raw_sample;
+    if (bits <= 8) return set_err(FFV1HIP_AVERROR_INVALIDDATA, "bits_per_raw_sample invalid");
+    if (ac == 0) ac = 2;  // >8 bit forces the range coder
+    version = std::max(version, 1);
+  }
+  if (!bits) bits = 8;
+  if (o->context < 0 || o->context > 1) return set_err(-22, "context model %d", o->context);
+  p.chroma_planes = f->planes == 3;
+  p.chroma_h_shift = f->planes == 3 ? f->hs : 0;
+  p.chroma_v_shift = f->planes == 3 ? f->vs : 0;
+  p.bits_per_raw_sample = bits;
+  p.packed_at_lsb = packed;
+  p.sample_bytes = f->depth > 8 ? 2 : 1;
+  p.version = version;
+  p.ac = ac;
+  p.context_model = o->context;
+  p.num_h_slices = p.num_v_slices = 1;
+  // slice grid (ffv1enc.c:988-1000); allow_large_grid extends it to the
+  // decoder's MAX_SLICES=256 (ffv1.h:77) for 8K.
+  if (version > 1) {
+    const int max_v = o->allow_large_grid ? 16 : 8;
+    const int max_slices = o->allow_large_grid ? 256 : 64;
+    int nv = (o->width > 352 || o->height > 288 || !o->slices) ? 2 : 1;
+    bool ok = false;
+    for (; nv <= max_v && !ok; nv++)
+      for (int nh = nv; nh < 2 * nv && !ok; nh++)
+        if ((o->slices == nh * nv && o->slices <= max_slices) || !o->slices) {
+          p.num_h_slices = nh;
+          p.num_v_slices = nv;
+          ok = true;
+        }
+    if (!ok) return set_err(-38, "unsupported number of slices %d", o->slices);
+  }
+  *out = p;
+  return 0;
+}
+
+static int build_extradata(ffv1hip_ctx* c) {
+  const ffv1hip_params& p = c->P;
+  c->extradata.clear();
+  if (p.version < 2) return 0;
+  HostRac r(&c->dflt);
+  uint8_t st[32];
+  std::memset(st, 128, 32);
+  r.symbol(st, p.version, false);
+  if (p.version > 2) r.symbol(st, p.version == 3 ? 4 : 2, false);
+  r.symbol(st, p.ac, false);
+  if (p.ac == 2)
+    for (int i = 1; i < 256; i++) r.symbol(st, c->frame.to1[i] - c->dflt.to1[i], true);
+  r.symbol(st, 0, false);  // YUV colorspace
+  r.symbol(st, p.bits_per_raw_sample, false);
+  r.put(st, p.chroma_planes);
+  r.symbol(st, p.chroma_h_shift, false);
+  r.symbol(st, p.chroma_v_shift, false);
+  r.put(st, 0);  // transparency
+  r.symbol(st, p.num_h_slices - 1, false);
+  r.symbol(st, p.num_v_slices - 1, false);
+  r.symbol(st, 2, false);  // quant_table_count
+  for (int set = 0; set < 2; set++) {
+    int16_t qt[5][256];
+    quant_set(qt, set, p.bits_per_raw_sample);
+    for (int t = 0; t < 5; t++) {
+      uint8_t qs[32];
+      std::memset(qs, 128, 32);
+      int last = 0, i;
+      for (i = 1; i < 128; i++)
+        if (qt[t][i] != qt[t][i - 1]) { r.symbol(qs, i - last - 1, false); last = i; }
+      r.symbol(qs, i - last - 1, false);
+    }
+  }
+  r.put(st, 0);  // default initial states for both quant sets
+  r.put(st, 0);
+  if (p.version > 2) {
+    r.symbol(st, p.ec, false);
+    r.symbol(st, p.gop_size < 2, false);
+  }
+  r.finish();
+  c->extradata = r.out;
+  uint32_t crc = crc32_msb(c->extradata.data(), c->extradata.size());
+  for (int k = 3; k >= 0; k--) c->extradata.push_back(uint8_t(crc >> (8 * k)));
+  return 0;
+}
+
+// Header programs: per (key, slice), the decisions coded before the planes.
+static void build_ops(ffv1hip_ctx* c) {
+  const ffv1hip_params& p = c->P;
+  c->ops.assign(size_t(2) * c->nslices * kMaxOps, Op{0, 0, 0, 0});
+  c->nops.assign(size_t(2) * c->nslices, 0);
+  enum { kSetHdr = 0, kSetQ0 = 1, kSetKey = 6, kSetSlice = 7 };
+  for (int key = 0; key < 2; key++)
+    for (int s = 0; s < c->nslices; s++) {
+      OpList L;
+      if (s == 0) {
+        L.bit(kSetKey, 0, key);  // key bit, state 128, default table
+        if (key && p.version < 2) {  // write_header (ffv1enc.c:506-522)
+          L.sym(kSetHdr, 0, p.version, false);
+          L.sym(kSetHdr, 0, p.ac, false);
+          if (p.ac == 2)
+            for (int i = 1; i < 256; i++) L.sym(kSetHdr, 0, c->frame.to1[i] - c->dflt.to1[i], true);
+          L.sym(kSetHdr, 0, 0, false);
+          if (p.version > 0) L.sym(kSetHdr, 0, p.bits_per_raw_sample, false);
+          L.bit(kSetHdr, 0, p.chroma_planes);
+          L.sym(kSetHdr, 0, p.chroma_h_shift, false);
+          L.sym(kSetHdr, 0, p.chroma_v_shift, false);
+          L.bit(kSetHdr, 0, 0);
+          for (int t = 0; t < 5; t++) {
+            int last = 0, i;
+            for (i = 1; i < 128; i++)
+              if (c->qt[t][i] != c->qt[t][i - 1]) { L.sym(kSetQ0 + t, 0, i - last - 1, false); last = i; }
+            L.sym(kSetQ0 + t, 0, i - last - 1, false);
+          }
+        }
+      }
+      if (p.version > 2) {  // encode_slice_header (ffv1enc.c:1031-1051)
+        const int nh = p.num_h_slices, nv = p.num_v_slices;
+        const int sx = s % nh, sy = s / nh;
+        const int x0 = int(int64_t(p.width) * sx / nh), x1 = int(int64_t(p.width) * (sx + 1) / nh);
+        const int y0 = int(int64_t(p.height) * sy / nv), y1 = int(int64_t(p.height) * (sy + 1) / nv);
+        L.sym(kSetSlice, 1, int(int64_t(x0 + 1) * nh / p.width), false);
+        L.sym(kSetSlice, 1, int(int64_t(y0 + 1) * nv / p.height), false);
+        L.sym(kSetSlice, 1, int(int64_t(x1 - x0 + 1) * nh / p.width) - 1, false);
+        L.sym(kSetSlice, 1, int(int64_t(y1 - y0 + 1) * nv / p.height) - 1, false);
+        for (int j = 0; j < 2; j++) L.sym(kSetSlice, 1, p.context_model, false);
+        L.sym(kSetSlice, 1, 3, false);  // progressive
+        L.sym(kSetSlice, 1, p.sar_num, false);
+        L.sym(kSetSlice, 1, p.sar_den, false);
+      }
+      const size_t sel = size_t(key) * c->nslices + s;
+      c->nops[sel] = int(L.ops.size());
+      std::memcpy(&c->ops[sel * kMaxOps], L.ops.data(), L.ops.size() * sizeof(Op));
+    }
+}
+
+static void free_device(ffv1hip_ctx* c) {
+  void* ptrs[] = {c->d_frames, c->d_qt, c->d_tabs, c->d_ops, c->d_nops, c->d_segs, c->d_keys,
+                  c->d_slice_out, c->d_slice_bytes, c->d_packets, c->d_packet_size, c->d_persist,
+                  c->d_gstates, c->d_status};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+}
+
+static int alloc_device(ffv1hip_ctx* c) {
+  const ffv1hip_params& p = c->P;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  const int nb = c->max_batch;
+  HIP_TRY(hipMalloc(&c->d_frames, size_t(c->frame_bytes) * nb));
+  HIP_TRY(hipMalloc(&c->d_qt, sizeof(c->qt)));
+  HIP_TRY(hipMemcpy(c->d_qt, c->qt, sizeof(c->qt), hipMemcpyHostToDevice));
+  uint8_t tabs[1024];
+  std::memcpy(tabs, c->dflt.to0, 256);
+  std::memcpy(tabs + 256, c->dflt.to1, 256);
+  std::memcpy(tabs + 512, c->frame.to0, 256);
+  std::memcpy(tabs + 768, c->frame.to1, 256);
+  HIP_TRY(hipMalloc(&c->d_tabs, 1024));
+  HIP_TRY(hipMemcpy(c->d_tabs, tabs, 1024, hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&c->d_ops, c->ops.size() * sizeof(Op)));
+  HIP_TRY(hipMemcpy(c->d_ops, c->ops.data(), c->ops.size() * sizeof(Op), hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&c->d_nops, c->nops.size() * sizeof(int)));
+  HIP_TRY(hipMemcpy(c->d_nops, c->nops.data(), c->nops.size() * sizeof(int), hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&c->d_segs, sizeof(Segment) * (nb + 1)));
+  HIP_TRY(hipMalloc(&c->d_keys, nb));
+  HIP_TRY(hipMalloc(&c->d_slice_out, size_t(c->slice_cap) * c->nslices * nb));
+  HIP_TRY(hipMalloc(&c->d_slice_bytes, sizeof(int64_t) * c->nslices * nb));
+  HIP_TRY(hipMalloc(&c->d_packets, size_t(c->packet_stride) * nb));
+  HIP_TRY(hipMalloc(&c->d_packet_size, sizeof(int64_t) * nb));
+  const size_t state_bytes = size_t(2) * c->contexts * 32;
+  HIP_TRY(hipMalloc(&c->d_persist, state_bytes * c->nslices));
+  if (p.context_model) HIP_TRY(hipMalloc(&c->d_gstates, state_bytes * c->nslices * (nb + 1)));
+  HIP_TRY(hipMalloc(&c->d_status, sizeof(int) * 4));
+  return 0;
+}
+
+ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_batch_frames, int* err) {
+  auto fail = [&](int code) -> ffv1hip_ctx* {
+    if (err) *err = code;
+    return nullptr;
+  };
+  if (!params || max_batch_frames <= 0) return fail(set_err(-22, "invalid arguments"));
+  const ffv1hip_params& p = *params;
+  if (p.ac == 0)
+    return fail(set_err(-38, "Golomb-Rice coder (coder=0) is not on the device path yet"));
+  if (p.version == 2 || p.version > 3 || p.num_h_slices * p.num_v_slices > 256 ||
+      p.bits_per_raw_sample < 8 || p.bits_per_raw_sample > 16 || p.width <= 0 || p.height <= 0 ||
+      (p.sample_bytes == 1) != (p.bits_per_raw_sample == 8))
+    return fail(set_err(-38, "unsupported parameter set"));
+  if (p.num_h_slices > p.width || p.num_v_slices > p.height)
+    return fail(set_err(-22, "more slices than rows/columns"));
+  ffv1hip_ctx* c = new ffv1hip_ctx();
+  c->P = p;
+  c->device = device;
+  c->max_batch = max_batch_frames;
+  c->nslices = p.num_h_slices * p.num_v_slices;
+  c->contexts = contexts_of(p.context_model);
+  c->dflt = default_tables();
+  c->frame = p.ac == 2 ? custom_tables(c->dflt) : c->dflt;
+  quant_set(c->qt, p.context_model, p.bits_per_raw_sample);
+  build_extradata(c);
+  build_ops(c);
+  // layout of a frame in the batch buffer (planar, tightly packed)
+  const int cw = p.chroma_planes ? -((-p.width) >> p.chroma_h_shift) : 0;
+  const int ch = p.chroma_planes ? -((-p.height) >> p.chroma_v_shift) : 0;
+  c->plane_bytes[0] = int64_t(p.width) * p.height * p.sample_bytes;
+  c->plane_bytes[1] = c->plane_bytes[2] = int64_t(cw) * ch * p.sample_bytes;
+  c->frame_bytes = (c->plane_bytes[0] + 2 * c->plane_bytes[1] + 255) & ~int64_t(255);
+  // Slice byte budget: 4 bytes per coded sample (+4 KiB).  Real content
+  // codes below 2 bytes per 16-bit sample; exceeding it reports -ENOSPC.
+  int max_sw = 0, max_sh = 0;
+  for (int s = 0; s < c->nslices; s++) {
+    const int sx = s % p.num_h_slices, sy = s / p.num_h_slices;
+    max_sw = std::max<int>(max_sw, int(int64_t(p.width) * (sx + 1) / p.num_h_slices - int64_t(p.width) * sx / p.num_h_slices));
+    max_sh = std::max<int>(max_sh, int(int64_t(p.height) * (sy + 1) / p.num_v_slices - int64_t(p.height) * sy / p.num_v_slices));
+  }
+  const int64_t samples = int64_t(max_sw) * max_sh +
+                          (p.chroma_planes ? 2 * int64_t(-((-max_sw) >> p.chroma_h_shift)) * -((-max_sh) >> p.chroma_v_shift) : 0);
+  c->slice_cap = ((samples * 4 + 4096) + 255) & ~int64_t(255);
+  c->packet_stride = ((c->slice_cap + 16) * c->nslices + 255) & ~int64_t(255);
+  c->row_len = ((max_sw + 8) + 7) & ~7;
+  int rc = alloc_device(c);
+  if (rc < 0) {
+    free_device(c);
+    delete c;
+    return fail(rc);
+  }
+  if (err) *err = 0;
+  return c;
+}
+
+void ffv1hip_destroy(ffv1hip_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  free_device(c);
+  delete c;
+}
+
+int ffv1hip_extradata(ffv1hip_ctx* c, uint8_t* buf, int cap) {
+  if (!c) return set_err(-22, "null ctx");
+  const int n = int(c->extradata.size());
+  if (buf) {
+    if (cap < n) return set_err(-22, "extradata buffer too small");
+    std::memcpy(buf, c->extradata.data(), n);
+  }
+  return n;
+}
+
+int64_t ffv1hip_max_packet_size(const ffv1hip_ctx* c) { return c ? c->packet_stride : -22; }
+int64_t ffv1hip_picture_number(const ffv1hip_ctx* c) { return c ? c->picture_number : -22; }
+void ffv1hip_reset(ffv1hip_ctx* c) {
+  if (c) {
+    c->picture_number = 0;
+    c->have_states = false;
+  }
+}
+
+static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_bytes,
+                     const int64_t plane_off[3], const int plane_stride[3], int n, hipStream_t st) {
+  const ffv1hip_params& p = c->P;
+  if (n <= 0 || n > c->max_batch) return set_err(-22, "batch of %d frames (max %d)", n, c->max_batch);
+  // keyframes and state-chaining segments
+  std::vector<uint8_t> keys(n);
+  std::vector<Segment> segs;
+  for (int i = 0; i < n; i++) {
+    const int64_t pn = c->picture_number + i;
+    keys[i] = uint8_t(p.gop_size == 0 || pn % p.gop_size == 0);
+    if (i == 0 || keys[i]) segs.push_back(Segment{i, 0, 0, 0});
+    segs.back().nframes++;
+  }
+  if (!keys[0] && !c->have_states)
+    return set_err(-22, "P-frame without preceding keyframe state");
+  segs.front().load_states = !keys[0];
+  segs.back().save_states = 1;
+  HIP_TRY(hipMemcpyAsync(c->d_keys, keys.data(), n, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(c->d_segs, segs.data(), segs.size() * sizeof(Segment), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemsetAsync(c->d_status, 0, sizeof(int) * 4, st));
+
+  EncodeArgs a{};
+  a.frames = d_frames;
+  a.frame_bytes = frame_bytes;
+  for (int k = 0; k < 3; k++) {
+    a.plane_off[k] = plane_off[k];
+    a.plane_stride[k] = plane_stride[k];
+  }
+  a.width = p.width;
+  a.height = p.height;
+  a.nh = p.num_h_slices;
+  a.nv = p.num_v_slices;
+  a.nslices = c->nslices;
+  a.chroma_planes = p.chroma_planes;
+  a.hs = p.chroma_h_shift;
+  a.vs = p.chroma_v_shift;
+  a.sample_bytes = p.sample_bytes;
+  a.packed_at_lsb = p.packed_at_lsb;
+  a.msb_shift = 16 - p.bits_per_raw_sample;
+  a.coded_bits = p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample;
+  a.contexts = c->contexts;
+  a.model1 = p.context_model;
+  a.row_len = c->row_len;
+  a.qt = c->d_qt;
+  a.tabs = c->d_tabs;
+  a.segs = c->d_segs;
+  a.nsegs = int(segs.size());
+  a.keyflags = c->d_keys;
+  a.ops = c->d_ops;
+  a.nops = c->d_nops;
+  a.slice_out = c->d_slice_out;
+  a.slice_cap = c->slice_cap;
+  a.slice_bytes = c->d_slice_bytes;
+  a.persist = c->d_persist;
+  a.gstates = c->d_gstates;
+  a.status = c->d_status;
+  const bool lds_states = p.context_model == 0;
+  if (encode_lds_bytes(a, lds_states) > 160 * 1024)
+    return set_err(-38, "slice too wide for the LDS row buffers");
+  if (launch_encode(a, lds_states, st) < 0) return set_err(-5, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
+
+  AssembleArgs b{};
+  b.slice_out = c->d_slice_out;
+  b.slice_cap = c->slice_cap;
+  b.slice_bytes = c->d_slice_bytes;
+  b.packets = c->d_packets;
+  b.packet_stride = c->packet_stride;
+  b.packet_size = c->d_packet_size;
+  b.nslices = c->nslices;
+  b.version = p.version;
+  b.ec = p.ec;
+  if (launch_assemble(b, n, st) < 0) return set_err(-5, "assemble launch failed");
+
+  c->picture_number += n;
+  c->have_states = true;
+  c->last_n = n;
+  c->last_keys.assign(keys.begin(), keys.end());
+  return 0;
+}
+
+int ffv1hip_encode_device(ffv1hip_ctx* c, const void* d_frames, int64_t frame_bytes,
+                          const int64_t plane_offset[3], const int plane_stride[3], int n_frames,
+                          void* stream) {
+  if (!c || !d_frames) return set_err(-22, "null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  return run_batch(c, static_cast<const uint8_t*>(d_frames), frame_bytes, plane_offset, plane_stride,
+                   n_frames, stream ? reinterpret_cast<hipStream_t>(stream) : c->stream);
+}
+
+int ffv1hip_fetch(ffv1hip_ctx* c, uint8_t* out, int64_t out_cap, int64_t* sizes, int* key_flags) {
+  if (!c) return set_err(-22, "null ctx");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());
+  int status[4];
+  HIP_TRY(hipMemcpy(status, c->d_status, sizeof(status), hipMemcpyDeviceToHost));
+  if (status[0]) return set_err(-28, "%d slices exceeded the slice byte budget", status[0]);
+  const int n = c->last_n;
+  std::vector<int64_t> sz(n);
+  HIP_TRY(hipMemcpy(sz.data(), c->d_packet_size, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
+  int64_t pos = 0;
+  for (int i = 0; i < n; i++) {
+    if (out) {
+      if (pos + sz[i] > out_cap) return set_err(-22, "output buffer too small");
+      HIP_TRY(hipMemcpy(out + pos, c->d_packets + int64_t(i) * c->packet_stride, sz[i], hipMemcpyDeviceToHost));
+    }
+    pos += sz[i];
+    if (sizes) sizes[i] = sz[i];
+    if (key_flags) key_flags[i] = c->last_keys[i];
+  }
+  return 0;
+}
+
+int ffv1hip_device_packets(ffv1hip_ctx* c, void** d_packets, int64_t* packet_stride, void** d_sizes) {
+  if (!c) return set_err(-22, "null ctx");
+  if (d_packets) *d_packets = c->d_packets;
+  if (packet_stride) *packet_stride = c->packet_stride;
+  if (d_sizes) *d_sizes = c->d_packet_size;
+  return 0;
+}
+
+int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides, int n_frames,
+                   uint8_t* out, int64_t out_cap, int64_t* sizes, int* key_flags) {
+  if (!c || !planes || !strides) return set_err(-22, "null argument");
+  const ffv1hip_params& p = c->P;
+  HIP_TRY(hipSetDevice(c->device));
+  const int np = p.chroma_planes ? 3 : 1;
+  const int cw = -((-p.width) >> p.chroma_h_shift), ch = -((-p.height) >> p.chroma_v_shift);
+  int64_t off[3] = {0, c->plane_bytes[0], c->plane_bytes[0] + c->plane_bytes[1]};
+  int pst[3] = {p.width * p.sample_bytes, cw * p.sample_bytes, cw * p.sample_bytes};
+  int64_t used = 0;
+  std::vector<int64_t> local_sizes(size_t(c->max_batch));
+  for (int base = 0; base < n_frames; base += c->max_batch) {
+    const int n = std::min(c->max_batch, n_frames - base);
+    for (int i = 0; i < n; i++)
+      for (int k = 0; k < np; k++) {
+        const int rows = k ? ch : p.height;
+        HIP_TRY(hipMemcpy2DAsync(c->d_frames + int64_t(i) * c->frame_bytes + off[k], pst[k],
+                                 planes[3 * (base + i) + k], strides[3 * (base + i) + k], pst[k], rows,
+                                 hipMemcpyHostToDevice, c->stream));
+      }
+    int rc = run_batch(c, c->d_frames, c->frame_bytes, off, pst, n, c->stream);
+    if (rc < 0) return rc;
+    rc = ffv1hip_fetch(c, out ? out + used : nullptr, out_cap - used, local_sizes.data(),
+                       key_flags ? key_flags + base : nullptr);
+    if (rc < 0) return rc;
+    for (int i = 0; i < n; i++) {
+      if (sizes) sizes[base + i] = local_sizes[i];
+      used += local_sizes[i];
+    }
+  }
+  return 0;
+}
+
+int64_t ffv1hip_get_slice_states(ffv1hip_ctx* c, uint8_t* buf, int64_t cap) {
+  if (!c) return set_err(-22, "null ctx");
+  const int64_t n = int64_t(2) * c->contexts * 32 * c->nslices;
+  if (!buf) return n;
+  if (cap < n) return set_err(-22, "buffer too small");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(buf, c->d_persist, n, hipMemcpyDeviceToHost));
+  return n;
+}
+
+int ffv1hip_set_slice_states(ffv1hip_ctx* c, const uint8_t* buf, int64_t size) {
+  if (!c || !buf) return set_err(-22, "null argument");
+  const int64_t n = int64_t(2) * c->contexts * 32 * c->nslices;
+  if (size != n) return set_err(-22, "state blob is %lld bytes, expected %lld", (long long)size, (long long)n);
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpy(c->d_persist, buf, n, hipMemcpyHostToDevice));
+  c->have_states = true;
+  return 0;
+}
+
+}  // extern "C"

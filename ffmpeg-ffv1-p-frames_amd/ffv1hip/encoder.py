@@ -1,0 +1,328 @@
+"""Host-side mirror of the reference's FFV1 AVCodec, backed by the HIP C-ABI.
+
+The reference plugs its encoder into FFmpeg as ``ff_ffv1_encoder``
+(libavcodec/ffv1enc.c:1415-1444): ``init`` = encode_init (:669),
+``encode2`` = encode_frame (:1222), ``close`` = encode_close (:1375), with
+``AV_CODEC_CAP_DELAY`` so frames may be buffered and drained by a NULL frame.
+:class:`FFV1Encoder` keeps those names, argument meanings and error
+behaviour; every call goes through ``lib/libffv1hip.so``
+(include/ffv1hip.h).  There is no CPU fallback: if the HIP library is
+missing or no GPU is visible, construction raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _paths
+
+AVERROR_INVALIDDATA = -1094995529
+
+
+class Options(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int), ("height", ctypes.c_int), ("pix_fmt", ctypes.c_char_p),
+                ("slices", ctypes.c_int), ("level", ctypes.c_int), ("coder", ctypes.c_int),
+                ("context", ctypes.c_int), ("gop_size", ctypes.c_int),
+                ("bits_per_raw_sample", ctypes.c_int), ("slicecrc", ctypes.c_int),
+                ("allow_large_grid", ctypes.c_int)]
+
+
+class Params(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "width", "height", "chroma_planes", "chroma_h_shift", "chroma_v_shift",
+        "bits_per_raw_sample", "packed_at_lsb", "sample_bytes", "version", "ac", "ec",
+        "context_model", "num_h_slices", "num_v_slices", "gop_size", "sar_num", "sar_den")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+    @property
+    def nslices(self):
+        return self.num_h_slices * self.num_v_slices
+
+    def plane_shapes(self):
+        cw = -((-self.width) >> self.chroma_h_shift)
+        ch = -((-self.height) >> self.chroma_v_shift)
+        shapes = [(self.height, self.width)]
+        if self.chroma_planes:
+            shapes += [(ch, cw), (ch, cw)]
+        return shapes
+
+
+EXPORTED_SYMBOLS = (
+    "ffv1hip_configure", "ffv1hip_create", "ffv1hip_destroy", "ffv1hip_extradata",
+    "ffv1hip_max_packet_size", "ffv1hip_encode", "ffv1hip_encode_device", "ffv1hip_fetch",
+    "ffv1hip_device_packets", "ffv1hip_picture_number", "ffv1hip_reset",
+    "ffv1hip_get_slice_states", "ffv1hip_set_slice_states", "ffv1hip_last_error",
+    "ffv1hip_abi_version",
+)
+
+_lib = None
+
+
+def load_library():
+    """Load lib/libffv1hip.so and declare the C-ABI.  Raises if missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    L = ctypes.CDLL(_paths.hip_lib())
+    P = ctypes.POINTER
+    vp, i64, u8p = ctypes.c_void_p, ctypes.c_int64, P(ctypes.c_uint8)
+    L.ffv1hip_configure.argtypes = [P(Params), P(Options)]
+    L.ffv1hip_configure.restype = ctypes.c_int
+    L.ffv1hip_create.argtypes = [P(Params), ctypes.c_int, ctypes.c_int, P(ctypes.c_int)]
+    L.ffv1hip_create.restype = vp
+    L.ffv1hip_destroy.argtypes = [vp]
+    L.ffv1hip_destroy.restype = None
+    L.ffv1hip_extradata.argtypes = [vp, u8p, ctypes.c_int]
+    L.ffv1hip_extradata.restype = ctypes.c_int
+    L.ffv1hip_max_packet_size.argtypes = [vp]
+    L.ffv1hip_max_packet_size.restype = i64
+    L.ffv1hip_encode.argtypes = [vp, P(vp), P(ctypes.c_int), ctypes.c_int, u8p, i64, P(i64), P(ctypes.c_int)]
+    L.ffv1hip_encode.restype = ctypes.c_int
+    L.ffv1hip_encode_device.argtypes = [vp, vp, i64, P(i64), P(ctypes.c_int), ctypes.c_int, vp]
+    L.ffv1hip_encode_device.restype = ctypes.c_int
+    L.ffv1hip_fetch.argtypes = [vp, u8p, i64, P(i64), P(ctypes.c_int)]
+    L.ffv1hip_fetch.restype = ctypes.c_int
+    L.ffv1hip_device_packets.argtypes = [vp, P(vp), P(i64), P(vp)]
+    L.ffv1hip_device_packets.restype = ctypes.c_int
+    L.ffv1hip_picture_number.argtypes = [vp]
+    L.ffv1hip_picture_number.restype = i64
+    L.ffv1hip_reset.argtypes = [vp]
+    L.ffv1hip_reset.restype = None
+    L.ffv1hip_get_slice_states.argtypes = [vp, u8p, i64]
+    L.ffv1hip_get_slice_states.restype = i64
+    L.ffv1hip_set_slice_states.argtypes = [vp, u8p, i64]
+    L.ffv1hip_set_slice_states.restype = ctypes.c_int
+    L.ffv1hip_last_error.argtypes = []
+    L.ffv1hip_last_error.restype = ctypes.c_char_p
+    L.ffv1hip_abi_version.argtypes = []
+    L.ffv1hip_abi_version.restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+class FFV1Error(RuntimeError):
+    def __init__(self, code: int, what: str):
+        msg = load_library().ffv1hip_last_error().decode(errors="replace")
+        super().__init__(f"{what}: error {code}: {msg}")
+        self.code = code
+
+
+def configure(width: int, height: int, pix_fmt: str, slices: int = 0, level: int = -1,
+              coder: int = -1, context: int = 0, gop_size: int = 12,
+              bits_per_raw_sample: int = 0, slicecrc: int = -1,
+              allow_large_grid: bool = False) -> Params:
+    """encode_init's option -> bitstream-parameter derivation (ffv1enc.c:669-1029)."""
+    L = load_library()
+    o = Options(width, height, pix_fmt.encode(), slices, level, coder, context, gop_size,
+                bits_per_raw_sample, slicecrc, int(allow_large_grid))
+    p = Params()
+    rc = L.ffv1hip_configure(ctypes.byref(p), ctypes.byref(o))
+    if rc < 0:
+        raise FFV1Error(rc, "ffv1hip_configure")
+    return p
+
+
+def _u8p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+class HipEncoder:
+    """Thin owner of one ``ffv1hip_ctx`` (one stream, P-frame state on device)."""
+
+    def __init__(self, params: Params, device: int = 0, max_batch: int = 16):
+        L = load_library()
+        self.params = params
+        self.max_batch = max_batch
+        err = ctypes.c_int(0)
+        self._h = L.ffv1hip_create(ctypes.byref(params), device, max_batch, ctypes.byref(err))
+        if not self._h:
+            raise FFV1Error(err.value, "ffv1hip_create")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().ffv1hip_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def extradata(self) -> bytes:
+        L = load_library()
+        n = L.ffv1hip_extradata(self._h, None, 0)
+        buf = np.zeros(max(n, 1), np.uint8)
+        n = L.ffv1hip_extradata(self._h, _u8p(buf), buf.size)
+        if n < 0:
+            raise FFV1Error(n, "ffv1hip_extradata")
+        return buf[:n].tobytes()
+
+    @property
+    def picture_number(self) -> int:
+        return load_library().ffv1hip_picture_number(self._h)
+
+    def max_packet_size(self) -> int:
+        return load_library().ffv1hip_max_packet_size(self._h)
+
+    def encode(self, frames: Sequence[Sequence[np.ndarray]]) -> List[Tuple[bytes, bool]]:
+        """Encode host frames (each a list of 2-D uint8/uint16 planes) in order."""
+        L = load_library()
+        n = len(frames)
+        np_planes = 3 if self.params.chroma_planes else 1
+        ptrs = (ctypes.c_void_p * (3 * n))()
+        strides = (ctypes.c_int * (3 * n))()
+        keep = []
+        for i, fr in enumerate(frames):
+            for k in range(3):
+                a = fr[min(k, np_planes - 1)]
+                a = np.ascontiguousarray(a)
+                keep.append(a)
+                ptrs[3 * i + k] = a.ctypes.data
+                strides[3 * i + k] = a.strides[0]
+        total_in = sum(a.nbytes for a in keep)
+        cap = total_in * 4 + 65536 * n
+        out = np.empty(cap, np.uint8)
+        sizes = (ctypes.c_int64 * n)()
+        keys = (ctypes.c_int * n)()
+        rc = L.ffv1hip_encode(self._h, ptrs, strides, n, _u8p(out), cap, sizes, keys)
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_encode")
+        res, pos = [], 0
+        for i in range(n):
+            res.append((out[pos:pos + sizes[i]].tobytes(), bool(keys[i])))
+            pos += sizes[i]
+        return res
+
+    def encode_device(self, d_frames: int, frame_bytes: int, plane_offset, plane_stride,
+                      n_frames: int, stream: int = 0):
+        L = load_library()
+        off = (ctypes.c_int64 * 3)(*plane_offset)
+        st = (ctypes.c_int * 3)(*plane_stride)
+        rc = L.ffv1hip_encode_device(self._h, ctypes.c_void_p(d_frames), frame_bytes, off, st,
+                                     n_frames, ctypes.c_void_p(stream) if stream else None)
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_encode_device")
+
+    def fetch(self, n_frames: int) -> List[Tuple[bytes, bool]]:
+        L = load_library()
+        sizes = (ctypes.c_int64 * n_frames)()
+        keys = (ctypes.c_int * n_frames)()
+        rc = L.ffv1hip_fetch(self._h, None, 0, sizes, keys)
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_fetch")
+        total = sum(sizes)
+        out = np.empty(max(total, 1), np.uint8)
+        rc = L.ffv1hip_fetch(self._h, _u8p(out), total, sizes, keys)
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_fetch")
+        res, pos = [], 0
+        for i in range(n_frames):
+            res.append((out[pos:pos + sizes[i]].tobytes(), bool(keys[i])))
+            pos += sizes[i]
+        return res
+
+    def device_packets(self):
+        L = load_library()
+        d_p, d_s = ctypes.c_void_p(), ctypes.c_void_p()
+        stride = ctypes.c_int64()
+        L.ffv1hip_device_packets(self._h, ctypes.byref(d_p), ctypes.byref(stride), ctypes.byref(d_s))
+        return d_p.value, stride.value, d_s.value
+
+    def slice_states(self) -> bytes:
+        L = load_library()
+        n = L.ffv1hip_get_slice_states(self._h, None, 0)
+        buf = np.empty(n, np.uint8)
+        rc = L.ffv1hip_get_slice_states(self._h, _u8p(buf), n)
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_get_slice_states")
+        return buf.tobytes()
+
+
+@dataclass
+class AVPacket:
+    data: bytes
+    pts: int
+    dts: int
+    key: bool
+
+    @property
+    def flags(self) -> int:  # AV_PKT_FLAG_KEY
+        return 1 if self.key else 0
+
+
+@dataclass
+class AVCodecContext:
+    """The AVCodecContext fields encode_init/encode_frame read."""
+    width: int
+    height: int
+    pix_fmt: str
+    gop_size: int = 12
+    slices: int = 0
+    level: int = -1
+    coder: int = -1
+    context: int = 0
+    bits_per_raw_sample: int = 0
+    slicecrc: int = -1
+    extradata: bytes = b""
+    allow_large_grid: bool = False
+    priv: dict = field(default_factory=dict)
+
+
+class FFV1Encoder:
+    """Mirror of ff_ffv1_encoder (ffv1enc.c:1415-1444), name "ffv1_hip".
+
+    ``encode2`` follows AV_CODEC_CAP_DELAY: frames are queued and encoded in
+    batches of ``batch`` on the GPU; a ``None`` frame drains the queue.  It
+    returns the list of packets made available by this call (the "got_packet"
+    outputs), in order, each with pts = dts = the frame's pts.
+    """
+
+    name = "ffv1_hip"
+    long_name = "FFmpeg video codec #1 (MI355X HIP)"
+    capabilities = ("SLICE_THREADS", "DELAY")
+    pix_fmts = ("yuv420p", "yuv422p", "yuv444p", "yuv440p", "yuv411p", "yuv410p", "gray",
+                "yuv420p9", "yuv422p9", "yuv444p9", "yuv420p10", "yuv422p10", "yuv444p10",
+                "yuv420p16", "yuv422p16", "yuv444p16", "gray16")
+
+    def __init__(self, batch: int = 12, device: int = 0):
+        self.batch = batch
+        self.device = device
+        self.avctx: Optional[AVCodecContext] = None
+        self.params: Optional[Params] = None
+        self._enc: Optional[HipEncoder] = None
+        self._queue: List[Tuple[List[np.ndarray], int]] = []
+
+    def init(self, avctx: AVCodecContext) -> int:
+        self.avctx = avctx
+        self.params = configure(avctx.width, avctx.height, avctx.pix_fmt, avctx.slices,
+                                avctx.level, avctx.coder, avctx.context, avctx.gop_size,
+                                avctx.bits_per_raw_sample, avctx.slicecrc,
+                                avctx.allow_large_grid)
+        self._enc = HipEncoder(self.params, self.device, self.batch)
+        avctx.extradata = self._enc.extradata()
+        return 0
+
+    def encode2(self, frame: Optional[Sequence[np.ndarray]], pts: Optional[int] = None) -> List[AVPacket]:
+        if frame is not None:
+            self._queue.append(([np.ascontiguousarray(p) for p in frame],
+                                pts if pts is not None else self._enc.picture_number + len(self._queue)))
+            if len(self._queue) < self.batch:
+                return []
+        return self._drain()
+
+    def _drain(self) -> List[AVPacket]:
+        if not self._queue:
+            return []
+        frames = [f for f, _ in self._queue]
+        pts = [p for _, p in self._queue]
+        self._queue = []
+        out = self._enc.encode(frames)
+        return [AVPacket(d, t, t, k) for (d, k), t in zip(out, pts)]
+
+    def close(self) -> int:
+        if self._enc is not None:
+            self._enc.close()
+            self._enc = None
+        return 0

@@ -1,0 +1,130 @@
+/*
+ * ffv1hip.h -- C-ABI of the MI355X FFV1 encoder (the drop-in boundary).
+ *
+ * The reference exposes this path as an AVCodec (libavcodec/ffv1enc.c:1415-
+ * 1444, ff_ffv1_encoder) whose .init/.encode2/.close callbacks are invoked by
+ * avcodec_open2 (libavcodec/utils.c:1571) and avcodec_encode_video2
+ * (utils.c:1962).  This header is the plain-C surface a thin AVCodec shim
+ *  binds instead; it carries no FFmpeg or torch types:
+ * plain structs, pointers and sizes.  All functions return 0 (or a size) on
+ * success and a negative errno-style code on failure:
+ *   -EINVAL (-22) bad argument      -ENOSYS (-38) unsupported parameters
+ *   -ENOMEM (-12) allocation        -ENOSPC (-28) slice byte budget exceeded
+ *   -EIO     (-5) HIP runtime error (message via ffv1hip_last_error)
+ * plus FFV1HIP_AVERROR_INVALIDDATA for the reference's InvalidData cases.
+ */
+#ifndef FFV1HIP_H
+#define FFV1HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FFV1HIP_ABI_VERSION 1
+#define FFV1HIP_AVERROR_INVALIDDATA (-1094995529)
+
+/* AVCodecContext fields + codec private options that encode_init reads
+ * (ffv1enc.c:669-1029, options ffv1enc.c:1383-1399, defaults :1408-1413). */
+typedef struct ffv1hip_options {
+    int width, height;
+    const char *pix_fmt;      /* "yuv420p", "yuv420p10", "yuv444p16", ...   */
+    int slices;               /* avctx->slices (0 = auto)                   */
+    int level;                /* avctx->level (-1 = unset)                  */
+    int coder;                /* -1 default, 0 rice, 1/2 range_tab, -2 range_def */
+    int context;              /* context model 0/1                          */
+    int gop_size;             /* avctx->gop_size (default 12)               */
+    int bits_per_raw_sample;  /* 0 = from pix_fmt                           */
+    int slicecrc;             /* -1 default (on for v3)                     */
+    int allow_large_grid;     /* 1: accept up to 256 slices (16x16), which the
+                                 reference decoder reads but its encoder
+                                 refuses (ffv1enc.c:988-1000); used for 8K  */
+} ffv1hip_options;
+
+/* Effective bitstream parameters (what encode_init derives). */
+typedef struct ffv1hip_params {
+    int width, height;
+    int chroma_planes;        /* 1 YUV, 0 gray                              */
+    int chroma_h_shift, chroma_v_shift;
+    int bits_per_raw_sample;
+    int packed_at_lsb;        /* u16 samples LSB-aligned (yuv*p9/p10)       */
+    int sample_bytes;         /* 1 or 2 bytes per stored sample             */
+    int version;              /* 0, 1 or 3                                  */
+    int ac;                   /* 0 Golomb-Rice, 1 range default, 2 range custom */
+    int ec;                   /* slice CRC-32 trailers                      */
+    int context_model;        /* 0: 666 contexts, 1: 7563                   */
+    int num_h_slices, num_v_slices;
+    int gop_size;
+    int sar_num, sar_den;
+} ffv1hip_params;
+
+typedef struct ffv1hip_ctx ffv1hip_ctx;
+
+/* encode_init's parameter contract (ffv1enc.c:669-1029). */
+int ffv1hip_configure(ffv1hip_params *out, const ffv1hip_options *opt);
+
+/* AVCodec.init (ffv1enc.c:669 encode_init): allocates device state for up
+ * to max_batch_frames frames per call on HIP device `device`. */
+ffv1hip_ctx *ffv1hip_create(const ffv1hip_params *params, int device,
+                            int max_batch_frames, int *err);
+
+/* AVCodec.close (ffv1enc.c:1375 encode_close). */
+void ffv1hip_destroy(ffv1hip_ctx *ctx);
+
+/* avctx->extradata as written by write_extradata (ffv1enc.c:545-619); 0
+ * bytes for version < 2.  Returns the size or a negative error. */
+int ffv1hip_extradata(ffv1hip_ctx *ctx, uint8_t *buf, int cap);
+
+/* Upper bound of one packet produced by this context. */
+int64_t ffv1hip_max_packet_size(const ffv1hip_ctx *ctx);
+
+/* AVCodec.encode2 over a batch (ffv1enc.c:1222 encode_frame, called once
+ * per frame in order).  planes[3*i + p] / strides[3*i + p] describe plane p
+ * of frame i in HOST memory.  Packets are written back to back into `out`;
+ * sizes[i] and key_flags[i] describe packet i.  P-frame context state
+ * carries across calls exactly as across encode_frame calls. */
+int ffv1hip_encode(ffv1hip_ctx *ctx, const void *const *planes,
+                   const int *strides, int n_frames, uint8_t *out,
+                   int64_t out_cap, int64_t *sizes, int *key_flags);
+
+/* Device-resident variant: frames already in HBM at d_frames + i*frame_bytes
+ * with plane p at byte offset plane_offset[p] and row stride plane_stride[p].
+ * Encodes on `stream` (a hipStream_t, may be NULL) and leaves the packets in
+ * HBM; nothing is synchronised.  Use ffv1hip_fetch to read them back. */
+int ffv1hip_encode_device(ffv1hip_ctx *ctx, const void *d_frames,
+                          int64_t frame_bytes, const int64_t plane_offset[3],
+                          const int plane_stride[3], int n_frames,
+                          void *stream);
+
+/* Synchronises and copies the packets of the last encode_device call. */
+int ffv1hip_fetch(ffv1hip_ctx *ctx, uint8_t *out, int64_t out_cap,
+                  int64_t *sizes, int *key_flags);
+
+/* Device pointers of the last call's packet slots: packet i starts at
+ * (*d_packets + i * (*packet_stride)); sizes live in *d_sizes (int64). */
+int ffv1hip_device_packets(ffv1hip_ctx *ctx, void **d_packets,
+                           int64_t *packet_stride, void **d_sizes);
+
+/* Next picture number (frames encoded so far) and a reset to a fresh
+ * stream (next frame is a keyframe). */
+int64_t ffv1hip_picture_number(const ffv1hip_ctx *ctx);
+void ffv1hip_reset(ffv1hip_ctx *ctx);
+
+/* Per-slice context-state snapshot (the P-frame carry) of the last frame of
+ * the last call: [slice][plane_ctx 0..1][context][32] bytes.  Returns the
+ * byte count written (or needed when buf is NULL). */
+int64_t ffv1hip_get_slice_states(ffv1hip_ctx *ctx, uint8_t *buf, int64_t cap);
+int     ffv1hip_set_slice_states(ffv1hip_ctx *ctx, const uint8_t *buf,
+                                 int64_t size);
+
+/* Name of the HIP device kernels in the last launch, for profiling, and
+ * the last error message. */
+const char *ffv1hip_last_error(void);
+int ffv1hip_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,97 @@
+"""CPU checks of the product's C-ABI (no GPU compute is called here).
+
+* lib/libffv1hip.so loads and exports every function include/ffv1hip.h declares;
+* ffv1hip_configure (encode_init's parameter contract, host-only) agrees with
+  the oracle's restatement over a grid of options;
+* without a GPU, creating an encoder fails loudly (no CPU fallback).
+"""
+import ctypes
+import os
+import re
+
+import pytest
+
+from helpers import PARITY_STREAMS
+from oracle import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "ffv1hip.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(ffv1hip_\w+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    from ffv1hip import load_library, EXPORTED_SYMBOLS
+    lib = load_library()
+    names = declared_functions()
+    assert len(names) >= 10
+    for n in names:
+        assert hasattr(lib, n), f"{n} declared in include/ffv1hip.h but not exported"
+    assert set(names) == set(EXPORTED_SYMBOLS)
+    assert lib.ffv1hip_abi_version() == 1
+
+
+FIELDS = ["width", "height", "chroma_planes", "chroma_h_shift", "chroma_v_shift",
+          "bits_per_raw_sample", "packed_at_lsb", "sample_bytes", "version", "ac", "ec",
+          "context_model", "num_h_slices", "num_v_slices", "gop_size"]
+
+OPTION_GRID = [
+    (352, 288, "yuv420p", 0, -1, -1, 0, 12, 0),
+    (352, 288, "yuv420p", 4, -1, -1, 0, 12, 0),
+    (352, 288, "yuv420p", 0, 3, 1, 0, 12, 0),
+    (352, 288, "yuv422p10", 0, 3, -1, 0, 12, 0),
+    (352, 288, "yuv444p16", 0, 3, -1, 0, 12, 0),
+    (1920, 1080, "yuv420p", 24, -1, 1, 0, 1, 0),
+    (1920, 1080, "yuv420p", 0, -1, 1, 1, 12, 0),
+    (3840, 2160, "yuv420p10", 64, -1, 1, 0, 12, 0),
+    (3840, 2160, "yuv444p16", 64, -1, 1, 0, 12, 12),
+    (176, 144, "yuv420p10", 0, -1, 1, 0, 3, 0),
+    (176, 144, "gray", 0, -1, 0, 0, 12, 0),
+    (176, 144, "yuv410p", 9, -1, -2, 0, 12, 0),
+    (720, 576, "yuv420p9", 0, -1, 0, 0, 12, 0),
+]
+
+
+@pytest.mark.parametrize("opt", OPTION_GRID)
+def test_configure_matches_oracle_contract(opt):
+    from ffv1hip import configure
+    w, h, fmt, slices, level, coder, context, gop, bpr = opt
+    ref = oracle.configure(w, h, fmt, slices=slices, level=level, coder=coder, context=context,
+                           gop_size=gop, bits_per_raw_sample=bpr).as_dict()
+    got = configure(w, h, fmt, slices=slices, level=level, coder=coder, context=context,
+                    gop_size=gop, bits_per_raw_sample=bpr).as_dict()
+    for f in FIELDS:
+        assert got[f] == ref[f], f
+
+
+def test_configure_rejections_match():
+    from ffv1hip import configure, FFV1Error
+    for args in [(1920, 1080, "yuv420p", 5), (7680, 4320, "yuv420p10", 256),
+                 (352, 288, "rgb48", 0)]:
+        with pytest.raises(FFV1Error):
+            configure(*args)
+        with pytest.raises((ValueError, Exception)):
+            oracle.configure(*args)
+    p = configure(7680, 4320, "yuv420p10", slices=256, coder=1, allow_large_grid=True)
+    assert (p.num_h_slices, p.num_v_slices, p.version) == (16, 16, 3)
+
+
+def test_no_silent_cpu_fallback_without_gpu():
+    import torch
+    from ffv1hip import configure, HipEncoder, FFV1Error
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(FFV1Error):
+        HipEncoder(configure(352, 288, "yuv420p", coder=1, slices=4), 0, 2)
+
+
+def test_golomb_is_reported_not_faked():
+    from ffv1hip import configure, HipEncoder, FFV1Error
+    p = configure(352, 288, "yuv420p", coder=0)
+    with pytest.raises(FFV1Error) as e:
+        HipEncoder(p, 0, 1)
+    assert e.value.code in (-38, -5)

@@ -1,0 +1,123 @@
+"""CPU oracle checks: pinned against the reference's own known answers.
+
+The oracle (oracle/ffv1_oracle.c) is the parity checker for the GPU path, so
+it is pinned first: it must reproduce the reference encoder's recorded
+packet MD5s (tests/golden/known_answers.json), and its decoder
+must invert every stream of the parity matrix losslessly.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from helpers import PARITY_STREAMS, Stream, load_golden, md5, oracle_encode
+from oracle import oracle
+
+PINS = {p["name"]: p for p in load_golden("known_answers.json")["streams"]}
+
+
+def _check_pin(pin, stream):
+    cfg, ex, pkts = oracle_encode(stream)
+    if "extradata_md5_prefix" in pin:
+        assert len(ex) == pin["extradata_size"]
+        assert md5(ex).startswith(pin["extradata_md5_prefix"])
+    for i, size in pin.get("frame_sizes", {}).items():
+        assert len(pkts[int(i)][0]) == size
+    for i, pre in pin.get("frame_md5_prefix", {}).items():
+        assert md5(pkts[int(i)][0]).startswith(pre)
+    h = hashlib.md5()
+    for p, _ in pkts:
+        h.update(p)
+    assert h.hexdigest() == pin["stream_md5"]
+    return pkts
+
+
+def test_pin_config1_cif_golomb_v0():
+    pin = PINS["config1_cif_yuv420p_coder0_g1"]
+    _check_pin(pin, Stream("c1", 352, 288, "yuv420p", pin["frames"], coder=0, gop_size=1))
+
+
+@pytest.mark.slow
+def test_pin_config2_1080p_range_intra():
+    pin = PINS["config2_1080p_yuv420p_coder1_slices24_g1"]
+    _check_pin(pin, Stream("c2", 1920, 1080, "yuv420p", pin["frames"], slices=24, gop_size=1))
+
+
+@pytest.mark.slow
+def test_pin_config3_4k_p10_pframes():
+    pin = PINS["config3_4k_yuv420p10_coder1_slices64_g12"]
+    pkts = _check_pin(pin, Stream("c3", 3840, 2160, "yuv420p10", pin["frames"], slices=64,
+                                  gop_size=12, depth=10))
+    assert [k for _, k in pkts] == [i % 12 == 0 for i in range(len(pkts))]
+
+
+def test_config_derivation_matches_reference_contract():
+    # CIF defaults => v0 Golomb, 1 slice; >8 bit forces the range coder (v1)
+    c = oracle.configure(352, 288, "yuv420p")
+    assert (c.version, c.ac, c.num_h_slices * c.num_v_slices, c.ec) == (0, 0, 1, 0)
+    c = oracle.configure(352, 288, "yuv420p10")
+    assert (c.version, c.ac) == (1, 2)
+    c = oracle.configure(1920, 1080, "yuv420p", coder=1, slices=24)
+    assert (c.version, c.num_h_slices, c.num_v_slices, c.ec) == (3, 6, 4, 1)
+    c = oracle.configure(3840, 2160, "yuv420p10", coder=1, slices=64)
+    assert (c.num_h_slices, c.num_v_slices, c.packed_at_lsb, c.bits_per_raw_sample) == (8, 8, 1, 10)
+    c = oracle.configure(3840, 2160, "yuv444p16", coder=1, slices=64, bits_per_raw_sample=12)
+    assert (c.packed_at_lsb, c.bits_per_raw_sample, c.chroma_h_shift) == (0, 12, 0)
+    with pytest.raises(ValueError):  # slices > 64 are refused (ffv1enc.c:992)
+        oracle.configure(7680, 4320, "yuv420p10", coder=1, slices=256)
+    with pytest.raises(ValueError):  # 5 slices: no grid
+        oracle.configure(1920, 1080, "yuv420p", slices=5)
+
+
+@pytest.mark.parametrize("stream", PARITY_STREAMS[:-1], ids=[s.name for s in PARITY_STREAMS[:-1]])
+def test_oracle_roundtrip_lossless(stream):
+    if not stream.lossless:
+        pytest.skip("reference leaves chroma columns uncoded for this geometry")
+    frames = list(stream.frames())
+    cfg, ex, pkts = oracle_encode(stream, frames)
+    dec = oracle.Decoder(cfg, ex)
+    for (p, key), f in zip(pkts, frames):
+        planes, k = dec.decode(p)
+        assert k == key
+        for a, b in zip(planes, f):
+            if cfg.sample_bytes == 2 and not cfg.packed_at_lsb:
+                b = (b >> (16 - cfg.bits_per_raw_sample)) << (16 - cfg.bits_per_raw_sample)
+            np.testing.assert_array_equal(a, b)
+
+
+def test_oracle_golomb_roundtrip_and_pframes():
+    s = Stream("golomb_v3", 176, 144, "yuv420p", 6, slices=4, coder=0, gop_size=3)
+    frames = list(s.frames())
+    cfg, ex, pkts = oracle_encode(s, frames)
+    assert cfg.version == 3 and cfg.ac == 0
+    dec = oracle.Decoder(cfg, ex)
+    for (p, key), f in zip(pkts, frames):
+        planes, _ = dec.decode(p)
+        for a, b in zip(planes, f):
+            np.testing.assert_array_equal(a, b)
+
+
+def test_slice_crc_residue_is_zero():
+    s = Stream("crc", 176, 144, "yuv420p", 2, slices=4, gop_size=2)
+    cfg, ex, pkts = oracle_encode(s)
+    assert oracle.crc32(ex) == 0  # extradata CRC (ffv1dec.c:619-626)
+    data = pkts[1][0]
+    end, n = len(data), 0
+    while end > 0:  # walk the slice chain backwards (ffv1dec.c:948-989)
+        size = int.from_bytes(data[end - 8:end - 5], "big")
+        start = end - size - 8
+        assert oracle.crc32(data[start:end]) == 0
+        end, n = start, n + 1
+    assert n == 4
+
+
+def test_pframes_smaller_than_keyframes_and_state_carry_matters():
+    s = Stream("carry", 352, 288, "yuv420p10", 4, slices=4, gop_size=4, depth=10)
+    frames = list(s.frames())
+    _, _, pk = oracle_encode(s, frames)
+    intra = Stream("intra", 352, 288, "yuv420p10", 4, slices=4, gop_size=1, depth=10)
+    _, _, pi = oracle_encode(intra, frames)
+    assert pk[0][0] == pi[0][0]
+    for i in range(1, 4):
+        assert not pk[i][1] and pi[i][1]
+        assert len(pk[i][0]) < len(pi[i][0])
