@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""Benchmark: Mpixels/s of bit-exact FFV1 P-frame encoding on MI355X.
+
+Workload (BASELINE.json configs[2], the metric's config): 3840x2160
+yuv420p10le, coder=1 (range coder, custom state table), slices=64 (8x8),
+keyint=12, i.e. FFV1 v3 with P-frames whose context states carry across the
+GOP.  Input is the reference's own synthetic clip (tests/videogen, widened
+to 10 bit) or the LSB-active D2 clip (--data d2), generated on the host and
+made resident in HBM before timing.
+
+A "step" = one pass of the encoder over a batch of --gops GOPs (12 frames
+each) already in HBM: slice coding + packet assembly, packets left in HBM.
+Multi-GPU: one process per GPU, each encodes its own GOPs (GOPs are
+independent: keyframes reset every context state), no data-path collective;
+value = all frames of all ranks / max-over-ranks time.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ffmpeg-ffv1-p-frames_amd"))
+
+W, H, PIX_FMT, SLICES, GOP = 3840, 2160, "yuv420p10", 64, 12
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PIN_MD5_24 = "08e3975d4d0f5f2e5c82cd4037764789"  # tests/golden/known_answers.json (config 3)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_frames(n, data):
+    from ffv1hip import synth
+    if data == "d1":
+        gen = synth.videogen_frames(W, H, n, depth=10)
+    else:
+        gen = synth.d2_frames(W, H, n, depth=10)
+    return [f for f in gen]
+
+
+def pack_batch(frames, frame_bytes):
+    buf = np.zeros((len(frames), frame_bytes), np.uint8)
+    for i, f in enumerate(frames):
+        flat = np.concatenate([p.reshape(-1).view(np.uint8) for p in f])
+        buf[i, :flat.size] = flat
+    return buf
+
+
+def cpu_baseline(frames, threads):
+    """The CPU oracle (a port of the reference encoder, oracle/) on host cores.
+
+    Bounded sample: GOP-sharded threads, each encoding the first 3 frames
+    (1 key + 2 P) of the batch with its own encoder, plus a 1-thread run of
+    the same 3 frames.  ctypes drops the GIL, so threads run in parallel.
+    """
+    sys.path.insert(0, ROOT)
+    from oracle import oracle
+    cfg = oracle.configure(W, H, PIX_FMT, slices=SLICES, coder=1, gop_size=GOP)
+    sample = frames[:3]
+
+    def one():
+        enc = oracle.Encoder(cfg)
+        for f in sample:
+            enc.encode(f)
+
+    t0 = time.perf_counter()
+    one()
+    t1 = time.perf_counter()
+    single = len(sample) * W * H / (t1 - t0) / 1e6
+    ths = [threading.Thread(target=one) for _ in range(threads)]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    t1 = time.perf_counter()
+    multi = threads * len(sample) * W * H / (t1 - t0) / 1e6
+    return {
+        "value": round(multi, 3), "unit": "Mpixels/s", "cores": threads, "kind": "port",
+        "sample": f"{threads} threads x 3 frames (1 key + 2 P, one GOP each) of the same 4K 10-bit "
+                  f"clip, oracle/ffv1_oracle.c, GOP-sharded",
+        "single_thread": {"value": round(single, 3), "cores": 1, "sample": "3 frames"},
+    }
+
+
+def load_traffic(frames_per_step):
+    """HBM bytes per launch of ffv1_encode_slices from the committed PMC profile."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        if d.get("frames_per_launch") == frames_per_step and d.get("config") == f"{W}x{H} {PIX_FMT}":
+            return d.get("encode_hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--gops", type=int, default=12, help="GOPs (x12 frames) per rank per step")
+    ap.add_argument("--data", choices=("d1", "d2"), default="d1")
+    ap.add_argument("--cpu-threads", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+
+    import torch
+    from ffv1hip import HipEncoder, configure
+
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    B = args.gops * GOP
+    params = configure(W, H, PIX_FMT, slices=SLICES, coder=1, gop_size=GOP)
+    shapes = params.plane_shapes()
+    plane_bytes = [h * w * 2 for h, w in shapes]
+    frame_bytes = (sum(plane_bytes) + 255) // 256 * 256
+    offs = [0, plane_bytes[0], plane_bytes[0] + plane_bytes[1]]
+    strides = [shapes[0][1] * 2, shapes[1][1] * 2, shapes[2][1] * 2]
+
+    t0 = time.perf_counter()
+    frames = make_frames(B, args.data)
+    host = pack_batch(frames, frame_bytes)
+    d_frames = torch.from_numpy(host).to(f"cuda:{local_rank}")
+    del host
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] {B} frames generated and resident in HBM in {time.perf_counter() - t0:.1f}s")
+
+    enc = HipEncoder(params, device=local_rank, max_batch=B)
+    enc.set_profiling(True)
+
+    def step():
+        enc.encode_device(d_frames.data_ptr(), frame_bytes, offs, strides, B)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    kern, stats = [], []
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        kern.append(enc.last_kernel_ms())
+        stats.append(enc.last_kernel_stats())
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+        t = torch.tensor([elapsed], device=f"cuda:{local_rank}", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # packets of the last step (outside the timed region): size + bit-exactness
+    pkts = enc.fetch(B)
+    out_bytes = sum(len(p) for p, _ in pkts)
+    bitexact = None
+    if args.data == "d1" and B >= 24:
+        h = hashlib.md5()
+        for p, _ in pkts[:24]:
+            h.update(p)
+        bitexact = h.hexdigest() == PIN_MD5_24
+
+    sym_ms = float(np.mean([s["symbols_ms"] for s in stats]))
+    code_ms = float(np.mean([s["code_ms"] for s in stats]))
+    asm_ms = float(np.mean([s["assemble_ms"] for s in stats]))
+    n_code = stats[-1]["code_launches"]
+    in_bytes = B * sum(plane_bytes)
+    # Dominant kernel: ffv1_code, launched once per frame index of the GOP,
+    # each launch coding one frame of every GOP in the batch.  Algorithmic
+    # bytes per launch: the input planes of the frames it codes
+    # (3.0 B per luma pixel at 4:2:0 10 bit) + the packet bytes they produce.
+    algo_per_launch = (in_bytes + out_bytes) / n_code
+    code_ms_per_launch = code_ms / n_code
+    achieved = algo_per_launch / (code_ms_per_launch * 1e-3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        ncpu = min(args.cpu_threads, os.cpu_count() or 1)
+        cpu = cpu_baseline(frames, ncpu)
+
+    mpix = args.steps * B * W * H * world / elapsed / 1e6
+    if rank == 0:
+        res = {
+            "metric": "Mpixels/s encoded (bit-exact) 4K yuv420p10 FFV1 P-frames",
+            "value": round(mpix, 2),
+            "unit": "Mpixels/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u16",
+            "data": f"synthetic ({'tests/videogen clip widened to 10 bit' if args.data == 'd1' else 'D2 seeded noisy clip'}), HBM-resident",
+            "config": {
+                "workload": "4K 3840x2160 yuv420p10le, coder=1 (range, custom table), slices=64, keyint=12 P-frames",
+                "frames_per_step_per_gpu": B,
+                "gops_per_step_per_gpu": args.gops,
+                "parallelism": f"gop-sharded x{world}",
+            },
+            "bits_per_pixel": round(out_bytes * 8 / (B * W * H), 4),
+            "bitexact_vs_reference_pin": bitexact,
+            "kernel_ms_per_step": {"ffv1_symbols": round(sym_ms, 3), "ffv1_code": round(code_ms, 3),
+                                   "ffv1_assemble_packets": round(asm_ms, 3),
+                                   "launches": {"ffv1_symbols": n_code, "ffv1_code": n_code,
+                                                "ffv1_assemble_packets": 1}},
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "ffv1_code",
+                "achieved": round(achieved, 3),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6),
+                "traffic": load_traffic(B),
+                "algorithmic_bytes_per_launch": int(algo_per_launch),
+                "avg_launch_ms": round(code_ms_per_launch, 3),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(res), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -216,7 +216,11 @@ struct ffv1hip_ctx {
   int64_t plane_bytes[3]{};
   int64_t picture_number = 0;
   bool have_states = false;  // persistent states valid (a frame was coded)
-  int row_len = 0;
+  int max_slots = 0;          // segments (= frame slots) per call
+  int64_t frame_samples = 0;  // symbols of one frame (each slice padded to 4)
+  int64_t digit_cap = 0;      // renorm digits per chain
+  int max_ops = 0;
+  std::vector<SliceGeom> geom;
   // device buffers
   uint8_t* d_frames = nullptr;
   int16_t* d_qt = nullptr;
@@ -230,11 +234,20 @@ struct ffv1hip_ctx {
   uint8_t* d_packets = nullptr;
   int64_t* d_packet_size = nullptr;
   uint8_t* d_persist = nullptr;
-  uint8_t* d_gstates = nullptr;
+  uint8_t* d_tables = nullptr;   // [slot][slice][2][contexts][32]
+  uint32_t* d_sym = nullptr;     // [slot][frame_samples]
+  uint32_t* d_digits = nullptr;  // [slot][slice][digit_cap/2]
+  SliceGeom* d_geom = nullptr;
+  int* d_slot_frames = nullptr;  // [j][slot]
   int* d_status = nullptr;
   hipStream_t stream = nullptr;
   int last_n = 0;
   std::vector<int> last_keys;
+  bool profiling = false;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  std::vector<hipEvent_t> kev;  // [2 * launches]: start/stop per kernel launch
+  std::vector<int> kev_kind;    // 0 symbols, 1 code
+  int last_nsegs = 0;
 };
 
 extern "C" {
@@ -426,14 +439,17 @@ static void build_ops(ffv1hip_ctx* c) {
 static void free_device(ffv1hip_ctx* c) {
   void* ptrs[] = {c->d_frames, c->d_qt, c->d_tabs, c->d_ops, c->d_nops, c->d_segs, c->d_keys,
                   c->d_slice_out, c->d_slice_bytes, c->d_packets, c->d_packet_size, c->d_persist,
-                  c->d_gstates, c->d_status};
+                  c->d_tables, c->d_sym, c->d_digits, c->d_geom, c->d_slot_frames, c->d_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  for (hipEvent_t& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t& e : c->kev)
+    if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
 static int alloc_device(ffv1hip_ctx* c) {
-  const ffv1hip_params& p = c->P;
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   const int nb = c->max_batch;
@@ -459,7 +475,13 @@ static int alloc_device(ffv1hip_ctx* c) {
   HIP_TRY(hipMalloc(&c->d_packet_size, sizeof(int64_t) * nb));
   const size_t state_bytes = size_t(2) * c->contexts * 32;
   HIP_TRY(hipMalloc(&c->d_persist, state_bytes * c->nslices));
-  if (p.context_model) HIP_TRY(hipMalloc(&c->d_gstates, state_bytes * c->nslices * (nb + 1)));
+  const size_t chains = size_t(c->max_slots) * c->nslices;
+  HIP_TRY(hipMalloc(&c->d_tables, state_bytes * chains));
+  HIP_TRY(hipMalloc(&c->d_sym, sizeof(uint32_t) * size_t(c->frame_samples) * c->max_slots));
+  HIP_TRY(hipMalloc(&c->d_digits, sizeof(uint32_t) * size_t(c->digit_cap / 2) * chains));
+  HIP_TRY(hipMalloc(&c->d_geom, sizeof(SliceGeom) * c->nslices));
+  HIP_TRY(hipMemcpy(c->d_geom, c->geom.data(), sizeof(SliceGeom) * c->nslices, hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&c->d_slot_frames, sizeof(int) * size_t(c->max_slots) * (nb + 1)));
   HIP_TRY(hipMalloc(&c->d_status, sizeof(int) * 4));
   return 0;
 }
@@ -496,19 +518,45 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
   c->plane_bytes[0] = int64_t(p.width) * p.height * p.sample_bytes;
   c->plane_bytes[1] = c->plane_bytes[2] = int64_t(cw) * ch * p.sample_bytes;
   c->frame_bytes = (c->plane_bytes[0] + 2 * c->plane_bytes[1] + 255) & ~int64_t(255);
-  // Slice byte budget: 4 bytes per coded sample (+4 KiB).  Real content
-  // codes below 2 bytes per 16-bit sample; exceeding it reports -ENOSPC.
-  int max_sw = 0, max_sh = 0;
+  // Per-slice geometry and symbol-stream layout (ffv1.c:117-145,
+  // ffv1enc.c:1185-1196); each slice's stream is padded to 4 symbols.
+  c->geom.resize(c->nslices);
+  int64_t off = 0, max_nsym = 0;
   for (int s = 0; s < c->nslices; s++) {
+    SliceGeom& g = c->geom[s];
     const int sx = s % p.num_h_slices, sy = s / p.num_h_slices;
-    max_sw = std::max<int>(max_sw, int(int64_t(p.width) * (sx + 1) / p.num_h_slices - int64_t(p.width) * sx / p.num_h_slices));
-    max_sh = std::max<int>(max_sh, int(int64_t(p.height) * (sy + 1) / p.num_v_slices - int64_t(p.height) * sy / p.num_v_slices));
+    const int x0 = int(int64_t(p.width) * sx / p.num_h_slices);
+    const int y0 = int(int64_t(p.height) * sy / p.num_v_slices);
+    const int sw = int(int64_t(p.width) * (sx + 1) / p.num_h_slices) - x0;
+    const int sh = int(int64_t(p.height) * (sy + 1) / p.num_v_slices) - y0;
+    g.px[0] = x0; g.py[0] = y0; g.pw[0] = sw; g.ph[0] = sh;
+    for (int k = 1; k < 3; k++) {
+      g.pw[k] = p.chroma_planes ? -((-sw) >> p.chroma_h_shift) : 0;
+      g.ph[k] = p.chroma_planes ? -((-sh) >> p.chroma_v_shift) : 0;
+      g.px[k] = x0 >> p.chroma_h_shift;
+      g.py[k] = y0 >> p.chroma_v_shift;
+    }
+    int64_t n = 0;
+    for (int k = 0; k < 3; k++) {
+      g.plane_sym_off[k] = n;
+      n += int64_t(g.pw[k]) * g.ph[k];
+    }
+    g.nsym = n;
+    g.sym_off = off;
+    off += (n + 3) & ~int64_t(3);
+    max_nsym = std::max(max_nsym, n);
   }
-  const int64_t samples = int64_t(max_sw) * max_sh +
-                          (p.chroma_planes ? 2 * int64_t(-((-max_sw) >> p.chroma_h_shift)) * -((-max_sh) >> p.chroma_v_shift) : 0);
-  c->slice_cap = ((samples * 4 + 4096) + 255) & ~int64_t(255);
+  c->frame_samples = off;
+  // Slice byte budget: 4 bytes per coded sample (+4 KiB); real content codes
+  // below 2 bytes per 16-bit sample.  Exceeding it reports -ENOSPC.
+  c->slice_cap = ((max_nsym * 4 + 4096) + 255) & ~int64_t(255);
+  c->digit_cap = c->slice_cap + 16;
   c->packet_stride = ((c->slice_cap + 16) * c->nslices + 255) & ~int64_t(255);
-  c->row_len = ((max_sw + 8) + 7) & ~7;
+  // frame slots (segments) per call: one per GOP touched by the batch
+  c->max_slots = p.gop_size > 1 ? std::min(max_batch_frames, (max_batch_frames + p.gop_size - 2) / p.gop_size + 1)
+                                : max_batch_frames;
+  c->max_ops = 0;
+  for (int v : c->nops) c->max_ops = std::max(c->max_ops, v);
   int rc = alloc_device(c);
   if (rc < 0) {
     free_device(c);
@@ -566,45 +614,80 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   HIP_TRY(hipMemcpyAsync(c->d_segs, segs.data(), segs.size() * sizeof(Segment), hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemsetAsync(c->d_status, 0, sizeof(int) * 4, st));
 
-  EncodeArgs a{};
-  a.frames = d_frames;
-  a.frame_bytes = frame_bytes;
+  const int nsegs = int(segs.size());
+  if (nsegs > c->max_slots) return set_err(-22, "batch spans %d GOPs (max %d)", nsegs, c->max_slots);
+  int maxlen = 0;
+  for (const Segment& g : segs) maxlen = std::max(maxlen, g.nframes);
+  std::vector<int> slot_frames(size_t(maxlen) * nsegs, -1);
+  for (int j = 0; j < maxlen; j++)
+    for (int k = 0; k < nsegs; k++)
+      if (j < segs[k].nframes) slot_frames[size_t(j) * nsegs + k] = segs[k].first_frame + j;
+  HIP_TRY(hipMemcpyAsync(c->d_slot_frames, slot_frames.data(), sizeof(int) * slot_frames.size(),
+                         hipMemcpyHostToDevice, st));
+
+  SymbolArgs sa{};
+  sa.frames = d_frames;
+  sa.frame_bytes = frame_bytes;
   for (int k = 0; k < 3; k++) {
-    a.plane_off[k] = plane_off[k];
-    a.plane_stride[k] = plane_stride[k];
+    sa.plane_off[k] = plane_off[k];
+    sa.plane_stride[k] = plane_stride[k];
   }
-  a.width = p.width;
-  a.height = p.height;
-  a.nh = p.num_h_slices;
-  a.nv = p.num_v_slices;
-  a.nslices = c->nslices;
-  a.chroma_planes = p.chroma_planes;
-  a.hs = p.chroma_h_shift;
-  a.vs = p.chroma_v_shift;
-  a.sample_bytes = p.sample_bytes;
-  a.packed_at_lsb = p.packed_at_lsb;
-  a.msb_shift = 16 - p.bits_per_raw_sample;
-  a.coded_bits = p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample;
-  a.contexts = c->contexts;
-  a.model1 = p.context_model;
-  a.row_len = c->row_len;
-  a.qt = c->d_qt;
-  a.tabs = c->d_tabs;
-  a.segs = c->d_segs;
-  a.nsegs = int(segs.size());
-  a.keyflags = c->d_keys;
-  a.ops = c->d_ops;
-  a.nops = c->d_nops;
-  a.slice_out = c->d_slice_out;
-  a.slice_cap = c->slice_cap;
-  a.slice_bytes = c->d_slice_bytes;
-  a.persist = c->d_persist;
-  a.gstates = c->d_gstates;
-  a.status = c->d_status;
-  const bool lds_states = p.context_model == 0;
-  if (encode_lds_bytes(a, lds_states) > 160 * 1024)
-    return set_err(-38, "slice too wide for the LDS row buffers");
-  if (launch_encode(a, lds_states, st) < 0) return set_err(-5, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
+  sa.nslots = nsegs;
+  sa.geom = c->d_geom;
+  sa.nslices = c->nslices;
+  sa.nplanes = p.chroma_planes ? 3 : 1;
+  sa.sample_bytes = p.sample_bytes;
+  sa.packed_at_lsb = p.packed_at_lsb;
+  sa.msb_shift = 16 - p.bits_per_raw_sample;
+  sa.coded_bits = p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample;
+  sa.contexts = c->contexts;
+  sa.model1 = p.context_model;
+  sa.qt = c->d_qt;
+  sa.sym = c->d_sym;
+  sa.frame_samples = c->frame_samples;
+
+  CodeArgs ca{};
+  ca.sym = c->d_sym;
+  ca.frame_samples = c->frame_samples;
+  ca.geom = c->d_geom;
+  ca.nslices = c->nslices;
+  ca.nsegs = nsegs;
+  ca.segs = c->d_segs;
+  ca.keyflags = c->d_keys;
+  ca.ops = c->d_ops;
+  ca.nops = c->d_nops;
+  ca.max_ops = c->max_ops;
+  ca.tabs = c->d_tabs;
+  ca.state_bytes = int64_t(2) * c->contexts * 32;
+  ca.tables = c->d_tables;
+  ca.persist = c->d_persist;
+  ca.digits = c->d_digits;
+  ca.digit_cap = c->digit_cap;
+  ca.slice_out = c->d_slice_out;
+  ca.slice_cap = c->slice_cap;
+  ca.slice_bytes = c->d_slice_bytes;
+  ca.status = c->d_status;
+
+  if (c->profiling) {
+    HIP_TRY(hipEventRecord(c->ev[0], st));
+    while (c->kev.size() < size_t(4) * maxlen) {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreate(&e));
+      c->kev.push_back(e);
+    }
+    c->kev_kind.assign(size_t(2) * maxlen, 0);
+  }
+  for (int j = 0; j < maxlen; j++) {
+    sa.frame_of_slot = c->d_slot_frames + size_t(j) * nsegs;
+    if (c->profiling) HIP_TRY(hipEventRecord(c->kev[4 * j + 0], st));
+    if (launch_symbols(sa, st) < 0) return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (c->profiling) HIP_TRY(hipEventRecord(c->kev[4 * j + 1], st));
+    ca.j = j;
+    if (c->profiling) HIP_TRY(hipEventRecord(c->kev[4 * j + 2], st));
+    if (launch_code(ca, st) < 0) return set_err(-5, "code launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (c->profiling) HIP_TRY(hipEventRecord(c->kev[4 * j + 3], st));
+  }
+  c->last_nsegs = nsegs;
 
   AssembleArgs b{};
   b.slice_out = c->d_slice_out;
@@ -616,7 +699,9 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   b.nslices = c->nslices;
   b.version = p.version;
   b.ec = p.ec;
+  if (c->profiling) HIP_TRY(hipEventRecord(c->ev[1], st));
   if (launch_assemble(b, n, st) < 0) return set_err(-5, "assemble launch failed");
+  if (c->profiling) HIP_TRY(hipEventRecord(c->ev[2], st));
 
   c->picture_number += n;
   c->have_states = true;
@@ -695,6 +780,50 @@ int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides
       used += local_sizes[i];
     }
   }
+  return 0;
+}
+
+int ffv1hip_set_profiling(ffv1hip_ctx* c, int enable) {
+  if (!c) return set_err(-22, "null ctx");
+  HIP_TRY(hipSetDevice(c->device));
+  for (hipEvent_t& e : c->ev)
+    if (!e) HIP_TRY(hipEventCreate(&e));
+  c->profiling = enable != 0;
+  return 0;
+}
+
+int ffv1hip_last_kernel_ms(ffv1hip_ctx* c, float* encode_ms, float* assemble_ms) {
+  if (!c || !c->profiling) return set_err(-22, "profiling not enabled");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipEventSynchronize(c->ev[2]));
+  float a = 0.f, b = 0.f;
+  HIP_TRY(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+  HIP_TRY(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+  if (encode_ms) *encode_ms = a;
+  if (assemble_ms) *assemble_ms = b;
+  return 0;
+}
+
+int ffv1hip_last_kernel_stats(ffv1hip_ctx* c, ffv1hip_kernel_stats* out) {
+  if (!c || !out || !c->profiling) return set_err(-22, "profiling not enabled");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipEventSynchronize(c->ev[2]));
+  ffv1hip_kernel_stats s{};
+  const int n = int(c->kev_kind.size() / 2);
+  for (int j = 0; j < n; j++) {
+    float a = 0.f, b = 0.f;
+    HIP_TRY(hipEventElapsedTime(&a, c->kev[4 * j + 0], c->kev[4 * j + 1]));
+    HIP_TRY(hipEventElapsedTime(&b, c->kev[4 * j + 2], c->kev[4 * j + 3]));
+    s.symbols_ms += a;
+    s.code_ms += b;
+  }
+  s.symbols_launches = s.code_launches = n;
+  float asmb = 0.f;
+  HIP_TRY(hipEventElapsedTime(&asmb, c->ev[1], c->ev[2]));
+  s.assemble_ms = asmb;
+  s.assemble_launches = 1;
+  s.frames_coded_per_launch_max = c->last_nsegs;
+  *out = s;
   return 0;
 }
 

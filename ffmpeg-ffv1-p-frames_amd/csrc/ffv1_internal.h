@@ -6,10 +6,10 @@
 
 namespace ffv1hip {
 
-// One "header op" executed by the slice coder before the planes: the key
-// bit (ffv1enc.c:1299-1307), the v0/v1 in-band header (ffv1enc.c:498-522)
-// and the v3 slice header (ffv1enc.c:1031-1062).  Every op names one of
-// kOpSets private 32-byte state vectors (all 128 at slice start) and which
+// One "header op" coded before the planes of a slice: the key bit
+// (ffv1enc.c:1299-1307), the v0/v1 in-band header (ffv1enc.c:498-522) and
+// the v3 slice header (ffv1enc.c:1031-1062).  Every op names one of kOpSets
+// private 32-byte state vectors (all 128 at slice start) and which
 // transition table it adapts with.
 enum OpKind : int16_t { kOpSymU = 0, kOpSymS = 1, kOpBit = 2 };
 struct Op {
@@ -32,31 +32,55 @@ struct Segment {
   int save_states;  // 1: store the final states for the next call
 };
 
-struct EncodeArgs {
-  const uint8_t* frames;     // batch base in HBM
-  int64_t frame_bytes;       // distance between frames
-  int64_t plane_off[3];      // byte offset of Y, Cb, Cr inside a frame
-  int plane_stride[3];       // row stride in bytes
-  int width, height;
-  int nh, nv, nslices;
-  int chroma_planes, hs, vs;
+// Per-slice geometry (ffv1.c:117-145 + the chroma rounding of
+// ffv1enc.c:1185-1196) and the slice's place in a frame's symbol stream.
+struct SliceGeom {
+  int px[3], py[3], pw[3], ph[3];  // plane rectangles
+  int64_t sym_off;                 // first symbol of this slice in the frame stream
+  int64_t plane_sym_off[3];        // first symbol of each plane, relative to sym_off
+  int64_t nsym;                    // all planes
+};
+
+// Kernel 1: prediction + context + fold for every sample of a set of frames.
+struct SymbolArgs {
+  const uint8_t* frames;
+  int64_t frame_bytes;
+  int64_t plane_off[3];
+  int plane_stride[3];
+  const int* frame_of_slot;   // [slot] batch frame index coded in this launch, -1 = none
+  int nslots;
+  const SliceGeom* geom;
+  int nslices, nplanes;
   int sample_bytes, packed_at_lsb, msb_shift, coded_bits;
-  int contexts;              // per plane context (666 / 7563)
-  int model1;                // context model 1 (5 taps)
-  int row_len;               // LDS row buffer length in samples (>= max plane width + 8)
-  const int16_t* qt;         // [5][256]
-  const uint8_t* tabs;       // [2 tables][to0[256], to1[256]]: default, frame
+  int contexts, model1;
+  const int16_t* qt;          // [5][256]
+  uint32_t* sym;              // [slot][frame_samples]: (row << 16) | (uint16)diff
+  int64_t frame_samples;
+};
+
+// Kernel 2: the SIMT range coder, one lane per (segment, slice) chain, one
+// frame of every segment per launch.
+struct CodeArgs {
+  const uint32_t* sym;        // from kernel 1 (slot = segment)
+  int64_t frame_samples;
+  const SliceGeom* geom;
+  int nslices, nsegs;
+  int j;                      // frame index inside each segment
   const Segment* segs;
-  int nsegs;
-  const uint8_t* keyflags;   // [frame]
-  const Op* ops;             // [key 0/1][slice][kMaxOps]
-  const int* nops;           // [key 0/1][slice]
-  uint8_t* slice_out;        // [frame][slice] regions of slice_cap bytes
+  const uint8_t* keyflags;    // [batch frame]
+  const Op* ops;              // [key][slice][kMaxOps]
+  const int* nops;            // [key][slice]
+  int max_ops;
+  const uint8_t* tabs;        // [default to0|to1][frame to0|to1]
+  int64_t state_bytes;        // 2 * contexts * 32
+  uint8_t* tables;            // [chain][state_bytes] working context states
+  uint8_t* persist;           // [slice][state_bytes]
+  uint32_t* digits;           // [chain][digit_cap / 2] packed renorm digits
+  int64_t digit_cap;          // digits per chain
+  uint8_t* slice_out;         // [batch frame][slice][slice_cap]
   int64_t slice_cap;
-  int64_t* slice_bytes;      // [frame][slice]
-  uint8_t* persist;          // [slice][2][contexts][32]
-  uint8_t* gstates;          // context model 1 working states [seg][slice][2][contexts][32]
-  int* status;               // [0]: overflow count
+  int64_t* slice_bytes;       // [batch frame][slice]
+  int* status;                // [0] overflow count
 };
 
 struct AssembleArgs {
@@ -71,8 +95,8 @@ struct AssembleArgs {
   int ec;
 };
 
-size_t encode_lds_bytes(const EncodeArgs& a, bool lds_states);
-int launch_encode(const EncodeArgs& a, bool lds_states, void* stream);
+int launch_symbols(const SymbolArgs& a, void* stream);
+int launch_code(const CodeArgs& a, void* stream);
 int launch_assemble(const AssembleArgs& a, int nframes, void* stream);
 
 }  // namespace ffv1hip

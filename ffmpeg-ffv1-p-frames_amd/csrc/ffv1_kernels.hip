@@ -1,19 +1,32 @@
 // ffv1_kernels.hip -- CDNA4 (gfx950) kernels of the FFV1 P-frame encoder.
 //
-// Hot path:
-//   ffv1_encode_slices  one 64-lane wavefront per (slice, frame segment).
-//     * rows of the slice plane are staged through LDS; the 64 lanes
-//       compute median prediction + quantised-gradient contexts + fold for
-//       a whole row in parallel (ffv1.h:148-190, ffv1enc.c:306-317);
-//     * the adaptive binary range coder (rangecoder.h:52-102) and symbol
-//       binarisation (ffv1enc.c:185-231) then run wave-uniformly over that
-//       row: it is the serial part of the bitstream;
-//     * the per-slice context-state table (the P-frame carry,
-//       ffv1enc.c:1171-1172) lives in LDS for the whole frame segment.
-//   ffv1_assemble_packets  one workgroup per (slice, frame): packet
-//     placement (prefix over slice sizes), 3-byte size, 0x00 and the slice
-//     CRC-32 computed chunk-parallel and combined in GF(2)
-//     (ffv1enc.c:1326-1354, crc.c:357).
+// Hot path, three kernels per batch:
+//
+//   ffv1_symbols   fully parallel: one thread per sample computes median
+//                  prediction, the quantised-gradient context and the folded
+//                  residual (ffv1.h:148-190, ffv1enc.c:306-317), with the
+//                  reference's ring-buffer edge rules (ffv1enc.c:381-388).
+//                  Output: one 32-bit symbol per sample, in coding order.
+//
+//   ffv1_code      the range coder (rangecoder.h:52-102) + binarisation
+//                  (ffv1enc.c:185-231), SIMT: ONE LANE PER (segment, slice)
+//                  CHAIN.  A slice's bitstream is inherently serial, so
+//                  parallelism comes from coding 64 independent slice streams
+//                  per wavefront.  Each lane keeps its current context's 32
+//                  adaptive states in 8 VGPRs; the binarisation is laid out as
+//                  static slot positions, so every state byte is extracted and
+//                  re-inserted at a compile-time offset.  Renormalisation does
+//                  not emit bytes inline: it stores a 10-bit "digit" (the top
+//                  byte of `low`, its carry, and the 0xFF-deferral flag) and a
+//                  per-lane post-pass replays the reference's pending-byte /
+//                  0xFF-run logic exactly.  The per-chain context tables (the
+//                  P-frame carry, ffv1enc.c:1171-1172) live in HBM/L2 and are
+//                  gathered one 32-byte row per context change, with the next
+//                  symbol's row prefetched while the current one codes.
+//
+//   ffv1_assemble_packets  packet placement (prefix over slice sizes), the
+//                  3-byte size, 0x00 and the slice CRC-32 computed chunk-
+//                  parallel and combined in GF(2) (ffv1enc.c:1326-1354).
 #include <hip/hip_runtime.h>
 
 #include "ffv1_internal.h"
@@ -24,273 +37,378 @@ namespace {
 
 constexpr int kWave = 64;
 
-// ---------------------------------------------------------------------------
-// Range coder: wave-uniform register state.  Bytes are packed into a 32-bit
-// word and lane 0 stores whole dwords; the pending-byte / 0xFF-run logic of
-// renorm_encoder is kept verbatim in meaning so the output is identical.
-struct Rac {
-  int low, range;
-  int pending;    // outstanding_byte (-1 = none yet)
-  int run;        // outstanding_count (deferred 0xFF bytes)
-  uint32_t word;  // bytes not yet stored
-  int nword;
-  int64_t pos;    // bytes stored so far
-};
-
-struct Sink {
-  uint8_t* out;
-  int64_t cap;
-  bool lane0;
-};
-
-__device__ __forceinline__ void rac_emit(Rac& c, const Sink& s, int b) {
-  c.word |= (uint32_t)(b & 0xFF) << (8 * c.nword);
-  if (++c.nword == 4) {
-    if (s.lane0 && c.pos + 4 <= s.cap)
-      *reinterpret_cast<uint32_t*>(s.out + c.pos) = c.word;
-    c.pos += 4;
-    c.word = 0;
-    c.nword = 0;
-  }
-}
-
-__device__ __forceinline__ void rac_shift(Rac& c, const Sink& s) {
-  if (c.pending < 0) {
-    c.pending = c.low >> 8;
-  } else if (c.low <= 0xFF00) {
-    rac_emit(c, s, c.pending);
-    for (; c.run; c.run--) rac_emit(c, s, 0xFF);
-    c.pending = c.low >> 8;
-  } else if (c.low >= 0x10000) {
-    rac_emit(c, s, c.pending + 1);
-    for (; c.run; c.run--) rac_emit(c, s, 0x00);
-    c.pending = (c.low >> 8) & 0xFF;
-  } else {
-    c.run++;
-  }
-  c.low = (c.low & 0xFF) << 8;
-  c.range <<= 8;
-}
-
-// One binary decision with adaptive state st; returns the next state.
-// tab = [to0[256] | to1[256]] in LDS.
-__device__ __forceinline__ int rac_put(Rac& c, const Sink& s, int st, int bit,
-                                       const uint8_t* tab) {
-  const int r1 = (c.range * st) >> 8;
-  if (bit) {
-    c.low += c.range - r1;
-    c.range = r1;
-  } else {
-    c.range -= r1;
-  }
-  // the interval never shrinks below 1, so one byte shift always suffices
-  if (c.range < 0x100) rac_shift(c, s);
-  return tab[(bit << 8) | st];
-}
-
-__device__ __forceinline__ void rac_put_mem(Rac& c, const Sink& s, uint8_t* sp,
-                                            int bit, const uint8_t* tab) {
-  *sp = (uint8_t)rac_put(c, s, *sp, bit, tab);
-}
-
-// put_symbol: zero flag, unary exponent, mantissa MSB first, sign.
-__device__ __forceinline__ void rac_symbol(Rac& c, const Sink& s, uint8_t* st,
-                                           int v, bool is_signed,
-                                           const uint8_t* tab) {
-  if (v == 0) {
-    rac_put_mem(c, s, st, 1, tab);
-    return;
-  }
-  const unsigned a = v < 0 ? 0u - (unsigned)v : (unsigned)v;
-  const int e = 31 - __builtin_clz(a);
-  rac_put_mem(c, s, st, 0, tab);
-  for (int i = 0; i < e; i++) rac_put_mem(c, s, st + 1 + min(i, 9), 1, tab);
-  rac_put_mem(c, s, st + 1 + min(e, 9), 0, tab);
-  for (int i = e - 1; i >= 0; i--)
-    rac_put_mem(c, s, st + 22 + min(i, 9), (a >> i) & 1, tab);
-  if (is_signed) rac_put_mem(c, s, st + 11 + min(e, 10), v < 0, tab);
-}
-
-__device__ __forceinline__ int64_t rac_finish(Rac& c, const Sink& s) {
-  c.range = 0xFF;
-  c.low += 0xFF;
-  while (c.range < 0x100) rac_shift(c, s);
-  c.range = 0xFF;
-  while (c.range < 0x100) rac_shift(c, s);
-  // flush the partial word byte by byte
-  if (s.lane0)
-    for (int k = 0; k < c.nword; k++)
-      if (c.pos + k < s.cap) s.out[c.pos + k] = (uint8_t)(c.word >> (8 * k));
-  return c.pos + c.nword;
-}
-
 __device__ __forceinline__ int median3(int a, int b, int c) {
   return max(min(a, b), min(max(a, b), c));
 }
 
+// fold() (ffv1.h:148-159) == sign-extension of the low `bits` bits
 __device__ __forceinline__ int fold_bits(int d, int bits) {
-  if (bits == 8) return (int)(int8_t)d;
   const int sh = 32 - bits;
-  return (d << sh) >> sh;  // sign-extend the low `bits` bits
-}
-
-__device__ __forceinline__ size_t align16(size_t v) { return (v + 15) & ~size_t(15); }
-
-struct LdsLayout {
-  size_t states, tabs, qt, opsets, rows, sym, total;
-};
-
-__host__ __device__ inline LdsLayout lds_layout(const EncodeArgs& a, bool lds_states) {
-  LdsLayout L;
-  size_t off = 0;
-  L.states = off;
-  if (lds_states) off += ((size_t)2 * a.contexts * 32 + 15) & ~size_t(15);
-  L.tabs = off;   off += 1024;
-  L.qt = off;     off += 5 * 256 * 2;
-  L.opsets = off; off += kOpSets * 32;
-  L.rows = off;   off += ((size_t)3 * a.row_len * 2 + 15) & ~size_t(15);
-  L.sym = off;    off += (size_t)a.row_len * 4;
-  L.total = off;
-  return L;
+  return (d << sh) >> sh;
 }
 
 // ---------------------------------------------------------------------------
-template <bool kLdsStates>
-__global__ __launch_bounds__(kWave) void ffv1_encode_slices(EncodeArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const LdsLayout L = lds_layout(a, kLdsStates);
-  const int lane = threadIdx.x;
-  const int slice = blockIdx.x;
-  const Segment seg = a.segs[blockIdx.y];
+// Kernel 1: symbols.
+constexpr int kSymThreads = 256;
 
-  uint8_t* tabs = smem + L.tabs;
-  int16_t* qt = reinterpret_cast<int16_t*>(smem + L.qt);
-  uint8_t* opsets = smem + L.opsets;
-  int16_t* rows = reinterpret_cast<int16_t*>(smem + L.rows);
-  int32_t* sym = reinterpret_cast<int32_t*>(smem + L.sym);
-  const int64_t state_bytes = (int64_t)2 * a.contexts * 32;
-  uint8_t* states =
-      kLdsStates ? smem + L.states
-                 : a.gstates + ((int64_t)blockIdx.y * a.nslices + slice) * state_bytes;
-
-  for (int i = lane; i < 1024; i += kWave) tabs[i] = a.tabs[i];
-  for (int i = lane; i < 5 * 256; i += kWave) qt[i] = a.qt[i];
-  if (seg.load_states) {
-    const uint8_t* src = a.persist + (int64_t)slice * state_bytes;
-    for (int64_t i = lane * 4; i < state_bytes; i += kWave * 4)
-      *reinterpret_cast<uint32_t*>(states + i) = *reinterpret_cast<const uint32_t*>(src + i);
-  }
+__global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
+  __shared__ int16_t qt[5 * 256];
+  for (int i = threadIdx.x; i < 5 * 256; i += kSymThreads) qt[i] = a.qt[i];
   __syncthreads();
+  const int slice = blockIdx.x, slot = blockIdx.y, p = blockIdx.z;
+  if (p >= a.nplanes) return;
+  const int f = a.frame_of_slot[slot];
+  if (f < 0) return;
+  const SliceGeom& g = a.geom[slice];
+  const int pw = g.pw[p], ph = g.ph[p], px = g.px[p], py = g.py[p];
+  const uint8_t* base = a.frames + (int64_t)f * a.frame_bytes + a.plane_off[p];
+  const int stride = a.plane_stride[p];
+  uint32_t* out = a.sym + (int64_t)slot * a.frame_samples + g.sym_off + g.plane_sym_off[p];
+  const int row0 = p ? a.contexts : 0;  // plane context 1 rows follow plane 0's
 
-  // slice rectangle (ffv1.c:117-145)
-  const int sx = slice % a.nh, sy = slice / a.nh;
-  const int x0 = (int)((int64_t)a.width * sx / a.nh);
-  const int y0 = (int)((int64_t)a.height * sy / a.nv);
-  const int sw = (int)((int64_t)a.width * (sx + 1) / a.nh) - x0;
-  const int sh = (int)((int64_t)a.height * (sy + 1) / a.nv) - y0;
-  const uint8_t* ftab = tabs + 512;
-  const int nplanes = a.chroma_planes ? 3 : 1;
+  auto load = [&](int x, int y) -> int {  // sample of the slice plane, as int16 (ffv1enc.c:390-407)
+    const uint8_t* r = base + (int64_t)(py + y) * stride;
+    if (a.sample_bytes == 1) return r[px + x];
+    unsigned v = reinterpret_cast<const uint16_t*>(r)[px + x];
+    if (!a.packed_at_lsb) v >>= a.msb_shift;
+    return (int16_t)v;
+  };
 
-  for (int f = seg.first_frame; f < seg.first_frame + seg.nframes; f++) {
-    const int key = a.keyflags[f];
-    if (key) {  // ff_ffv1_clear_slice_state: initial states are all 128
-      for (int64_t i = lane * 4; i < state_bytes; i += kWave * 4)
-        *reinterpret_cast<uint32_t*>(states + i) = 0x80808080u;
+  for (int64_t idx = threadIdx.x; idx < (int64_t)pw * ph; idx += kSymThreads) {
+    const int y = (int)(idx / pw), x = (int)(idx - (int64_t)y * pw);
+    // neighbourhood as the zeroed two/three-row ring exposes it:
+    // rows above the slice read 0; L(x=0) = T; LT(x=0) = sample two rows up
+    // in column 0; RT past the right edge = T; LL(x=0) = 0, LL(x=1) = T(0).
+    const int X = load(x, y);
+    const int T = y ? load(x, y - 1) : 0;
+    const int T0 = y ? load(0, y - 1) : 0;
+    const int L = x ? load(x - 1, y) : T0;
+    const int LT = x ? (y ? load(x - 1, y - 1) : 0) : (y >= 2 ? load(0, y - 2) : 0);
+    const int RT = x + 1 < pw ? (y ? load(x + 1, y - 1) : 0) : T;
+    int ctx = qt[(L - LT) & 0xFF] + qt[256 + ((LT - T) & 0xFF)] + qt[512 + ((T - RT) & 0xFF)];
+    if (a.model1) {
+      const int LL = x >= 2 ? load(x - 2, y) : (x == 1 ? T0 : 0);
+      const int TT = y >= 2 ? load(x, y - 2) : 0;
+      ctx += qt[768 + ((LL - L) & 0xFF)] + qt[1024 + ((TT - T) & 0xFF)];
     }
-    for (int i = lane; i < kOpSets * 32; i += kWave) opsets[i] = 128;
-    __syncthreads();
-
-    Rac c{0, 0xFF00, -1, 0, 0u, 0, 0};
-    const Sink snk{a.slice_out + ((int64_t)f * a.nslices + slice) * a.slice_cap,
-                   a.slice_cap, lane == 0};
-
-    // key bit / in-band header / slice header
-    {
-      const int sel = key * a.nslices + slice;
-      const Op* ops = a.ops + (int64_t)sel * kMaxOps;
-      const int n = a.nops[sel];
-      for (int k = 0; k < n; k++) {
-        const Op op = ops[k];
-        const uint8_t* t = tabs + (op.tab ? 512 : 0);
-        uint8_t* st = opsets + op.set * 32;
-        if (op.kind == kOpBit)
-          rac_put_mem(c, snk, st, op.value, t);
-        else
-          rac_symbol(c, snk, st, op.value, op.kind == kOpSymS, t);
-      }
+    int diff = X - median3(L, L + T - LT, T);
+    if (ctx < 0) {
+      ctx = -ctx;
+      diff = -diff;
     }
+    diff = fold_bits(diff, a.coded_bits);
+    out[idx] = ((uint32_t)(row0 + ctx) << 16) | (uint16_t)diff;
+  }
+}
 
-    for (int p = 0; p < nplanes; p++) {
-      int px = x0, py = y0, pw = sw, ph = sh;
-      if (p) {
-        pw = -((-sw) >> a.hs);
-        ph = -((-sh) >> a.vs);
-        px = x0 >> a.hs;
-        py = y0 >> a.vs;
-      }
-      uint8_t* pst = states + (int64_t)(p ? 1 : 0) * a.contexts * 32;
-      const uint8_t* pbase = a.frames + (int64_t)f * a.frame_bytes + a.plane_off[p];
-      const int stride = a.plane_stride[p];
+// ---------------------------------------------------------------------------
+// Kernel 2: SIMT range coder.
+struct Lane {
+  int low, range;
+  uint32_t r0, r1, r2, r3, r4, r5, r6, r7;  // states of the current context row (byte k = slot k)
+  uint32_t dw;         // digit word being filled (2 x 16-bit digits)
+  int dn;              // digits in dw
+  int dpos;            // dwords of digits stored
+  int dcap;            // dword capacity
 
-      for (int i = lane; i < 3 * a.row_len; i += kWave) rows[i] = 0;
-      __syncthreads();
+  template <int D>
+  __device__ __forceinline__ uint32_t& w() {
+    static_assert(D >= 0 && D < 8, "row word");
+    if constexpr (D == 0) return r0;
+    else if constexpr (D == 1) return r1;
+    else if constexpr (D == 2) return r2;
+    else if constexpr (D == 3) return r3;
+    else if constexpr (D == 4) return r4;
+    else if constexpr (D == 5) return r5;
+    else if constexpr (D == 6) return r6;
+    else return r7;
+  }
+};
 
-      for (int y = 0; y < ph; y++) {
-        int16_t* cur = rows + (y % 3) * a.row_len + 4;
-        int16_t* prev = rows + ((y + 2) % 3) * a.row_len + 4;
-        int16_t* prev2 = rows + ((y + 1) % 3) * a.row_len + 4;
-        const uint8_t* src = pbase + (int64_t)(py + y) * stride;
-        if (a.sample_bytes == 1) {
-          for (int x = lane; x < pw; x += kWave) cur[x] = src[px + x];
-        } else {
-          const uint16_t* s16 = reinterpret_cast<const uint16_t*>(src) + px;
-          for (int x = lane; x < pw; x += kWave) {
-            unsigned v = s16[x];
-            if (!a.packed_at_lsb) v >>= a.msb_shift;
-            cur[x] = (int16_t)v;
-          }
-        }
-        __syncthreads();
-        if (lane == 0) {  // ring-buffer edge taps (ffv1enc.c:387-388)
-          cur[-1] = prev[0];
-          prev[pw] = prev[pw - 1];
-        }
-        __syncthreads();
-        for (int x = lane; x < pw; x += kWave) {
-          const int X = cur[x], L = cur[x - 1], T = prev[x], LT = prev[x - 1], RT = prev[x + 1];
-          int ctx = qt[(L - LT) & 0xFF] + qt[256 + ((LT - T) & 0xFF)] + qt[512 + ((T - RT) & 0xFF)];
-          if (a.model1)
-            ctx += qt[768 + ((cur[x - 2] - L) & 0xFF)] + qt[1024 + ((prev2[x] - T) & 0xFF)];
-          int diff = X - median3(L, L + T - LT, T);
-          if (ctx < 0) {
-            ctx = -ctx;
-            diff = -diff;
-          }
-          diff = fold_bits(diff, a.coded_bits);
-          sym[x] = (int32_t)(((uint32_t)ctx << 16) | (uint16_t)diff);
-        }
-        __syncthreads();
-        for (int x = 0; x < pw; x++) {
-          const int32_t s = sym[x];
-          rac_symbol(c, snk, pst + (int64_t)(s >> 16) * 32, (int16_t)(s & 0xFFFF), true, ftab);
-        }
-        __syncthreads();
-      }
+// Renormalisation (rangecoder.h:52-75) deferred: record low's top byte with
+// its carry (bit 8) and whether the reference would defer it as an 0xFF run
+// (bit 9: 0xFF00 < low < 0x10000), then shift.
+__device__ __forceinline__ void renorm_digit(Lane& L, uint32_t* digits) {
+  const uint32_t d = ((uint32_t)L.low >> 8) | ((L.low > 0xFF00 && L.low < 0x10000) ? 0x200u : 0u);
+  L.dw |= d << (L.dn << 4);
+  if (++L.dn == 2) {
+    if (L.dpos < L.dcap) digits[L.dpos] = L.dw;
+    L.dpos++;
+    L.dw = 0;
+    L.dn = 0;
+  }
+  L.low = (L.low & 0xFF) << 8;
+  L.range <<= 8;
+}
+
+__device__ __forceinline__ void rac_core(Lane& L, int s, int bit) {
+  const int r1 = (L.range * s) >> 8;
+  const int r0 = L.range - r1;
+  L.low += bit ? r0 : 0;
+  L.range = bit ? r1 : r0;
+}
+
+// One decision on the static slot K of the current row.
+template <int K>
+__device__ __forceinline__ void step(Lane& L, uint32_t* digits, bool act, int bit, const uint8_t* tab) {
+  if (act) {
+    constexpr int D = K >> 2, SH = (K & 3) * 8;
+    const uint32_t w = L.w<D>();
+    const int s = (w >> SH) & 0xFF;
+    rac_core(L, s, bit);
+    const uint32_t ns = tab[(bit << 8) | s];
+    L.w<D>() = (w & ~(0xFFu << SH)) | (ns << SH);
+    if (L.range < 0x100) renorm_digit(L, digits);
+  }
+}
+
+// The sign decision's slot 11 + min(e,10) varies per lane (dwords 2..5).
+__device__ __forceinline__ void sign_step(Lane& L, uint32_t* digits, bool act, int m, int bit,
+                                          const uint8_t* tab) {
+  if (act) {
+    const int k = 11 + m, d = k >> 2, sh = (k & 3) * 8;
+    // mask selects (not ternaries): a select between members would be folded
+    // into an indexed load and push the whole Lane into scratch
+    const uint32_t m2 = 0u - (uint32_t)(d == 2), m3 = 0u - (uint32_t)(d == 3);
+    const uint32_t m4 = 0u - (uint32_t)(d == 4), m5 = 0u - (uint32_t)(d == 5);
+    const uint32_t w = (L.r2 & m2) | (L.r3 & m3) | (L.r4 & m4) | (L.r5 & m5);
+    const int s = (w >> sh) & 0xFF;
+    rac_core(L, s, bit);
+    const uint32_t ns = tab[(bit << 8) | s];
+    const uint32_t nw = (w & ~(0xFFu << sh)) | (ns << sh);
+    L.r2 = (nw & m2) | (L.r2 & ~m2);
+    L.r3 = (nw & m3) | (L.r3 & ~m3);
+    L.r4 = (nw & m4) | (L.r4 & ~m4);
+    L.r5 = (nw & m5) | (L.r5 & ~m5);
+    if (L.range < 0x100) renorm_digit(L, digits);
+  }
+}
+
+__device__ __forceinline__ int wave_max(int v) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Generic decision on a per-lane LDS state (header ops; rare).
+__device__ __forceinline__ void put_lds(Lane& L, uint32_t* digits, uint8_t* st, int bit,
+                                        const uint8_t* tab) {
+  const int s = *st;
+  rac_core(L, s, bit);
+  *st = tab[(bit << 8) | s];
+  if (L.range < 0x100) renorm_digit(L, digits);
+}
+
+__device__ __forceinline__ void symbol_lds(Lane& L, uint32_t* dg, uint8_t* st, int v, bool sgn,
+                                           const uint8_t* tab) {
+  if (v == 0) {
+    put_lds(L, dg, st, 1, tab);
+    return;
+  }
+  const unsigned a = v < 0 ? 0u - (unsigned)v : (unsigned)v;
+  const int e = 31 - __builtin_clz(a);
+  put_lds(L, dg, st, 0, tab);
+  for (int i = 0; i < e; i++) put_lds(L, dg, st + 1 + min(i, 9), 1, tab);
+  put_lds(L, dg, st + 1 + min(e, 9), 0, tab);
+  for (int i = e - 1; i >= 0; i--) put_lds(L, dg, st + 22 + min(i, 9), (a >> i) & 1, tab);
+  if (sgn) put_lds(L, dg, st + 11 + min(e, 10), v < 0, tab);
+}
+
+__device__ __forceinline__ void store_row(const Lane& L, uint8_t* row) {
+  reinterpret_cast<uint4*>(row)[0] = make_uint4(L.r0, L.r1, L.r2, L.r3);
+  reinterpret_cast<uint4*>(row)[1] = make_uint4(L.r4, L.r5, L.r6, L.r7);
+}
+
+constexpr int kCodeThreads = kWave;
+constexpr int kOpsetBytes = kOpSets * 32;
+
+__global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t tabs[1024];
+  __shared__ __attribute__((aligned(16))) uint8_t opsets[kCodeThreads * kOpsetBytes];
+  for (int i = threadIdx.x; i < 1024; i += kCodeThreads) tabs[i] = a.tabs[i];
+  __syncthreads();
+  const uint8_t* dtab = tabs;        // default table (key bit, v0/v1 header)
+  const uint8_t* ftab = tabs + 512;  // frame table
+
+  const int lane = threadIdx.x;
+  const int64_t chain = (int64_t)blockIdx.x * kCodeThreads + lane;
+  const int seg_i = (int)(chain / a.nslices), slice = (int)(chain % a.nslices);
+  bool live = seg_i < a.nsegs;
+  Segment seg{0, 0, 0, 0};
+  if (live) seg = a.segs[seg_i];
+  live = live && a.j < seg.nframes;
+  const int f = seg.first_frame + a.j;
+  const int key = live ? a.keyflags[f] : 0;
+  uint8_t* table = a.tables + chain * a.state_bytes;
+
+  // context states: continue, or reset at a keyframe (ff_ffv1_clear_slice_state)
+  if (live) {
+    if (a.j == 0 && seg.load_states) {
+      const uint4* src = reinterpret_cast<const uint4*>(a.persist + (int64_t)slice * a.state_bytes);
+      for (int64_t i = 0; i < a.state_bytes / 16; i++) reinterpret_cast<uint4*>(table)[i] = src[i];
+    } else if (key) {
+      const uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
+      for (int64_t i = 0; i < a.state_bytes / 16; i++) reinterpret_cast<uint4*>(table)[i] = v;
     }
-    // slice end: a 0 decision on state 129, then terminate (ffv1enc.c:1331-1334)
-    (void)rac_put(c, snk, 129, 0, ftab);
-    const int64_t bytes = rac_finish(c, snk);
-    if (lane == 0) {
-      a.slice_bytes[(int64_t)f * a.nslices + slice] = bytes;
-      if (bytes > a.slice_cap) atomicAdd(a.status, 1);
-    }
-    __syncthreads();
   }
 
-  if (seg.save_states) {
-    uint8_t* dst = a.persist + (int64_t)slice * state_bytes;
-    for (int64_t i = lane * 4; i < state_bytes; i += kWave * 4)
-      *reinterpret_cast<uint32_t*>(dst + i) = *reinterpret_cast<const uint32_t*>(states + i);
+  Lane L;
+  L.low = 0;
+  L.range = 0xFF00;
+  L.dw = 0;
+  L.dn = 0;
+  L.dpos = 0;
+  L.dcap = (int)(a.digit_cap / 2);
+  L.r0 = L.r1 = L.r2 = L.r3 = L.r4 = L.r5 = L.r6 = L.r7 = 0;
+  uint32_t* const digits = a.digits + chain * (a.digit_cap / 2);
+
+  // header ops: key bit, in-band v0/v1 header, v3 slice header
+  {
+    uint8_t* os = opsets + lane * kOpsetBytes;
+    for (int i = 0; i < kOpsetBytes; i++) os[i] = 128;
+    const int sel = key * a.nslices + slice;
+    const int n = live ? a.nops[sel] : 0;
+    const Op* ops = a.ops + (int64_t)sel * kMaxOps;
+    for (int q = 0; q < a.max_ops; q++) {
+      if (q < n) {
+        const Op op = ops[q];
+        const uint8_t* t = op.tab ? ftab : dtab;
+        uint8_t* st = os + op.set * 32;
+        if (op.kind == kOpBit)
+          put_lds(L, digits, st, op.value, t);
+        else
+          symbol_lds(L, digits, st, op.value, op.kind == kOpSymS, t);
+      }
+    }
+  }
+
+  const SliceGeom& g = a.geom[slice];
+  const int64_t nsym = live ? g.nsym : 0;
+  const int64_t nmax = wave_max((int)nsym);
+  // g.sym_off and frame_samples are multiples of 4 (host-side padding)
+  const uint4* sp = reinterpret_cast<const uint4*>(a.sym + (int64_t)seg_i * a.frame_samples + g.sym_off);
+
+  int cur = -1, pfrow = -1;
+  uint4 PFa = make_uint4(0, 0, 0, 0), PFb = make_uint4(0, 0, 0, 0);
+  uint4 G = make_uint4(0, 0, 0, 0), GN = make_uint4(0, 0, 0, 0);
+  if (nsym > 0) G = sp[0];
+  if (nsym > 4) GN = sp[1];
+
+  for (int64_t i = 0; i < nmax; i++) {
+    const bool act = i < nsym;
+    const int q = (int)(i & 3);
+    if (q == 0 && i > 0) {
+      G = GN;
+      if (act && i + 4 < nsym) GN = sp[(i >> 2) + 1];
+    }
+    const uint32_t sv = q == 0 ? G.x : q == 1 ? G.y : q == 2 ? G.z : G.w;
+    const uint32_t sn = q == 0 ? G.y : q == 1 ? G.z : q == 2 ? G.w : GN.x;
+    const int row = (int)(sv >> 16);
+    const int v = (int16_t)(sv & 0xFFFF);
+    if (act && row != cur) {  // context switch: write back, take the prefetch
+      if (cur >= 0) store_row(L, table + (int64_t)cur * 32);
+      uint4 ra = PFa, rb = PFb;
+      if (row != pfrow) {
+        ra = reinterpret_cast<const uint4*>(table + (int64_t)row * 32)[0];
+        rb = reinterpret_cast<const uint4*>(table + (int64_t)row * 32)[1];
+      }
+      L.r0 = ra.x; L.r1 = ra.y; L.r2 = ra.z; L.r3 = ra.w;
+      L.r4 = rb.x; L.r5 = rb.y; L.r6 = rb.z; L.r7 = rb.w;
+      cur = row;
+    }
+    pfrow = -1;
+    if (act && i + 1 < nsym) {  // prefetch the next symbol's row
+      const int nrow = (int)(sn >> 16);
+      if (nrow != cur) {
+        PFa = reinterpret_cast<const uint4*>(table + (int64_t)nrow * 32)[0];
+        PFb = reinterpret_cast<const uint4*>(table + (int64_t)nrow * 32)[1];
+        pfrow = nrow;
+      }
+    }
+
+    // put_symbol_inline over static slots
+    const bool nz = act && v != 0;
+    const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
+    const int e = nz ? 31 - __builtin_clz(mag) : -1;
+    step<0>(L, digits, act, v == 0, ftab);
+    const int emax = wave_max(e);
+    if (emax >= 0) {
+      // unary exponent: slots 1..10, 1-bits then the terminating 0
+#define UNARY(I) if (I <= emax) step<1 + I>(L, digits, nz && I <= e, I < e, ftab);
+      UNARY(0) UNARY(1) UNARY(2) UNARY(3) UNARY(4) UNARY(5) UNARY(6) UNARY(7) UNARY(8) UNARY(9)
+#undef UNARY
+      for (int i2 = 10; i2 <= emax; i2++) step<10>(L, digits, nz && i2 <= e, i2 < e, ftab);
+      // mantissa MSB -> LSB: slots 22 + min(i, 9)
+      for (int i2 = emax - 1; i2 >= 10; i2--) step<31>(L, digits, nz && i2 < e, (mag >> i2) & 1, ftab);
+#define MANT(I) if (I < emax) step<22 + I>(L, digits, nz && I < e, (mag >> I) & 1, ftab);
+      MANT(9) MANT(8) MANT(7) MANT(6) MANT(5) MANT(4) MANT(3) MANT(2) MANT(1) MANT(0)
+#undef MANT
+      sign_step(L, digits, nz, min(e, 10), v < 0, ftab);
+    }
+  }
+  if (cur >= 0) store_row(L, table + (int64_t)cur * 32);
+
+  if (live) {
+    // slice end: a 0 decision on state 129, then ff_rac_terminate
+    rac_core(L, 129, 0);
+    if (L.range < 0x100) renorm_digit(L, digits);
+    L.range = 0xFF;
+    L.low += 0xFF;
+    renorm_digit(L, digits);
+    L.range = 0xFF;
+    renorm_digit(L, digits);
+    const int odd = L.dn;
+    if (L.dn) {
+      if (L.dpos < L.dcap) digits[L.dpos] = L.dw;
+      L.dpos++;
+    }
+    const int64_t ndig = (int64_t)L.dpos * 2 - (odd ? 1 : 0);
+    int64_t nbytes = 0;
+    if (L.dpos > L.dcap) {
+      atomicAdd(a.status, 1);
+    } else {
+      // replay renorm_encoder's pending byte / 0xFF-run logic over the digits
+      uint8_t* out = a.slice_out + ((int64_t)f * a.nslices + slice) * a.slice_cap;
+      const int64_t cap = a.slice_cap;
+      uint32_t ow = 0;
+      int on = 0;
+      int64_t opos = 0;
+      int pending = -1, run = 0;
+      auto emit = [&](int b) {
+        ow |= (uint32_t)(b & 0xFF) << (on << 3);
+        if (++on == 4) {
+          if (opos + 4 <= cap) *reinterpret_cast<uint32_t*>(out + opos) = ow;
+          opos += 4;
+          ow = 0;
+          on = 0;
+        }
+      };
+      for (int64_t t = 0; t < ndig; t++) {
+        const uint32_t d = (digits[t >> 1] >> ((t & 1) << 4)) & 0x3FF;
+        const int qv = d & 0x1FF;
+        if (pending < 0) {
+          pending = qv;
+        } else if (d & 0x200) {
+          run++;
+        } else if (qv < 0x100) {
+          emit(pending);
+          for (; run; run--) emit(0xFF);
+          pending = qv;
+        } else {
+          emit(pending + 1);
+          for (; run; run--) emit(0x00);
+          pending = qv & 0xFF;
+        }
+      }
+      for (int k = 0; k < on; k++)
+        if (opos + k < cap) out[opos + k] = (uint8_t)(ow >> (k << 3));
+      nbytes = opos + on;
+      if (nbytes > cap) atomicAdd(a.status, 1);
+    }
+    a.slice_bytes[(int64_t)f * a.nslices + slice] = nbytes;
+    if (a.j == seg.nframes - 1 && seg.save_states) {
+      uint4* dst = reinterpret_cast<uint4*>(a.persist + (int64_t)slice * a.state_bytes);
+      for (int64_t i = 0; i < a.state_bytes / 16; i++) dst[i] = reinterpret_cast<const uint4*>(table)[i];
+    }
   }
 }
 
@@ -385,25 +503,16 @@ __global__ __launch_bounds__(kAsmThreads) void ffv1_assemble_packets(AssembleArg
 
 }  // namespace
 
-size_t encode_lds_bytes(const EncodeArgs& a, bool lds_states) {
-  return lds_layout(a, lds_states).total;
+int launch_symbols(const SymbolArgs& a, void* stream) {
+  dim3 grid(a.nslices, a.nslots, a.nplanes), block(kSymThreads);
+  hipLaunchKernelGGL(ffv1_symbols, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_encode(const EncodeArgs& a, bool lds_states, void* stream) {
-  const size_t lds = encode_lds_bytes(a, lds_states);
-  dim3 grid(a.nslices, a.nsegs), block(kWave);
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (lds_states) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&ffv1_encode_slices<true>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-      return -1;
-    hipLaunchKernelGGL(ffv1_encode_slices<true>, grid, block, lds, st, a);
-  } else {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&ffv1_encode_slices<false>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-      return -1;
-    hipLaunchKernelGGL(ffv1_encode_slices<false>, grid, block, lds, st, a);
-  }
+int launch_code(const CodeArgs& a, void* stream) {
+  const int64_t chains = (int64_t)a.nsegs * a.nslices;
+  dim3 grid((unsigned)((chains + kCodeThreads - 1) / kCodeThreads)), block(kCodeThreads);
+  hipLaunchKernelGGL(ffv1_code, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -57,8 +57,19 @@ EXPORTED_SYMBOLS = (
     "ffv1hip_max_packet_size", "ffv1hip_encode", "ffv1hip_encode_device", "ffv1hip_fetch",
     "ffv1hip_device_packets", "ffv1hip_picture_number", "ffv1hip_reset",
     "ffv1hip_get_slice_states", "ffv1hip_set_slice_states", "ffv1hip_last_error",
-    "ffv1hip_abi_version",
+    "ffv1hip_abi_version", "ffv1hip_set_profiling", "ffv1hip_last_kernel_ms",
+    "ffv1hip_last_kernel_stats",
 )
+
+
+class KernelStats(ctypes.Structure):
+    _fields_ = [("symbols_ms", ctypes.c_float), ("code_ms", ctypes.c_float),
+                ("assemble_ms", ctypes.c_float), ("symbols_launches", ctypes.c_int),
+                ("code_launches", ctypes.c_int), ("assemble_launches", ctypes.c_int),
+                ("frames_coded_per_launch_max", ctypes.c_int64)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
 
 _lib = None
 
@@ -99,6 +110,12 @@ def load_library():
     L.ffv1hip_set_slice_states.restype = ctypes.c_int
     L.ffv1hip_last_error.argtypes = []
     L.ffv1hip_last_error.restype = ctypes.c_char_p
+    L.ffv1hip_set_profiling.argtypes = [vp, ctypes.c_int]
+    L.ffv1hip_set_profiling.restype = ctypes.c_int
+    L.ffv1hip_last_kernel_ms.argtypes = [vp, P(ctypes.c_float), P(ctypes.c_float)]
+    L.ffv1hip_last_kernel_ms.restype = ctypes.c_int
+    L.ffv1hip_last_kernel_stats.argtypes = [vp, P(KernelStats)]
+    L.ffv1hip_last_kernel_stats.restype = ctypes.c_int
     L.ffv1hip_abi_version.argtypes = []
     L.ffv1hip_abi_version.restype = ctypes.c_int
     _lib = L
@@ -229,6 +246,25 @@ class HipEncoder:
         stride = ctypes.c_int64()
         L.ffv1hip_device_packets(self._h, ctypes.byref(d_p), ctypes.byref(stride), ctypes.byref(d_s))
         return d_p.value, stride.value, d_s.value
+
+    def set_profiling(self, on: bool = True):
+        rc = load_library().ffv1hip_set_profiling(self._h, int(on))
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_set_profiling")
+
+    def last_kernel_ms(self):
+        e, a = ctypes.c_float(), ctypes.c_float()
+        rc = load_library().ffv1hip_last_kernel_ms(self._h, ctypes.byref(e), ctypes.byref(a))
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_last_kernel_ms")
+        return e.value, a.value
+
+    def last_kernel_stats(self) -> dict:
+        st = KernelStats()
+        rc = load_library().ffv1hip_last_kernel_stats(self._h, ctypes.byref(st))
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_last_kernel_stats")
+        return st.as_dict()
 
     def slice_states(self) -> bytes:
         L = load_library()

@@ -119,8 +119,25 @@ int64_t ffv1hip_get_slice_states(ffv1hip_ctx *ctx, uint8_t *buf, int64_t cap);
 int     ffv1hip_set_slice_states(ffv1hip_ctx *ctx, const uint8_t *buf,
                                  int64_t size);
 
-/* Name of the HIP device kernels in the last launch, for profiling, and
- * the last error message. */
+/* Kernel timing: when enabled, HIP events are recorded on the launch stream
+ * around each kernel of every call; ffv1hip_last_kernel_ms synchronises and
+ * returns the durations (ms) of the last call's slice-coder kernel
+ * (ffv1_encode_slices) and packet-assembly kernel (ffv1_assemble_packets). */
+int ffv1hip_set_profiling(ffv1hip_ctx *ctx, int enable);
+int ffv1hip_last_kernel_ms(ffv1hip_ctx *ctx, float *encode_ms, float *assemble_ms);
+
+/* Per-kernel totals of the last call (profiling enabled): summed HIP-event
+ * durations and launch counts of ffv1_symbols (prediction/context, one
+ * launch per frame index of the GOP), ffv1_code (range coder, same count)
+ * and ffv1_assemble_packets (one launch). */
+typedef struct ffv1hip_kernel_stats {
+    float symbols_ms, code_ms, assemble_ms;
+    int symbols_launches, code_launches, assemble_launches;
+    int64_t frames_coded_per_launch_max;   /* segments (GOPs) in the batch */
+} ffv1hip_kernel_stats;
+int ffv1hip_last_kernel_stats(ffv1hip_ctx *ctx, ffv1hip_kernel_stats *out);
+
+/* Last error message (thread-local) and the ABI version. */
 const char *ffv1hip_last_error(void);
 int ffv1hip_abi_version(void);
 
