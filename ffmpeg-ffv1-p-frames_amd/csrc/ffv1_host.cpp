@@ -493,8 +493,6 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
   };
   if (!params || max_batch_frames <= 0) return fail(set_err(-22, "invalid arguments"));
   const ffv1hip_params& p = *params;
-  if (p.ac == 0)
-    return fail(set_err(-38, "Golomb-Rice coder (coder=0) is not on the device path yet"));
   if (p.version == 2 || p.version > 3 || p.num_h_slices * p.num_v_slices > 256 ||
       p.bits_per_raw_sample < 8 || p.bits_per_raw_sample > 16 || p.width <= 0 || p.height <= 0 ||
       (p.sample_bytes == 1) != (p.bits_per_raw_sample == 8))
@@ -667,6 +665,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   ca.slice_cap = c->slice_cap;
   ca.slice_bytes = c->d_slice_bytes;
   ca.status = c->d_status;
+  ca.version = p.version;
+  ca.coded_bits = p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample;
 
   if (c->profiling) {
     HIP_TRY(hipEventRecord(c->ev[0], st));
@@ -684,7 +684,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     if (c->profiling) HIP_TRY(hipEventRecord(c->kev[4 * j + 1], st));
     ca.j = j;
     if (c->profiling) HIP_TRY(hipEventRecord(c->kev[4 * j + 2], st));
-    if (launch_code(ca, st) < 0) return set_err(-5, "code launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if ((p.ac ? launch_code(ca, st) : launch_code_golomb(ca, st)) < 0)
+      return set_err(-5, "code launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (c->profiling) HIP_TRY(hipEventRecord(c->kev[4 * j + 3], st));
   }
   c->last_nsegs = nsegs;

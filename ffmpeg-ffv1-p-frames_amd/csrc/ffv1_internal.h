@@ -81,6 +81,8 @@ struct CodeArgs {
   int64_t slice_cap;
   int64_t* slice_bytes;       // [batch frame][slice]
   int* status;                // [0] overflow count
+  int version;                // bitstream version (Golomb: v3 adds a 129/0 decision)
+  int coded_bits;             // "bits" of encode_line (8 for <=8-bit)
 };
 
 struct AssembleArgs {
@@ -97,6 +99,7 @@ struct AssembleArgs {
 
 int launch_symbols(const SymbolArgs& a, void* stream);
 int launch_code(const CodeArgs& a, void* stream);
+int launch_code_golomb(const CodeArgs& a, void* stream);
 int launch_assemble(const AssembleArgs& a, int nframes, void* stream);
 
 }  // namespace ffv1hip

@@ -221,6 +221,82 @@ __device__ __forceinline__ void store_row(const Lane& L, uint8_t* row) {
 constexpr int kCodeThreads = kWave;
 constexpr int kOpsetBytes = kOpSets * 32;
 
+// Replay renorm_encoder's pending byte / 0xFF-run logic (rangecoder.h:52-75)
+// over the recorded digits; returns the byte count (ff_rac_terminate's).
+__device__ __forceinline__ int64_t replay_digits(const uint32_t* digits, int64_t ndig, uint8_t* out,
+                                                 int64_t cap) {
+  uint32_t ow = 0;
+  int on = 0;
+  int64_t opos = 0;
+  int pending = -1, run = 0;
+  auto emit = [&](int b) {
+    ow |= (uint32_t)(b & 0xFF) << (on << 3);
+    if (++on == 4) {
+      if (opos + 4 <= cap) *reinterpret_cast<uint32_t*>(out + opos) = ow;
+      opos += 4;
+      ow = 0;
+      on = 0;
+    }
+  };
+  for (int64_t t = 0; t < ndig; t++) {
+    const uint32_t d = (digits[t >> 1] >> ((t & 1) << 4)) & 0x3FF;
+    const int qv = d & 0x1FF;
+    if (pending < 0) {
+      pending = qv;
+    } else if (d & 0x200) {
+      run++;
+    } else if (qv < 0x100) {
+      emit(pending);
+      for (; run; run--) emit(0xFF);
+      pending = qv;
+    } else {
+      emit(pending + 1);
+      for (; run; run--) emit(0x00);
+      pending = qv & 0xFF;
+    }
+  }
+  for (int k = 0; k < on; k++)
+    if (opos + k < cap) out[opos + k] = (uint8_t)(ow >> (k << 3));
+  return opos + on;
+}
+
+// ff_rac_terminate in digit form; returns the digit count.
+__device__ __forceinline__ int64_t finish_digits(Lane& L, uint32_t* digits) {
+  L.range = 0xFF;
+  L.low += 0xFF;
+  renorm_digit(L, digits);
+  L.range = 0xFF;
+  renorm_digit(L, digits);
+  const int odd = L.dn;
+  if (L.dn) {
+    if (L.dpos < L.dcap) digits[L.dpos] = L.dw;
+    L.dpos++;
+  }
+  return (int64_t)L.dpos * 2 - (odd ? 1 : 0);
+}
+
+// Key bit / in-band v0/v1 header / v3 slice header (per-lane op program).
+__device__ __forceinline__ void run_header_ops(const CodeArgs& a, Lane& L, uint32_t* digits,
+                                               uint8_t* os, int key, int slice, bool live,
+                                               const uint8_t* dtab, const uint8_t* ftab) {
+  for (int i = 0; i < kOpsetBytes; i++) os[i] = 128;
+  const int sel = key * a.nslices + slice;
+  const int n = live ? a.nops[sel] : 0;
+  const Op* ops = a.ops + (int64_t)sel * kMaxOps;
+  for (int q = 0; q < a.max_ops; q++) {
+    if (q < n) {
+      const Op op = ops[q];
+      const uint8_t* t = op.tab ? ftab : dtab;
+      uint8_t* st = os + op.set * 32;
+      if (op.kind == kOpBit)
+        put_lds(L, digits, st, op.value, t);
+      else
+        symbol_lds(L, digits, st, op.value, op.kind == kOpSymS, t);
+    }
+  }
+}
+
+
 __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t tabs[1024];
   __shared__ __attribute__((aligned(16))) uint8_t opsets[kCodeThreads * kOpsetBytes];
@@ -262,24 +338,7 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
   uint32_t* const digits = a.digits + chain * (a.digit_cap / 2);
 
   // header ops: key bit, in-band v0/v1 header, v3 slice header
-  {
-    uint8_t* os = opsets + lane * kOpsetBytes;
-    for (int i = 0; i < kOpsetBytes; i++) os[i] = 128;
-    const int sel = key * a.nslices + slice;
-    const int n = live ? a.nops[sel] : 0;
-    const Op* ops = a.ops + (int64_t)sel * kMaxOps;
-    for (int q = 0; q < a.max_ops; q++) {
-      if (q < n) {
-        const Op op = ops[q];
-        const uint8_t* t = op.tab ? ftab : dtab;
-        uint8_t* st = os + op.set * 32;
-        if (op.kind == kOpBit)
-          put_lds(L, digits, st, op.value, t);
-        else
-          symbol_lds(L, digits, st, op.value, op.kind == kOpSymS, t);
-      }
-    }
-  }
+  run_header_ops(a, L, digits, opsets + lane * kOpsetBytes, key, slice, live, dtab, ftab);
 
   const SliceGeom& g = a.geom[slice];
   const int64_t nsym = live ? g.nsym : 0;
@@ -351,64 +410,191 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
     // slice end: a 0 decision on state 129, then ff_rac_terminate
     rac_core(L, 129, 0);
     if (L.range < 0x100) renorm_digit(L, digits);
-    L.range = 0xFF;
-    L.low += 0xFF;
-    renorm_digit(L, digits);
-    L.range = 0xFF;
-    renorm_digit(L, digits);
-    const int odd = L.dn;
-    if (L.dn) {
-      if (L.dpos < L.dcap) digits[L.dpos] = L.dw;
-      L.dpos++;
-    }
-    const int64_t ndig = (int64_t)L.dpos * 2 - (odd ? 1 : 0);
+    const int64_t ndig = finish_digits(L, digits);
     int64_t nbytes = 0;
     if (L.dpos > L.dcap) {
       atomicAdd(a.status, 1);
     } else {
-      // replay renorm_encoder's pending byte / 0xFF-run logic over the digits
-      uint8_t* out = a.slice_out + ((int64_t)f * a.nslices + slice) * a.slice_cap;
-      const int64_t cap = a.slice_cap;
-      uint32_t ow = 0;
-      int on = 0;
-      int64_t opos = 0;
-      int pending = -1, run = 0;
-      auto emit = [&](int b) {
-        ow |= (uint32_t)(b & 0xFF) << (on << 3);
-        if (++on == 4) {
-          if (opos + 4 <= cap) *reinterpret_cast<uint32_t*>(out + opos) = ow;
-          opos += 4;
-          ow = 0;
-          on = 0;
-        }
-      };
-      for (int64_t t = 0; t < ndig; t++) {
-        const uint32_t d = (digits[t >> 1] >> ((t & 1) << 4)) & 0x3FF;
-        const int qv = d & 0x1FF;
-        if (pending < 0) {
-          pending = qv;
-        } else if (d & 0x200) {
-          run++;
-        } else if (qv < 0x100) {
-          emit(pending);
-          for (; run; run--) emit(0xFF);
-          pending = qv;
-        } else {
-          emit(pending + 1);
-          for (; run; run--) emit(0x00);
-          pending = qv & 0xFF;
-        }
-      }
-      for (int k = 0; k < on; k++)
-        if (opos + k < cap) out[opos + k] = (uint8_t)(ow >> (k << 3));
-      nbytes = opos + on;
-      if (nbytes > cap) atomicAdd(a.status, 1);
+      nbytes = replay_digits(digits, ndig, a.slice_out + ((int64_t)f * a.nslices + slice) * a.slice_cap,
+                             a.slice_cap);
+      if (nbytes > a.slice_cap) atomicAdd(a.status, 1);
     }
     a.slice_bytes[(int64_t)f * a.nslices + slice] = nbytes;
     if (a.j == seg.nframes - 1 && seg.save_states) {
       uint4* dst = reinterpret_cast<uint4*>(a.persist + (int64_t)slice * a.state_bytes);
       for (int64_t i = 0; i < a.state_bytes / 16; i++) dst[i] = reinterpret_cast<const uint4*>(table)[i];
     }
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// Kernel 2b: SIMT Golomb-Rice coder (coder=0; ffv1enc.c:240-370,
+// golomb.h:508-563, ffv1.h:192-224), one lane per (segment, slice) chain.
+// Per-context VlcState lives in the chain's table as one 8-byte record:
+// drift (int16) | error_sum (u16) << 16 | bias (int8) << 32 | count << 40.
+__constant__ uint8_t kLog2Run[41] = {
+    0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 5, 5, 6,
+    6, 7, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24};
+
+struct BitSink {
+  uint64_t acc;
+  int nacc;
+  int64_t pos;  // bytes written
+  uint8_t* out;
+  int64_t cap;
+  __device__ __forceinline__ void put(int n, uint32_t v) {  // put_bits: MSB first
+    acc = (acc << n) | v;
+    nacc += n;
+    while (nacc >= 8) {
+      nacc -= 8;
+      if (pos < cap) out[pos] = (uint8_t)(acc >> nacc);
+      pos++;
+    }
+    acc &= (1ull << nacc) - 1;
+  }
+  __device__ __forceinline__ void flush() {  // flush_put_bits: zero pad
+    if (nacc) put(8 - nacc, 0);
+  }
+};
+
+constexpr uint64_t kVlcInit = (uint64_t)4 << 16 | (uint64_t)1 << 40;
+
+__device__ __forceinline__ void vlc_put(BitSink& b, uint64_t& rec, int v, int bits) {
+  int drift = (int16_t)(rec & 0xFFFF);
+  int error_sum = (int)((rec >> 16) & 0xFFFF);
+  int bias = (int8_t)((rec >> 32) & 0xFF);
+  int count = (int)((rec >> 40) & 0xFF);
+  v = fold_bits(v - bias, bits);
+  // k = smallest k with count << k >= error_sum
+  int k = max(0, (31 - __builtin_clz((unsigned)max(error_sum, 1))) - (31 - __builtin_clz((unsigned)count)));
+  if ((count << k) < error_sum) k++;
+  const int code = v ^ ((2 * drift + count) >> 31);
+  const unsigned u = code >= 0 ? 2u * (unsigned)code : (unsigned)(-2 * code - 1);
+  const unsigned q = u >> k;
+  if (q < 12)
+    b.put((int)q + k + 1, (1u << k) + (u & ((1u << k) - 1)));
+  else
+    b.put(12 + bits, u - 11);
+  // update_vlc_state
+  error_sum = (error_sum + (v < 0 ? -v : v)) & 0xFFFF;
+  drift += v;
+  if (count == 128) {
+    count >>= 1;
+    drift >>= 1;
+    error_sum >>= 1;
+  }
+  count++;
+  if (drift <= -count) {
+    if (bias > -128) bias--;
+    drift += count;
+    if (drift <= -count) drift = -count + 1;
+  } else if (drift > 0) {
+    if (bias < 127) bias++;
+    drift -= count;
+    if (drift > 0) drift = 0;
+  }
+  rec = (uint64_t)(uint16_t)drift | (uint64_t)(uint16_t)error_sum << 16 |
+        (uint64_t)(uint8_t)bias << 32 | (uint64_t)(uint8_t)count << 40;
+}
+
+__global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t tabs[1024];
+  __shared__ __attribute__((aligned(16))) uint8_t opsets[kCodeThreads * kOpsetBytes];
+  for (int i = threadIdx.x; i < 1024; i += kCodeThreads) tabs[i] = a.tabs[i];
+  __syncthreads();
+  const int lane = threadIdx.x;
+  const int64_t chain = (int64_t)blockIdx.x * kCodeThreads + lane;
+  const int seg_i = (int)(chain / a.nslices), slice = (int)(chain % a.nslices);
+  bool live = seg_i < a.nsegs;
+  Segment seg{0, 0, 0, 0};
+  if (live) seg = a.segs[seg_i];
+  live = live && a.j < seg.nframes;
+  const int f = seg.first_frame + a.j;
+  const int key = live ? a.keyflags[f] : 0;
+  uint64_t* table = reinterpret_cast<uint64_t*>(a.tables + chain * a.state_bytes);
+  const int64_t nrec = a.state_bytes / 32;  // 2 * contexts records
+
+  if (live) {
+    if (a.j == 0 && seg.load_states) {
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(a.persist + (int64_t)slice * a.state_bytes);
+      for (int64_t i = 0; i < nrec; i++) table[i] = src[i];
+    } else if (key) {
+      for (int64_t i = 0; i < nrec; i++) table[i] = kVlcInit;  // ff_ffv1_clear_slice_state
+    }
+  }
+
+  // range-coded prefix: key bit / header / slice header, then (v3) a 0 on
+  // state 129 and ff_rac_terminate (ffv1enc.c:1173-1183)
+  Lane L;
+  L.low = 0;
+  L.range = 0xFF00;
+  L.dw = 0;
+  L.dn = 0;
+  L.dpos = 0;
+  L.dcap = (int)(a.digit_cap / 2);
+  uint32_t* const digits = a.digits + chain * (a.digit_cap / 2);
+  run_header_ops(a, L, digits, opsets + lane * kOpsetBytes, key, slice, live, tabs, tabs + 512);
+  if (!live) return;
+  if (a.version > 2) {
+    rac_core(L, 129, 0);
+    if (L.range < 0x100) renorm_digit(L, digits);
+  }
+  const int64_t ndig = finish_digits(L, digits);
+  uint8_t* out = a.slice_out + ((int64_t)f * a.nslices + slice) * a.slice_cap;
+  const int64_t ac_bytes = L.dpos > L.dcap ? a.slice_cap + 1 : replay_digits(digits, ndig, out, a.slice_cap);
+
+  BitSink b{0ull, 0, ac_bytes, out, a.slice_cap};
+  const SliceGeom& g = a.geom[slice];
+  const uint32_t* sp = a.sym + (int64_t)seg_i * a.frame_samples + g.sym_off;
+  const int bits = a.coded_bits;
+  int64_t idx = 0;
+  for (int p = 0; p < 3; p++) {
+    const int pw = g.pw[p], ph = g.ph[p];
+    int run_index = 0;  // per plane (ffv1enc.c:379)
+    for (int y = 0; y < ph; y++) {
+      int run_count = 0, run_mode = 0;
+      for (int x = 0; x < pw; x++, idx++) {
+        const uint32_t sv = sp[idx];
+        const int row = (int)(sv >> 16);
+        const int ctx = p ? row - a.state_bytes / 64 : row;  // context inside its plane
+        int diff = (int16_t)(sv & 0xFFFF);
+        if (ctx == 0) run_mode = 1;
+        if (run_mode) {
+          if (diff) {
+            while (run_count >= (1 << kLog2Run[run_index])) {
+              run_count -= 1 << kLog2Run[run_index];
+              run_index++;
+              b.put(1, 1);
+            }
+            b.put(1 + kLog2Run[run_index], run_count);
+            if (run_index) run_index--;
+            run_count = 0;
+            run_mode = 0;
+            if (diff > 0) diff--;
+          } else {
+            run_count++;
+          }
+        }
+        if (!run_mode) vlc_put(b, table[row], diff, bits);
+      }
+      if (run_mode) {
+        while (run_count >= (1 << kLog2Run[run_index])) {
+          run_count -= 1 << kLog2Run[run_index];
+          run_index++;
+          b.put(1, 1);
+        }
+        if (run_count) b.put(1, 1);
+      }
+    }
+  }
+  b.flush();
+  const int64_t nbytes = b.pos;
+  if (nbytes > a.slice_cap) atomicAdd(a.status, 1);
+  a.slice_bytes[(int64_t)f * a.nslices + slice] = nbytes;
+  if (a.j == seg.nframes - 1 && seg.save_states) {
+    uint64_t* dst = reinterpret_cast<uint64_t*>(a.persist + (int64_t)slice * a.state_bytes);
+    for (int64_t i = 0; i < nrec; i++) dst[i] = table[i];
   }
 }
 
@@ -513,6 +699,13 @@ int launch_code(const CodeArgs& a, void* stream) {
   const int64_t chains = (int64_t)a.nsegs * a.nslices;
   dim3 grid((unsigned)((chains + kCodeThreads - 1) / kCodeThreads)), block(kCodeThreads);
   hipLaunchKernelGGL(ffv1_code, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_code_golomb(const CodeArgs& a, void* stream) {
+  const int64_t chains = (int64_t)a.nsegs * a.nslices;
+  dim3 grid((unsigned)((chains + kCodeThreads - 1) / kCodeThreads)), block(kCodeThreads);
+  hipLaunchKernelGGL(ffv1_code_golomb, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -114,4 +114,11 @@ PARITY_STREAMS = [
     Stream("gray16", 96, 64, "gray16", 3, slices=4, gop_size=2, source="random"),
     Stream("grid16x16", 960, 544, "yuv420p10", 3, slices=256, gop_size=2, source="d2", depth=10,
            allow_large_grid=True, extra={"grid": (16, 16)}),
+    # Golomb-Rice (coder=0): v0 single slice with in-band header, v3 P-frames,
+    # context model 1, and the odd 34x34 geometry of FATE vsynth3
+    Stream("golomb_v0_cif_intra", 352, 288, "yuv420p", 3, coder=0, gop_size=1),
+    Stream("golomb_v3_pframes", 352, 288, "yuv420p", 7, slices=4, coder=0, gop_size=4),
+    Stream("golomb_ctx1", 176, 144, "yuv422p", 4, slices=4, coder=0, context=1, gop_size=3,
+           source="random"),
+    Stream("golomb_vsynth3", 34, 34, "yuv420p", 13, slices=4, coder=0, gop_size=12),
 ]

@@ -89,9 +89,10 @@ def test_no_silent_cpu_fallback_without_gpu():
         HipEncoder(configure(352, 288, "yuv420p", coder=1, slices=4), 0, 2)
 
 
-def test_golomb_is_reported_not_faked():
+def test_unsupported_parameters_are_refused():
     from ffv1hip import configure, HipEncoder, FFV1Error
-    p = configure(352, 288, "yuv420p", coder=0)
+    p = configure(352, 288, "yuv420p", coder=1, slices=4)
+    p.version = 2  # experimental in the reference (ffv1enc.c:703-706)
     with pytest.raises(FFV1Error) as e:
         HipEncoder(p, 0, 1)
-    assert e.value.code in (-38, -5)
+    assert e.value.code == -38

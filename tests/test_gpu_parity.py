@@ -64,6 +64,19 @@ def _pinned(name):
     return next(p for p in load_golden("known_answers.json")["streams"] if p["name"] == name)
 
 
+def test_config1_cif_golomb_known_answer():
+    pin = _pinned("config1_cif_yuv420p_coder0_g1")
+    s = Stream("c1", 352, 288, "yuv420p", pin["frames"], coder=0, gop_size=1)
+    ex, pkts = hip_encode(s, list(s.frames()), batch=30)
+    assert ex == b""
+    for i, size in pin["frame_sizes"].items():
+        assert len(pkts[int(i)][0]) == size
+    h = hashlib.md5()
+    for p, _ in pkts:
+        h.update(p)
+    assert h.hexdigest() == pin["stream_md5"]
+
+
 def test_config2_1080p_intra_known_answer():
     pin = _pinned("config2_1080p_yuv420p_coder1_slices24_g1")
     s = Stream("c2", 1920, 1080, "yuv420p", pin["frames"], slices=24, gop_size=1)

@@ -1,0 +1,88 @@
+"""N>1 path on CPU: GOP-sharded encoding over torch.distributed (gloo, world 2).
+
+Each rank encodes its round-robin share of GOPs with its own encoder and the
+packets are gathered to rank 0; the gathered stream must be byte-identical to
+a single-process encode of the whole stream (GOP independence, ffv1enc.c:
+1171-1172).  The encoder here is the CPU oracle (no GPU in this container);
+the GPU bench uses the same sharding with the HIP encoder per rank.
+"""
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+W, H, N, GOP = 176, 144, 11, 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _frames():
+    from ffv1hip import synth
+    return list(synth.videogen_frames(W, H, N, depth=10))
+
+
+def _oracle_encoder():
+    from oracle import oracle
+
+    class Enc:
+        def __init__(self):
+            self.e = oracle.Encoder(oracle.configure(W, H, "yuv420p10", slices=4, coder=1,
+                                                     gop_size=GOP))
+
+        def encode(self, frames):
+            return [self.e.encode(f) for f in frames]
+
+    return Enc()
+
+
+def _worker(rank, world, port, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "ffmpeg-ffv1-p-frames_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from ffv1hip import parallel
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    frames = _frames()
+    mine = parallel.shard_gops(N, GOP, world, rank)
+    local = parallel.encode_shard(_oracle_encoder, lambda i: frames[i], mine)
+    got = parallel.gather_packets(local, N, dist, rank, world)
+    if rank == 0:
+        q.put(got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gop_ranges_cover_stream_once():
+    from ffv1hip import parallel
+    for n, g, w in [(11, 3, 2), (24, 12, 8), (5, 1, 3), (7, 12, 4)]:
+        owned = sorted(r for k in range(w) for r in parallel.shard_gops(n, g, w, k))
+        assert owned == parallel.gop_ranges(n, g)
+        assert sum(e - s for s, e in owned) == n
+
+
+def test_gop_sharded_gloo_world2_matches_single_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    frames = _frames()
+    enc = _oracle_encoder()
+    ref = enc.encode(frames)
+    assert [k for _, k in got] == [i % GOP == 0 for i in range(N)]
+    assert got == ref
