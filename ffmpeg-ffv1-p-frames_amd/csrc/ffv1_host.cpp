@@ -478,7 +478,7 @@ static int alloc_device(ffv1hip_ctx* c) {
   const size_t chains = size_t(c->max_slots) * c->nslices;
   HIP_TRY(hipMalloc(&c->d_tables, state_bytes * chains));
   HIP_TRY(hipMalloc(&c->d_sym, sizeof(uint32_t) * size_t(c->frame_samples) * c->max_slots));
-  HIP_TRY(hipMalloc(&c->d_digits, sizeof(uint32_t) * size_t(c->digit_cap / 2) * chains));
+  HIP_TRY(hipMalloc(&c->d_digits, sizeof(uint16_t) * size_t(c->digit_cap) * chains));
   HIP_TRY(hipMalloc(&c->d_geom, sizeof(SliceGeom) * c->nslices));
   HIP_TRY(hipMemcpy(c->d_geom, c->geom.data(), sizeof(SliceGeom) * c->nslices, hipMemcpyHostToDevice));
   HIP_TRY(hipMalloc(&c->d_slot_frames, sizeof(int) * size_t(c->max_slots) * (nb + 1)));

@@ -106,10 +106,8 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
 struct Lane {
   int low, range;
   uint32_t r0, r1, r2, r3, r4, r5, r6, r7;  // states of the current context row (byte k = slot k)
-  uint32_t dw;         // digit word being filled (2 x 16-bit digits)
-  int dn;              // digits in dw
-  int dpos;            // dwords of digits stored
-  int dcap;            // dword capacity
+  int dpos;            // digits stored
+  int dcap;            // digit capacity
 
   template <int D>
   __device__ __forceinline__ uint32_t& w() {
@@ -128,15 +126,17 @@ struct Lane {
 // Renormalisation (rangecoder.h:52-75) deferred: record low's top byte with
 // its carry (bit 8) and whether the reference would defer it as an 0xFF run
 // (bit 9: 0xFF00 < low < 0x10000), then shift.
-__device__ __forceinline__ void renorm_digit(Lane& L, uint32_t* digits) {
+#ifndef FFV1_ABLATE
+#define FFV1_ABLATE 0  // timing-only experiment builds (tools/ablate.sh); 0 in the product
+#endif
+
+__device__ __forceinline__ void renorm_digit(Lane& L, uint16_t* digits) {
   const uint32_t d = ((uint32_t)L.low >> 8) | ((L.low > 0xFF00 && L.low < 0x10000) ? 0x200u : 0u);
-  L.dw |= d << (L.dn << 4);
-  if (++L.dn == 2) {
-    if (L.dpos < L.dcap) digits[L.dpos] = L.dw;
-    L.dpos++;
-    L.dw = 0;
-    L.dn = 0;
-  }
+  if (!(FFV1_ABLATE & 1))
+    digits[min(L.dpos, L.dcap - 1)] = (uint16_t)d;  // overflow is reported, never written past
+  else
+    asm volatile("" ::"v"(d));
+  L.dpos++;
   L.low = (L.low & 0xFF) << 8;
   L.range <<= 8;
 }
@@ -150,7 +150,7 @@ __device__ __forceinline__ void rac_core(Lane& L, int s, int bit) {
 
 // One decision on the static slot K of the current row.
 template <int K>
-__device__ __forceinline__ void step(Lane& L, uint32_t* digits, bool act, int bit, const uint8_t* tab) {
+__device__ __forceinline__ void step(Lane& L, uint16_t* digits, bool act, int bit, const uint8_t* tab) {
   if (act) {
     constexpr int D = K >> 2, SH = (K & 3) * 8;
     const uint32_t w = L.w<D>();
@@ -162,8 +162,34 @@ __device__ __forceinline__ void step(Lane& L, uint32_t* digits, bool act, int bi
   }
 }
 
+// Batched form (no slot repeats inside the symbol, e <= 9): the decision
+// reads the old state and issues its successor lookup; the caller inserts
+// all successors after the last decision, so no LDS latency sits between
+// two decisions.
+template <int K>
+__device__ __forceinline__ uint32_t step_b(Lane& L, uint16_t* digits, bool act, int bit,
+                                           const uint8_t* tab) {
+  constexpr int D = K >> 2, SH = (K & 3) * 8;
+  const int s = (L.w<D>() >> SH) & 0xFF;
+  const int r1 = (L.range * s) >> 8;
+  const int r0 = L.range - r1;
+  const int nl = L.low + (bit ? r0 : 0);
+  const int nr = bit ? r1 : r0;
+  L.low = act ? nl : L.low;
+  L.range = act ? nr : L.range;
+  if (act && L.range < 0x100) renorm_digit(L, digits);
+  return tab[(bit << 8) | s];
+}
+
+template <int K>
+__device__ __forceinline__ void insert_b(Lane& L, bool act, uint32_t ns) {
+  constexpr int D = K >> 2, SH = (K & 3) * 8;
+  const uint32_t w = L.w<D>();
+  L.w<D>() = act ? ((w & ~(0xFFu << SH)) | (ns << SH)) : w;
+}
+
 // The sign decision's slot 11 + min(e,10) varies per lane (dwords 2..5).
-__device__ __forceinline__ void sign_step(Lane& L, uint32_t* digits, bool act, int m, int bit,
+__device__ __forceinline__ void sign_step(Lane& L, uint16_t* digits, bool act, int m, int bit,
                                           const uint8_t* tab) {
   if (act) {
     const int k = 11 + m, d = k >> 2, sh = (k & 3) * 8;
@@ -190,7 +216,7 @@ __device__ __forceinline__ int wave_max(int v) {
 }
 
 // Generic decision on a per-lane LDS state (header ops; rare).
-__device__ __forceinline__ void put_lds(Lane& L, uint32_t* digits, uint8_t* st, int bit,
+__device__ __forceinline__ void put_lds(Lane& L, uint16_t* digits, uint8_t* st, int bit,
                                         const uint8_t* tab) {
   const int s = *st;
   rac_core(L, s, bit);
@@ -198,7 +224,7 @@ __device__ __forceinline__ void put_lds(Lane& L, uint32_t* digits, uint8_t* st, 
   if (L.range < 0x100) renorm_digit(L, digits);
 }
 
-__device__ __forceinline__ void symbol_lds(Lane& L, uint32_t* dg, uint8_t* st, int v, bool sgn,
+__device__ __forceinline__ void symbol_lds(Lane& L, uint16_t* dg, uint8_t* st, int v, bool sgn,
                                            const uint8_t* tab) {
   if (v == 0) {
     put_lds(L, dg, st, 1, tab);
@@ -223,7 +249,7 @@ constexpr int kOpsetBytes = kOpSets * 32;
 
 // Replay renorm_encoder's pending byte / 0xFF-run logic (rangecoder.h:52-75)
 // over the recorded digits; returns the byte count (ff_rac_terminate's).
-__device__ __forceinline__ int64_t replay_digits(const uint32_t* digits, int64_t ndig, uint8_t* out,
+__device__ __forceinline__ int64_t replay_digits(const uint16_t* digits, int64_t ndig, uint8_t* out,
                                                  int64_t cap) {
   uint32_t ow = 0;
   int on = 0;
@@ -239,7 +265,7 @@ __device__ __forceinline__ int64_t replay_digits(const uint32_t* digits, int64_t
     }
   };
   for (int64_t t = 0; t < ndig; t++) {
-    const uint32_t d = (digits[t >> 1] >> ((t & 1) << 4)) & 0x3FF;
+    const uint32_t d = digits[t];
     const int qv = d & 0x1FF;
     if (pending < 0) {
       pending = qv;
@@ -261,22 +287,17 @@ __device__ __forceinline__ int64_t replay_digits(const uint32_t* digits, int64_t
 }
 
 // ff_rac_terminate in digit form; returns the digit count.
-__device__ __forceinline__ int64_t finish_digits(Lane& L, uint32_t* digits) {
+__device__ __forceinline__ int64_t finish_digits(Lane& L, uint16_t* digits) {
   L.range = 0xFF;
   L.low += 0xFF;
   renorm_digit(L, digits);
   L.range = 0xFF;
   renorm_digit(L, digits);
-  const int odd = L.dn;
-  if (L.dn) {
-    if (L.dpos < L.dcap) digits[L.dpos] = L.dw;
-    L.dpos++;
-  }
-  return (int64_t)L.dpos * 2 - (odd ? 1 : 0);
+  return L.dpos;
 }
 
 // Key bit / in-band v0/v1 header / v3 slice header (per-lane op program).
-__device__ __forceinline__ void run_header_ops(const CodeArgs& a, Lane& L, uint32_t* digits,
+__device__ __forceinline__ void run_header_ops(const CodeArgs& a, Lane& L, uint16_t* digits,
                                                uint8_t* os, int key, int slice, bool live,
                                                const uint8_t* dtab, const uint8_t* ftab) {
   for (int i = 0; i < kOpsetBytes; i++) os[i] = 128;
@@ -330,12 +351,10 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
   Lane L;
   L.low = 0;
   L.range = 0xFF00;
-  L.dw = 0;
-  L.dn = 0;
   L.dpos = 0;
-  L.dcap = (int)(a.digit_cap / 2);
+  L.dcap = (int)a.digit_cap;
   L.r0 = L.r1 = L.r2 = L.r3 = L.r4 = L.r5 = L.r6 = L.r7 = 0;
-  uint32_t* const digits = a.digits + chain * (a.digit_cap / 2);
+  uint16_t* const digits = reinterpret_cast<uint16_t*>(a.digits) + chain * a.digit_cap;
 
   // header ops: key bit, in-band v0/v1 header, v3 slice header
   run_header_ops(a, L, digits, opsets + lane * kOpsetBytes, key, slice, live, dtab, ftab);
@@ -357,14 +376,14 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
     const int q = (int)(i & 3);
     if (q == 0 && i > 0) {
       G = GN;
-      if (act && i + 4 < nsym) GN = sp[(i >> 2) + 1];
+      if (act && i + 4 < nsym) GN = sp[(FFV1_ABLATE & 2) ? ((i >> 2) & 15) + 1 : (i >> 2) + 1];
     }
     const uint32_t sv = q == 0 ? G.x : q == 1 ? G.y : q == 2 ? G.z : G.w;
     const uint32_t sn = q == 0 ? G.y : q == 1 ? G.z : q == 2 ? G.w : GN.x;
     const int row = (int)(sv >> 16);
     const int v = (int16_t)(sv & 0xFFFF);
     if (act && row != cur) {  // context switch: write back, take the prefetch
-      if (cur >= 0) store_row(L, table + (int64_t)cur * 32);
+      if (cur >= 0 && !(FFV1_ABLATE & 4)) store_row(L, table + (int64_t)cur * 32);
       uint4 ra = PFa, rb = PFb;
       if (row != pfrow) {
         ra = reinterpret_cast<const uint4*>(table + (int64_t)row * 32)[0];
@@ -388,9 +407,53 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
     const bool nz = act && v != 0;
     const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
     const int e = nz ? 31 - __builtin_clz(mag) : -1;
-    step<0>(L, digits, act, v == 0, ftab);
     const int emax = wave_max(e);
-    if (emax >= 0) {
+    if (emax < 10) {
+      // batched: every decision reads the symbol's starting states
+      const uint32_t n0 = step_b<0>(L, digits, act, v == 0, ftab);
+      uint32_t nu[10], nm[10], nsg = 0;
+      const int sgk = 11 + max(e, 0), sgd = sgk >> 2, sgsh = (sgk & 3) * 8;
+      const uint32_t m2 = 0u - (uint32_t)(sgd == 2), m3 = 0u - (uint32_t)(sgd == 3);
+      const uint32_t m4 = 0u - (uint32_t)(sgd == 4), m5 = 0u - (uint32_t)(sgd == 5);
+      if (emax >= 0) {
+#define UNARY(I) nu[I] = (I <= emax) ? step_b<1 + I>(L, digits, nz && I <= e, I < e, ftab) : 0u;
+        UNARY(0) UNARY(1) UNARY(2) UNARY(3) UNARY(4) UNARY(5) UNARY(6) UNARY(7) UNARY(8) UNARY(9)
+#undef UNARY
+#define MANT(I) nm[I] = (I < emax) ? step_b<22 + I>(L, digits, nz && I < e, (mag >> I) & 1, ftab) : 0u;
+        MANT(9) MANT(8) MANT(7) MANT(6) MANT(5) MANT(4) MANT(3) MANT(2) MANT(1) MANT(0)
+#undef MANT
+        // sign: per-lane slot 11 + e, read from the starting row
+        const uint32_t w = (L.r2 & m2) | (L.r3 & m3) | (L.r4 & m4) | (L.r5 & m5);
+        const int ss = (w >> sgsh) & 0xFF;
+        const int bit = v < 0;
+        const int r1 = (L.range * ss) >> 8;
+        const int r0 = L.range - r1;
+        const int nl = L.low + (bit ? r0 : 0);
+        const int nr = bit ? r1 : r0;
+        L.low = nz ? nl : L.low;
+        L.range = nz ? nr : L.range;
+        if (nz && L.range < 0x100) renorm_digit(L, digits);
+        nsg = ftab[(bit << 8) | ss];
+      }
+      // successor states
+      insert_b<0>(L, act, n0);
+      if (emax >= 0) {
+#define UNARY(I) if (I <= emax) insert_b<1 + I>(L, nz && I <= e, nu[I]);
+        UNARY(0) UNARY(1) UNARY(2) UNARY(3) UNARY(4) UNARY(5) UNARY(6) UNARY(7) UNARY(8) UNARY(9)
+#undef UNARY
+#define MANT(I) if (I < emax) insert_b<22 + I>(L, nz && I < e, nm[I]);
+        MANT(9) MANT(8) MANT(7) MANT(6) MANT(5) MANT(4) MANT(3) MANT(2) MANT(1) MANT(0)
+#undef MANT
+        const uint32_t msk = ~(0xFFu << sgsh), val = nsg << sgsh;
+        const uint32_t g2 = nz ? m2 : 0u, g3 = nz ? m3 : 0u, g4 = nz ? m4 : 0u, g5 = nz ? m5 : 0u;
+        L.r2 = (((L.r2 & msk) | val) & g2) | (L.r2 & ~g2);
+        L.r3 = (((L.r3 & msk) | val) & g3) | (L.r3 & ~g3);
+        L.r4 = (((L.r4 & msk) | val) & g4) | (L.r4 & ~g4);
+        L.r5 = (((L.r5 & msk) | val) & g5) | (L.r5 & ~g5);
+      }
+    } else {
+      // e >= 10 somewhere in the wave (slots 10 / 31 repeat): serial updates
+    step<0>(L, digits, act, v == 0, ftab);
       // unary exponent: slots 1..10, 1-bits then the terminating 0
 #define UNARY(I) if (I <= emax) step<1 + I>(L, digits, nz && I <= e, I < e, ftab);
       UNARY(0) UNARY(1) UNARY(2) UNARY(3) UNARY(4) UNARY(5) UNARY(6) UNARY(7) UNARY(8) UNARY(9)
@@ -529,11 +592,9 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
   Lane L;
   L.low = 0;
   L.range = 0xFF00;
-  L.dw = 0;
-  L.dn = 0;
   L.dpos = 0;
-  L.dcap = (int)(a.digit_cap / 2);
-  uint32_t* const digits = a.digits + chain * (a.digit_cap / 2);
+  L.dcap = (int)a.digit_cap;
+  uint16_t* const digits = reinterpret_cast<uint16_t*>(a.digits) + chain * a.digit_cap;
   run_header_ops(a, L, digits, opsets + lane * kOpsetBytes, key, slice, live, tabs, tabs + 512);
   if (!live) return;
   if (a.version > 2) {

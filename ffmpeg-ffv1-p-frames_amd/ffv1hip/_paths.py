@@ -19,7 +19,7 @@ def synth_lib() -> str:
 
 
 def hip_lib() -> str:
-    p = os.path.join(LIB_DIR, "libffv1hip.so")
+    p = os.environ.get("FFV1HIP_LIB") or os.path.join(LIB_DIR, "libffv1hip.so")
     if not os.path.exists(p):
         raise FileNotFoundError(
             f"{p} missing: the HIP encoder is not built (run `python ffmpeg-ffv1-p-frames_amd/build.py`)")

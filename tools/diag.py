@@ -34,11 +34,12 @@ def run(w, h, slices, nframes, gop, label, reps=2):
                       "bytes": sum(len(x) for x, _ in pk)}), flush=True)
     enc.close()
 
-run(480, 270, 1, 1, 12, "1chain_480x270_1frame")
-run(480, 270, 1, 4, 12, "1chain_480x270_4frames")
-run(960, 540, 4, 1, 12, "4chains")
-run(3840, 2160, 64, 1, 12, "64chains_4k_1frame")
-run(3840, 2160, 64, 12, 12, "64chains_4k_12frames")
-run(3840, 2160, 64, 48, 12, "256chains_4k_48frames")
-run(3840, 2160, 64, 96, 12, "512chains_4k_96frames")
-run(3840, 2160, 64, 144, 12, "768chains_4k_144frames", reps=1)
+if __name__ == "__main__":
+  run(480, 270, 1, 1, 12, "1chain_480x270_1frame")
+  run(480, 270, 1, 4, 12, "1chain_480x270_4frames")
+  run(960, 540, 4, 1, 12, "4chains")
+  run(3840, 2160, 64, 1, 12, "64chains_4k_1frame")
+  run(3840, 2160, 64, 12, 12, "64chains_4k_12frames")
+  run(3840, 2160, 64, 48, 12, "256chains_4k_48frames")
+  run(3840, 2160, 64, 96, 12, "512chains_4k_96frames")
+  run(3840, 2160, 64, 144, 12, "768chains_4k_144frames", reps=1)
