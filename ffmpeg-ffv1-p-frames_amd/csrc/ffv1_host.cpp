@@ -217,8 +217,8 @@ struct ffv1hip_ctx {
   int64_t picture_number = 0;
   bool have_states = false;  // persistent states valid (a frame was coded)
   int max_slots = 0;          // segments (= frame slots) per call
+  bool frames_mode = false;   // states walk + frame-parallel coder (range coder, LDS-sized tables)
   int64_t frame_samples = 0;  // symbols of one frame (each slice padded to 4)
-  int64_t digit_cap = 0;      // renorm digits per chain
   int max_ops = 0;
   std::vector<SliceGeom> geom;
   // device buffers
@@ -235,8 +235,8 @@ struct ffv1hip_ctx {
   int64_t* d_packet_size = nullptr;
   uint8_t* d_persist = nullptr;
   uint8_t* d_tables = nullptr;   // [slot][slice][2][contexts][32]
-  uint32_t* d_sym = nullptr;     // [slot][frame_samples]
-  uint32_t* d_digits = nullptr;  // [slot][slice][digit_cap/2]
+  uint32_t* d_sym = nullptr;     // [slot][frame_samples]; frames mode: [batch frame][frame_samples]
+  uint8_t* d_snap = nullptr;     // frames mode: [batch frame][slice][state_bytes], grid-padded
   SliceGeom* d_geom = nullptr;
   int* d_slot_frames = nullptr;  // [j][slot]
   int* d_status = nullptr;
@@ -246,7 +246,8 @@ struct ffv1hip_ctx {
   bool profiling = false;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> kev;  // [2 * launches]: start/stop per kernel launch
-  std::vector<int> kev_kind;    // 0 symbols, 1 code
+  std::vector<int> kev_kind;    // per launch: 0 symbols, 1 code, 2 states
+  int nkev = 0;
   int last_nsegs = 0;
 };
 
@@ -439,7 +440,7 @@ static void build_ops(ffv1hip_ctx* c) {
 static void free_device(ffv1hip_ctx* c) {
   void* ptrs[] = {c->d_frames, c->d_qt, c->d_tabs, c->d_ops, c->d_nops, c->d_segs, c->d_keys,
                   c->d_slice_out, c->d_slice_bytes, c->d_packets, c->d_packet_size, c->d_persist,
-                  c->d_tables, c->d_sym, c->d_digits, c->d_geom, c->d_slot_frames, c->d_status};
+                  c->d_tables, c->d_sym, c->d_snap, c->d_geom, c->d_slot_frames, c->d_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (hipEvent_t& e : c->ev)
@@ -475,10 +476,16 @@ static int alloc_device(ffv1hip_ctx* c) {
   HIP_TRY(hipMalloc(&c->d_packet_size, sizeof(int64_t) * nb));
   const size_t state_bytes = size_t(2) * c->contexts * 32;
   HIP_TRY(hipMalloc(&c->d_persist, state_bytes * c->nslices));
-  const size_t chains = size_t(c->max_slots) * c->nslices;
-  HIP_TRY(hipMalloc(&c->d_tables, state_bytes * chains));
-  HIP_TRY(hipMalloc(&c->d_sym, sizeof(uint32_t) * size_t(c->frame_samples) * c->max_slots));
-  HIP_TRY(hipMalloc(&c->d_digits, sizeof(uint16_t) * size_t(c->digit_cap) * chains));
+  // the coder grid is padded to whole waves and idle lanes touch their own table
+  if (c->frames_mode) {
+    const size_t chains = (size_t(nb) * c->nslices + 63) & ~size_t(63);
+    HIP_TRY(hipMalloc(&c->d_snap, state_bytes * chains));
+    HIP_TRY(hipMalloc(&c->d_sym, sizeof(uint32_t) * size_t(c->frame_samples) * nb));
+  } else {
+    const size_t chains = (size_t(c->max_slots) * c->nslices + 63) & ~size_t(63);
+    HIP_TRY(hipMalloc(&c->d_tables, state_bytes * chains));
+    HIP_TRY(hipMalloc(&c->d_sym, sizeof(uint32_t) * size_t(c->frame_samples) * c->max_slots));
+  }
   HIP_TRY(hipMalloc(&c->d_geom, sizeof(SliceGeom) * c->nslices));
   HIP_TRY(hipMemcpy(c->d_geom, c->geom.data(), sizeof(SliceGeom) * c->nslices, hipMemcpyHostToDevice));
   HIP_TRY(hipMalloc(&c->d_slot_frames, sizeof(int) * size_t(c->max_slots) * (nb + 1)));
@@ -548,13 +555,20 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
   // Slice byte budget: 4 bytes per coded sample (+4 KiB); real content codes
   // below 2 bytes per 16-bit sample.  Exceeding it reports -ENOSPC.
   c->slice_cap = ((max_nsym * 4 + 4096) + 255) & ~int64_t(255);
-  c->digit_cap = c->slice_cap + 16;
   c->packet_stride = ((c->slice_cap + 16) * c->nslices + 255) & ~int64_t(255);
   // frame slots (segments) per call: one per GOP touched by the batch
   c->max_slots = p.gop_size > 1 ? std::min(max_batch_frames, (max_batch_frames + p.gop_size - 2) / p.gop_size + 1)
                                 : max_batch_frames;
   c->max_ops = 0;
   for (int v : c->nops) c->max_ops = std::max(c->max_ops, v);
+  // Range coder with a table that fits the states walk's LDS: code all frames
+  // of a batch in parallel from per-frame state snapshots.  FFV1HIP_CODER=chain
+  // keeps the chained per-GOP coder (a test hook: both must give equal bytes).
+  {
+    const char* mode = std::getenv("FFV1HIP_CODER");
+    const int64_t lds = int64_t(2) * c->contexts * 32 + 512 + 64;
+    c->frames_mode = p.ac && lds <= kStateLdsMax && !(mode && std::strcmp(mode, "chain") == 0);
+  }
   int rc = alloc_device(c);
   if (rc < 0) {
     free_device(c);
@@ -659,8 +673,6 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   ca.state_bytes = int64_t(2) * c->contexts * 32;
   ca.tables = c->d_tables;
   ca.persist = c->d_persist;
-  ca.digits = c->d_digits;
-  ca.digit_cap = c->digit_cap;
   ca.slice_out = c->d_slice_out;
   ca.slice_cap = c->slice_cap;
   ca.slice_bytes = c->d_slice_bytes;
@@ -668,27 +680,63 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   ca.version = p.version;
   ca.coded_bits = p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample;
 
-  if (c->profiling) {
-    HIP_TRY(hipEventRecord(c->ev[0], st));
-    while (c->kev.size() < size_t(4) * maxlen) {
-      hipEvent_t e;
-      HIP_TRY(hipEventCreate(&e));
-      c->kev.push_back(e);
+  c->nkev = 0;
+  if (c->profiling) HIP_TRY(hipEventRecord(c->ev[0], st));
+  // brackets one launch with events when profiling (kind: 0 symbols, 1 code, 2 states)
+  auto timed = [&](int kind, auto&& launch) -> int {
+    if (c->profiling) {
+      while (c->kev.size() < size_t(2) * (c->nkev + 1)) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return -1;
+        c->kev.push_back(e);
+      }
+      if (c->kev_kind.size() < size_t(c->nkev + 1)) c->kev_kind.resize(c->nkev + 1);
+      c->kev_kind[c->nkev] = kind;
+      if (hipEventRecord(c->kev[2 * c->nkev], st) != hipSuccess) return -1;
     }
-    c->kev_kind.assign(size_t(2) * maxlen, 0);
-  }
-  for (int j = 0; j < maxlen; j++) {
-    sa.frame_of_slot = c->d_slot_frames + size_t(j) * nsegs;
-    if (c->profiling) HIP_TRY(hipEventRecord(c->kev[4 * j + 0], st));
-    if (launch_symbols(sa, st) < 0) return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
-    if (c->profiling) HIP_TRY(hipEventRecord(c->kev[4 * j + 1], st));
-    ca.j = j;
-    if (c->profiling) HIP_TRY(hipEventRecord(c->kev[4 * j + 2], st));
-    if ((p.ac ? launch_code(ca, st) : launch_code_golomb(ca, st)) < 0)
+    const int rc = launch();
+    if (c->profiling) {
+      if (hipEventRecord(c->kev[2 * c->nkev + 1], st) != hipSuccess) return -1;
+      c->nkev++;
+    }
+    return rc;
+  };
+  if (c->frames_mode) {
+    // symbols of every frame, the states walk, then all (frame, slice) streams at once
+    std::vector<int> ident(n);
+    for (int i = 0; i < n; i++) ident[i] = i;
+    HIP_TRY(hipMemcpyAsync(c->d_slot_frames, ident.data(), sizeof(int) * n, hipMemcpyHostToDevice, st));
+    sa.frame_of_slot = c->d_slot_frames;
+    sa.nslots = n;
+    if (timed(0, [&] { return launch_symbols(sa, st); }) < 0)
+      return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
+    StateArgs wa{};
+    wa.sym = c->d_sym;
+    wa.frame_samples = c->frame_samples;
+    wa.geom = c->d_geom;
+    wa.nslices = c->nslices;
+    wa.segs = c->d_segs;
+    wa.ftab = c->d_tabs + 512;
+    wa.state_bytes = ca.state_bytes;
+    wa.persist = c->d_persist;
+    wa.snap = c->d_snap;
+    if (timed(2, [&] { return launch_states(wa, nsegs, st); }) < 0)
+      return set_err(-5, "states launch failed: %s", hipGetErrorString(hipGetLastError()));
+    ca.snap = c->d_snap;
+    ca.nframes = n;
+    if (timed(1, [&] { return launch_code_frames(ca, st); }) < 0)
       return set_err(-5, "code launch failed: %s", hipGetErrorString(hipGetLastError()));
-    if (c->profiling) HIP_TRY(hipEventRecord(c->kev[4 * j + 3], st));
+  } else {
+    for (int j = 0; j < maxlen; j++) {
+      sa.frame_of_slot = c->d_slot_frames + size_t(j) * nsegs;
+      if (timed(0, [&] { return launch_symbols(sa, st); }) < 0)
+        return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
+      ca.j = j;
+      if (timed(1, [&] { return p.ac ? launch_code(ca, st) : launch_code_golomb(ca, st); }) < 0)
+        return set_err(-5, "code launch failed: %s", hipGetErrorString(hipGetLastError()));
+    }
   }
-  c->last_nsegs = nsegs;
+  c->last_nsegs = c->frames_mode ? n : nsegs;
 
   AssembleArgs b{};
   b.slice_out = c->d_slice_out;
@@ -810,15 +858,15 @@ int ffv1hip_last_kernel_stats(ffv1hip_ctx* c, ffv1hip_kernel_stats* out) {
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipEventSynchronize(c->ev[2]));
   ffv1hip_kernel_stats s{};
-  const int n = int(c->kev_kind.size() / 2);
-  for (int j = 0; j < n; j++) {
-    float a = 0.f, b = 0.f;
-    HIP_TRY(hipEventElapsedTime(&a, c->kev[4 * j + 0], c->kev[4 * j + 1]));
-    HIP_TRY(hipEventElapsedTime(&b, c->kev[4 * j + 2], c->kev[4 * j + 3]));
-    s.symbols_ms += a;
-    s.code_ms += b;
+  for (int j = 0; j < c->nkev; j++) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->kev[2 * j], c->kev[2 * j + 1]));
+    switch (c->kev_kind[j]) {
+      case 0: s.symbols_ms += ms; s.symbols_launches++; break;
+      case 1: s.code_ms += ms; s.code_launches++; break;
+      default: s.states_ms += ms; s.states_launches++; break;
+    }
   }
-  s.symbols_launches = s.code_launches = n;
   float asmb = 0.f;
   HIP_TRY(hipEventElapsedTime(&asmb, c->ev[1], c->ev[2]));
   s.assemble_ms = asmb;

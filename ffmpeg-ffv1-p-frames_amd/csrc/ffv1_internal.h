@@ -73,16 +73,35 @@ struct CodeArgs {
   int max_ops;
   const uint8_t* tabs;        // [default to0|to1][frame to0|to1]
   int64_t state_bytes;        // 2 * contexts * 32
-  uint8_t* tables;            // [chain][state_bytes] working context states
+  uint8_t* tables;            // [chain][state_bytes] working context states (grid-padded)
   uint8_t* persist;           // [slice][state_bytes]
-  uint32_t* digits;           // [chain][digit_cap / 2] packed renorm digits
-  int64_t digit_cap;          // digits per chain
   uint8_t* slice_out;         // [batch frame][slice][slice_cap]
   int64_t slice_cap;
   int64_t* slice_bytes;       // [batch frame][slice]
   int* status;                // [0] overflow count
   int version;                // bitstream version (Golomb: v3 adds a 129/0 decision)
   int coded_bits;             // "bits" of encode_line (8 for <=8-bit)
+  // frame-parallel mode (launch_code_frames): one lane per (frame, slice),
+  // starting from the per-frame state snapshots ffv1_states wrote
+  uint8_t* snap;              // [frame][slice][state_bytes] (grid-padded)
+  int nframes;
+};
+
+// Kernel 2a: the context-state walk.  The adaptive states a slice's range
+// coder sees depend only on the decisions of the earlier frames of its GOP,
+// not on the coder's arithmetic, so one wave per (segment, slice) replays
+// just the state transitions (table in LDS) and writes the states at the
+// start of every frame; the coding of all frames then runs in parallel.
+struct StateArgs {
+  const uint32_t* sym;        // [batch frame][frame_samples]
+  int64_t frame_samples;
+  const SliceGeom* geom;
+  int nslices;
+  const Segment* segs;
+  const uint8_t* ftab;        // frame transition table [bit][state]
+  int64_t state_bytes;
+  uint8_t* persist;           // [slice][state_bytes]
+  uint8_t* snap;              // [batch frame][slice][state_bytes]
 };
 
 struct AssembleArgs {
@@ -99,6 +118,9 @@ struct AssembleArgs {
 
 int launch_symbols(const SymbolArgs& a, void* stream);
 int launch_code(const CodeArgs& a, void* stream);
+int launch_code_frames(const CodeArgs& a, void* stream);
+int launch_states(const StateArgs& a, int nsegs, void* stream);
+constexpr int64_t kStateLdsMax = 64 * 1024;  // states walk: table + transition table in LDS
 int launch_code_golomb(const CodeArgs& a, void* stream);
 int launch_assemble(const AssembleArgs& a, int nframes, void* stream);
 

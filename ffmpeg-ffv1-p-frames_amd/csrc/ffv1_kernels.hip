@@ -29,6 +29,8 @@
 //                  parallel and combined in GF(2) (ffv1enc.c:1326-1354).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "ffv1_internal.h"
 
 namespace ffv1hip {
@@ -103,11 +105,24 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
 
 // ---------------------------------------------------------------------------
 // Kernel 2: SIMT range coder.
+//
+// Everything on the per-decision path is branch-free: a data-dependent scalar
+// branch costs ~66 cycles on gfx950 (tools/ubench), more than the ~20 VALU
+// ops of a whole decision, and with 64 independent streams per wave some lane
+// renormalises on almost every decision anyway.
+constexpr int kRing = 128;       // renorm digits per lane held in LDS before a flush
+constexpr int kFlushAt = 59;     // flush when any lane holds more (2 steps x 34 digits fit)
+
+// Keeps a value's computation where it is written: without it the compiler
+// sinks the successor-state lookups of lanes that may be idle into an
+// exec-masked block behind a branch, which costs more than the lookups.
+__device__ __forceinline__ void pin(uint32_t& v) { asm volatile("" : "+v"(v)); }
+
 struct Lane {
   int low, range;
   uint32_t r0, r1, r2, r3, r4, r5, r6, r7;  // states of the current context row (byte k = slot k)
-  int dpos;            // digits stored
-  int dcap;            // digit capacity
+  int dc;              // digits in the LDS ring
+  uint32_t* ring;      // this lane's ring column (LDS, stride kWave)
 
   template <int D>
   __device__ __forceinline__ uint32_t& w() {
@@ -123,139 +138,15 @@ struct Lane {
   }
 };
 
-// Renormalisation (rangecoder.h:52-75) deferred: record low's top byte with
-// its carry (bit 8) and whether the reference would defer it as an 0xFF run
-// (bit 9: 0xFF00 < low < 0x10000), then shift.
-#ifndef FFV1_ABLATE
-#define FFV1_ABLATE 0  // timing-only experiment builds (tools/ablate.sh); 0 in the product
-#endif
+// Byte writer: renorm_encoder's outstanding-byte / 0xFF-run logic
+// (rangecoder.h:52-75) replayed over the recorded values of `low`.
+struct Sink {
+  uint8_t* out;
+  int64_t cap, opos;
+  uint32_t ow;
+  int on, pending, run;
 
-__device__ __forceinline__ void renorm_digit(Lane& L, uint16_t* digits) {
-  const uint32_t d = ((uint32_t)L.low >> 8) | ((L.low > 0xFF00 && L.low < 0x10000) ? 0x200u : 0u);
-  if (!(FFV1_ABLATE & 1))
-    digits[min(L.dpos, L.dcap - 1)] = (uint16_t)d;  // overflow is reported, never written past
-  else
-    asm volatile("" ::"v"(d));
-  L.dpos++;
-  L.low = (L.low & 0xFF) << 8;
-  L.range <<= 8;
-}
-
-__device__ __forceinline__ void rac_core(Lane& L, int s, int bit) {
-  const int r1 = (L.range * s) >> 8;
-  const int r0 = L.range - r1;
-  L.low += bit ? r0 : 0;
-  L.range = bit ? r1 : r0;
-}
-
-// One decision on the static slot K of the current row.
-template <int K>
-__device__ __forceinline__ void step(Lane& L, uint16_t* digits, bool act, int bit, const uint8_t* tab) {
-  if (act) {
-    constexpr int D = K >> 2, SH = (K & 3) * 8;
-    const uint32_t w = L.w<D>();
-    const int s = (w >> SH) & 0xFF;
-    rac_core(L, s, bit);
-    const uint32_t ns = tab[(bit << 8) | s];
-    L.w<D>() = (w & ~(0xFFu << SH)) | (ns << SH);
-    if (L.range < 0x100) renorm_digit(L, digits);
-  }
-}
-
-// Batched form (no slot repeats inside the symbol, e <= 9): the decision
-// reads the old state and issues its successor lookup; the caller inserts
-// all successors after the last decision, so no LDS latency sits between
-// two decisions.
-template <int K>
-__device__ __forceinline__ uint32_t step_b(Lane& L, uint16_t* digits, bool act, int bit,
-                                           const uint8_t* tab) {
-  constexpr int D = K >> 2, SH = (K & 3) * 8;
-  const int s = (L.w<D>() >> SH) & 0xFF;
-  const int r1 = (L.range * s) >> 8;
-  const int r0 = L.range - r1;
-  const int nl = L.low + (bit ? r0 : 0);
-  const int nr = bit ? r1 : r0;
-  L.low = act ? nl : L.low;
-  L.range = act ? nr : L.range;
-  if (act && L.range < 0x100) renorm_digit(L, digits);
-  return tab[(bit << 8) | s];
-}
-
-template <int K>
-__device__ __forceinline__ void insert_b(Lane& L, bool act, uint32_t ns) {
-  constexpr int D = K >> 2, SH = (K & 3) * 8;
-  const uint32_t w = L.w<D>();
-  L.w<D>() = act ? ((w & ~(0xFFu << SH)) | (ns << SH)) : w;
-}
-
-// The sign decision's slot 11 + min(e,10) varies per lane (dwords 2..5).
-__device__ __forceinline__ void sign_step(Lane& L, uint16_t* digits, bool act, int m, int bit,
-                                          const uint8_t* tab) {
-  if (act) {
-    const int k = 11 + m, d = k >> 2, sh = (k & 3) * 8;
-    // mask selects (not ternaries): a select between members would be folded
-    // into an indexed load and push the whole Lane into scratch
-    const uint32_t m2 = 0u - (uint32_t)(d == 2), m3 = 0u - (uint32_t)(d == 3);
-    const uint32_t m4 = 0u - (uint32_t)(d == 4), m5 = 0u - (uint32_t)(d == 5);
-    const uint32_t w = (L.r2 & m2) | (L.r3 & m3) | (L.r4 & m4) | (L.r5 & m5);
-    const int s = (w >> sh) & 0xFF;
-    rac_core(L, s, bit);
-    const uint32_t ns = tab[(bit << 8) | s];
-    const uint32_t nw = (w & ~(0xFFu << sh)) | (ns << sh);
-    L.r2 = (nw & m2) | (L.r2 & ~m2);
-    L.r3 = (nw & m3) | (L.r3 & ~m3);
-    L.r4 = (nw & m4) | (L.r4 & ~m4);
-    L.r5 = (nw & m5) | (L.r5 & ~m5);
-    if (L.range < 0x100) renorm_digit(L, digits);
-  }
-}
-
-__device__ __forceinline__ int wave_max(int v) {
-  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
-  return v;
-}
-
-// Generic decision on a per-lane LDS state (header ops; rare).
-__device__ __forceinline__ void put_lds(Lane& L, uint16_t* digits, uint8_t* st, int bit,
-                                        const uint8_t* tab) {
-  const int s = *st;
-  rac_core(L, s, bit);
-  *st = tab[(bit << 8) | s];
-  if (L.range < 0x100) renorm_digit(L, digits);
-}
-
-__device__ __forceinline__ void symbol_lds(Lane& L, uint16_t* dg, uint8_t* st, int v, bool sgn,
-                                           const uint8_t* tab) {
-  if (v == 0) {
-    put_lds(L, dg, st, 1, tab);
-    return;
-  }
-  const unsigned a = v < 0 ? 0u - (unsigned)v : (unsigned)v;
-  const int e = 31 - __builtin_clz(a);
-  put_lds(L, dg, st, 0, tab);
-  for (int i = 0; i < e; i++) put_lds(L, dg, st + 1 + min(i, 9), 1, tab);
-  put_lds(L, dg, st + 1 + min(e, 9), 0, tab);
-  for (int i = e - 1; i >= 0; i--) put_lds(L, dg, st + 22 + min(i, 9), (a >> i) & 1, tab);
-  if (sgn) put_lds(L, dg, st + 11 + min(e, 10), v < 0, tab);
-}
-
-__device__ __forceinline__ void store_row(const Lane& L, uint8_t* row) {
-  reinterpret_cast<uint4*>(row)[0] = make_uint4(L.r0, L.r1, L.r2, L.r3);
-  reinterpret_cast<uint4*>(row)[1] = make_uint4(L.r4, L.r5, L.r6, L.r7);
-}
-
-constexpr int kCodeThreads = kWave;
-constexpr int kOpsetBytes = kOpSets * 32;
-
-// Replay renorm_encoder's pending byte / 0xFF-run logic (rangecoder.h:52-75)
-// over the recorded digits; returns the byte count (ff_rac_terminate's).
-__device__ __forceinline__ int64_t replay_digits(const uint16_t* digits, int64_t ndig, uint8_t* out,
-                                                 int64_t cap) {
-  uint32_t ow = 0;
-  int on = 0;
-  int64_t opos = 0;
-  int pending = -1, run = 0;
-  auto emit = [&](int b) {
+  __device__ __forceinline__ void emit(int b) {
     ow |= (uint32_t)(b & 0xFF) << (on << 3);
     if (++on == 4) {
       if (opos + 4 <= cap) *reinterpret_cast<uint32_t*>(out + opos) = ow;
@@ -263,13 +154,12 @@ __device__ __forceinline__ int64_t replay_digits(const uint16_t* digits, int64_t
       ow = 0;
       on = 0;
     }
-  };
-  for (int64_t t = 0; t < ndig; t++) {
-    const uint32_t d = digits[t];
-    const int qv = d & 0x1FF;
+  }
+  __device__ __forceinline__ void digit(int low) {
+    const int qv = low >> 8;
     if (pending < 0) {
       pending = qv;
-    } else if (d & 0x200) {
+    } else if (low > 0xFF00 && low < 0x10000) {
       run++;
     } else if (qv < 0x100) {
       emit(pending);
@@ -281,25 +171,246 @@ __device__ __forceinline__ int64_t replay_digits(const uint16_t* digits, int64_t
       pending = qv & 0xFF;
     }
   }
-  for (int k = 0; k < on; k++)
-    if (opos + k < cap) out[opos + k] = (uint8_t)(ow >> (k << 3));
-  return opos + on;
+  // bytes so far (ff_rac_terminate's count once the terminate digits are in)
+  __device__ __forceinline__ int64_t finish() {
+    for (int k = 0; k < on; k++)
+      if (opos + k < cap) out[opos + k] = (uint8_t)(ow >> (k << 3));
+    return opos + on;
+  }
+};
+
+__device__ __forceinline__ Sink make_sink(uint8_t* out, int64_t cap) {
+  Sink s;
+  s.out = out;
+  s.cap = cap;
+  s.opos = 0;
+  s.ow = 0;
+  s.on = 0;
+  s.pending = -1;
+  s.run = 0;
+  return s;
 }
 
-// ff_rac_terminate in digit form; returns the digit count.
-__device__ __forceinline__ int64_t finish_digits(Lane& L, uint16_t* digits) {
-  L.range = 0xFF;
-  L.low += 0xFF;
-  renorm_digit(L, digits);
-  L.range = 0xFF;
-  renorm_digit(L, digits);
-  return L.dpos;
+// Renormalisation (range < 0x100 needs at most one shift after a decision):
+// the value of `low` is always written at the ring head and the head only
+// advances when a byte is really shifted out.
+__device__ __forceinline__ void renorm(Lane& L) {
+  const bool need = L.range < 0x100;
+  L.ring[L.dc * kWave] = (uint32_t)L.low;
+  L.dc += need ? 1 : 0;
+  L.low = need ? ((L.low & 0xFF) << 8) : L.low;
+  L.range = need ? (L.range << 8) : L.range;
 }
+
+__device__ __forceinline__ void flush(Lane& L, Sink& S) {
+  for (int t = 0; t < L.dc; t++) S.digit((int)L.ring[t * kWave]);
+  L.dc = 0;
+}
+
+__device__ __forceinline__ void flush_if(Lane& L, Sink& S, int above) {
+  if (__ballot(L.dc > above)) flush(L, S);
+}
+
+__device__ __forceinline__ void rac_core(Lane& L, int s, int bit) {
+  const int r1 = (int)(__umul24((unsigned)L.range, (unsigned)s) >> 8);  // range < 2^16, s < 2^8
+  const int r0 = L.range - r1;
+  L.low += bit ? r0 : 0;
+  L.range = bit ? r1 : r0;
+}
+
+// put_rac (rangecoder.h:90-102) on lanes where `act`, leaving the others.
+__device__ __forceinline__ void rac_sel(Lane& L, bool act, int s, int bit) {
+  const int r1 = (int)(__umul24((unsigned)L.range, (unsigned)s) >> 8);  // range < 2^16, s < 2^8
+  const int r0 = L.range - r1;
+  const int nl = L.low + (bit ? r0 : 0);
+  const int nr = bit ? r1 : r0;
+  L.low = act ? nl : L.low;
+  L.range = act ? nr : L.range;
+  renorm(L);
+}
+
+// One decision on the static slot K of the current row, successor inserted.
+template <int K>
+__device__ __forceinline__ void step(Lane& L, bool act, int bit, const uint8_t* tab) {
+  constexpr int D = K >> 2, SH = (K & 3) * 8;
+  const uint32_t w = L.w<D>();
+  const int s = (w >> SH) & 0xFF;
+  rac_sel(L, act, s, bit);
+  const uint32_t ns = tab[(bit << 8) | s];
+  L.w<D>() = act ? ((w & ~(0xFFu << SH)) | (ns << SH)) : w;
+}
+
+// Batched form (no slot repeats inside the symbol, e <= 9): the decision
+// reads the old state and issues its successor lookup; the caller inserts
+// all successors after the last decision, so no LDS latency sits between
+// two decisions.
+template <int K>
+__device__ __forceinline__ uint32_t step_b(Lane& L, bool act, int bit, const uint8_t* tab) {
+  constexpr int D = K >> 2, SH = (K & 3) * 8;
+  const int s = (L.w<D>() >> SH) & 0xFF;
+  rac_sel(L, act, s, bit);
+  uint32_t ns = tab[(bit << 8) | s];
+  pin(ns);
+  return ns;
+}
+
+template <int K>
+__device__ __forceinline__ void insert_b(Lane& L, bool act, uint32_t ns) {
+  constexpr int D = K >> 2, SH = (K & 3) * 8;
+  const uint32_t w = L.w<D>();
+  L.w<D>() = act ? ((w & ~(0xFFu << SH)) | (ns << SH)) : w;
+}
+
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// The sign decision's slot 11 + min(e,10) varies per lane (dwords 2..5).
+// Mask selects (not ternaries): a select between members would be folded
+// into an indexed load and push the whole Lane into scratch.
+struct SignSlot {
+  uint32_t m2, m3, m4, m5;
+  int sh;
+  __device__ __forceinline__ SignSlot(int k) {
+    const int d = k >> 2;
+    sh = (k & 3) * 8;
+    m2 = 0u - (uint32_t)(d == 2);
+    m3 = 0u - (uint32_t)(d == 3);
+    m4 = 0u - (uint32_t)(d == 4);
+    m5 = 0u - (uint32_t)(d == 5);
+  }
+  __device__ __forceinline__ int get(const Lane& L) const {
+    const uint32_t w = (L.r2 & m2) | (L.r3 & m3) | (L.r4 & m4) | (L.r5 & m5);
+    return (w >> sh) & 0xFF;
+  }
+  __device__ __forceinline__ void put(Lane& L, bool act, uint32_t ns) const {
+    const uint32_t msk = ~(0xFFu << sh), val = ns << sh;
+    const uint32_t g2 = act ? m2 : 0u, g3 = act ? m3 : 0u, g4 = act ? m4 : 0u, g5 = act ? m5 : 0u;
+    L.r2 = (((L.r2 & msk) | val) & g2) | (L.r2 & ~g2);
+    L.r3 = (((L.r3 & msk) | val) & g3) | (L.r3 & ~g3);
+    L.r4 = (((L.r4 & msk) | val) & g4) | (L.r4 & ~g4);
+    L.r5 = (((L.r5 & msk) | val) & g5) | (L.r5 & ~g5);
+  }
+};
+
+// put_symbol_inline (ffv1enc.c:185-231) for a wave whose largest exponent is
+// EM <= 9: zero flag (slot 0), unary exponent (slots 1..e+1), mantissa MSB
+// first (slots 22+i), sign (slot 11+e).  Fully unrolled for EM.  Activity is
+// written as comparisons on e alone (e = -1 for a zero or idle lane): with a
+// shared `nz &&` factor the compiler wraps the inserts in an exec-masked branch.
+template <int EM>
+__device__ __forceinline__ void code_symbol(Lane& L, bool act, bool nz, int v, unsigned mag, int e,
+                                            const uint8_t* tab) {
+  const uint32_t n0 = step_b<0>(L, act, v == 0, tab);
+  if constexpr (EM >= 0) {
+    uint32_t nu[EM + 1], nm[EM + 1], nsg;
+    static_for<0, EM + 1>([&](auto ic) {
+      constexpr int I = decltype(ic)::value;
+      nu[I] = step_b<1 + I>(L, I <= e, I < e, tab);
+    });
+    static_for<0, EM>([&](auto ic) {
+      constexpr int I = EM - 1 - decltype(ic)::value;
+      nm[I] = step_b<22 + I>(L, I < e, (mag >> I) & 1, tab);
+    });
+    const SignSlot sg(11 + max(e, 0));
+    {
+      const int ss = sg.get(L);
+      const int bit = v < 0;
+      rac_sel(L, e >= 0, ss, bit);
+      nsg = tab[(bit << 8) | ss];
+      pin(nsg);
+    }
+    insert_b<0>(L, act, n0);
+    static_for<0, EM + 1>([&](auto ic) {
+      constexpr int I = decltype(ic)::value;
+      insert_b<1 + I>(L, I <= e, nu[I]);
+    });
+    static_for<0, EM>([&](auto ic) {
+      constexpr int I = decltype(ic)::value;
+      insert_b<22 + I>(L, I < e, nm[I]);
+    });
+    sg.put(L, e >= 0, nsg);
+  } else {
+    insert_b<0>(L, act, n0);
+  }
+}
+
+// Any exponent (slots 10 and 31 repeat beyond e = 9): serial updates.
+__device__ __forceinline__ void code_symbol_long(Lane& L, bool act, bool nz, int v, unsigned mag, int e,
+                                              int emax, const uint8_t* tab) {
+  step<0>(L, act, v == 0, tab);
+  static_for<0, 10>([&](auto ic) {
+    constexpr int I = decltype(ic)::value;
+    step<1 + I>(L, nz && I <= e, I < e, tab);
+  });
+  for (int i = 10; i <= emax; i++) step<10>(L, nz && i <= e, i < e, tab);
+  for (int i = emax - 1; i >= 10; i--) step<31>(L, nz && i < e, (mag >> i) & 1, tab);
+  static_for<0, 10>([&](auto ic) {
+    constexpr int I = 9 - decltype(ic)::value;
+    step<22 + I>(L, nz && I < e, (mag >> I) & 1, tab);
+  });
+  const SignSlot sg(11 + min(max(e, 0), 10));
+  const int ss = sg.get(L);
+  const int bit = v < 0;
+  rac_sel(L, nz, ss, bit);
+  sg.put(L, nz, tab[(bit << 8) | ss]);
+}
+
+__device__ __forceinline__ int wave_max(int v) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Wave-uniform max of x in [0, 31] from five ballots (no shuffles, no branches).
+__device__ __forceinline__ int wave_max5(int x) {
+  int m = 0;
+#pragma unroll
+  for (int b = 4; b >= 0; b--) {
+    const int t = m | (1 << b);
+    m = __ballot(x >= t) ? t : m;
+  }
+  return __builtin_amdgcn_readfirstlane(m);
+}
+
+// Generic decision on a per-lane LDS state (header ops; rare).
+__device__ __forceinline__ void put_lds(Lane& L, uint8_t* st, int bit, const uint8_t* tab) {
+  const int s = *st;
+  rac_core(L, s, bit);
+  *st = tab[(bit << 8) | s];
+  renorm(L);
+}
+
+__device__ __forceinline__ void symbol_lds(Lane& L, uint8_t* st, int v, bool sgn, const uint8_t* tab) {
+  if (v == 0) {
+    put_lds(L, st, 1, tab);
+    return;
+  }
+  const unsigned a = v < 0 ? 0u - (unsigned)v : (unsigned)v;
+  const int e = 31 - __builtin_clz(a);
+  put_lds(L, st, 0, tab);
+  for (int i = 0; i < e; i++) put_lds(L, st + 1 + min(i, 9), 1, tab);
+  put_lds(L, st + 1 + min(e, 9), 0, tab);
+  for (int i = e - 1; i >= 0; i--) put_lds(L, st + 22 + min(i, 9), (a >> i) & 1, tab);
+  if (sgn) put_lds(L, st + 11 + min(e, 10), v < 0, tab);
+}
+
+__device__ __forceinline__ void store_row(const Lane& L, uint8_t* row) {
+  reinterpret_cast<uint4*>(row)[0] = make_uint4(L.r0, L.r1, L.r2, L.r3);
+  reinterpret_cast<uint4*>(row)[1] = make_uint4(L.r4, L.r5, L.r6, L.r7);
+}
+
+constexpr int kCodeThreads = kWave;
+constexpr int kOpsetBytes = kOpSets * 32;
 
 // Key bit / in-band v0/v1 header / v3 slice header (per-lane op program).
-__device__ __forceinline__ void run_header_ops(const CodeArgs& a, Lane& L, uint16_t* digits,
-                                               uint8_t* os, int key, int slice, bool live,
-                                               const uint8_t* dtab, const uint8_t* ftab) {
+// One op codes at most 65 decisions.
+__device__ __forceinline__ void run_header_ops(const CodeArgs& a, Lane& L, Sink& S, uint8_t* os, int key,
+                                               int slice, bool live, const uint8_t* dtab,
+                                               const uint8_t* ftab) {
   for (int i = 0; i < kOpsetBytes; i++) os[i] = 128;
   const int sel = key * a.nslices + slice;
   const int n = live ? a.nops[sel] : 0;
@@ -310,35 +421,77 @@ __device__ __forceinline__ void run_header_ops(const CodeArgs& a, Lane& L, uint1
       const uint8_t* t = op.tab ? ftab : dtab;
       uint8_t* st = os + op.set * 32;
       if (op.kind == kOpBit)
-        put_lds(L, digits, st, op.value, t);
+        put_lds(L, st, op.value, t);
       else
-        symbol_lds(L, digits, st, op.value, op.kind == kOpSymS, t);
+        symbol_lds(L, st, op.value, op.kind == kOpSymS, t);
     }
+    flush_if(L, S, kRing - 67);
   }
 }
 
+__device__ __forceinline__ void lane_init(Lane& L, uint32_t* ring) {
+  L.low = 0;
+  L.range = 0xFF00;
+  L.dc = 0;
+  L.ring = ring;
+  L.r0 = L.r1 = L.r2 = L.r3 = L.r4 = L.r5 = L.r6 = L.r7 = 0;
+}
 
+// slice end: a 0 decision on state 129, then ff_rac_terminate
+__device__ __forceinline__ int64_t terminate(Lane& L, Sink& S, bool state129) {
+  flush_if(L, S, kRing - 4);
+  if (state129) {
+    rac_core(L, 129, 0);
+    renorm(L);
+  }
+  L.range = 0xFF;
+  L.low += 0xFF;
+  renorm(L);
+  L.range = 0xFF;
+  renorm(L);
+  flush(L, S);
+  return S.finish();
+}
+
+// FRAMES = false: one lane per (segment, slice) chain coding frame j of every
+// segment, the chain's states carried in `tables` from frame to frame.
+// FRAMES = true: one lane per (frame, slice) of the whole batch, each
+// starting from the snapshot ffv1_states wrote for its frame.
+template <bool FRAMES>
 __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t tabs[1024];
   __shared__ __attribute__((aligned(16))) uint8_t opsets[kCodeThreads * kOpsetBytes];
+  __shared__ uint32_t ring[kRing * kWave];
   for (int i = threadIdx.x; i < 1024; i += kCodeThreads) tabs[i] = a.tabs[i];
   __syncthreads();
   const uint8_t* dtab = tabs;        // default table (key bit, v0/v1 header)
   const uint8_t* ftab = tabs + 512;  // frame table
 
   const int lane = threadIdx.x;
-  const int64_t chain = (int64_t)blockIdx.x * kCodeThreads + lane;
-  const int seg_i = (int)(chain / a.nslices), slice = (int)(chain % a.nslices);
-  bool live = seg_i < a.nsegs;
+  const int64_t chain = (int64_t)blockIdx.x * kCodeThreads + lane;  // tables exist for the padded grid
+  int seg_i, slice, f;
+  bool live;
   Segment seg{0, 0, 0, 0};
-  if (live) seg = a.segs[seg_i];
-  live = live && a.j < seg.nframes;
-  const int f = seg.first_frame + a.j;
+  uint8_t* table;
+  if constexpr (FRAMES) {
+    f = (int)(chain / a.nslices);
+    slice = (int)(chain % a.nslices);
+    seg_i = f;
+    live = f < a.nframes;
+    table = a.snap + chain * a.state_bytes;
+  } else {
+    seg_i = (int)(chain / a.nslices);
+    slice = (int)(chain % a.nslices);
+    live = seg_i < a.nsegs;
+    if (live) seg = a.segs[seg_i];
+    live = live && a.j < seg.nframes;
+    f = seg.first_frame + a.j;
+    table = a.tables + chain * a.state_bytes;
+  }
   const int key = live ? a.keyflags[f] : 0;
-  uint8_t* table = a.tables + chain * a.state_bytes;
 
   // context states: continue, or reset at a keyframe (ff_ffv1_clear_slice_state)
-  if (live) {
+  if (!FRAMES && live) {
     if (a.j == 0 && seg.load_states) {
       const uint4* src = reinterpret_cast<const uint4*>(a.persist + (int64_t)slice * a.state_bytes);
       for (int64_t i = 0; i < a.state_bytes / 16; i++) reinterpret_cast<uint4*>(table)[i] = src[i];
@@ -349,144 +502,188 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
   }
 
   Lane L;
-  L.low = 0;
-  L.range = 0xFF00;
-  L.dpos = 0;
-  L.dcap = (int)a.digit_cap;
-  L.r0 = L.r1 = L.r2 = L.r3 = L.r4 = L.r5 = L.r6 = L.r7 = 0;
-  uint16_t* const digits = reinterpret_cast<uint16_t*>(a.digits) + chain * a.digit_cap;
+  lane_init(L, ring + lane);
+  uint8_t* const out = a.slice_out + ((int64_t)(live ? f : 0) * a.nslices + slice) * a.slice_cap;
+  Sink S = make_sink(out, live ? a.slice_cap : 0);  // idle lanes write nothing
 
-  // header ops: key bit, in-band v0/v1 header, v3 slice header
-  run_header_ops(a, L, digits, opsets + lane * kOpsetBytes, key, slice, live, dtab, ftab);
+  run_header_ops(a, L, S, opsets + lane * kOpsetBytes, key, slice, live, dtab, ftab);
 
   const SliceGeom& g = a.geom[slice];
   const int64_t nsym = live ? g.nsym : 0;
   const int64_t nmax = wave_max((int)nsym);
-  // g.sym_off and frame_samples are multiples of 4 (host-side padding)
-  const uint4* sp = reinterpret_cast<const uint4*>(a.sym + (int64_t)seg_i * a.frame_samples + g.sym_off);
+  // g.sym_off and frame_samples are multiples of 4 (host-side padding);
+  // idle lanes read group 0 of slot 0
+  const uint4* sp = reinterpret_cast<const uint4*>(live ? a.sym + (int64_t)seg_i * a.frame_samples + g.sym_off
+                                                        : a.sym);
+  const int64_t glast = nsym > 0 ? (nsym - 1) >> 2 : 0;
 
-  int cur = -1, pfrow = -1;
+  uint4 G = sp[0], GN = sp[min((int64_t)1, glast)];
+  int cur = nsym > 0 ? (int)(G.x >> 16) : 0;
+  {
+    const uint4* r = reinterpret_cast<const uint4*>(table + (int64_t)cur * 32);
+    const uint4 ra = r[0], rb = r[1];
+    L.r0 = ra.x; L.r1 = ra.y; L.r2 = ra.z; L.r3 = ra.w;
+    L.r4 = rb.x; L.r5 = rb.y; L.r6 = rb.z; L.r7 = rb.w;
+  }
   uint4 PFa = make_uint4(0, 0, 0, 0), PFb = make_uint4(0, 0, 0, 0);
-  uint4 G = make_uint4(0, 0, 0, 0), GN = make_uint4(0, 0, 0, 0);
-  if (nsym > 0) G = sp[0];
-  if (nsym > 4) GN = sp[1];
+  flush_if(L, S, kFlushAt);
 
-  for (int64_t i = 0; i < nmax; i++) {
-    const bool act = i < nsym;
-    const int q = (int)(i & 3);
-    if (q == 0 && i > 0) {
-      G = GN;
-      if (act && i + 4 < nsym) GN = sp[(FFV1_ABLATE & 2) ? ((i >> 2) & 15) + 1 : (i >> 2) + 1];
+  auto sym_step = [&](int64_t ii, uint32_t sv, uint32_t sn) {
+    const bool act = ii < nsym;
+    const int row = act ? (int)(sv >> 16) : cur;
+    const bool sw = row != cur;  // context switch: take the prefetched row
+    L.r0 = sw ? PFa.x : L.r0; L.r1 = sw ? PFa.y : L.r1; L.r2 = sw ? PFa.z : L.r2; L.r3 = sw ? PFa.w : L.r3;
+    L.r4 = sw ? PFb.x : L.r4; L.r5 = sw ? PFb.y : L.r5; L.r6 = sw ? PFb.z : L.r6; L.r7 = sw ? PFb.w : L.r7;
+    cur = row;
+    {  // prefetch the next symbol's row (stale and unused when it is this row)
+      const int nrow = ii + 1 < nsym ? (int)(sn >> 16) : cur;
+      const uint4* r = reinterpret_cast<const uint4*>(table + (int64_t)nrow * 32);
+      PFa = r[0];
+      PFb = r[1];
     }
-    const uint32_t sv = q == 0 ? G.x : q == 1 ? G.y : q == 2 ? G.z : G.w;
-    const uint32_t sn = q == 0 ? G.y : q == 1 ? G.z : q == 2 ? G.w : GN.x;
-    const int row = (int)(sv >> 16);
     const int v = (int16_t)(sv & 0xFFFF);
-    if (act && row != cur) {  // context switch: write back, take the prefetch
-      if (cur >= 0 && !(FFV1_ABLATE & 4)) store_row(L, table + (int64_t)cur * 32);
-      uint4 ra = PFa, rb = PFb;
-      if (row != pfrow) {
-        ra = reinterpret_cast<const uint4*>(table + (int64_t)row * 32)[0];
-        rb = reinterpret_cast<const uint4*>(table + (int64_t)row * 32)[1];
-      }
-      L.r0 = ra.x; L.r1 = ra.y; L.r2 = ra.z; L.r3 = ra.w;
-      L.r4 = rb.x; L.r5 = rb.y; L.r6 = rb.z; L.r7 = rb.w;
-      cur = row;
-    }
-    pfrow = -1;
-    if (act && i + 1 < nsym) {  // prefetch the next symbol's row
-      const int nrow = (int)(sn >> 16);
-      if (nrow != cur) {
-        PFa = reinterpret_cast<const uint4*>(table + (int64_t)nrow * 32)[0];
-        PFb = reinterpret_cast<const uint4*>(table + (int64_t)nrow * 32)[1];
-        pfrow = nrow;
-      }
-    }
-
-    // put_symbol_inline over static slots
     const bool nz = act && v != 0;
     const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
     const int e = nz ? 31 - __builtin_clz(mag) : -1;
-    const int emax = wave_max(e);
-    if (emax < 10) {
-      // batched: every decision reads the symbol's starting states
-      const uint32_t n0 = step_b<0>(L, digits, act, v == 0, ftab);
-      uint32_t nu[10], nm[10], nsg = 0;
-      const int sgk = 11 + max(e, 0), sgd = sgk >> 2, sgsh = (sgk & 3) * 8;
-      const uint32_t m2 = 0u - (uint32_t)(sgd == 2), m3 = 0u - (uint32_t)(sgd == 3);
-      const uint32_t m4 = 0u - (uint32_t)(sgd == 4), m5 = 0u - (uint32_t)(sgd == 5);
-      if (emax >= 0) {
-#define UNARY(I) nu[I] = (I <= emax) ? step_b<1 + I>(L, digits, nz && I <= e, I < e, ftab) : 0u;
-        UNARY(0) UNARY(1) UNARY(2) UNARY(3) UNARY(4) UNARY(5) UNARY(6) UNARY(7) UNARY(8) UNARY(9)
-#undef UNARY
-#define MANT(I) nm[I] = (I < emax) ? step_b<22 + I>(L, digits, nz && I < e, (mag >> I) & 1, ftab) : 0u;
-        MANT(9) MANT(8) MANT(7) MANT(6) MANT(5) MANT(4) MANT(3) MANT(2) MANT(1) MANT(0)
-#undef MANT
-        // sign: per-lane slot 11 + e, read from the starting row
-        const uint32_t w = (L.r2 & m2) | (L.r3 & m3) | (L.r4 & m4) | (L.r5 & m5);
-        const int ss = (w >> sgsh) & 0xFF;
-        const int bit = v < 0;
-        const int r1 = (L.range * ss) >> 8;
-        const int r0 = L.range - r1;
-        const int nl = L.low + (bit ? r0 : 0);
-        const int nr = bit ? r1 : r0;
-        L.low = nz ? nl : L.low;
-        L.range = nz ? nr : L.range;
-        if (nz && L.range < 0x100) renorm_digit(L, digits);
-        nsg = ftab[(bit << 8) | ss];
-      }
-      // successor states
-      insert_b<0>(L, act, n0);
-      if (emax >= 0) {
-#define UNARY(I) if (I <= emax) insert_b<1 + I>(L, nz && I <= e, nu[I]);
-        UNARY(0) UNARY(1) UNARY(2) UNARY(3) UNARY(4) UNARY(5) UNARY(6) UNARY(7) UNARY(8) UNARY(9)
-#undef UNARY
-#define MANT(I) if (I < emax) insert_b<22 + I>(L, nz && I < e, nm[I]);
-        MANT(9) MANT(8) MANT(7) MANT(6) MANT(5) MANT(4) MANT(3) MANT(2) MANT(1) MANT(0)
-#undef MANT
-        const uint32_t msk = ~(0xFFu << sgsh), val = nsg << sgsh;
-        const uint32_t g2 = nz ? m2 : 0u, g3 = nz ? m3 : 0u, g4 = nz ? m4 : 0u, g5 = nz ? m5 : 0u;
-        L.r2 = (((L.r2 & msk) | val) & g2) | (L.r2 & ~g2);
-        L.r3 = (((L.r3 & msk) | val) & g3) | (L.r3 & ~g3);
-        L.r4 = (((L.r4 & msk) | val) & g4) | (L.r4 & ~g4);
-        L.r5 = (((L.r5 & msk) | val) & g5) | (L.r5 & ~g5);
-      }
-    } else {
-      // e >= 10 somewhere in the wave (slots 10 / 31 repeat): serial updates
-    step<0>(L, digits, act, v == 0, ftab);
-      // unary exponent: slots 1..10, 1-bits then the terminating 0
-#define UNARY(I) if (I <= emax) step<1 + I>(L, digits, nz && I <= e, I < e, ftab);
-      UNARY(0) UNARY(1) UNARY(2) UNARY(3) UNARY(4) UNARY(5) UNARY(6) UNARY(7) UNARY(8) UNARY(9)
-#undef UNARY
-      for (int i2 = 10; i2 <= emax; i2++) step<10>(L, digits, nz && i2 <= e, i2 < e, ftab);
-      // mantissa MSB -> LSB: slots 22 + min(i, 9)
-      for (int i2 = emax - 1; i2 >= 10; i2--) step<31>(L, digits, nz && i2 < e, (mag >> i2) & 1, ftab);
-#define MANT(I) if (I < emax) step<22 + I>(L, digits, nz && I < e, (mag >> I) & 1, ftab);
-      MANT(9) MANT(8) MANT(7) MANT(6) MANT(5) MANT(4) MANT(3) MANT(2) MANT(1) MANT(0)
-#undef MANT
-      sign_step(L, digits, nz, min(e, 10), v < 0, ftab);
+    const int emax = wave_max5(e + 1) - 1;
+    switch (emax) {
+      case -1: code_symbol<-1>(L, act, nz, v, mag, e, ftab); break;
+      case 0: code_symbol<0>(L, act, nz, v, mag, e, ftab); break;
+      case 1: code_symbol<1>(L, act, nz, v, mag, e, ftab); break;
+      case 2: code_symbol<2>(L, act, nz, v, mag, e, ftab); break;
+      case 3: code_symbol<3>(L, act, nz, v, mag, e, ftab); break;
+      case 4: code_symbol<4>(L, act, nz, v, mag, e, ftab); break;
+      case 5: code_symbol<5>(L, act, nz, v, mag, e, ftab); break;
+      case 6: code_symbol<6>(L, act, nz, v, mag, e, ftab); break;
+      case 7: code_symbol<7>(L, act, nz, v, mag, e, ftab); break;
+      case 8: code_symbol<8>(L, act, nz, v, mag, e, ftab); break;
+      case 9: code_symbol<9>(L, act, nz, v, mag, e, ftab); break;
+      default: code_symbol_long(L, act, nz, v, mag, e, emax, ftab); break;
     }
+    store_row(L, table + (int64_t)cur * 32);  // write back every step: no divergent store
+  };
+
+  for (int64_t i = 0, gi = 0; i < nmax; i += 4, gi++) {
+    sym_step(i, G.x, G.y);
+    sym_step(i + 1, G.y, G.z);
+    flush_if(L, S, kFlushAt);
+    sym_step(i + 2, G.z, G.w);
+    sym_step(i + 3, G.w, GN.x);
+    flush_if(L, S, kFlushAt);
+    G = GN;
+    GN = sp[min(gi + 2, glast)];
   }
-  if (cur >= 0) store_row(L, table + (int64_t)cur * 32);
 
   if (live) {
-    // slice end: a 0 decision on state 129, then ff_rac_terminate
-    rac_core(L, 129, 0);
-    if (L.range < 0x100) renorm_digit(L, digits);
-    const int64_t ndig = finish_digits(L, digits);
-    int64_t nbytes = 0;
-    if (L.dpos > L.dcap) {
-      atomicAdd(a.status, 1);
-    } else {
-      nbytes = replay_digits(digits, ndig, a.slice_out + ((int64_t)f * a.nslices + slice) * a.slice_cap,
-                             a.slice_cap);
-      if (nbytes > a.slice_cap) atomicAdd(a.status, 1);
-    }
+    const int64_t nbytes = terminate(L, S, true);
+    if (nbytes > a.slice_cap) atomicAdd(a.status, 1);
     a.slice_bytes[(int64_t)f * a.nslices + slice] = nbytes;
-    if (a.j == seg.nframes - 1 && seg.save_states) {
+    if (!FRAMES && a.j == seg.nframes - 1 && seg.save_states) {
       uint4* dst = reinterpret_cast<uint4*>(a.persist + (int64_t)slice * a.state_bytes);
       for (int64_t i = 0; i < a.state_bytes / 16; i++) dst[i] = reinterpret_cast<const uint4*>(table)[i];
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 2a: context-state walk (see StateArgs).  One wave per (segment,
+// slice); the slice's 2 x contexts x 32 states live in LDS.  Symbols are
+// taken one at a time (wave-uniform row and value); lane k owns slot k of
+// the row and applies that slot's decisions of put_symbol_inline
+// (ffv1enc.c:185-231) through the transition table.
+constexpr int kStateThreads = kWave;
+
+__device__ __forceinline__ void copy_states(uint4* dst, const uint4* src, int64_t n16, int lane) {
+  for (int64_t i = lane; i < n16; i += kStateThreads) dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(kStateThreads) void ffv1_states(StateArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t* const tbl = lds;                       // [2 * contexts][32]
+  uint8_t* const tab = lds + a.state_bytes;       // [bit][state]
+  uint8_t* const sink = tab + 512;                // writes of lanes 32..63 land here
+  const int lane = threadIdx.x;
+  for (int i = lane; i < 512; i += kStateThreads) tab[i] = a.ftab[i];
+  const int seg_i = blockIdx.x / a.nslices, slice = blockIdx.x % a.nslices;
+  const Segment seg = a.segs[seg_i];
+  const int64_t n16 = a.state_bytes / 16;
+  uint4* const t4 = reinterpret_cast<uint4*>(tbl);
+  if (seg.load_states) {
+    copy_states(t4, reinterpret_cast<const uint4*>(a.persist + (int64_t)slice * a.state_bytes), n16, lane);
+  } else {  // the segment starts at a keyframe (ff_ffv1_clear_slice_state)
+    const uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
+    for (int64_t i = lane; i < n16; i += kStateThreads) t4[i] = v;
+  }
+  __syncthreads();
+
+  // lane roles: slot k = lane (lanes 32..63 idle)
+  const int k = lane & 31;
+  const bool on = lane < 32;
+  const int kind = k == 0 ? 0 : k <= 10 ? 1 : k <= 21 ? 2 : 3;  // zero, unary, sign, mantissa
+  const int ki = kind == 1 ? k - 1 : kind == 2 ? k - 11 : kind == 3 ? k - 22 : 0;
+
+  const SliceGeom& g = a.geom[slice];
+  const int64_t nsym = g.nsym;
+  for (int j = 0; j < seg.nframes; j++) {
+    const int f = seg.first_frame + j;
+    copy_states(reinterpret_cast<uint4*>(a.snap + ((int64_t)f * a.nslices + slice) * a.state_bytes), t4, n16,
+                lane);
+    if (j == seg.nframes - 1 && !seg.save_states) break;
+    const uint32_t* sp = a.sym + (int64_t)f * a.frame_samples + g.sym_off;
+    uint32_t next = lane < nsym ? sp[lane] : 0u;
+    for (int64_t base = 0; base < nsym; base += kStateThreads) {
+      const uint32_t mine = next;
+      if (base + kStateThreads + lane < nsym) next = sp[base + kStateThreads + lane];
+      const int cnt = (int)min((int64_t)kStateThreads, nsym - base);
+      for (int t = 0; t < cnt; t++) {
+        const uint32_t sv = __builtin_amdgcn_readlane(mine, t);
+        const int row = (int)(sv >> 16);
+        const int v = (int16_t)(sv & 0xFFFF);
+        const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
+        const int e = v ? 31 - __builtin_clz(mag) : -1;
+        const int addr = on ? row * 32 + k : (int)(sink - tbl) + lane;
+        if (e < 10) {
+          bool touched, bit;
+          if (kind == 0) {
+            touched = true;
+            bit = v == 0;
+          } else if (kind == 1) {
+            touched = ki <= e;
+            bit = ki < e;
+          } else if (kind == 2) {
+            touched = ki == e;
+            bit = v < 0;
+          } else {
+            touched = ki < e;
+            bit = (mag >> ki) & 1;
+          }
+          const int st = tbl[addr];
+          const int ns = tab[(bit << 8) | st];
+          tbl[addr] = (on && touched) ? ns : st;
+        } else {
+          // slots 10 and 31 take several decisions (e - 9 repeats), sign is slot 21
+          int n = 0;
+          if (kind == 0) n = 1;
+          else if (kind == 1) n = ki < 9 ? 1 : e - 8;
+          else if (kind == 2) n = ki == 10 ? 1 : 0;
+          else n = ki < 9 ? 1 : e - 9;
+          int st = tbl[addr];
+          for (int d = 0; d < n; d++) {
+            int bit;
+            if (kind == 0) bit = 0;
+            else if (kind == 1) bit = ki < 9 ? 1 : (d < e - 9);
+            else if (kind == 2) bit = v < 0;
+            else bit = (mag >> (ki < 9 ? ki : e - 1 - d)) & 1;
+            st = tab[(bit << 8) | st];
+          }
+          tbl[addr] = st;
+        }
+      }
+    }
+  }
+  if (seg.save_states) {
+    __syncthreads();
+    copy_states(reinterpret_cast<uint4*>(a.persist + (int64_t)slice * a.state_bytes), t4, n16, lane);
   }
 }
 
@@ -564,6 +761,7 @@ __device__ __forceinline__ void vlc_put(BitSink& b, uint64_t& rec, int v, int bi
 __global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t tabs[1024];
   __shared__ __attribute__((aligned(16))) uint8_t opsets[kCodeThreads * kOpsetBytes];
+  __shared__ uint32_t ring[kRing * kWave];
   for (int i = threadIdx.x; i < 1024; i += kCodeThreads) tabs[i] = a.tabs[i];
   __syncthreads();
   const int lane = threadIdx.x;
@@ -590,20 +788,12 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
   // range-coded prefix: key bit / header / slice header, then (v3) a 0 on
   // state 129 and ff_rac_terminate (ffv1enc.c:1173-1183)
   Lane L;
-  L.low = 0;
-  L.range = 0xFF00;
-  L.dpos = 0;
-  L.dcap = (int)a.digit_cap;
-  uint16_t* const digits = reinterpret_cast<uint16_t*>(a.digits) + chain * a.digit_cap;
-  run_header_ops(a, L, digits, opsets + lane * kOpsetBytes, key, slice, live, tabs, tabs + 512);
+  lane_init(L, ring + lane);
+  uint8_t* const out = a.slice_out + ((int64_t)(live ? f : 0) * a.nslices + slice) * a.slice_cap;
+  Sink S = make_sink(out, live ? a.slice_cap : 0);  // idle lanes write nothing
+  run_header_ops(a, L, S, opsets + lane * kOpsetBytes, key, slice, live, tabs, tabs + 512);
+  const int64_t ac_bytes = terminate(L, S, a.version > 2);
   if (!live) return;
-  if (a.version > 2) {
-    rac_core(L, 129, 0);
-    if (L.range < 0x100) renorm_digit(L, digits);
-  }
-  const int64_t ndig = finish_digits(L, digits);
-  uint8_t* out = a.slice_out + ((int64_t)f * a.nslices + slice) * a.slice_cap;
-  const int64_t ac_bytes = L.dpos > L.dcap ? a.slice_cap + 1 : replay_digits(digits, ndig, out, a.slice_cap);
 
   BitSink b{0ull, 0, ac_bytes, out, a.slice_cap};
   const SliceGeom& g = a.geom[slice];
@@ -759,7 +949,22 @@ int launch_symbols(const SymbolArgs& a, void* stream) {
 int launch_code(const CodeArgs& a, void* stream) {
   const int64_t chains = (int64_t)a.nsegs * a.nslices;
   dim3 grid((unsigned)((chains + kCodeThreads - 1) / kCodeThreads)), block(kCodeThreads);
-  hipLaunchKernelGGL(ffv1_code, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
+  hipLaunchKernelGGL(ffv1_code<false>, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_code_frames(const CodeArgs& a, void* stream) {
+  const int64_t chains = (int64_t)a.nframes * a.nslices;
+  dim3 grid((unsigned)((chains + kCodeThreads - 1) / kCodeThreads)), block(kCodeThreads);
+  hipLaunchKernelGGL(ffv1_code<true>, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_states(const StateArgs& a, int nsegs, void* stream) {
+  const size_t lds = (size_t)a.state_bytes + 512 + kStateThreads;
+  if ((int64_t)lds > kStateLdsMax) return -1;
+  dim3 grid((unsigned)(nsegs * a.nslices)), block(kStateThreads);
+  hipLaunchKernelGGL(ffv1_states, grid, block, lds, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -66,7 +66,8 @@ class KernelStats(ctypes.Structure):
     _fields_ = [("symbols_ms", ctypes.c_float), ("code_ms", ctypes.c_float),
                 ("assemble_ms", ctypes.c_float), ("symbols_launches", ctypes.c_int),
                 ("code_launches", ctypes.c_int), ("assemble_launches", ctypes.c_int),
-                ("frames_coded_per_launch_max", ctypes.c_int64)]
+                ("frames_coded_per_launch_max", ctypes.c_int64), ("states_ms", ctypes.c_float),
+                ("states_launches", ctypes.c_int)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

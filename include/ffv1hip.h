@@ -133,7 +133,9 @@ int ffv1hip_last_kernel_ms(ffv1hip_ctx *ctx, float *encode_ms, float *assemble_m
 typedef struct ffv1hip_kernel_stats {
     float symbols_ms, code_ms, assemble_ms;
     int symbols_launches, code_launches, assemble_launches;
-    int64_t frames_coded_per_launch_max;   /* segments (GOPs) in the batch */
+    int64_t frames_coded_per_launch_max;   /* slice streams per coder launch / nslices */
+    float states_ms;                       /* context-state walk (frame-parallel mode) */
+    int states_launches;
 } ffv1hip_kernel_stats;
 int ffv1hip_last_kernel_stats(ffv1hip_ctx *ctx, ffv1hip_kernel_stats *out);
 

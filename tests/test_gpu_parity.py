@@ -52,6 +52,18 @@ def test_hip_matches_oracle(stream):
             pytest.fail(f"frame {i}: {len(g)} vs {len(r)} bytes, first diff at {first}")
 
 
+@pytest.mark.parametrize("stream", [s for s in PARITY_STREAMS if s.coder != 0][:6],
+                         ids=[s.name for s in PARITY_STREAMS if s.coder != 0][:6])
+def test_chained_coder_matches_oracle(stream, monkeypatch):
+    """The per-GOP chained range coder (FFV1HIP_CODER=chain) gives the same
+    bytes as the frame-parallel default."""
+    monkeypatch.setenv("FFV1HIP_CODER", "chain")
+    frames = list(stream.frames())
+    _, _, ref = oracle_encode(stream, frames)
+    _, got = hip_encode(stream, frames, batch=4)
+    assert got == ref
+
+
 def test_whole_batch_equals_split_batches():
     s = PARITY_STREAMS[1]
     frames = list(s.frames())
