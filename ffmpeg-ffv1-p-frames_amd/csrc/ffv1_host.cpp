@@ -566,7 +566,7 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
   // keeps the chained per-GOP coder (a test hook: both must give equal bytes).
   {
     const char* mode = std::getenv("FFV1HIP_CODER");
-    const int64_t lds = int64_t(2) * c->contexts * 32 + 512 + 64;
+    const int64_t lds = int64_t(c->contexts) * 32 + 512 + 64;  // one plane group per walk
     c->frames_mode = p.ac && lds <= kStateLdsMax && !(mode && std::strcmp(mode, "chain") == 0);
   }
   int rc = alloc_device(c);

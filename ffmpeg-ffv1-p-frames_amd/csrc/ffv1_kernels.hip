@@ -588,105 +588,160 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
 // ---------------------------------------------------------------------------
 // Kernel 2a: context-state walk (see StateArgs).  One wave per (segment,
 // slice); the slice's 2 x contexts x 32 states live in LDS.  Symbols are
-// taken one at a time (wave-uniform row and value); lane k owns slot k of
-// the row and applies that slot's decisions of put_symbol_inline
-// (ffv1enc.c:185-231) through the transition table.
+// taken two at a time: lanes 0..31 apply symbol t and lanes 32..63 symbol
+// t+1, lane k of a half owning slot k of its symbol's row, each applying that
+// slot's decisions of put_symbol_inline (ffv1enc.c:185-231) through the
+// transition table.  When both symbols share a row, the upper half continues
+// from the lower half's results (v_permlane32_swap) and only it writes back.
 constexpr int kStateThreads = kWave;
 
 __device__ __forceinline__ void copy_states(uint4* dst, const uint4* src, int64_t n16, int lane) {
   for (int64_t i = lane; i < n16; i += kStateThreads) dst[i] = src[i];
 }
 
+struct SymDec {  // one symbol, wave-uniform
+  int row, v, e;
+  unsigned mag;
+};
+
+__device__ __forceinline__ SymDec decode_sym(uint32_t sv) {
+  SymDec d;
+  d.row = (int)(sv >> 16);
+  d.v = (int16_t)(sv & 0xFFFF);
+  d.mag = d.v < 0 ? 0u - (unsigned)d.v : (unsigned)d.v;
+  d.e = d.v ? 31 - __builtin_clz(d.mag) : -1;
+  return d;
+}
+
+// Exponents >= 10 (slots 10 and 31 take e - 9 repeated decisions, the sign
+// goes to slot 21): lane k < 32 applies all of its slot's decisions.
+__device__ __forceinline__ void walk_long(uint8_t* tbl, const uint8_t* tab, const SymDec& d, int lane,
+                                          int kind, int ki, int sink) {
+  const int e = d.e;
+  int n = 0;
+  if (kind == 0) n = 1;
+  else if (kind == 1) n = ki <= min(e, 9) ? (ki < 9 ? 1 : max(e - 8, 1)) : 0;
+  else if (kind == 2) n = ki == min(e, 10) && e >= 0 ? 1 : 0;
+  else n = ki < min(e, 9) ? 1 : (ki == 9 && e > 9 ? e - 9 : 0);
+  const int addr = lane < 32 ? d.row * 32 + lane : sink + lane;
+  int st = tbl[addr];
+  for (int j = 0; j < n; j++) {
+    int bit;
+    if (kind == 0) bit = d.v == 0;
+    else if (kind == 1) bit = ki < 9 ? (ki < e) : (j < e - 9);
+    else if (kind == 2) bit = d.v < 0;
+    else bit = (d.mag >> (ki < 9 ? ki : e - 1 - j)) & 1;
+    st = tab[(bit << 8) | st];
+  }
+  tbl[addr] = st;
+}
+
+// Slot activity (bit k: slot k takes a decision) and decision bits of one
+// symbol with e <= 9: slot 0 zero flag, 1..e+1 unary, 11+e sign, 22..21+e
+// mantissa (put_symbol_inline, ffv1enc.c:185-231).
+__device__ __forceinline__ void slot_masks(int v, uint32_t& tm, uint32_t& bm) {
+  const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
+  const int e = v ? 31 - __builtin_clz(mag) : -1;
+  const uint32_t lo = v ? (1u << e) - 1u : 0u;  // e ones
+  tm = v ? (1u | (((2u << e) - 1u) << 1) | (1u << (11 + e)) | (lo << 22)) : 1u;
+  bm = v ? ((lo << 1) | ((uint32_t)(v < 0) << (11 + e)) | ((mag & lo) << 22)) : 1u;
+}
+
+// Grid: (segment, slice, plane group); group 0 = luma contexts, 1 = the
+// chroma contexts Cb and Cr share (ffv1enc.c:1194-1195): independent chains.
 __global__ __launch_bounds__(kStateThreads) void ffv1_states(StateArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  uint8_t* const tbl = lds;                       // [2 * contexts][32]
-  uint8_t* const tab = lds + a.state_bytes;       // [bit][state]
-  uint8_t* const sink = tab + 512;                // writes of lanes 32..63 land here
+  const int64_t half = a.state_bytes / 2;         // one plane group's [contexts][32]
+  uint8_t* const tbl = lds;
+  uint8_t* const tab = lds + half;                // [bit][state]
+  const int sink = (int)half + 512;               // 64 bytes taking writes that must not land
   const int lane = threadIdx.x;
   for (int i = lane; i < 512; i += kStateThreads) tab[i] = a.ftab[i];
-  const int seg_i = blockIdx.x / a.nslices, slice = blockIdx.x % a.nslices;
+  const int grp = blockIdx.x & 1;
+  const int chain = blockIdx.x >> 1;
+  const int seg_i = chain / a.nslices, slice = chain % a.nslices;
   const Segment seg = a.segs[seg_i];
-  const int64_t n16 = a.state_bytes / 16;
+  const SliceGeom& g = a.geom[slice];
+  const int64_t s0 = grp ? g.plane_sym_off[1] : 0, s1 = grp ? g.nsym : g.plane_sym_off[1];
+  if (s0 >= s1 && grp) return;  // no chroma
+  const int rowbase = grp ? (int)(half / 32) : 0;
+  const int64_t n16 = half / 16;
   uint4* const t4 = reinterpret_cast<uint4*>(tbl);
+  const int64_t goff = grp * half;
   if (seg.load_states) {
-    copy_states(t4, reinterpret_cast<const uint4*>(a.persist + (int64_t)slice * a.state_bytes), n16, lane);
+    copy_states(t4, reinterpret_cast<const uint4*>(a.persist + (int64_t)slice * a.state_bytes + goff), n16, lane);
   } else {  // the segment starts at a keyframe (ff_ffv1_clear_slice_state)
     const uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
     for (int64_t i = lane; i < n16; i += kStateThreads) t4[i] = v;
   }
   __syncthreads();
 
-  // lane roles: slot k = lane (lanes 32..63 idle)
+  // lane roles: half h = lane / 32 takes symbol t + h; slot k = lane % 32
   const int k = lane & 31;
-  const bool on = lane < 32;
+  const bool hi = lane >= 32;
   const int kind = k == 0 ? 0 : k <= 10 ? 1 : k <= 21 ? 2 : 3;  // zero, unary, sign, mantissa
   const int ki = kind == 1 ? k - 1 : kind == 2 ? k - 11 : kind == 3 ? k - 22 : 0;
 
-  const SliceGeom& g = a.geom[slice];
-  const int64_t nsym = g.nsym;
+  const int64_t nsym = s1 - s0;
   for (int j = 0; j < seg.nframes; j++) {
     const int f = seg.first_frame + j;
-    copy_states(reinterpret_cast<uint4*>(a.snap + ((int64_t)f * a.nslices + slice) * a.state_bytes), t4, n16,
-                lane);
+    copy_states(reinterpret_cast<uint4*>(a.snap + ((int64_t)f * a.nslices + slice) * a.state_bytes + goff), t4,
+                n16, lane);
     if (j == seg.nframes - 1 && !seg.save_states) break;
-    const uint32_t* sp = a.sym + (int64_t)f * a.frame_samples + g.sym_off;
+    const uint32_t* sp = a.sym + (int64_t)f * a.frame_samples + g.sym_off + s0;
     uint32_t next = lane < nsym ? sp[lane] : 0u;
     for (int64_t base = 0; base < nsym; base += kStateThreads) {
       const uint32_t mine = next;
       if (base + kStateThreads + lane < nsym) next = sp[base + kStateThreads + lane];
       const int cnt = (int)min((int64_t)kStateThreads, nsym - base);
-      for (int t = 0; t < cnt; t++) {
-        const uint32_t sv = __builtin_amdgcn_readlane(mine, t);
-        const int row = (int)(sv >> 16);
-        const int v = (int16_t)(sv & 0xFFFF);
-        const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
-        const int e = v ? 31 - __builtin_clz(mag) : -1;
-        const int addr = on ? row * 32 + k : (int)(sink - tbl) + lane;
-        if (e < 10) {
-          bool touched, bit;
-          if (kind == 0) {
-            touched = true;
-            bit = v == 0;
-          } else if (kind == 1) {
-            touched = ki <= e;
-            bit = ki < e;
-          } else if (kind == 2) {
-            touched = ki == e;
-            bit = v < 0;
-          } else {
-            touched = ki < e;
-            bit = (mag >> ki) & 1;
-          }
-          const int st = tbl[addr];
-          const int ns = tab[(bit << 8) | st];
-          tbl[addr] = (on && touched) ? ns : st;
-        } else {
-          // slots 10 and 31 take several decisions (e - 9 repeats), sign is slot 21
-          int n = 0;
-          if (kind == 0) n = 1;
-          else if (kind == 1) n = ki < 9 ? 1 : e - 8;
-          else if (kind == 2) n = ki == 10 ? 1 : 0;
-          else n = ki < 9 ? 1 : e - 9;
-          int st = tbl[addr];
-          for (int d = 0; d < n; d++) {
-            int bit;
-            if (kind == 0) bit = 0;
-            else if (kind == 1) bit = ki < 9 ? 1 : (d < e - 9);
-            else if (kind == 2) bit = v < 0;
-            else bit = (mag >> (ki < 9 ? ki : e - 1 - d)) & 1;
-            st = tab[(bit << 8) | st];
-          }
-          tbl[addr] = st;
+      // decode the chunk's 64 symbols at once, one per lane
+      const bool valid = lane < cnt;
+      const int mv = valid ? (int16_t)(mine & 0xFFFF) : 0;
+      const int maddr = valid ? ((int)(mine >> 16) - rowbase) * 32 : 0;
+      if (__ballot(mv >= 1024 || mv <= -1024)) {  // e >= 10 somewhere: one at a time
+        for (int t = 0; t < cnt; t++) {
+          const SymDec d = decode_sym(__builtin_amdgcn_readlane(mine, t));
+          SymDec dl = d;
+          dl.row -= rowbase;
+          walk_long(tbl, tab, dl, lane, kind, ki, sink);
         }
+        continue;
+      }
+      uint32_t mtm, mbm;
+      slot_masks(mv, mtm, mbm);
+      if (!valid) mtm = mbm = 0;
+      for (int t = 0; t < cnt; t += 2) {
+        const int tb = min(t + 1, kStateThreads - 1);
+        const uint64_t T = (uint64_t)__builtin_amdgcn_readlane(mtm, tb) << 32 | __builtin_amdgcn_readlane(mtm, t);
+        const uint64_t Bm = (uint64_t)__builtin_amdgcn_readlane(mbm, tb) << 32 | __builtin_amdgcn_readlane(mbm, t);
+        const int addrA = __builtin_amdgcn_readlane(maddr, t);
+        const int addrB = __builtin_amdgcn_readlane(maddr, tb);
+        const bool haveB = t + 1 < cnt;  // else T/Bm upper words are 0 (invalid lane) or unused
+        const uint32_t touched = (uint32_t)(T >> lane) & 1u;
+        const uint32_t bit = (uint32_t)(Bm >> lane) & 1u;
+        const int addr = (hi ? addrB : addrA) + k;
+        const int st = tbl[addr];
+        uint32_t ns1 = tab[(bit << 8) | st];
+        pin(ns1);
+        // lower half's post-state, seen by the upper half when the rows match
+        const int postA = touched ? (int)ns1 : st;
+        const int fromA = __builtin_amdgcn_permlane32_swap(postA, postA, false, false)[0];
+        const bool same = haveB && addrA == addrB;
+        const int stB = same ? fromA : st;
+        uint32_t ns2 = tab[(bit << 8) | stB];
+        pin(ns2);
+        const int fin = hi ? (touched ? (int)ns2 : stB) : postA;
+        // disjoint rows: both halves write; shared row: the upper half holds both updates
+        const bool wr = hi ? haveB : !same;
+        tbl[wr ? addr : sink + lane] = (uint8_t)fin;
       }
     }
   }
   if (seg.save_states) {
     __syncthreads();
-    copy_states(reinterpret_cast<uint4*>(a.persist + (int64_t)slice * a.state_bytes), t4, n16, lane);
+    copy_states(reinterpret_cast<uint4*>(a.persist + (int64_t)slice * a.state_bytes + goff), t4, n16, lane);
   }
 }
-
 
 // ---------------------------------------------------------------------------
 // Kernel 2b: SIMT Golomb-Rice coder (coder=0; ffv1enc.c:240-370,
@@ -961,9 +1016,9 @@ int launch_code_frames(const CodeArgs& a, void* stream) {
 }
 
 int launch_states(const StateArgs& a, int nsegs, void* stream) {
-  const size_t lds = (size_t)a.state_bytes + 512 + kStateThreads;
+  const size_t lds = (size_t)a.state_bytes / 2 + 512 + kStateThreads;
   if ((int64_t)lds > kStateLdsMax) return -1;
-  dim3 grid((unsigned)(nsegs * a.nslices)), block(kStateThreads);
+  dim3 grid((unsigned)(nsegs * a.nslices * 2)), block(kStateThreads);
   hipLaunchKernelGGL(ffv1_states, grid, block, lds, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
