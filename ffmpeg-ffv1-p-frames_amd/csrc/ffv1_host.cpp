@@ -218,6 +218,7 @@ struct ffv1hip_ctx {
   bool have_states = false;  // persistent states valid (a frame was coded)
   int max_slots = 0;          // segments (= frame slots) per call
   bool frames_mode = false;   // states walk + frame-parallel coder (range coder, LDS-sized tables)
+  int coder_lanes = 16;       // frame-parallel coder: streams per wave (measured: 16 < 32 < 64; 8 and 4 overflow one dispatch round)
   int64_t frame_samples = 0;  // symbols of one frame (each slice padded to 4)
   int max_ops = 0;
   std::vector<SliceGeom> geom;
@@ -478,7 +479,7 @@ static int alloc_device(ffv1hip_ctx* c) {
   HIP_TRY(hipMalloc(&c->d_persist, state_bytes * c->nslices));
   // the coder grid is padded to whole waves and idle lanes touch their own table
   if (c->frames_mode) {
-    const size_t chains = (size_t(nb) * c->nslices + 63) & ~size_t(63);
+    const size_t chains = size_t(nb) * c->nslices + 64;  // + spare tables for idle coder lanes
     HIP_TRY(hipMalloc(&c->d_snap, state_bytes * chains));
     HIP_TRY(hipMalloc(&c->d_sym, sizeof(uint32_t) * size_t(c->frame_samples) * nb));
   } else {
@@ -568,6 +569,8 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
     const char* mode = std::getenv("FFV1HIP_CODER");
     const int64_t lds = int64_t(c->contexts) * 32 + 512 + 64;  // one plane group per walk
     c->frames_mode = p.ac && lds <= kStateLdsMax && !(mode && std::strcmp(mode, "chain") == 0);
+    const char* lanes = std::getenv("FFV1HIP_LANES");  // tuning hook
+    if (lanes) c->coder_lanes = std::max(1, std::min(64, std::atoi(lanes)));
   }
   int rc = alloc_device(c);
   if (rc < 0) {
@@ -724,6 +727,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       return set_err(-5, "states launch failed: %s", hipGetErrorString(hipGetLastError()));
     ca.snap = c->d_snap;
     ca.nframes = n;
+    ca.lanes = c->coder_lanes;
+    ca.spare = int64_t(c->max_batch) * c->nslices;
     if (timed(1, [&] { return launch_code_frames(ca, st); }) < 0)
       return set_err(-5, "code launch failed: %s", hipGetErrorString(hipGetLastError()));
   } else {

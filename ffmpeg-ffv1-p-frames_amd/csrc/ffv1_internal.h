@@ -83,8 +83,10 @@ struct CodeArgs {
   int coded_bits;             // "bits" of encode_line (8 for <=8-bit)
   // frame-parallel mode (launch_code_frames): one lane per (frame, slice),
   // starting from the per-frame state snapshots ffv1_states wrote
-  uint8_t* snap;              // [frame][slice][state_bytes] (grid-padded)
+  uint8_t* snap;              // [frame][slice][state_bytes] + 64 spare tables for idle lanes
   int nframes;
+  int lanes;                  // streams per wave (1..64); the other lanes idle
+  int64_t spare;              // index of the first spare table
 };
 
 // Kernel 2a: the context-state walk.  The adaptive states a slice's range

@@ -249,9 +249,7 @@ __device__ __forceinline__ uint32_t step_b(Lane& L, bool act, int bit, const uin
   constexpr int D = K >> 2, SH = (K & 3) * 8;
   const int s = (L.w<D>() >> SH) & 0xFF;
   rac_sel(L, act, s, bit);
-  uint32_t ns = tab[(bit << 8) | s];
-  pin(ns);
-  return ns;
+  return tab[(bit << 8) | s];
 }
 
 template <int K>
@@ -322,7 +320,6 @@ __device__ __forceinline__ void code_symbol(Lane& L, bool act, bool nz, int v, u
       const int bit = v < 0;
       rac_sel(L, e >= 0, ss, bit);
       nsg = tab[(bit << 8) | ss];
-      pin(nsg);
     }
     insert_b<0>(L, act, n0);
     static_for<0, EM + 1>([&](auto ic) {
@@ -468,17 +465,26 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
   const uint8_t* ftab = tabs + 512;  // frame table
 
   const int lane = threadIdx.x;
-  const int64_t chain = (int64_t)blockIdx.x * kCodeThreads + lane;  // tables exist for the padded grid
+  int64_t chain = (int64_t)blockIdx.x * kCodeThreads + lane;  // tables exist for the padded grid
   int seg_i, slice, f;
   bool live;
   Segment seg{0, 0, 0, 0};
   uint8_t* table;
   if constexpr (FRAMES) {
+    // a.lanes streams per wave: fewer streams, less padding to the wave's
+    // largest exponent; idle lanes work on spare tables
+    const bool used = lane < a.lanes;
+    chain = (int64_t)blockIdx.x * a.lanes + lane;
     f = (int)(chain / a.nslices);
     slice = (int)(chain % a.nslices);
     seg_i = f;
-    live = f < a.nframes;
-    table = a.snap + chain * a.state_bytes;
+    live = used && f < a.nframes;
+    table = a.snap + (live ? chain : a.spare + lane) * a.state_bytes;
+    if (!live) {
+      f = 0;
+      slice = 0;
+      seg_i = 0;
+    }
   } else {
     seg_i = (int)(chain / a.nslices);
     slice = (int)(chain % a.nslices);
@@ -1009,8 +1015,9 @@ int launch_code(const CodeArgs& a, void* stream) {
 }
 
 int launch_code_frames(const CodeArgs& a, void* stream) {
+  if (a.lanes < 1 || a.lanes > kCodeThreads) return -1;
   const int64_t chains = (int64_t)a.nframes * a.nslices;
-  dim3 grid((unsigned)((chains + kCodeThreads - 1) / kCodeThreads)), block(kCodeThreads);
+  dim3 grid((unsigned)((chains + a.lanes - 1) / a.lanes)), block(kCodeThreads);
   hipLaunchKernelGGL(ffv1_code<true>, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
