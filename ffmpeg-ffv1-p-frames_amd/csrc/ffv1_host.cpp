@@ -236,8 +236,12 @@ struct ffv1hip_ctx {
   int64_t* d_packet_size = nullptr;
   uint8_t* d_persist = nullptr;
   uint8_t* d_tables = nullptr;   // [slot][slice][2][contexts][32]
-  uint32_t* d_sym = nullptr;     // [slot][frame_samples]; frames mode: [batch frame][frame_samples]
-  uint8_t* d_snap = nullptr;     // frames mode: [batch frame][slice][state_bytes], grid-padded
+  uint32_t* d_sym = nullptr;     // [slot][frame_samples]; frames mode: 2 x [batch frame][frame_samples]
+  uint8_t* d_snap = nullptr;     // frames mode: 2 x ([batch frame][slice][state_bytes] + spare)
+  uint8_t* d_keys2 = nullptr;    // frames mode: keyflags of the batch the coder stream is on
+  int buf = 0;                   // frames mode: buffer set of the next batch
+  hipStream_t code_stream = nullptr;  // frames mode: ffv1_code + assembly, behind the states walk
+  hipEvent_t walked[2] = {nullptr, nullptr};
   SliceGeom* d_geom = nullptr;
   int* d_slot_frames = nullptr;  // [j][slot]
   int* d_status = nullptr;
@@ -247,7 +251,7 @@ struct ffv1hip_ctx {
   bool profiling = false;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> kev;  // [2 * launches]: start/stop per kernel launch
-  std::vector<int> kev_kind;    // per launch: 0 symbols, 1 code, 2 states
+  std::vector<int> kev_kind;    // per launch: 0 symbols, 1 code, 2 states, 3 assembly
   int nkev = 0;
   int last_nsegs = 0;
 };
@@ -441,7 +445,7 @@ static void build_ops(ffv1hip_ctx* c) {
 static void free_device(ffv1hip_ctx* c) {
   void* ptrs[] = {c->d_frames, c->d_qt, c->d_tabs, c->d_ops, c->d_nops, c->d_segs, c->d_keys,
                   c->d_slice_out, c->d_slice_bytes, c->d_packets, c->d_packet_size, c->d_persist,
-                  c->d_tables, c->d_sym, c->d_snap, c->d_geom, c->d_slot_frames, c->d_status};
+                  c->d_tables, c->d_sym, c->d_snap, c->d_keys2, c->d_geom, c->d_slot_frames, c->d_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (hipEvent_t& e : c->ev)
@@ -449,6 +453,9 @@ static void free_device(ffv1hip_ctx* c) {
   for (hipEvent_t& e : c->kev)
     if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->code_stream) (void)hipStreamDestroy(c->code_stream);
+  for (hipEvent_t& e : c->walked)
+    if (e) (void)hipEventDestroy(e);
 }
 
 static int alloc_device(ffv1hip_ctx* c) {
@@ -479,9 +486,13 @@ static int alloc_device(ffv1hip_ctx* c) {
   HIP_TRY(hipMalloc(&c->d_persist, state_bytes * c->nslices));
   // the coder grid is padded to whole waves and idle lanes touch their own table
   if (c->frames_mode) {
+    // double-buffered: the states walk of batch k+1 runs while batch k codes
     const size_t chains = size_t(nb) * c->nslices + 64;  // + spare tables for idle coder lanes
-    HIP_TRY(hipMalloc(&c->d_snap, state_bytes * chains));
-    HIP_TRY(hipMalloc(&c->d_sym, sizeof(uint32_t) * size_t(c->frame_samples) * nb));
+    HIP_TRY(hipMalloc(&c->d_snap, 2 * state_bytes * chains));
+    HIP_TRY(hipMalloc(&c->d_sym, 2 * sizeof(uint32_t) * size_t(c->frame_samples) * nb));
+    HIP_TRY(hipMalloc(&c->d_keys2, 2 * size_t(nb)));
+    HIP_TRY(hipStreamCreateWithFlags(&c->code_stream, hipStreamNonBlocking));
+    for (hipEvent_t& e : c->walked) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   } else {
     const size_t chains = (size_t(c->max_slots) * c->nslices + 63) & ~size_t(63);
     HIP_TRY(hipMalloc(&c->d_tables, state_bytes * chains));
@@ -625,9 +636,13 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     return set_err(-22, "P-frame without preceding keyframe state");
   segs.front().load_states = !keys[0];
   segs.back().save_states = 1;
-  HIP_TRY(hipMemcpyAsync(c->d_keys, keys.data(), n, hipMemcpyHostToDevice, st));
+  // frames mode: the coder stream may still be on the previous batch, so the
+  // buffers it reads (symbols, snapshots, key flags) alternate between two sets
+  const int fb = c->buf;
+  uint8_t* const d_keys = c->frames_mode ? c->d_keys2 + size_t(fb) * c->max_batch : c->d_keys;
+  hipStream_t const cst = c->frames_mode ? c->code_stream : st;
+  HIP_TRY(hipMemcpyAsync(d_keys, keys.data(), n, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(c->d_segs, segs.data(), segs.size() * sizeof(Segment), hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemsetAsync(c->d_status, 0, sizeof(int) * 4, st));
 
   const int nsegs = int(segs.size());
   if (nsegs > c->max_slots) return set_err(-22, "batch spans %d GOPs (max %d)", nsegs, c->max_slots);
@@ -658,17 +673,22 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   sa.contexts = c->contexts;
   sa.model1 = p.context_model;
   sa.qt = c->d_qt;
-  sa.sym = c->d_sym;
+  uint32_t* const d_sym = c->frames_mode ? c->d_sym + size_t(fb) * c->frame_samples * c->max_batch : c->d_sym;
+  uint8_t* const d_snap =
+      c->frames_mode ? c->d_snap + size_t(fb) * (size_t(c->max_batch) * c->nslices + 64) * 2 * c->contexts * 32
+                     : nullptr;
+  sa.sym = d_sym;
   sa.frame_samples = c->frame_samples;
 
   CodeArgs ca{};
-  ca.sym = c->d_sym;
+  ca.sym = d_sym;
   ca.frame_samples = c->frame_samples;
   ca.geom = c->d_geom;
   ca.nslices = c->nslices;
   ca.nsegs = nsegs;
   ca.segs = c->d_segs;
-  ca.keyflags = c->d_keys;
+  ca.keyflags = d_keys;
+  ca.lanes = kCodeLanesChained;
   ca.ops = c->d_ops;
   ca.nops = c->d_nops;
   ca.max_ops = c->max_ops;
@@ -683,10 +703,9 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   ca.version = p.version;
   ca.coded_bits = p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample;
 
-  c->nkev = 0;
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev[0], st));
   // brackets one launch with events when profiling (kind: 0 symbols, 1 code, 2 states)
-  auto timed = [&](int kind, auto&& launch) -> int {
+  auto timed = [&](int kind, hipStream_t st, auto&& launch) -> int {
     if (c->profiling) {
       while (c->kev.size() < size_t(2) * (c->nkev + 1)) {
         hipEvent_t e;
@@ -711,10 +730,10 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     HIP_TRY(hipMemcpyAsync(c->d_slot_frames, ident.data(), sizeof(int) * n, hipMemcpyHostToDevice, st));
     sa.frame_of_slot = c->d_slot_frames;
     sa.nslots = n;
-    if (timed(0, [&] { return launch_symbols(sa, st); }) < 0)
+    if (timed(0, st, [&] { return launch_symbols(sa, st); }) < 0)
       return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
     StateArgs wa{};
-    wa.sym = c->d_sym;
+    wa.sym = d_sym;
     wa.frame_samples = c->frame_samples;
     wa.geom = c->d_geom;
     wa.nslices = c->nslices;
@@ -722,22 +741,29 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     wa.ftab = c->d_tabs + 512;
     wa.state_bytes = ca.state_bytes;
     wa.persist = c->d_persist;
-    wa.snap = c->d_snap;
-    if (timed(2, [&] { return launch_states(wa, nsegs, st); }) < 0)
+    wa.snap = d_snap;
+    if (timed(2, st, [&] { return launch_states(wa, nsegs, st); }) < 0)
       return set_err(-5, "states launch failed: %s", hipGetErrorString(hipGetLastError()));
-    ca.snap = c->d_snap;
+    // the coder stream continues once this batch's walk is done; the walk of
+    // the next batch (on st) then overlaps this batch's coding
+    HIP_TRY(hipEventRecord(c->walked[fb], st));
+    HIP_TRY(hipStreamWaitEvent(cst, c->walked[fb], 0));
+    HIP_TRY(hipMemsetAsync(c->d_status, 0, sizeof(int) * 4, cst));
+    ca.snap = d_snap;
     ca.nframes = n;
     ca.lanes = c->coder_lanes;
     ca.spare = int64_t(c->max_batch) * c->nslices;
-    if (timed(1, [&] { return launch_code_frames(ca, st); }) < 0)
+    if (timed(1, cst, [&] { return launch_code_frames(ca, cst); }) < 0)
       return set_err(-5, "code launch failed: %s", hipGetErrorString(hipGetLastError()));
+    c->buf ^= 1;
   } else {
+    HIP_TRY(hipMemsetAsync(c->d_status, 0, sizeof(int) * 4, st));
     for (int j = 0; j < maxlen; j++) {
       sa.frame_of_slot = c->d_slot_frames + size_t(j) * nsegs;
-      if (timed(0, [&] { return launch_symbols(sa, st); }) < 0)
+      if (timed(0, st, [&] { return launch_symbols(sa, st); }) < 0)
         return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
       ca.j = j;
-      if (timed(1, [&] { return p.ac ? launch_code(ca, st) : launch_code_golomb(ca, st); }) < 0)
+      if (timed(1, st, [&] { return p.ac ? launch_code(ca, st) : launch_code_golomb(ca, st); }) < 0)
         return set_err(-5, "code launch failed: %s", hipGetErrorString(hipGetLastError()));
     }
   }
@@ -753,9 +779,9 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   b.nslices = c->nslices;
   b.version = p.version;
   b.ec = p.ec;
-  if (c->profiling) HIP_TRY(hipEventRecord(c->ev[1], st));
-  if (launch_assemble(b, n, st) < 0) return set_err(-5, "assemble launch failed");
-  if (c->profiling) HIP_TRY(hipEventRecord(c->ev[2], st));
+  if (c->profiling) HIP_TRY(hipEventRecord(c->ev[1], cst));
+  if (timed(3, cst, [&] { return launch_assemble(b, n, cst); }) < 0) return set_err(-5, "assemble launch failed");
+  if (c->profiling) HIP_TRY(hipEventRecord(c->ev[2], cst));
 
   c->picture_number += n;
   c->have_states = true;
@@ -793,6 +819,14 @@ int ffv1hip_fetch(ffv1hip_ctx* c, uint8_t* out, int64_t out_cap, int64_t* sizes,
     if (sizes) sizes[i] = sz[i];
     if (key_flags) key_flags[i] = c->last_keys[i];
   }
+  return 0;
+}
+
+int ffv1hip_synchronize(ffv1hip_ctx* c) {
+  if (!c) return set_err(-22, "null ctx");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->code_stream) HIP_TRY(hipStreamSynchronize(c->code_stream));
   return 0;
 }
 
@@ -843,6 +877,7 @@ int ffv1hip_set_profiling(ffv1hip_ctx* c, int enable) {
   for (hipEvent_t& e : c->ev)
     if (!e) HIP_TRY(hipEventCreate(&e));
   c->profiling = enable != 0;
+  c->nkev = 0;  // kernel stats accumulate from here
   return 0;
 }
 
@@ -869,13 +904,10 @@ int ffv1hip_last_kernel_stats(ffv1hip_ctx* c, ffv1hip_kernel_stats* out) {
     switch (c->kev_kind[j]) {
       case 0: s.symbols_ms += ms; s.symbols_launches++; break;
       case 1: s.code_ms += ms; s.code_launches++; break;
-      default: s.states_ms += ms; s.states_launches++; break;
+      case 2: s.states_ms += ms; s.states_launches++; break;
+      default: s.assemble_ms += ms; s.assemble_launches++; break;
     }
   }
-  float asmb = 0.f;
-  HIP_TRY(hipEventElapsedTime(&asmb, c->ev[1], c->ev[2]));
-  s.assemble_ms = asmb;
-  s.assemble_launches = 1;
   s.frames_coded_per_launch_max = c->last_nsegs;
   *out = s;
   return 0;
@@ -897,6 +929,7 @@ int ffv1hip_set_slice_states(ffv1hip_ctx* c, const uint8_t* buf, int64_t size) {
   const int64_t n = int64_t(2) * c->contexts * 32 * c->nslices;
   if (size != n) return set_err(-22, "state blob is %lld bytes, expected %lld", (long long)size, (long long)n);
   HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(c->d_persist, buf, n, hipMemcpyHostToDevice));
   c->have_states = true;
   return 0;

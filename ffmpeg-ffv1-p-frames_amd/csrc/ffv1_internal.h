@@ -20,6 +20,7 @@ struct Op {
 };
 static_assert(sizeof(Op) == 8, "op layout");
 constexpr int kMaxOps = 512;
+constexpr int kCodeLanesChained = 64;  // chained coder: one stream per lane of a full wave
 constexpr int kOpSets = 8;
 
 // A run of consecutive frames of one batch whose context states chain

@@ -110,8 +110,10 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
 // branch costs ~66 cycles on gfx950 (tools/ubench), more than the ~20 VALU
 // ops of a whole decision, and with 64 independent streams per wave some lane
 // renormalises on almost every decision anyway.
-constexpr int kRing = 128;       // renorm digits per lane held in LDS before a flush
-constexpr int kFlushAt = 59;     // flush when any lane holds more (2 steps x 34 digits fit)
+constexpr int kRing = 96;        // renorm digits per lane held in LDS before a flush
+constexpr int kRingStride = kRing + 1;  // [lane][kRing + 1]: lanes at equal heads hit distinct banks
+constexpr int kFlushAt = kRing - 69;    // checked every second symbol step (<= 34 digits per symbol)
+constexpr int kHeaderFlushAt = kRing - 30;  // per header op (host-checked |value| < 2^14: <= 29 digits)
 
 // Keeps a value's computation where it is written: without it the compiler
 // sinks the successor-state lookups of lanes that may be idle into an
@@ -122,7 +124,7 @@ struct Lane {
   int low, range;
   uint32_t r0, r1, r2, r3, r4, r5, r6, r7;  // states of the current context row (byte k = slot k)
   int dc;              // digits in the LDS ring
-  uint32_t* ring;      // this lane's ring column (LDS, stride kWave)
+  uint32_t* ring;      // this lane's ring row (LDS)
 
   template <int D>
   __device__ __forceinline__ uint32_t& w() {
@@ -196,14 +198,14 @@ __device__ __forceinline__ Sink make_sink(uint8_t* out, int64_t cap) {
 // advances when a byte is really shifted out.
 __device__ __forceinline__ void renorm(Lane& L) {
   const bool need = L.range < 0x100;
-  L.ring[L.dc * kWave] = (uint32_t)L.low;
+  L.ring[L.dc] = (uint32_t)L.low;
   L.dc += need ? 1 : 0;
   L.low = need ? ((L.low & 0xFF) << 8) : L.low;
   L.range = need ? (L.range << 8) : L.range;
 }
 
 __device__ __forceinline__ void flush(Lane& L, Sink& S) {
-  for (int t = 0; t < L.dc; t++) S.digit((int)L.ring[t * kWave]);
+  for (int t = 0; t < L.dc; t++) S.digit((int)L.ring[t]);
   L.dc = 0;
 }
 
@@ -404,7 +406,6 @@ constexpr int kCodeThreads = kWave;
 constexpr int kOpsetBytes = kOpSets * 32;
 
 // Key bit / in-band v0/v1 header / v3 slice header (per-lane op program).
-// One op codes at most 65 decisions.
 __device__ __forceinline__ void run_header_ops(const CodeArgs& a, Lane& L, Sink& S, uint8_t* os, int key,
                                                int slice, bool live, const uint8_t* dtab,
                                                const uint8_t* ftab) {
@@ -422,7 +423,7 @@ __device__ __forceinline__ void run_header_ops(const CodeArgs& a, Lane& L, Sink&
       else
         symbol_lds(L, st, op.value, op.kind == kOpSymS, t);
     }
-    flush_if(L, S, kRing - 67);
+    flush_if(L, S, kHeaderFlushAt);
   }
 }
 
@@ -454,13 +455,20 @@ __device__ __forceinline__ int64_t terminate(Lane& L, Sink& S, bool state129) {
 // segment, the chain's states carried in `tables` from frame to frame.
 // FRAMES = true: one lane per (frame, slice) of the whole batch, each
 // starting from the snapshot ffv1_states wrote for its frame.
+// Dynamic LDS for a.lanes streams (+1 column shared by idle lanes).
+__host__ __device__ constexpr size_t code_lds_bytes(int lanes) {
+  return 1024 + (size_t)(lanes + 1) * (kOpsetBytes + kRingStride * 4);
+}
+
 template <bool FRAMES>
 __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t tabs[1024];
-  __shared__ __attribute__((aligned(16))) uint8_t opsets[kCodeThreads * kOpsetBytes];
-  __shared__ uint32_t ring[kRing * kWave];
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t* const tabs = lds;
+  uint8_t* const opsets = lds + 1024;                                           // [col][kOpsetBytes]
+  uint32_t* const ring = reinterpret_cast<uint32_t*>(opsets + (a.lanes + 1) * kOpsetBytes);  // [col][stride]
   for (int i = threadIdx.x; i < 1024; i += kCodeThreads) tabs[i] = a.tabs[i];
   __syncthreads();
+  const int col = min((int)threadIdx.x, a.lanes);  // idle lanes share the spare column
   const uint8_t* dtab = tabs;        // default table (key bit, v0/v1 header)
   const uint8_t* ftab = tabs + 512;  // frame table
 
@@ -508,11 +516,11 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
   }
 
   Lane L;
-  lane_init(L, ring + lane);
+  lane_init(L, ring + col * kRingStride);
   uint8_t* const out = a.slice_out + ((int64_t)(live ? f : 0) * a.nslices + slice) * a.slice_cap;
   Sink S = make_sink(out, live ? a.slice_cap : 0);  // idle lanes write nothing
 
-  run_header_ops(a, L, S, opsets + lane * kOpsetBytes, key, slice, live, dtab, ftab);
+  run_header_ops(a, L, S, opsets + col * kOpsetBytes, key, slice, live, dtab, ftab);
 
   const SliceGeom& g = a.geom[slice];
   const int64_t nsym = live ? g.nsym : 0;
@@ -822,7 +830,7 @@ __device__ __forceinline__ void vlc_put(BitSink& b, uint64_t& rec, int v, int bi
 __global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t tabs[1024];
   __shared__ __attribute__((aligned(16))) uint8_t opsets[kCodeThreads * kOpsetBytes];
-  __shared__ uint32_t ring[kRing * kWave];
+  __shared__ uint32_t ring[kRingStride * kWave];
   for (int i = threadIdx.x; i < 1024; i += kCodeThreads) tabs[i] = a.tabs[i];
   __syncthreads();
   const int lane = threadIdx.x;
@@ -849,7 +857,7 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
   // range-coded prefix: key bit / header / slice header, then (v3) a 0 on
   // state 129 and ff_rac_terminate (ffv1enc.c:1173-1183)
   Lane L;
-  lane_init(L, ring + lane);
+  lane_init(L, ring + lane * kRingStride);
   uint8_t* const out = a.slice_out + ((int64_t)(live ? f : 0) * a.nslices + slice) * a.slice_cap;
   Sink S = make_sink(out, live ? a.slice_cap : 0);  // idle lanes write nothing
   run_header_ops(a, L, S, opsets + lane * kOpsetBytes, key, slice, live, tabs, tabs + 512);
@@ -1010,7 +1018,8 @@ int launch_symbols(const SymbolArgs& a, void* stream) {
 int launch_code(const CodeArgs& a, void* stream) {
   const int64_t chains = (int64_t)a.nsegs * a.nslices;
   dim3 grid((unsigned)((chains + kCodeThreads - 1) / kCodeThreads)), block(kCodeThreads);
-  hipLaunchKernelGGL(ffv1_code<false>, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
+  if (a.lanes != kCodeThreads) return -1;
+  hipLaunchKernelGGL(ffv1_code<false>, grid, block, code_lds_bytes(a.lanes), reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1018,7 +1027,7 @@ int launch_code_frames(const CodeArgs& a, void* stream) {
   if (a.lanes < 1 || a.lanes > kCodeThreads) return -1;
   const int64_t chains = (int64_t)a.nframes * a.nslices;
   dim3 grid((unsigned)((chains + a.lanes - 1) / a.lanes)), block(kCodeThreads);
-  hipLaunchKernelGGL(ffv1_code<true>, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
+  hipLaunchKernelGGL(ffv1_code<true>, grid, block, code_lds_bytes(a.lanes), reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

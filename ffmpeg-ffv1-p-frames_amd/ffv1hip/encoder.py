@@ -58,7 +58,7 @@ EXPORTED_SYMBOLS = (
     "ffv1hip_device_packets", "ffv1hip_picture_number", "ffv1hip_reset",
     "ffv1hip_get_slice_states", "ffv1hip_set_slice_states", "ffv1hip_last_error",
     "ffv1hip_abi_version", "ffv1hip_set_profiling", "ffv1hip_last_kernel_ms",
-    "ffv1hip_last_kernel_stats",
+    "ffv1hip_last_kernel_stats", "ffv1hip_synchronize",
 )
 
 
@@ -99,6 +99,8 @@ def load_library():
     L.ffv1hip_encode_device.restype = ctypes.c_int
     L.ffv1hip_fetch.argtypes = [vp, u8p, i64, P(i64), P(ctypes.c_int)]
     L.ffv1hip_fetch.restype = ctypes.c_int
+    L.ffv1hip_synchronize.argtypes = [vp]
+    L.ffv1hip_synchronize.restype = ctypes.c_int
     L.ffv1hip_device_packets.argtypes = [vp, P(vp), P(i64), P(vp)]
     L.ffv1hip_device_packets.restype = ctypes.c_int
     L.ffv1hip_picture_number.argtypes = [vp]
@@ -240,6 +242,12 @@ class HipEncoder:
             res.append((out[pos:pos + sizes[i]].tobytes(), bool(keys[i])))
             pos += sizes[i]
         return res
+
+    def synchronize(self) -> None:
+        """Wait for all of the encoder's queued work (encode_device is asynchronous)."""
+        rc = load_library().ffv1hip_synchronize(self._h)
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_synchronize")
 
     def device_packets(self):
         L = load_library()

@@ -91,12 +91,17 @@ int ffv1hip_encode(ffv1hip_ctx *ctx, const void *const *planes,
 
 /* Device-resident variant: frames already in HBM at d_frames + i*frame_bytes
  * with plane p at byte offset plane_offset[p] and row stride plane_stride[p].
- * Encodes on `stream` (a hipStream_t, may be NULL) and leaves the packets in
- * HBM; nothing is synchronised.  Use ffv1hip_fetch to read them back. */
+ * The frames are read on `stream` (a hipStream_t, may be NULL: the context's
+ * own stream); the coding may continue on the context's internal stream so
+ * that consecutive calls overlap.  Nothing is synchronised: the packets are
+ * valid after ffv1hip_synchronize or ffv1hip_fetch. */
 int ffv1hip_encode_device(ffv1hip_ctx *ctx, const void *d_frames,
                           int64_t frame_bytes, const int64_t plane_offset[3],
                           const int plane_stride[3], int n_frames,
                           void *stream);
+
+/* Waits for all work of the context (every stream it uses). */
+int ffv1hip_synchronize(ffv1hip_ctx *ctx);
 
 /* Synchronises and copies the packets of the last encode_device call. */
 int ffv1hip_fetch(ffv1hip_ctx *ctx, uint8_t *out, int64_t out_cap,
@@ -126,10 +131,12 @@ int     ffv1hip_set_slice_states(ffv1hip_ctx *ctx, const uint8_t *buf,
 int ffv1hip_set_profiling(ffv1hip_ctx *ctx, int enable);
 int ffv1hip_last_kernel_ms(ffv1hip_ctx *ctx, float *encode_ms, float *assemble_ms);
 
-/* Per-kernel totals of the last call (profiling enabled): summed HIP-event
- * durations and launch counts of ffv1_symbols (prediction/context, one
- * launch per frame index of the GOP), ffv1_code (range coder, same count)
- * and ffv1_assemble_packets (one launch). */
+/* Per-kernel totals of every call since profiling was (re)enabled: summed
+ * HIP-event durations (events on each kernel's own stream) and launch counts
+ * of ffv1_symbols (prediction/context), ffv1_states (context-state walk,
+ * frame-parallel mode), ffv1_code (range coder) and ffv1_assemble_packets.
+ * Frame-parallel mode launches each once per call; the chained mode launches
+ * symbols and code once per frame index of the GOP. */
 typedef struct ffv1hip_kernel_stats {
     float symbols_ms, code_ms, assemble_ms;
     int symbols_launches, code_launches, assemble_launches;
