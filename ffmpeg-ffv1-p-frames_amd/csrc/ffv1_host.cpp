@@ -217,8 +217,8 @@ struct ffv1hip_ctx {
   int64_t picture_number = 0;
   bool have_states = false;  // persistent states valid (a frame was coded)
   int max_slots = 0;          // segments (= frame slots) per call
-  bool frames_mode = false;   // states walk + frame-parallel coder (range coder, LDS-sized tables)
-  int coder_lanes = 16;       // frame-parallel coder: streams per wave (measured: 16 < 32 < 64; 8 and 4 overflow one dispatch round)
+  bool frames_mode = false;   // states walk + decision-stream coder (range coder, LDS-sized tables)
+  int wmax = 0;               // most decisions one symbol can take (2 * coded bits + 1)
   int64_t frame_samples = 0;  // symbols of one frame (each slice padded to 4)
   int max_ops = 0;
   std::vector<SliceGeom> geom;
@@ -236,12 +236,20 @@ struct ffv1hip_ctx {
   int64_t* d_packet_size = nullptr;
   uint8_t* d_persist = nullptr;
   uint8_t* d_tables = nullptr;   // [slot][slice][2][contexts][32]
-  uint32_t* d_sym = nullptr;     // [slot][frame_samples]; frames mode: 2 x [batch frame][frame_samples]
-  uint8_t* d_snap = nullptr;     // frames mode: 2 x ([batch frame][slice][state_bytes] + spare)
-  uint8_t* d_keys2 = nullptr;    // frames mode: keyflags of the batch the coder stream is on
-  int buf = 0;                   // frames mode: buffer set of the next batch
-  hipStream_t code_stream = nullptr;  // frames mode: ffv1_code + assembly, behind the states walk
+  uint32_t* d_sym = nullptr;     // [slot][frame_samples]; frames mode: walk records (uint4), 2 x [batch frame][frame_samples]
+  // frames mode, two buffer sets: the walk of batch k+1 runs while batch k codes
+  uint8_t* d_keys2 = nullptr;    // 2 x [batch frame] keyflags
+  int* d_dcount = nullptr;       // 2 x [batch frame][slice][3] decisions per plane
+  int64_t* d_dbase = nullptr;    // 2 x [batch frame][slice] first decision of each stream
+  int64_t* d_dtotal = nullptr;   // [2] decisions of the batch (incl. alignment)
+  int64_t* h_dtotal = nullptr;   // pinned readback of d_dtotal
+  uint8_t* d_pre[2] = {nullptr, nullptr};    // [decision] state before the decision
+  uint32_t* d_bits[2] = {nullptr, nullptr};  // [decision / 32] decision bits
+  int64_t dcap[2] = {0, 0};      // decisions d_pre/d_bits hold
+  int buf = 0;                   // buffer set of the next batch
+  hipStream_t code_stream = nullptr;  // ffv1_dcode + assembly, behind the states walk
   hipEvent_t walked[2] = {nullptr, nullptr};
+  hipEvent_t coded[2] = {nullptr, nullptr};  // the coder of the batch that last used set k is done
   SliceGeom* d_geom = nullptr;
   int* d_slot_frames = nullptr;  // [j][slot]
   int* d_status = nullptr;
@@ -445,9 +453,11 @@ static void build_ops(ffv1hip_ctx* c) {
 static void free_device(ffv1hip_ctx* c) {
   void* ptrs[] = {c->d_frames, c->d_qt, c->d_tabs, c->d_ops, c->d_nops, c->d_segs, c->d_keys,
                   c->d_slice_out, c->d_slice_bytes, c->d_packets, c->d_packet_size, c->d_persist,
-                  c->d_tables, c->d_sym, c->d_snap, c->d_keys2, c->d_geom, c->d_slot_frames, c->d_status};
+                  c->d_tables, c->d_sym, c->d_keys2, c->d_dcount, c->d_dbase, c->d_dtotal, c->d_pre[0],
+                  c->d_pre[1], c->d_bits[0], c->d_bits[1], c->d_geom, c->d_slot_frames, c->d_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  if (c->h_dtotal) (void)hipHostFree(c->h_dtotal);
   for (hipEvent_t& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t& e : c->kev)
@@ -456,6 +466,24 @@ static void free_device(ffv1hip_ctx* c) {
   if (c->code_stream) (void)hipStreamDestroy(c->code_stream);
   for (hipEvent_t& e : c->walked)
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t& e : c->coded)
+    if (e) (void)hipEventDestroy(e);
+}
+
+// Decision-stream buffers of set k for `need` decisions.  The set's previous
+// user (the coder of batch k-2) must be done: the caller waits on coded[k].
+static int grow_decisions(ffv1hip_ctx* c, int k, int64_t need) {
+  if (need <= c->dcap[k]) return 0;
+  if (c->d_pre[k]) HIP_TRY(hipFree(c->d_pre[k]));
+  if (c->d_bits[k]) HIP_TRY(hipFree(c->d_bits[k]));
+  c->d_pre[k] = nullptr;
+  c->d_bits[k] = nullptr;
+  c->dcap[k] = 0;
+  const int64_t cap = (need + 4095) & ~int64_t(4095);
+  HIP_TRY(hipMalloc(&c->d_pre[k], size_t(cap)));
+  HIP_TRY(hipMalloc(&c->d_bits[k], size_t(cap / 8)));
+  c->dcap[k] = cap;
+  return 0;
 }
 
 static int alloc_device(ffv1hip_ctx* c) {
@@ -487,12 +515,23 @@ static int alloc_device(ffv1hip_ctx* c) {
   // the coder grid is padded to whole waves and idle lanes touch their own table
   if (c->frames_mode) {
     // double-buffered: the states walk of batch k+1 runs while batch k codes
-    const size_t chains = size_t(nb) * c->nslices + 64;  // + spare tables for idle coder lanes
-    HIP_TRY(hipMalloc(&c->d_snap, 2 * state_bytes * chains));
-    HIP_TRY(hipMalloc(&c->d_sym, 2 * sizeof(uint32_t) * size_t(c->frame_samples) * nb));
+    HIP_TRY(hipMalloc(&c->d_sym, 2 * sizeof(uint4) * size_t(c->frame_samples) * nb));  // walk records
     HIP_TRY(hipMalloc(&c->d_keys2, 2 * size_t(nb)));
+    HIP_TRY(hipMalloc(&c->d_dcount, 2 * sizeof(int) * 3 * size_t(nb) * c->nslices));
+    HIP_TRY(hipMalloc(&c->d_dbase, 2 * sizeof(int64_t) * size_t(nb) * c->nslices));
+    HIP_TRY(hipMalloc(&c->d_dtotal, 2 * sizeof(int64_t)));
+    HIP_TRY(hipHostMalloc(&c->h_dtotal, 2 * sizeof(int64_t), hipHostMallocDefault));
     HIP_TRY(hipStreamCreateWithFlags(&c->code_stream, hipStreamNonBlocking));
     for (hipEvent_t& e : c->walked) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (hipEvent_t& e : c->coded) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    // decision capacity: the worst case when it is small, else ~12 per symbol
+    // (real content codes ~10); a batch that needs more grows the set
+    const int64_t align = int64_t(nb) * c->nslices * kStreamAlign;
+    const int64_t worst = int64_t(nb) * c->frame_samples * c->wmax + align;
+    const int64_t guess = int64_t(nb) * c->frame_samples * 12 + align;
+    const int64_t cap = worst <= (int64_t(1) << 31) ? worst : std::min(worst, guess);
+    for (int k = 0; k < 2; k++)
+      if (grow_decisions(c, k, cap) < 0) return -5;
   } else {
     const size_t chains = (size_t(c->max_slots) * c->nslices + 63) & ~size_t(63);
     HIP_TRY(hipMalloc(&c->d_tables, state_bytes * chains));
@@ -502,6 +541,7 @@ static int alloc_device(ffv1hip_ctx* c) {
   HIP_TRY(hipMemcpy(c->d_geom, c->geom.data(), sizeof(SliceGeom) * c->nslices, hipMemcpyHostToDevice));
   HIP_TRY(hipMalloc(&c->d_slot_frames, sizeof(int) * size_t(c->max_slots) * (nb + 1)));
   HIP_TRY(hipMalloc(&c->d_status, sizeof(int) * 4));
+  HIP_TRY(hipMemset(c->d_status, 0, sizeof(int) * 4));
   return 0;
 }
 
@@ -573,15 +613,15 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
                                 : max_batch_frames;
   c->max_ops = 0;
   for (int v : c->nops) c->max_ops = std::max(c->max_ops, v);
-  // Range coder with a table that fits the states walk's LDS: code all frames
-  // of a batch in parallel from per-frame state snapshots.  FFV1HIP_CODER=chain
-  // keeps the chained per-GOP coder (a test hook: both must give equal bytes).
+  // Range coder with a table that fits the states walk's LDS: walk the
+  // context states per GOP, recording every decision's state, then code all
+  // (frame, slice) streams of a batch in parallel.  FFV1HIP_CODER=chain keeps
+  // the chained per-GOP coder (a test hook: both must give equal bytes).
   {
     const char* mode = std::getenv("FFV1HIP_CODER");
-    const int64_t lds = int64_t(c->contexts) * 32 + 512 + 64;  // one plane group per walk
-    c->frames_mode = p.ac && lds <= kStateLdsMax && !(mode && std::strcmp(mode, "chain") == 0);
-    const char* lanes = std::getenv("FFV1HIP_LANES");  // tuning hook
-    if (lanes) c->coder_lanes = std::max(1, std::min(64, std::atoi(lanes)));
+    const int64_t lds = walk_lds_bytes(int64_t(2) * c->contexts * 32);
+    c->frames_mode = p.ac && lds <= kWalkLdsMax && !(mode && std::strcmp(mode, "chain") == 0);
+    c->wmax = 2 * (p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample) + 1;
   }
   int rc = alloc_device(c);
   if (rc < 0) {
@@ -637,10 +677,14 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   segs.front().load_states = !keys[0];
   segs.back().save_states = 1;
   // frames mode: the coder stream may still be on the previous batch, so the
-  // buffers it reads (symbols, snapshots, key flags) alternate between two sets
+  // buffers it reads alternate between two sets; set fb was last read by the
+  // coder of batch k-2, which must be done before this batch rewrites it
   const int fb = c->buf;
   uint8_t* const d_keys = c->frames_mode ? c->d_keys2 + size_t(fb) * c->max_batch : c->d_keys;
-  hipStream_t const cst = c->frames_mode ? c->code_stream : st;
+  // FFV1HIP_SERIAL=1 (measurement hook): no walk/code overlap
+  static const bool serial = std::getenv("FFV1HIP_SERIAL") && std::atoi(std::getenv("FFV1HIP_SERIAL"));
+  hipStream_t const cst = c->frames_mode && !serial ? c->code_stream : st;
+  if (c->frames_mode) HIP_TRY(hipStreamWaitEvent(st, c->coded[fb], 0));
   HIP_TRY(hipMemcpyAsync(d_keys, keys.data(), n, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(c->d_segs, segs.data(), segs.size() * sizeof(Segment), hipMemcpyHostToDevice, st));
 
@@ -673,10 +717,11 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   sa.contexts = c->contexts;
   sa.model1 = p.context_model;
   sa.qt = c->d_qt;
-  uint32_t* const d_sym = c->frames_mode ? c->d_sym + size_t(fb) * c->frame_samples * c->max_batch : c->d_sym;
-  uint8_t* const d_snap =
-      c->frames_mode ? c->d_snap + size_t(fb) * (size_t(c->max_batch) * c->nslices + 64) * 2 * c->contexts * 32
-                     : nullptr;
+  uint32_t* const d_sym = c->frames_mode ? nullptr : c->d_sym;
+  uint4* const d_rec =
+      c->frames_mode ? reinterpret_cast<uint4*>(c->d_sym) + size_t(fb) * c->frame_samples * c->max_batch : nullptr;
+  int* const d_dcount = c->frames_mode ? c->d_dcount + size_t(fb) * 3 * c->max_batch * c->nslices : nullptr;
+  int64_t* const d_dbase = c->frames_mode ? c->d_dbase + size_t(fb) * c->max_batch * c->nslices : nullptr;
   sa.sym = d_sym;
   sa.frame_samples = c->frame_samples;
 
@@ -688,7 +733,6 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   ca.nsegs = nsegs;
   ca.segs = c->d_segs;
   ca.keyflags = d_keys;
-  ca.lanes = kCodeLanesChained;
   ca.ops = c->d_ops;
   ca.nops = c->d_nops;
   ca.max_ops = c->max_ops;
@@ -724,16 +768,32 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     return rc;
   };
   if (c->frames_mode) {
-    // symbols of every frame, the states walk, then all (frame, slice) streams at once
+    // symbols of every frame, the decision layout, the states walk, then all
+    // (frame, slice) streams at once
     std::vector<int> ident(n);
     for (int i = 0; i < n; i++) ident[i] = i;
     HIP_TRY(hipMemcpyAsync(c->d_slot_frames, ident.data(), sizeof(int) * n, hipMemcpyHostToDevice, st));
     sa.frame_of_slot = c->d_slot_frames;
     sa.nslots = n;
+    sa.dcount = d_dcount;
+    sa.rec = d_rec;
     if (timed(0, st, [&] { return launch_symbols(sa, st); }) < 0)
       return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
-    StateArgs wa{};
-    wa.sym = d_sym;
+    if (timed(0, st, [&] { return launch_layout(d_dcount, n * c->nslices, d_dbase, c->d_dtotal + fb, st); }) < 0)
+      return set_err(-5, "layout launch failed: %s", hipGetErrorString(hipGetLastError()));
+    // decisions of this batch: the worst case fits without asking the device
+    int64_t need = int64_t(n) * c->frame_samples * c->wmax + int64_t(n) * c->nslices * kStreamAlign;
+    if (need > c->dcap[fb]) {
+      HIP_TRY(hipMemcpyAsync(c->h_dtotal + fb, c->d_dtotal + fb, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));  // also: set fb's previous coder is done (waited above)
+      need = c->h_dtotal[fb];
+      if (need > c->dcap[fb] && grow_decisions(c, fb, need + need / 8) < 0)
+        return set_err(-12, "decision buffers for %lld decisions: %s", (long long)need, g_err);
+    }
+    HIP_TRY(hipMemsetAsync(c->d_bits[fb], 0, size_t((need + 31) / 32) * 4, st));
+    DecisionStream ds{d_dcount, d_dbase, c->d_pre[fb], c->d_bits[fb]};
+    WalkArgs wa{};
+    wa.rec = d_rec;
     wa.frame_samples = c->frame_samples;
     wa.geom = c->d_geom;
     wa.nslices = c->nslices;
@@ -741,23 +801,18 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     wa.ftab = c->d_tabs + 512;
     wa.state_bytes = ca.state_bytes;
     wa.persist = c->d_persist;
-    wa.snap = d_snap;
-    if (timed(2, st, [&] { return launch_states(wa, nsegs, st); }) < 0)
-      return set_err(-5, "states launch failed: %s", hipGetErrorString(hipGetLastError()));
+    wa.ds = ds;
+    if (timed(2, st, [&] { return launch_walk(wa, nsegs, st); }) < 0)
+      return set_err(-5, "walk launch failed: %s", hipGetErrorString(hipGetLastError()));
     // the coder stream continues once this batch's walk is done; the walk of
     // the next batch (on st) then overlaps this batch's coding
     HIP_TRY(hipEventRecord(c->walked[fb], st));
     HIP_TRY(hipStreamWaitEvent(cst, c->walked[fb], 0));
-    HIP_TRY(hipMemsetAsync(c->d_status, 0, sizeof(int) * 4, cst));
-    ca.snap = d_snap;
     ca.nframes = n;
-    ca.lanes = c->coder_lanes;
-    ca.spare = int64_t(c->max_batch) * c->nslices;
-    if (timed(1, cst, [&] { return launch_code_frames(ca, cst); }) < 0)
+    ca.ds = ds;
+    if (timed(1, cst, [&] { return launch_dcode(ca, cst); }) < 0)
       return set_err(-5, "code launch failed: %s", hipGetErrorString(hipGetLastError()));
-    c->buf ^= 1;
   } else {
-    HIP_TRY(hipMemsetAsync(c->d_status, 0, sizeof(int) * 4, st));
     for (int j = 0; j < maxlen; j++) {
       sa.frame_of_slot = c->d_slot_frames + size_t(j) * nsegs;
       if (timed(0, st, [&] { return launch_symbols(sa, st); }) < 0)
@@ -782,6 +837,10 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev[1], cst));
   if (timed(3, cst, [&] { return launch_assemble(b, n, cst); }) < 0) return set_err(-5, "assemble launch failed");
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev[2], cst));
+  if (c->frames_mode) {
+    HIP_TRY(hipEventRecord(c->coded[fb], cst));
+    c->buf ^= 1;
+  }
 
   c->picture_number += n;
   c->have_states = true;
@@ -805,7 +864,10 @@ int ffv1hip_fetch(ffv1hip_ctx* c, uint8_t* out, int64_t out_cap, int64_t* sizes,
   HIP_TRY(hipDeviceSynchronize());
   int status[4];
   HIP_TRY(hipMemcpy(status, c->d_status, sizeof(status), hipMemcpyDeviceToHost));
-  if (status[0]) return set_err(-28, "%d slices exceeded the slice byte budget", status[0]);
+  if (status[0]) {  // counted since the last fetch
+    HIP_TRY(hipMemset(c->d_status, 0, sizeof(status)));
+    return set_err(-28, "%d slices exceeded the slice byte budget", status[0]);
+  }
   const int n = c->last_n;
   std::vector<int64_t> sz(n);
   HIP_TRY(hipMemcpy(sz.data(), c->d_packet_size, sizeof(int64_t) * n, hipMemcpyDeviceToHost));

@@ -2,6 +2,7 @@
 // of the MI355X FFV1 encoder.  Not part of the public C-ABI (include/ffv1hip.h).
 #pragma once
 
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace ffv1hip {
@@ -57,10 +58,37 @@ struct SymbolArgs {
   const int16_t* qt;          // [5][256]
   uint32_t* sym;              // [slot][frame_samples]: (row << 16) | (uint16)diff
   int64_t frame_samples;
+  int* dcount;                // optional [slot][slice][3]: range-coder decisions per plane
+  uint4* rec;                 // optional, instead of sym: [slot][frame_samples] walk records
 };
 
-// Kernel 2: the SIMT range coder, one lane per (segment, slice) chain, one
-// frame of every segment per launch.
+// Walk record of one sample (frame-parallel mode), written by ffv1_symbols.
+// A plane is walked in chunks of 64 consecutive samples (one per lane).
+//   x: row * 32 inside the plane group's table (bits 0..15) | (int16)diff << 16
+//   y, z: two bits per slot (slots 0..15, 16..31): 0/1 the slot's decision
+//         bit, 2 no decision (only for |diff| < 1024; see walk_long)
+//   w: D | (D + 2e) << 16, D = the symbol's first decision counted from the
+//      start of its chunk; bit 31: same row as the previous sample of the
+//      chunk
+constexpr uint32_t kRecSame = 0x80000000u;
+
+// Decision stream of one batch (frame-parallel mode).  Every (frame, slice)
+// stream's binary decisions, in coding order, start at decision index
+// dbase[frame][slice] (a multiple of 64); decision d has its adaptive state
+// as it stood before the decision in pre[d] and its value in bit d of
+// bits[] (bit d & 31 of word d >> 5).
+struct DecisionStream {
+  const int* dcount;          // [frame][slice][3] decisions per plane
+  const int64_t* dbase;       // [frame][slice]
+  uint8_t* pre;
+  uint32_t* bits;
+};
+
+// Kernel 2: the SIMT range coder.
+//  chained (launch_code): one lane per (segment, slice) chain, one frame of
+//    every segment per launch, context states carried in `tables`;
+//  decision stream (launch_dcode): one lane per (frame, slice) stream of the
+//    whole batch, pure range arithmetic over the states ffv1_walk recorded.
 struct CodeArgs {
   const uint32_t* sym;        // from kernel 1 (slot = segment)
   int64_t frame_samples;
@@ -82,21 +110,18 @@ struct CodeArgs {
   int* status;                // [0] overflow count
   int version;                // bitstream version (Golomb: v3 adds a 129/0 decision)
   int coded_bits;             // "bits" of encode_line (8 for <=8-bit)
-  // frame-parallel mode (launch_code_frames): one lane per (frame, slice),
-  // starting from the per-frame state snapshots ffv1_states wrote
-  uint8_t* snap;              // [frame][slice][state_bytes] + 64 spare tables for idle lanes
-  int nframes;
-  int lanes;                  // streams per wave (1..64); the other lanes idle
-  int64_t spare;              // index of the first spare table
+  int nframes;                // decision-stream mode: frames of the batch
+  DecisionStream ds;
 };
 
 // Kernel 2a: the context-state walk.  The adaptive states a slice's range
-// coder sees depend only on the decisions of the earlier frames of its GOP,
-// not on the coder's arithmetic, so one wave per (segment, slice) replays
-// just the state transitions (table in LDS) and writes the states at the
-// start of every frame; the coding of all frames then runs in parallel.
-struct StateArgs {
-  const uint32_t* sym;        // [batch frame][frame_samples]
+// coder sees depend only on the decisions of the earlier symbols of its GOP,
+// not on the coder's arithmetic.  One wave per (segment, slice, plane group)
+// replays just the state transitions (table in LDS) and records, for every
+// decision, the state it is coded with and its bit; the coding of all
+// (frame, slice) streams then runs in parallel (launch_dcode).
+struct WalkArgs {
+  const uint4* rec;           // [batch frame][frame_samples] walk records
   int64_t frame_samples;
   const SliceGeom* geom;
   int nslices;
@@ -104,7 +129,7 @@ struct StateArgs {
   const uint8_t* ftab;        // frame transition table [bit][state]
   int64_t state_bytes;
   uint8_t* persist;           // [slice][state_bytes]
-  uint8_t* snap;              // [batch frame][slice][state_bytes]
+  DecisionStream ds;
 };
 
 struct AssembleArgs {
@@ -121,9 +146,12 @@ struct AssembleArgs {
 
 int launch_symbols(const SymbolArgs& a, void* stream);
 int launch_code(const CodeArgs& a, void* stream);
-int launch_code_frames(const CodeArgs& a, void* stream);
-int launch_states(const StateArgs& a, int nsegs, void* stream);
-constexpr int64_t kStateLdsMax = 64 * 1024;  // states walk: table + transition table in LDS
+int launch_layout(const int* dcount, int nstreams, int64_t* dbase, int64_t* total, void* stream);
+int launch_walk(const WalkArgs& a, int nsegs, void* stream);
+int launch_dcode(const CodeArgs& a, void* stream);
+int64_t walk_lds_bytes(int64_t state_bytes);
+constexpr int64_t kWalkLdsMax = 64 * 1024;  // states walk: one plane group's table + T9 + staging in LDS
+constexpr int kStreamAlign = 64;            // decisions: every stream starts at a multiple
 int launch_code_golomb(const CodeArgs& a, void* stream);
 int launch_assemble(const AssembleArgs& a, int nframes, void* stream);
 

@@ -53,14 +53,59 @@ __device__ __forceinline__ int fold_bits(int d, int bits) {
 // Kernel 1: symbols.
 constexpr int kSymThreads = 256;
 
+// Range-coder decisions of one residual: put_symbol_inline (ffv1enc.c:185-231)
+// codes a zero flag, e+1 exponent decisions, e mantissa bits and a sign.
+__device__ __forceinline__ int decisions_of(int v) {
+  const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
+  return v ? 2 * (31 - __builtin_clz(mag)) + 3 : 1;
+}
+
+// 16 bits -> the even bits of a word
+__device__ __forceinline__ uint32_t spread16(uint32_t x) {
+  x &= 0xFFFFu;
+  x = (x | (x << 8)) & 0x00FF00FFu;
+  x = (x | (x << 4)) & 0x0F0F0F0Fu;
+  x = (x | (x << 2)) & 0x33333333u;
+  x = (x | (x << 1)) & 0x55555555u;
+  return x;
+}
+
+// Per-slot codes of one symbol with e <= 9, two bits per slot (slots 0..15
+// in the first word, 16..31 in the second): 0/1 the slot's decision bit,
+// 2 no decision.  Slot 0 zero flag, 1..e+1 unary, 11+e sign, 22..21+e
+// mantissa (put_symbol_inline, ffv1enc.c:185-231).
+__device__ __forceinline__ void slot_codes(int v, uint32_t& c0, uint32_t& c1) {
+  const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
+  const int e = v ? 31 - __builtin_clz(mag) : -1;
+  const uint32_t lo = v ? (1u << e) - 1u : 0u;  // e ones
+  const uint32_t tm = v ? (1u | (((2u << e) - 1u) << 1) | (1u << (11 + e)) | (lo << 22)) : 1u;
+  const uint32_t bm = v ? ((lo << 1) | ((uint32_t)(v < 0) << (11 + e)) | ((mag & lo) << 22)) : 1u;
+  const uint32_t nt = ~tm;
+  c0 = spread16(bm) | (spread16(nt) << 1);
+  c1 = spread16(bm >> 16) | (spread16(nt >> 16) << 1);
+}
+
+__device__ __forceinline__ int wave_incl_scan(int x, int lane) {
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  return x;
+}
+
 __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   __shared__ int16_t qt[5 * 256];
+  __shared__ int red[kSymThreads / kWave];
   for (int i = threadIdx.x; i < 5 * 256; i += kSymThreads) qt[i] = a.qt[i];
   __syncthreads();
   const int slice = blockIdx.x, slot = blockIdx.y, p = blockIdx.z;
-  if (p >= a.nplanes) return;
   const int f = a.frame_of_slot[slot];
   if (f < 0) return;
+  int* const count = a.dcount ? a.dcount + ((int64_t)slot * a.nslices + slice) * 3 + p : nullptr;
+  if (p >= a.nplanes) {
+    if (count && threadIdx.x == 0) *count = 0;
+    return;
+  }
   const SliceGeom& g = a.geom[slice];
   const int pw = g.pw[p], ph = g.ph[p], px = g.px[p], py = g.py[p];
   const uint8_t* base = a.frames + (int64_t)f * a.frame_bytes + a.plane_off[p];
@@ -76,8 +121,15 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
     return (int16_t)v;
   };
 
-  for (int64_t idx = threadIdx.x; idx < (int64_t)pw * ph; idx += kSymThreads) {
-    const int y = (int)(idx / pw), x = (int)(idx - (int64_t)y * pw);
+  int ndec = 0;
+  const int64_t n = (int64_t)pw * ph;
+  const int lane = threadIdx.x & (kWave - 1);
+  uint4* const rec = a.rec ? a.rec + (int64_t)slot * a.frame_samples + g.sym_off + g.plane_sym_off[p] : nullptr;
+  // whole waves per step: a wave's 64 consecutive samples are one walk chunk
+  for (int64_t base = 0; base < n; base += kSymThreads) {
+    const int64_t idx = base + threadIdx.x;
+    const bool valid = idx < n;
+    const int y = valid ? (int)(idx / pw) : 0, x = valid ? (int)(idx - (int64_t)y * pw) : 0;
     // neighbourhood as the zeroed two/three-row ring exposes it:
     // rows above the slice read 0; L(x=0) = T; LT(x=0) = sample two rows up
     // in column 0; RT past the right edge = T; LL(x=0) = 0, LL(x=1) = T(0).
@@ -99,7 +151,34 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
       diff = -diff;
     }
     diff = fold_bits(diff, a.coded_bits);
-    out[idx] = ((uint32_t)(row0 + ctx) << 16) | (uint16_t)diff;
+    const int nd = valid ? decisions_of(diff) : 0;
+    ndec += nd;
+    if (rec) {
+      // the walk record: row inside the plane group, slot codes, the decision
+      // offset inside the chunk (wave prefix sum), same-row flag
+      const int raddr = ctx * 32;
+      const int incl = wave_incl_scan(nd, lane);
+      const int d0 = incl - nd;
+      const unsigned mag = diff < 0 ? 0u - (unsigned)diff : (unsigned)diff;
+      const int e = diff ? 31 - __builtin_clz(mag) : 0;
+      const int prev = __shfl_up(raddr, 1);
+      uint32_t c0, c1;
+      slot_codes(diff, c0, c1);
+      const uint32_t w = (uint32_t)d0 | ((uint32_t)(d0 + 2 * e) << 16) | (lane > 0 && prev == raddr ? kRecSame : 0u);
+      if (valid) rec[idx] = make_uint4((uint32_t)raddr | ((uint32_t)(uint16_t)diff << 16), c0, c1, w);
+    } else if (valid) {
+      out[idx] = ((uint32_t)(row0 + ctx) << 16) | (uint16_t)diff;
+    }
+  }
+  if (count) {
+    for (int o = 32; o > 0; o >>= 1) ndec += __shfl_xor(ndec, o);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = ndec;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int t = 0;
+      for (int w = 0; w < kSymThreads / kWave; w++) t += red[w];
+      *count = t;
+    }
   }
 }
 
@@ -451,61 +530,36 @@ __device__ __forceinline__ int64_t terminate(Lane& L, Sink& S, bool state129) {
   return S.finish();
 }
 
-// FRAMES = false: one lane per (segment, slice) chain coding frame j of every
-// segment, the chain's states carried in `tables` from frame to frame.
-// FRAMES = true: one lane per (frame, slice) of the whole batch, each
-// starting from the snapshot ffv1_states wrote for its frame.
-// Dynamic LDS for a.lanes streams (+1 column shared by idle lanes).
+// One lane per (segment, slice) chain coding frame j of every segment, the
+// chain's states carried in `tables` from frame to frame.
 __host__ __device__ constexpr size_t code_lds_bytes(int lanes) {
-  return 1024 + (size_t)(lanes + 1) * (kOpsetBytes + kRingStride * 4);
+  return 1024 + (size_t)lanes * (kOpsetBytes + kRingStride * 4);
 }
 
-template <bool FRAMES>
 __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t* const tabs = lds;
-  uint8_t* const opsets = lds + 1024;                                           // [col][kOpsetBytes]
-  uint32_t* const ring = reinterpret_cast<uint32_t*>(opsets + (a.lanes + 1) * kOpsetBytes);  // [col][stride]
+  uint8_t* const opsets = lds + 1024;                                               // [lane][kOpsetBytes]
+  uint32_t* const ring = reinterpret_cast<uint32_t*>(opsets + kCodeThreads * kOpsetBytes);  // [lane][stride]
   for (int i = threadIdx.x; i < 1024; i += kCodeThreads) tabs[i] = a.tabs[i];
   __syncthreads();
-  const int col = min((int)threadIdx.x, a.lanes);  // idle lanes share the spare column
   const uint8_t* dtab = tabs;        // default table (key bit, v0/v1 header)
   const uint8_t* ftab = tabs + 512;  // frame table
 
   const int lane = threadIdx.x;
-  int64_t chain = (int64_t)blockIdx.x * kCodeThreads + lane;  // tables exist for the padded grid
-  int seg_i, slice, f;
-  bool live;
+  const int64_t chain = (int64_t)blockIdx.x * kCodeThreads + lane;  // tables exist for the padded grid
+  const int seg_i = (int)(chain / a.nslices);
+  const int slice = (int)(chain % a.nslices);
+  bool live = seg_i < a.nsegs;
   Segment seg{0, 0, 0, 0};
-  uint8_t* table;
-  if constexpr (FRAMES) {
-    // a.lanes streams per wave: fewer streams, less padding to the wave's
-    // largest exponent; idle lanes work on spare tables
-    const bool used = lane < a.lanes;
-    chain = (int64_t)blockIdx.x * a.lanes + lane;
-    f = (int)(chain / a.nslices);
-    slice = (int)(chain % a.nslices);
-    seg_i = f;
-    live = used && f < a.nframes;
-    table = a.snap + (live ? chain : a.spare + lane) * a.state_bytes;
-    if (!live) {
-      f = 0;
-      slice = 0;
-      seg_i = 0;
-    }
-  } else {
-    seg_i = (int)(chain / a.nslices);
-    slice = (int)(chain % a.nslices);
-    live = seg_i < a.nsegs;
-    if (live) seg = a.segs[seg_i];
-    live = live && a.j < seg.nframes;
-    f = seg.first_frame + a.j;
-    table = a.tables + chain * a.state_bytes;
-  }
+  if (live) seg = a.segs[seg_i];
+  live = live && a.j < seg.nframes;
+  const int f = seg.first_frame + a.j;
+  uint8_t* const table = a.tables + chain * a.state_bytes;
   const int key = live ? a.keyflags[f] : 0;
 
   // context states: continue, or reset at a keyframe (ff_ffv1_clear_slice_state)
-  if (!FRAMES && live) {
+  if (live) {
     if (a.j == 0 && seg.load_states) {
       const uint4* src = reinterpret_cast<const uint4*>(a.persist + (int64_t)slice * a.state_bytes);
       for (int64_t i = 0; i < a.state_bytes / 16; i++) reinterpret_cast<uint4*>(table)[i] = src[i];
@@ -516,11 +570,11 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
   }
 
   Lane L;
-  lane_init(L, ring + col * kRingStride);
+  lane_init(L, ring + lane * kRingStride);
   uint8_t* const out = a.slice_out + ((int64_t)(live ? f : 0) * a.nslices + slice) * a.slice_cap;
   Sink S = make_sink(out, live ? a.slice_cap : 0);  // idle lanes write nothing
 
-  run_header_ops(a, L, S, opsets + col * kOpsetBytes, key, slice, live, dtab, ftab);
+  run_header_ops(a, L, S, opsets + lane * kOpsetBytes, key, slice, live, dtab, ftab);
 
   const SliceGeom& g = a.geom[slice];
   const int64_t nsym = live ? g.nsym : 0;
@@ -592,7 +646,7 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
     const int64_t nbytes = terminate(L, S, true);
     if (nbytes > a.slice_cap) atomicAdd(a.status, 1);
     a.slice_bytes[(int64_t)f * a.nslices + slice] = nbytes;
-    if (!FRAMES && a.j == seg.nframes - 1 && seg.save_states) {
+    if (a.j == seg.nframes - 1 && seg.save_states) {
       uint4* dst = reinterpret_cast<uint4*>(a.persist + (int64_t)slice * a.state_bytes);
       for (int64_t i = 0; i < a.state_bytes / 16; i++) dst[i] = reinterpret_cast<const uint4*>(table)[i];
     }
@@ -600,17 +654,124 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Kernel 2a: context-state walk (see StateArgs).  One wave per (segment,
-// slice); the slice's 2 x contexts x 32 states live in LDS.  Symbols are
-// taken two at a time: lanes 0..31 apply symbol t and lanes 32..63 symbol
-// t+1, lane k of a half owning slot k of its symbol's row, each applying that
-// slot's decisions of put_symbol_inline (ffv1enc.c:185-231) through the
-// transition table.  When both symbols share a row, the upper half continues
-// from the lower half's results (v_permlane32_swap) and only it writes back.
-constexpr int kStateThreads = kWave;
+// Kernel 2, decision-stream form: one lane per (frame, slice) stream of the
+// batch.  ffv1_walk recorded every decision's state and bit, so what is
+// left is put_rac's arithmetic (rangecoder.h:90-102) and the renormalisation
+// (rangecoder.h:52-75), 32 decisions per step from 32 state bytes + one bit
+// word: no per-symbol structure, so no lane waits on another's exponent.
+template <bool TAIL>
+__device__ __forceinline__ void decide32(Lane& L, const uint4& wa, const uint4& wb, uint32_t bw, int rem) {
+  static_for<0, 32>([&](auto jc) {
+    constexpr int J = decltype(jc)::value;
+    constexpr int SH = (J & 3) * 8;
+    uint32_t w;
+    if constexpr (J < 4) w = wa.x;
+    else if constexpr (J < 8) w = wa.y;
+    else if constexpr (J < 12) w = wa.z;
+    else if constexpr (J < 16) w = wa.w;
+    else if constexpr (J < 20) w = wb.x;
+    else if constexpr (J < 24) w = wb.y;
+    else if constexpr (J < 28) w = wb.z;
+    else w = wb.w;
+    const unsigned s = (w >> SH) & 0xFF;
+    const int m = -(int)((bw >> J) & 1u);  // all ones for a 1 decision
+    const int r1 = (int)(__umul24((unsigned)L.range, s) >> 8);
+    const int r0 = L.range - r1;
+    int nl = L.low + (r0 & m);
+    int nr = (r1 & m) | (r0 & ~m);
+    if constexpr (TAIL) {
+      const bool act = J < rem;
+      nl = act ? nl : L.low;
+      nr = act ? nr : L.range;
+    }
+    L.low = nl;
+    L.range = nr;
+    renorm(L);
+  });
+}
 
-__device__ __forceinline__ void copy_states(uint4* dst, const uint4* src, int64_t n16, int lane) {
-  for (int64_t i = lane; i < n16; i += kStateThreads) dst[i] = src[i];
+__global__ __launch_bounds__(kCodeThreads) void ffv1_dcode(CodeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t* const tabs = lds;
+  uint8_t* const opsets = lds + 1024;
+  uint32_t* const ring = reinterpret_cast<uint32_t*>(opsets + kCodeThreads * kOpsetBytes);
+  for (int i = threadIdx.x; i < 1024; i += kCodeThreads) tabs[i] = a.tabs[i];
+  __syncthreads();
+  const int lane = threadIdx.x;
+  // slice-major: the lanes of a wave code one slice of consecutive frames,
+  // streams of similar length
+  const int64_t c = (int64_t)blockIdx.x * kCodeThreads + lane;
+  const bool live = c < (int64_t)a.nframes * a.nslices;
+  const int slice = live ? (int)(c / a.nframes) : 0;
+  const int f = live ? (int)(c % a.nframes) : 0;
+  const int key = live ? a.keyflags[f] : 0;
+
+  Lane L;
+  lane_init(L, ring + lane * kRingStride);
+  uint8_t* const out = a.slice_out + ((int64_t)f * a.nslices + slice) * a.slice_cap;
+  Sink S = make_sink(out, live ? a.slice_cap : 0);
+  run_header_ops(a, L, S, opsets + lane * kOpsetBytes, key, slice, live, tabs, tabs + 512);
+  flush_if(L, S, kRing - 33);
+
+  const int64_t st = (int64_t)f * a.nslices + slice;
+  const int* dc = a.ds.dcount + st * 3;
+  const int n = live ? dc[0] + dc[1] + dc[2] : 0;
+  const int64_t base = live ? a.ds.dbase[st] : 0;  // multiple of kStreamAlign
+  const uint4* P = reinterpret_cast<const uint4*>(a.ds.pre + base);
+  const uint32_t* B = a.ds.bits + (base >> 5);
+  const int nmax = wave_max(n);
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
+  uint4 na = z4, nb = z4;
+  uint32_t nw = 0u;
+  if (n > 0) {
+    na = P[0];
+    nb = P[1];  // streams are padded to 64 decisions
+    nw = B[0];
+  }
+  for (int i = 0; i < nmax; i += 32) {
+    const uint4 wa = na, wb = nb;
+    const uint32_t bw = nw;
+    if (i + 32 < n) {  // next block (streams are padded to 64 decisions)
+      na = P[(i >> 4) + 2];
+      nb = P[(i >> 4) + 3];
+      nw = B[(i >> 5) + 1];
+    }
+    if (i + 32 <= n)
+      decide32<false>(L, wa, wb, bw, 32);
+    else if (i < n)
+      decide32<true>(L, wa, wb, bw, n - i);
+    flush_if(L, S, kRing - 33);  // <= 32 digits per block
+  }
+  if (live) {
+    const int64_t nbytes = terminate(L, S, true);
+    if (nbytes > a.slice_cap) atomicAdd(a.status, 1);
+    a.slice_bytes[st] = nbytes;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 2a: context-state walk.  One wave per (segment, slice, plane group);
+// group 0 = the luma contexts, 1 = the chroma contexts Cb and Cr share
+// (ffv1enc.c:1194-1195): independent chains.  The group's [contexts][32]
+// states live in LDS.  Symbols are taken in chunks of 64: a prologue with
+// one symbol per lane computes decision counts, offsets (wave prefix sum),
+// decision bits and a per-symbol record (row, 2-bit slot codes, offset);
+// then the symbols are applied one per step, lane k < 32 owning slot k of
+// the symbol's row (put_symbol_inline, ffv1enc.c:185-231).  Each touched
+// lane records the state its decision is coded with at the decision's
+// index (LDS staging, copied out per chunk).
+//
+// Critical path per symbol: one LDS lookup, T3[code * 256 + state] (code 0/1
+// a decision bit, 2 no decision), plus a select: the next symbol's row
+// states are read from LDS a step ahead and, when it is the same row, taken
+// from the register just computed instead.
+constexpr int kWalkThreads = kWave;
+constexpr int kT3Bytes = 3 * 256;
+constexpr int kStageWords = 80;     // bits: >= (64 symbols * 33 bits + 31) / 32 + 1
+constexpr int kPreStage = 64 * 21;  // pre-states of one chunk of symbols with e <= 9
+
+int64_t walk_lds_bytes_dev(int64_t state_bytes) {
+  return state_bytes / 2 + kT3Bytes + (kWalkThreads + 2) * 16 + kStageWords * 4 + kPreStage + 32;
 }
 
 struct SymDec {  // one symbol, wave-uniform
@@ -627,134 +788,259 @@ __device__ __forceinline__ SymDec decode_sym(uint32_t sv) {
   return d;
 }
 
-// Exponents >= 10 (slots 10 and 31 take e - 9 repeated decisions, the sign
-// goes to slot 21): lane k < 32 applies all of its slot's decisions.
-__device__ __forceinline__ void walk_long(uint8_t* tbl, const uint8_t* tab, const SymDec& d, int lane,
-                                          int kind, int ki, int sink) {
-  const int e = d.e;
-  int n = 0;
-  if (kind == 0) n = 1;
-  else if (kind == 1) n = ki <= min(e, 9) ? (ki < 9 ? 1 : max(e - 8, 1)) : 0;
-  else if (kind == 2) n = ki == min(e, 10) && e >= 0 ? 1 : 0;
-  else n = ki < min(e, 9) ? 1 : (ki == 9 && e > 9 ? e - 9 : 0);
-  const int addr = lane < 32 ? d.row * 32 + lane : sink + lane;
+// Any exponent, one symbol: lane k < 32 applies all decisions of slot k in
+// order (slot 10 takes e-8 exponent decisions beyond e = 9, slot 31 the
+// mantissa bits >= 9, the sign goes to slot 21) and records their states.
+__device__ __forceinline__ void walk_long(uint8_t* tbl, const uint8_t* ftab, const SymDec& d, int lane,
+                                          uint8_t* pre) {
+  if (lane >= 32) return;
+  const int k = lane, e = d.e;
+  int n = 0, d0 = 0;  // decisions of this slot: indices d0 .. d0+n-1
+  if (k == 0) {
+    n = 1;
+  } else if (d.v == 0) {
+    n = 0;
+  } else if (k <= 9) {
+    n = k <= e + 1 ? 1 : 0;
+    d0 = k;
+  } else if (k == 10) {
+    n = e >= 9 ? e - 8 : 0;
+    d0 = 10;
+  } else if (k <= 21) {
+    n = k == 11 + min(e, 10) ? 1 : 0;
+    d0 = 2 * e + 2;
+  } else if (k <= 30) {
+    n = k - 22 < e ? 1 : 0;
+    d0 = 2 * e + 1 - (k - 22);
+  } else {
+    n = e >= 10 ? e - 9 : 0;
+    d0 = e + 2;
+  }
+  if (!n) return;
+  const int addr = d.row * 32 + k;
   int st = tbl[addr];
   for (int j = 0; j < n; j++) {
+    const int di = d0 + j;
     int bit;
-    if (kind == 0) bit = d.v == 0;
-    else if (kind == 1) bit = ki < 9 ? (ki < e) : (j < e - 9);
-    else if (kind == 2) bit = d.v < 0;
-    else bit = (d.mag >> (ki < 9 ? ki : e - 1 - j)) & 1;
-    st = tab[(bit << 8) | st];
+    if (k == 0) bit = d.v == 0;
+    else if (k <= 10) bit = di <= e;
+    else if (k <= 21) bit = d.v < 0;
+    else bit = (d.mag >> (2 * e + 1 - di)) & 1;
+    pre[di] = (uint8_t)st;
+    st = ftab[(bit << 8) | st];
   }
-  tbl[addr] = st;
+  tbl[addr] = (uint8_t)st;
 }
 
-// Slot activity (bit k: slot k takes a decision) and decision bits of one
-// symbol with e <= 9: slot 0 zero flag, 1..e+1 unary, 11+e sign, 22..21+e
-// mantissa (put_symbol_inline, ffv1enc.c:185-231).
-__device__ __forceinline__ void slot_masks(int v, uint32_t& tm, uint32_t& bm) {
+// The symbol's decision bits in coding order (bit d = decision d): zero flag,
+// e ones and a zero, the mantissa MSB first, the sign.
+__device__ __forceinline__ uint64_t decision_bits(int v) {
+  if (!v) return 1;
   const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
-  const int e = v ? 31 - __builtin_clz(mag) : -1;
-  const uint32_t lo = v ? (1u << e) - 1u : 0u;  // e ones
-  tm = v ? (1u | (((2u << e) - 1u) << 1) | (1u << (11 + e)) | (lo << 22)) : 1u;
-  bm = v ? ((lo << 1) | ((uint32_t)(v < 0) << (11 + e)) | ((mag & lo) << 22)) : 1u;
+  const int e = 31 - __builtin_clz(mag);
+  const uint64_t unary = (uint64_t)((1u << e) - 1u) << 1;
+  const uint64_t mant = e ? (uint64_t)(__brev(mag) >> (32 - e)) << (e + 2) : 0;
+  return unary | mant | ((uint64_t)(v < 0) << (2 * e + 2));
 }
 
-// Grid: (segment, slice, plane group); group 0 = luma contexts, 1 = the
-// chroma contexts Cb and Cr share (ffv1enc.c:1194-1195): independent chains.
-__global__ __launch_bounds__(kStateThreads) void ffv1_states(StateArgs a) {
+// One symbol of the chunk (records in LDS): lane k owns slot k.
+struct WalkLane {
+  int k, csh, hsh, kc;
+  bool lo16;
+};
+
+template <bool UNROLLED>
+__device__ __forceinline__ void walk_step(const uint4& r0, const uint4& r1, bool same, uint32_t& ldsv, uint32_t& ns,
+                                          uint8_t* tbl, const uint8_t* t3, uint8_t* pstage, int dummy,
+                                          const WalkLane& W) {
+  // start state: the register when the symbol continues the previous row
+  const uint32_t st = same ? ns : ldsv;
+  const int addr = (int)(r0.x & 0xFFFFu) + W.k;
+  ldsv = tbl[(int)(r1.x & 0xFFFFu) + W.k];  // next symbol's row, after every earlier write
+  const uint32_t code = ((W.lo16 ? r0.y : r0.z) >> W.csh) & 3u;
+  uint32_t nsv = t3[(code << 8) | st];
+  pin(nsv);
+  tbl[addr] = (uint8_t)nsv;  // lanes 32..63 repeat lanes 0..31: same address, same value
+  const int pos = (int)((r0.w >> W.hsh) & 0xFFFu) + W.kc;
+  pstage[code == 2u ? dummy : pos] = (uint8_t)st;
+  ns = nsv;
+}
+
+__global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int64_t half = a.state_bytes / 2;         // one plane group's [contexts][32]
+  const int64_t half = a.state_bytes / 2;  // one plane group's [contexts][32]
   uint8_t* const tbl = lds;
-  uint8_t* const tab = lds + half;                // [bit][state]
-  const int sink = (int)half + 512;               // 64 bytes taking writes that must not land
+  uint8_t* const t3 = lds + half;
+  uint4* const recs = reinterpret_cast<uint4*>(t3 + kT3Bytes);
+  uint32_t* const stage = reinterpret_cast<uint32_t*>(t3 + kT3Bytes + (kWalkThreads + 2) * 16);
+  uint8_t* const pstage = t3 + kT3Bytes + (kWalkThreads + 2) * 16 + kStageWords * 4;
   const int lane = threadIdx.x;
-  for (int i = lane; i < 512; i += kStateThreads) tab[i] = a.ftab[i];
+  for (int i = lane; i < kT3Bytes; i += kWalkThreads) t3[i] = i < 512 ? a.ftab[i] : (uint8_t)(i - 512);
   const int grp = blockIdx.x & 1;
   const int chain = blockIdx.x >> 1;
   const int seg_i = chain / a.nslices, slice = chain % a.nslices;
   const Segment seg = a.segs[seg_i];
   const SliceGeom& g = a.geom[slice];
-  const int64_t s0 = grp ? g.plane_sym_off[1] : 0, s1 = grp ? g.nsym : g.plane_sym_off[1];
-  if (s0 >= s1 && grp) return;  // no chroma
-  const int rowbase = grp ? (int)(half / 32) : 0;
+  const int p0 = grp ? 1 : 0, p1 = grp ? 3 : 1;  // planes of this group's chain
+  if (grp && g.plane_sym_off[1] >= g.nsym) return;  // no chroma
   const int64_t n16 = half / 16;
   uint4* const t4 = reinterpret_cast<uint4*>(tbl);
   const int64_t goff = grp * half;
   if (seg.load_states) {
-    copy_states(t4, reinterpret_cast<const uint4*>(a.persist + (int64_t)slice * a.state_bytes + goff), n16, lane);
+    const uint4* src = reinterpret_cast<const uint4*>(a.persist + (int64_t)slice * a.state_bytes + goff);
+    for (int64_t i = lane; i < n16; i += kWalkThreads) t4[i] = src[i];
   } else {  // the segment starts at a keyframe (ff_ffv1_clear_slice_state)
     const uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
-    for (int64_t i = lane; i < n16; i += kStateThreads) t4[i] = v;
+    for (int64_t i = lane; i < n16; i += kWalkThreads) t4[i] = v;
   }
+  for (int i = lane; i < kStageWords; i += kWalkThreads) stage[i] = 0;
   __syncthreads();
 
-  // lane roles: half h = lane / 32 takes symbol t + h; slot k = lane % 32
-  const int k = lane & 31;
-  const bool hi = lane >= 32;
-  const int kind = k == 0 ? 0 : k <= 10 ? 1 : k <= 21 ? 2 : 3;  // zero, unary, sign, mantissa
-  const int ki = kind == 1 ? k - 1 : kind == 2 ? k - 11 : kind == 3 ? k - 22 : 0;
+  WalkLane W;
+  W.k = lane & 31;
+  W.csh = (2 * W.k) & 31;
+  W.lo16 = W.k < 16;
+  const bool isU = W.k <= 10;            // zero flag / exponent slots: decision D + k
+  W.hsh = isU ? 0 : 16;                  // else from D + 2e: sign +2, mantissa 22+i: +1-i
+  W.kc = isU ? W.k : (W.k <= 21 ? 2 : 23 - W.k);
+  const int dummy = kPreStage + W.k;     // untouched slots store here
 
-  const int64_t nsym = s1 - s0;
   for (int j = 0; j < seg.nframes; j++) {
     const int f = seg.first_frame + j;
-    copy_states(reinterpret_cast<uint4*>(a.snap + ((int64_t)f * a.nslices + slice) * a.state_bytes + goff), t4,
-                n16, lane);
-    if (j == seg.nframes - 1 && !seg.save_states) break;
-    const uint32_t* sp = a.sym + (int64_t)f * a.frame_samples + g.sym_off + s0;
-    uint32_t next = lane < nsym ? sp[lane] : 0u;
-    for (int64_t base = 0; base < nsym; base += kStateThreads) {
-      const uint32_t mine = next;
-      if (base + kStateThreads + lane < nsym) next = sp[base + kStateThreads + lane];
-      const int cnt = (int)min((int64_t)kStateThreads, nsym - base);
-      // decode the chunk's 64 symbols at once, one per lane
-      const bool valid = lane < cnt;
-      const int mv = valid ? (int16_t)(mine & 0xFFFF) : 0;
-      const int maddr = valid ? ((int)(mine >> 16) - rowbase) * 32 : 0;
-      if (__ballot(mv >= 1024 || mv <= -1024)) {  // e >= 10 somewhere: one at a time
-        for (int t = 0; t < cnt; t++) {
-          const SymDec d = decode_sym(__builtin_amdgcn_readlane(mine, t));
-          SymDec dl = d;
-          dl.row -= rowbase;
-          walk_long(tbl, tab, dl, lane, kind, ki, sink);
+    const int64_t sid = (int64_t)f * a.nslices + slice;
+    const int* dc = a.ds.dcount + sid * 3;
+    const int64_t gbase = a.ds.dbase[sid] + (grp ? dc[0] : 0);  // first decision of the chain
+    int64_t wbase = gbase >> 5;  // bits word held in stage[0]
+    bool first_word = true;      // stage[0] may share its word with another chain
+    int64_t run = 0;             // decisions so far in this frame's chain
+    for (int pl = p0; pl < p1; pl++) {
+      const int64_t nsym = (pl < 2 ? g.plane_sym_off[pl + 1] : g.nsym) - g.plane_sym_off[pl];
+      const uint4* rp = a.rec + (int64_t)f * a.frame_samples + g.sym_off + g.plane_sym_off[pl];
+      uint4 next = lane < nsym ? rp[lane] : make_uint4(0, 0, 0, 0);
+      for (int64_t base = 0; base < nsym; base += kWalkThreads) {
+        const uint4 mine = next;
+        if (base + kWalkThreads + lane < nsym) next = rp[base + kWalkThreads + lane];
+        const int cnt = (int)min((int64_t)kWalkThreads, nsym - base);
+        const bool valid = lane < cnt;
+        const int v = valid ? (int)(int16_t)(mine.x >> 16) : 0;
+        const int d0 = (int)(mine.w & 0xFFFu);
+        const int nd = valid ? decisions_of(v) : 0;
+        const int total = __builtin_amdgcn_readlane(d0 + nd, cnt - 1);
+        uint8_t* const pre = a.ds.pre + gbase + run;
+
+        // decision bits -> stage (LDS) -> whole words to the bits array
+        {
+          const int64_t pos0 = gbase + run;                 // decision index of the chunk's first decision
+          const int off0 = (int)(pos0 - (wbase << 5));      // < 32
+          if (valid) {
+            const uint64_t bs = decision_bits(v);
+            const int q = off0 + d0, w = q >> 5, sh = q & 31;
+            const uint64_t x = bs << sh;                    // nd + sh <= 33 + 31 bits
+            atomicOr(&stage[w], (uint32_t)x);
+            if (nd + sh > 32) atomicOr(&stage[w + 1], (uint32_t)(x >> 32));
+          }
+          __syncthreads();
+          const int wend = (off0 + total) >> 5;             // complete words
+          const uint32_t sw = stage[lane];
+          const uint32_t carry = stage[wend];
+          if (lane < wend) {
+            if (lane == 0 && first_word) atomicOr(&a.ds.bits[wbase], sw);
+            else a.ds.bits[wbase + lane] = sw;
+          }
+          if (lane + kWalkThreads < wend) a.ds.bits[wbase + lane + kWalkThreads] = stage[lane + kWalkThreads];
+          __syncthreads();
+          stage[lane] = lane == 0 ? carry : 0u;
+          if (lane < kStageWords - kWalkThreads) stage[lane + kWalkThreads] = 0u;
+          if (wend > 0) first_word = false;
+          wbase += wend;
         }
-        continue;
-      }
-      uint32_t mtm, mbm;
-      slot_masks(mv, mtm, mbm);
-      if (!valid) mtm = mbm = 0;
-      for (int t = 0; t < cnt; t += 2) {
-        const int tb = min(t + 1, kStateThreads - 1);
-        const uint64_t T = (uint64_t)__builtin_amdgcn_readlane(mtm, tb) << 32 | __builtin_amdgcn_readlane(mtm, t);
-        const uint64_t Bm = (uint64_t)__builtin_amdgcn_readlane(mbm, tb) << 32 | __builtin_amdgcn_readlane(mbm, t);
-        const int addrA = __builtin_amdgcn_readlane(maddr, t);
-        const int addrB = __builtin_amdgcn_readlane(maddr, tb);
-        const bool haveB = t + 1 < cnt;  // else T/Bm upper words are 0 (invalid lane) or unused
-        const uint32_t touched = (uint32_t)(T >> lane) & 1u;
-        const uint32_t bit = (uint32_t)(Bm >> lane) & 1u;
-        const int addr = (hi ? addrB : addrA) + k;
-        const int st = tbl[addr];
-        uint32_t ns1 = tab[(bit << 8) | st];
-        pin(ns1);
-        // lower half's post-state, seen by the upper half when the rows match
-        const int postA = touched ? (int)ns1 : st;
-        const int fromA = __builtin_amdgcn_permlane32_swap(postA, postA, false, false)[0];
-        const bool same = haveB && addrA == addrB;
-        const int stB = same ? fromA : st;
-        uint32_t ns2 = tab[(bit << 8) | stB];
-        pin(ns2);
-        const int fin = hi ? (touched ? (int)ns2 : stB) : postA;
-        // disjoint rows: both halves write; shared row: the upper half holds both updates
-        const bool wr = hi ? haveB : !same;
-        tbl[wr ? addr : sink + lane] = (uint8_t)fin;
+
+        if (__ballot(v >= 1024 || v <= -1024)) {  // e >= 10 somewhere: one symbol at a time, no staging
+          __syncthreads();
+          for (int t = 0; t < cnt; t++) {
+            SymDec d;
+            d.row = (int)(__builtin_amdgcn_readlane(mine.x, t) & 0xFFFFu) / 32;
+            d.v = __builtin_amdgcn_readlane(v, t);
+            d.mag = d.v < 0 ? 0u - (unsigned)d.v : (unsigned)d.v;
+            d.e = d.v ? 31 - __builtin_clz(d.mag) : -1;
+            walk_long(tbl, a.ftab, d, lane, pre + __builtin_amdgcn_readlane(d0, t));
+          }
+          __syncthreads();
+          run += total;
+          continue;
+        }
+
+        recs[lane] = mine;
+        const uint64_t same = __ballot(valid && (mine.w & kRecSame));
+        __syncthreads();
+
+        uint4 r0 = recs[0];
+        uint4 r1 = recs[1];
+        uint32_t ldsv = tbl[(int)(r0.x & 0xFFFFu) + W.k];
+        uint32_t ns = 0;
+        if (cnt == kWalkThreads) {
+          static_for<0, kWalkThreads>([&](auto tc) {
+            constexpr int T = decltype(tc)::value;
+            const uint4 r2 = recs[T + 2];  // two ahead (past the chunk: unused)
+            walk_step<true>(r0, r1, (same >> T) & 1, ldsv, ns, tbl, t3, pstage, dummy, W);
+            r0 = r1;
+            r1 = r2;
+          });
+        } else {
+          for (int t = 0; t < cnt; t++) {
+            const uint4 r2 = recs[t + 2];
+            walk_step<false>(r0, r1, (same >> t) & 1, ldsv, ns, tbl, t3, pstage, dummy, W);
+            r0 = r1;
+            r1 = r2;
+          }
+        }
+        __syncthreads();
+        for (int i = lane; i < total; i += kWalkThreads) pre[i] = pstage[i];
+        run += total;
       }
     }
+    // the frame's last, partial bits word
+    if (lane == 0 && ((gbase + run) & 31)) atomicOr(&a.ds.bits[wbase], stage[0]);
+    __syncthreads();
+    for (int i = lane; i < kStageWords; i += kWalkThreads) stage[i] = 0;
+    __syncthreads();
   }
   if (seg.save_states) {
     __syncthreads();
-    copy_states(reinterpret_cast<uint4*>(a.persist + (int64_t)slice * a.state_bytes + goff), t4, n16, lane);
+    uint4* dst = reinterpret_cast<uint4*>(a.persist + (int64_t)slice * a.state_bytes + goff);
+    for (int64_t i = lane; i < n16; i += kWalkThreads) dst[i] = t4[i];
   }
+}
+
+// Decision-stream layout: stream (frame, slice) i starts at the sum of the
+// earlier streams' decisions, each rounded up to kStreamAlign.
+constexpr int kLayoutThreads = 1024;
+__global__ __launch_bounds__(kLayoutThreads) void ffv1_layout(const int* dcount, int nstreams, int64_t* dbase,
+                                                              int64_t* total) {
+  __shared__ int64_t part[kLayoutThreads];
+  const int t = threadIdx.x;
+  const int per = (nstreams + kLayoutThreads - 1) / kLayoutThreads;
+  const int lo = min(t * per, nstreams), hi = min(lo + per, nstreams);
+  auto len = [&](int i) -> int64_t {
+    const int64_t n = (int64_t)dcount[3 * i] + dcount[3 * i + 1] + dcount[3 * i + 2];
+    return (n + kStreamAlign - 1) / kStreamAlign * kStreamAlign;
+  };
+  int64_t sum = 0;
+  for (int i = lo; i < hi; i++) sum += len(i);
+  part[t] = sum;
+  __syncthreads();
+  for (int o = 1; o < kLayoutThreads; o <<= 1) {
+    const int64_t y = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += y;
+    __syncthreads();
+  }
+  int64_t acc = part[t] - sum;
+  for (int i = lo; i < hi; i++) {
+    dbase[i] = acc;
+    acc += len(i);
+  }
+  if (t == kLayoutThreads - 1) *total = part[t];
 }
 
 // ---------------------------------------------------------------------------
@@ -1010,7 +1296,7 @@ __global__ __launch_bounds__(kAsmThreads) void ffv1_assemble_packets(AssembleArg
 }  // namespace
 
 int launch_symbols(const SymbolArgs& a, void* stream) {
-  dim3 grid(a.nslices, a.nslots, a.nplanes), block(kSymThreads);
+  dim3 grid(a.nslices, a.nslots, a.dcount ? 3 : a.nplanes), block(kSymThreads);  // counts of absent planes: 0
   hipLaunchKernelGGL(ffv1_symbols, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -1018,24 +1304,30 @@ int launch_symbols(const SymbolArgs& a, void* stream) {
 int launch_code(const CodeArgs& a, void* stream) {
   const int64_t chains = (int64_t)a.nsegs * a.nslices;
   dim3 grid((unsigned)((chains + kCodeThreads - 1) / kCodeThreads)), block(kCodeThreads);
-  if (a.lanes != kCodeThreads) return -1;
-  hipLaunchKernelGGL(ffv1_code<false>, grid, block, code_lds_bytes(a.lanes), reinterpret_cast<hipStream_t>(stream), a);
+  hipLaunchKernelGGL(ffv1_code, grid, block, code_lds_bytes(kCodeThreads), reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_code_frames(const CodeArgs& a, void* stream) {
-  if (a.lanes < 1 || a.lanes > kCodeThreads) return -1;
-  const int64_t chains = (int64_t)a.nframes * a.nslices;
-  dim3 grid((unsigned)((chains + a.lanes - 1) / a.lanes)), block(kCodeThreads);
-  hipLaunchKernelGGL(ffv1_code<true>, grid, block, code_lds_bytes(a.lanes), reinterpret_cast<hipStream_t>(stream), a);
+int launch_dcode(const CodeArgs& a, void* stream) {
+  const int64_t streams = (int64_t)a.nframes * a.nslices;
+  dim3 grid((unsigned)((streams + kCodeThreads - 1) / kCodeThreads)), block(kCodeThreads);
+  hipLaunchKernelGGL(ffv1_dcode, grid, block, code_lds_bytes(kCodeThreads), reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_states(const StateArgs& a, int nsegs, void* stream) {
-  const size_t lds = (size_t)a.state_bytes / 2 + 512 + kStateThreads;
-  if ((int64_t)lds > kStateLdsMax) return -1;
-  dim3 grid((unsigned)(nsegs * a.nslices * 2)), block(kStateThreads);
-  hipLaunchKernelGGL(ffv1_states, grid, block, lds, reinterpret_cast<hipStream_t>(stream), a);
+int64_t walk_lds_bytes(int64_t state_bytes) { return walk_lds_bytes_dev(state_bytes); }
+
+int launch_walk(const WalkArgs& a, int nsegs, void* stream) {
+  const size_t lds = (size_t)walk_lds_bytes_dev(a.state_bytes);
+  if ((int64_t)lds > kWalkLdsMax) return -1;
+  dim3 grid((unsigned)(nsegs * a.nslices * 2)), block(kWalkThreads);
+  hipLaunchKernelGGL(ffv1_walk, grid, block, lds, reinterpret_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_layout(const int* dcount, int nstreams, int64_t* dbase, int64_t* total, void* stream) {
+  hipLaunchKernelGGL(ffv1_layout, dim3(1), dim3(kLayoutThreads), 0, reinterpret_cast<hipStream_t>(stream), dcount,
+                     nstreams, dbase, total);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
