@@ -220,6 +220,7 @@ struct ffv1hip_ctx {
   bool frames_mode = false;   // states walk + decision-stream coder (range coder, LDS-sized tables)
   int wmax = 0;               // most decisions one symbol can take (2 * coded bits + 1)
   int64_t frame_samples = 0;  // symbols of one frame (each slice padded to 4)
+  int64_t frame_chunks = 0;   // 64-sample walk chunks of one frame
   int max_ops = 0;
   std::vector<SliceGeom> geom;
   // device buffers
@@ -239,6 +240,7 @@ struct ffv1hip_ctx {
   uint32_t* d_sym = nullptr;     // [slot][frame_samples]; frames mode: walk records (uint4), 2 x [batch frame][frame_samples]
   // frames mode, two buffer sets: the walk of batch k+1 runs while batch k codes
   uint8_t* d_keys2 = nullptr;    // 2 x [batch frame] keyflags
+  uint32_t* d_cbits = nullptr;   // 2 x [batch frame][frame_chunks][kChunkWords] packed decision bits
   int* d_dcount = nullptr;       // 2 x [batch frame][slice][3] decisions per plane
   int64_t* d_dbase = nullptr;    // 2 x [batch frame][slice] first decision of each stream
   int64_t* d_dtotal = nullptr;   // [2] decisions of the batch (incl. alignment)
@@ -453,7 +455,7 @@ static void build_ops(ffv1hip_ctx* c) {
 static void free_device(ffv1hip_ctx* c) {
   void* ptrs[] = {c->d_frames, c->d_qt, c->d_tabs, c->d_ops, c->d_nops, c->d_segs, c->d_keys,
                   c->d_slice_out, c->d_slice_bytes, c->d_packets, c->d_packet_size, c->d_persist,
-                  c->d_tables, c->d_sym, c->d_keys2, c->d_dcount, c->d_dbase, c->d_dtotal, c->d_pre[0],
+                  c->d_tables, c->d_sym, c->d_keys2, c->d_cbits, c->d_dcount, c->d_dbase, c->d_dtotal, c->d_pre[0],
                   c->d_pre[1], c->d_bits[0], c->d_bits[1], c->d_geom, c->d_slot_frames, c->d_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -517,6 +519,7 @@ static int alloc_device(ffv1hip_ctx* c) {
     // double-buffered: the states walk of batch k+1 runs while batch k codes
     HIP_TRY(hipMalloc(&c->d_sym, 2 * sizeof(uint4) * size_t(c->frame_samples) * nb));  // walk records
     HIP_TRY(hipMalloc(&c->d_keys2, 2 * size_t(nb)));
+    HIP_TRY(hipMalloc(&c->d_cbits, 2 * sizeof(uint32_t) * kChunkWords * size_t(c->frame_chunks) * nb));
     HIP_TRY(hipMalloc(&c->d_dcount, 2 * sizeof(int) * 3 * size_t(nb) * c->nslices));
     HIP_TRY(hipMalloc(&c->d_dbase, 2 * sizeof(int64_t) * size_t(nb) * c->nslices));
     HIP_TRY(hipMalloc(&c->d_dtotal, 2 * sizeof(int64_t)));
@@ -597,6 +600,8 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
     for (int k = 0; k < 3; k++) {
       g.plane_sym_off[k] = n;
       n += int64_t(g.pw[k]) * g.ph[k];
+      g.chunk_off[k] = c->frame_chunks;
+      c->frame_chunks += (int64_t(g.pw[k]) * g.ph[k] + 63) / 64;
     }
     g.nsym = n;
     g.sym_off = off;
@@ -777,6 +782,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     sa.nslots = n;
     sa.dcount = d_dcount;
     sa.rec = d_rec;
+    sa.cbits = c->d_cbits + size_t(fb) * kChunkWords * c->frame_chunks * c->max_batch;
+    sa.frame_chunks = c->frame_chunks;
     if (timed(0, st, [&] { return launch_symbols(sa, st); }) < 0)
       return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (timed(0, st, [&] { return launch_layout(d_dcount, n * c->nslices, d_dbase, c->d_dtotal + fb, st); }) < 0)
@@ -794,6 +801,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     DecisionStream ds{d_dcount, d_dbase, c->d_pre[fb], c->d_bits[fb]};
     WalkArgs wa{};
     wa.rec = d_rec;
+    wa.cbits = sa.cbits;
+    wa.frame_chunks = c->frame_chunks;
     wa.frame_samples = c->frame_samples;
     wa.geom = c->d_geom;
     wa.nslices = c->nslices;
@@ -802,8 +811,32 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     wa.state_bytes = ca.state_bytes;
     wa.persist = c->d_persist;
     wa.ds = ds;
+    // FFV1HIP_WALKDBG=1 (measurement hook): per-block cycle split to stderr
+    static const bool walkdbg = std::getenv("FFV1HIP_WALKDBG") && std::atoi(std::getenv("FFV1HIP_WALKDBG"));
+    uint64_t* d_dbg = nullptr;
+    const int nblk = nsegs * ((c->nslices + 1) / 2) * 2;
+    if (walkdbg) {
+      HIP_TRY(hipMalloc(&d_dbg, sizeof(uint64_t) * 4 * nblk));
+      HIP_TRY(hipMemsetAsync(d_dbg, 0, sizeof(uint64_t) * 4 * nblk, st));
+      wa.dbg = d_dbg;
+    }
     if (timed(2, st, [&] { return launch_walk(wa, nsegs, st); }) < 0)
       return set_err(-5, "walk launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (walkdbg) {
+      std::vector<uint64_t> h(size_t(4) * nblk);
+      HIP_TRY(hipMemcpyAsync(h.data(), d_dbg, h.size() * 8, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      HIP_TRY(hipFree(d_dbg));
+      double all[2] = {0, 0}, loop[2] = {0, 0}, steps[2] = {0, 0};
+      for (int b = 0; b < nblk; b++) {
+        all[b & 1] += double(h[4 * b]);
+        loop[b & 1] += double(h[4 * b + 1]);
+        steps[b & 1] += double(h[4 * b + 2]);
+      }
+      for (int g = 0; g < 2; g++)
+        std::fprintf(stderr, "walkdbg grp %d: blocks %d, memtime per block %.3g, loop share %.3f, memtime/step %.1f\n", g,
+                     nblk / 2, all[g] / (nblk / 2), loop[g] / all[g], loop[g] / steps[g]);
+    }
     // the coder stream continues once this batch's walk is done; the walk of
     // the next batch (on st) then overlaps this batch's coding
     HIP_TRY(hipEventRecord(c->walked[fb], st));

@@ -41,7 +41,15 @@ struct SliceGeom {
   int64_t sym_off;                 // first symbol of this slice in the frame stream
   int64_t plane_sym_off[3];        // first symbol of each plane, relative to sym_off
   int64_t nsym;                    // all planes
+  int64_t chunk_off[3];            // first 64-sample walk chunk of each plane in the frame
 };
+
+// Per walk chunk (64 consecutive samples of a plane), written by ffv1_symbols:
+// word 0 = the chunk's decisions | kChunkLong (a |diff| >= 1024 in it), words
+// 1.. = the decision bits in coding order (bit d in word 1 + d / 32), then a
+// zero word.
+constexpr int kChunkWords = 68;
+constexpr uint32_t kChunkLong = 0x80000000u;
 
 // Kernel 1: prediction + context + fold for every sample of a set of frames.
 struct SymbolArgs {
@@ -60,6 +68,8 @@ struct SymbolArgs {
   int64_t frame_samples;
   int* dcount;                // optional [slot][slice][3]: range-coder decisions per plane
   uint4* rec;                 // optional, instead of sym: [slot][frame_samples] walk records
+  uint32_t* cbits;            // with rec: [slot][frame_chunks][kChunkWords]
+  int64_t frame_chunks;
 };
 
 // Walk record of one sample (frame-parallel mode), written by ffv1_symbols.
@@ -122,6 +132,8 @@ struct CodeArgs {
 // (frame, slice) streams then runs in parallel (launch_dcode).
 struct WalkArgs {
   const uint4* rec;           // [batch frame][frame_samples] walk records
+  const uint32_t* cbits;      // [batch frame][frame_chunks][kChunkWords]
+  int64_t frame_chunks;
   int64_t frame_samples;
   const SliceGeom* geom;
   int nslices;
@@ -130,6 +142,7 @@ struct WalkArgs {
   int64_t state_bytes;
   uint8_t* persist;           // [slice][state_bytes]
   DecisionStream ds;
+  uint64_t* dbg;              // optional [block][4] cycle counters (FFV1HIP_WALKDBG)
 };
 
 struct AssembleArgs {

@@ -60,6 +60,17 @@ __device__ __forceinline__ int decisions_of(int v) {
   return v ? 2 * (31 - __builtin_clz(mag)) + 3 : 1;
 }
 
+// The symbol's decision bits in coding order (bit d = decision d): zero flag,
+// e ones and a zero, the mantissa MSB first, the sign.
+__device__ __forceinline__ uint64_t decision_bits(int v) {
+  if (!v) return 1;
+  const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
+  const int e = 31 - __builtin_clz(mag);
+  const uint64_t unary = (uint64_t)((1u << e) - 1u) << 1;
+  const uint64_t mant = e ? (uint64_t)(__brev(mag) >> (32 - e)) << (e + 2) : 0;
+  return unary | mant | ((uint64_t)(v < 0) << (2 * e + 2));
+}
+
 // 16 bits -> the even bits of a word
 __device__ __forceinline__ uint32_t spread16(uint32_t x) {
   x &= 0xFFFFu;
@@ -96,6 +107,7 @@ __device__ __forceinline__ int wave_incl_scan(int x, int lane) {
 __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   __shared__ int16_t qt[5 * 256];
   __shared__ int red[kSymThreads / kWave];
+  __shared__ uint32_t cstage[kSymThreads / kWave][kChunkWords];  // a wave's chunk bits
   for (int i = threadIdx.x; i < 5 * 256; i += kSymThreads) qt[i] = a.qt[i];
   __syncthreads();
   const int slice = blockIdx.x, slot = blockIdx.y, p = blockIdx.z;
@@ -166,6 +178,25 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
       slot_codes(diff, c0, c1);
       const uint32_t w = (uint32_t)d0 | ((uint32_t)(d0 + 2 * e) << 16) | (lane > 0 && prev == raddr ? kRecSame : 0u);
       if (valid) rec[idx] = make_uint4((uint32_t)raddr | ((uint32_t)(uint16_t)diff << 16), c0, c1, w);
+      // the chunk's decision bits, packed in coding order, and its header
+      const int wv = threadIdx.x / kWave;
+      uint32_t* const cs = cstage[wv];
+      if (base + wv * kWave < n) {
+        cs[lane] = 0u;
+        if (lane < kChunkWords - kWave) cs[kWave + lane] = 0u;
+        if (valid) {
+          const uint64_t x = decision_bits(diff) << (d0 & 31);
+          atomicOr(&cs[1 + (d0 >> 5)], (uint32_t)x);
+          if ((uint32_t)(x >> 32)) atomicOr(&cs[2 + (d0 >> 5)], (uint32_t)(x >> 32));
+        }
+        const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
+        const bool lng = __ballot(valid && (diff >= 1024 || diff <= -1024)) != 0;
+        if (lane == 0) cs[0] = (uint32_t)total | (lng ? kChunkLong : 0u);
+        uint32_t* const dst = a.cbits + ((int64_t)slot * a.frame_chunks + g.chunk_off[p] + (base + wv * kWave) / kWave) *
+                                            kChunkWords;
+        dst[lane] = cs[lane];
+        if (lane < kChunkWords - kWave) dst[kWave + lane] = cs[kWave + lane];
+      }
     } else if (valid) {
       out[idx] = ((uint32_t)(row0 + ctx) << 16) | (uint16_t)diff;
     }
@@ -673,12 +704,13 @@ __device__ __forceinline__ void decide32(Lane& L, const uint4& wa, const uint4& 
     else if constexpr (J < 24) w = wb.y;
     else if constexpr (J < 28) w = wb.z;
     else w = wb.w;
-    const unsigned s = (w >> SH) & 0xFF;
-    const int m = -(int)((bw >> J) & 1u);  // all ones for a 1 decision
-    const int r1 = (int)(__umul24((unsigned)L.range, s) >> 8);
-    const int r0 = L.range - r1;
-    int nl = L.low + (r0 & m);
-    int nr = (r1 & m) | (r0 & ~m);
+    const unsigned sp = (w >> SH) & 0xFF;     // s' = bit ? state : 256 - state
+    const int m = -(int)((bw >> J) & 1u);     // all ones for a 1 decision
+    const unsigned c = (unsigned)~m & 255u;   // round-up term of a 0 decision
+    // put_rac: 1 -> range*s >> 8; 0 -> range - (range*s >> 8) = (range*(256-s) + 255) >> 8
+    const int nr0 = (int)(__umul24((unsigned)L.range, sp) + c) >> 8;
+    int nl = L.low + ((L.range - nr0) & m);
+    int nr = nr0;
     if constexpr (TAIL) {
       const bool act = J < rem;
       nl = act ? nl : L.low;
@@ -770,9 +802,7 @@ constexpr int kT3Bytes = 3 * 256;
 constexpr int kStageWords = 80;     // bits: >= (64 symbols * 33 bits + 31) / 32 + 1
 constexpr int kPreStage = 64 * 21;  // pre-states of one chunk of symbols with e <= 9
 
-int64_t walk_lds_bytes_dev(int64_t state_bytes) {
-  return state_bytes / 2 + kT3Bytes + (kWalkThreads + 2) * 16 + kStageWords * 4 + kPreStage + 32;
-}
+int64_t walk_lds_bytes_dev(int64_t state_bytes);
 
 struct SymDec {  // one symbol, wave-uniform
   int row, v, e;
@@ -788,17 +818,18 @@ __device__ __forceinline__ SymDec decode_sym(uint32_t sv) {
   return d;
 }
 
-// Any exponent, one symbol: lane k < 32 applies all decisions of slot k in
-// order (slot 10 takes e-8 exponent decisions beyond e = 9, slot 31 the
-// mantissa bits >= 9, the sign goes to slot 21) and records their states.
-__device__ __forceinline__ void walk_long(uint8_t* tbl, const uint8_t* ftab, const SymDec& d, int lane,
+// Any exponent, one symbol: lane k < 32 of a half applies all decisions of
+// slot k in order (slot 10 takes e-8 exponent decisions beyond e = 9, slot
+// 31 the mantissa bits >= 9, the sign goes to slot 21) and records s' for
+// each (see walk_step).  row_off: the slot's byte in the half's table.
+__device__ __forceinline__ void walk_long(uint8_t* tbl, const uint8_t* ftab, int v, int row_off, int k,
                                           uint8_t* pre) {
-  if (lane >= 32) return;
-  const int k = lane, e = d.e;
+  const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
+  const int e = v ? 31 - __builtin_clz(mag) : -1;
   int n = 0, d0 = 0;  // decisions of this slot: indices d0 .. d0+n-1
   if (k == 0) {
     n = 1;
-  } else if (d.v == 0) {
+  } else if (v == 0) {
     n = 0;
   } else if (k <= 9) {
     n = k <= e + 1 ? 1 : 0;
@@ -817,198 +848,319 @@ __device__ __forceinline__ void walk_long(uint8_t* tbl, const uint8_t* ftab, con
     d0 = e + 2;
   }
   if (!n) return;
-  const int addr = d.row * 32 + k;
-  int st = tbl[addr];
+  int st = tbl[row_off];
   for (int j = 0; j < n; j++) {
     const int di = d0 + j;
     int bit;
-    if (k == 0) bit = d.v == 0;
+    if (k == 0) bit = v == 0;
     else if (k <= 10) bit = di <= e;
-    else if (k <= 21) bit = d.v < 0;
-    else bit = (d.mag >> (2 * e + 1 - di)) & 1;
-    pre[di] = (uint8_t)st;
+    else if (k <= 21) bit = v < 0;
+    else bit = (mag >> (2 * e + 1 - di)) & 1;
+    pre[di] = (uint8_t)(bit ? st : 256 - st);  // s', as walk_step records it
     st = ftab[(bit << 8) | st];
   }
-  tbl[addr] = (uint8_t)st;
+  tbl[row_off] = (uint8_t)st;
 }
 
-// The symbol's decision bits in coding order (bit d = decision d): zero flag,
-// e ones and a zero, the mantissa MSB first, the sign.
-__device__ __forceinline__ uint64_t decision_bits(int v) {
-  if (!v) return 1;
-  const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
-  const int e = 31 - __builtin_clz(mag);
-  const uint64_t unary = (uint64_t)((1u << e) - 1u) << 1;
-  const uint64_t mant = e ? (uint64_t)(__brev(mag) >> (32 - e)) << (e + 2) : 0;
-  return unary | mant | ((uint64_t)(v < 0) << (2 * e + 2));
-}
+// Two chains per wave: half h = lane / 32 walks chain h of the block's pair
+// (two slices of one segment and plane group), lane k = lane % 32 owning
+// slot k of its chain's current row.  A wave is issue-bound, so two chains
+// per instruction stream walk at nearly twice the rate of one; LDS (one
+// table per chain) caps chains per CU either way.
+constexpr int kChunk = 64;                   // symbols per chunk (the records' D is chunk-relative)
+constexpr int kRecSlots = kChunk + 2;        // + two read-ahead slots (null records)
+constexpr int kPreHalf = (kPreStage + 4 + 32 + 15) & ~15;  // pre stage of a chain: +3 align slack, 32 dummies
 
-// One symbol of the chunk (records in LDS): lane k owns slot k.
+// LDS image of the walk: a fixed part (static, so every offset below is an
+// instruction immediate) and the two state tables (dynamic).
+constexpr int kLdsT3 = 0;                                     // u16 [3][256]: next | s' << 8
+constexpr int kLdsRecs = kLdsT3 + 2 * kT3Bytes;               // [2][kRecSlots] records
+constexpr int kLdsPre = kLdsRecs + 2 * kRecSlots * 16;        // [2 buffers][2][kPreHalf] recorded s'
+constexpr int kLdsFixed = kLdsPre + 4 * kPreHalf;
+
+// per-lane constants of the step
 struct WalkLane {
-  int k, csh, hsh, kc;
-  bool lo16;
+  int csh, hsh, kc;   // code shift; D or D+2e; slot offset from it
+  uint32_t mlo;       // all ones for slots 0..15 (codes in the record's y word)
+  int kk;             // k + this half's table base
+  int dummy;          // pre stage byte of untouched slots
 };
 
-template <bool UNROLLED>
-__device__ __forceinline__ void walk_step(const uint4& r0, const uint4& r1, bool same, uint32_t& ldsv, uint32_t& ns,
-                                          uint8_t* tbl, const uint8_t* t3, uint8_t* pstage, int dummy,
+// Symbol T: the lookup of T is issued first; T-1's table write, the read of
+// T+1's row and T's recorded state then fill the lookup's latency.  The row
+// read one symbol ahead misses T's write, so a symbol continuing its
+// predecessor's row takes the state from the register instead.
+// T3[code][state] = the state after the slot's decision (code 0/1 its bit,
+// 2 none) | s' << 8, s' = the recorded value: the state for a 1 decision,
+// 256 - state for a 0 one, so that put_rac's new range is
+// (range * s' + (bit ? 0 : 255)) >> 8.
+__device__ __forceinline__ void walk_step(uint8_t* fixed, uint8_t* tbl, const uint4& r0, const uint4& r1,
+                                          uint32_t& e1, uint32_t& l0, int& addr_prev, int kc,
                                           const WalkLane& W) {
-  // start state: the register when the symbol continues the previous row
-  const uint32_t st = same ? ns : ldsv;
-  const int addr = (int)(r0.x & 0xFFFFu) + W.k;
-  ldsv = tbl[(int)(r1.x & 0xFFFFu) + W.k];  // next symbol's row, after every earlier write
-  const uint32_t code = ((W.lo16 ? r0.y : r0.z) >> W.csh) & 3u;
-  uint32_t nsv = t3[(code << 8) | st];
-  pin(nsv);
-  tbl[addr] = (uint8_t)nsv;  // lanes 32..63 repeat lanes 0..31: same address, same value
-  const int pos = (int)((r0.w >> W.hsh) & 0xFFFu) + W.kc;
-  pstage[code == 2u ? dummy : pos] = (uint8_t)st;
-  ns = nsv;
+  uint32_t a1 = e1, a0 = l0;
+  pin(a1);
+  pin(a0);
+  const bool same = (int)r0.w < 0;  // kRecSame
+  const uint32_t st = same ? a1 : a0;  // low byte: the slot's state
+  const uint32_t code = (((r0.y & W.mlo) | (r0.z & ~W.mlo)) >> W.csh) & 3u;  // bitwise: a select
+                                                                              // of members would go to scratch
+  const uint32_t idx = __builtin_amdgcn_perm(code, st, 0x0c0c0400u);  // code << 8 | (st & 0xFF)
+  uint32_t ev = reinterpret_cast<const uint16_t*>(fixed + kLdsT3)[idx];
+  tbl[addr_prev] = (uint8_t)a1;                          // T-1 (lanes 32..63 repeat 0..31)
+  l0 = tbl[(int)(r1.x & 0xFFFFu) + W.kk];                // T+1's row, after every earlier write but T's
+  const int pos = (int)((r0.w >> W.hsh) & 0xFFFu) + kc;
+  addr_prev = (int)(r0.x & 0xFFFFu) + W.kk;
+  pin(ev);
+  fixed[kLdsPre + (code == 2u ? W.dummy : pos)] = (uint8_t)(ev >> 8);
+  e1 = ev;
+}
+
+int64_t walk_lds_bytes_dev(int64_t state_bytes) { return kLdsFixed + 2 * (state_bytes / 2 + 32); }
+
+// c ? a : b by value (b in registers, pinned there: a select between a load
+// and a local would become a load from a selected address, via scratch).
+// Pinning a instead would force a wait for its load right here.
+__device__ __forceinline__ uint4 pick(bool c, uint4 a, uint4 b) {
+  pin(b.x); pin(b.y); pin(b.z); pin(b.w);
+  return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
+
+// record i of a plane with n records, or the null record (reads a valid one)
+__device__ __forceinline__ uint4 rec_or_null(const uint4* rp, int64_t i, int64_t n, uint4 nul) {
+  const int64_t j = i < n ? i : 0;
+  return pick(i < n, rp[j], nul);
 }
 
 __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  __shared__ __attribute__((aligned(16))) uint8_t fixed[kLdsFixed];
+  extern __shared__ __attribute__((aligned(16))) uint8_t tbl[];  // [2][contexts + 1 dummy row][32]
   const int64_t half = a.state_bytes / 2;  // one plane group's [contexts][32]
-  uint8_t* const tbl = lds;
-  uint8_t* const t3 = lds + half;
-  uint4* const recs = reinterpret_cast<uint4*>(t3 + kT3Bytes);
-  uint32_t* const stage = reinterpret_cast<uint32_t*>(t3 + kT3Bytes + (kWalkThreads + 2) * 16);
-  uint8_t* const pstage = t3 + kT3Bytes + (kWalkThreads + 2) * 16 + kStageWords * 4;
+  const int tsz = (int)half + 32;
   const int lane = threadIdx.x;
-  for (int i = lane; i < kT3Bytes; i += kWalkThreads) t3[i] = i < 512 ? a.ftab[i] : (uint8_t)(i - 512);
-  const int grp = blockIdx.x & 1;
-  const int chain = blockIdx.x >> 1;
-  const int seg_i = chain / a.nslices, slice = chain % a.nslices;
-  const Segment seg = a.segs[seg_i];
-  const SliceGeom& g = a.geom[slice];
-  const int p0 = grp ? 1 : 0, p1 = grp ? 3 : 1;  // planes of this group's chain
-  if (grp && g.plane_sym_off[1] >= g.nsym) return;  // no chroma
-  const int64_t n16 = half / 16;
-  uint4* const t4 = reinterpret_cast<uint4*>(tbl);
-  const int64_t goff = grp * half;
-  if (seg.load_states) {
-    const uint4* src = reinterpret_cast<const uint4*>(a.persist + (int64_t)slice * a.state_bytes + goff);
-    for (int64_t i = lane; i < n16; i += kWalkThreads) t4[i] = src[i];
-  } else {  // the segment starts at a keyframe (ff_ffv1_clear_slice_state)
-    const uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
-    for (int64_t i = lane; i < n16; i += kWalkThreads) t4[i] = v;
+  const int h = lane >> 5, k = lane & 31;
+  for (int i = lane; i < kT3Bytes; i += kWalkThreads) {
+    const int code = i >> 8, st = i & 255;
+    const int next = code < 2 ? a.ftab[i] : st;
+    const int sp = code == 1 ? st : 256 - st;  // (st = 0 never occurs)
+    reinterpret_cast<uint16_t*>(fixed + kLdsT3)[i] = (uint16_t)(next | ((sp & 0xFF) << 8));
   }
-  for (int i = lane; i < kStageWords; i += kWalkThreads) stage[i] = 0;
+  const int grp = blockIdx.x & 1;
+  const int npairs = (a.nslices + 1) / 2;
+  const int seg_i = (blockIdx.x >> 1) / npairs, pair = (blockIdx.x >> 1) % npairs;
+  const Segment seg = a.segs[seg_i];
+  const int sl = 2 * pair + h;              // this half's slice
+  const bool live = sl < a.nslices;
+  const SliceGeom& g = a.geom[live ? sl : 2 * pair];
+  const int p0 = grp ? 1 : 0, p1 = grp ? 3 : 1;  // planes of this group's chain
+  if (grp && g.plane_sym_off[1] >= g.nsym) return;  // no chroma (uniform: geometry of a frame)
+  uint8_t* const mytbl = tbl + h * tsz;
+  uint4* const myrecs = reinterpret_cast<uint4*>(fixed + kLdsRecs) + h * kRecSlots;
+  const int64_t n16 = half / 16;
+  const int64_t goff = grp * half;
+  {
+    uint4* const t4 = reinterpret_cast<uint4*>(mytbl);
+    if (seg.load_states && live) {
+      const uint4* src = reinterpret_cast<const uint4*>(a.persist + (int64_t)sl * a.state_bytes + goff);
+      for (int64_t i = k; i < n16; i += 32) t4[i] = src[i];
+    } else {  // the segment starts at a keyframe (ff_ffv1_clear_slice_state)
+      const uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
+      for (int64_t i = k; i < n16; i += 32) t4[i] = v;
+    }
+    if (k < 2) t4[n16 + k] = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);  // dummy row
+  }
   __syncthreads();
 
   WalkLane W;
-  W.k = lane & 31;
-  W.csh = (2 * W.k) & 31;
-  W.lo16 = W.k < 16;
-  const bool isU = W.k <= 10;            // zero flag / exponent slots: decision D + k
-  W.hsh = isU ? 0 : 16;                  // else from D + 2e: sign +2, mantissa 22+i: +1-i
-  W.kc = isU ? W.k : (W.k <= 21 ? 2 : 23 - W.k);
-  const int dummy = kPreStage + W.k;     // untouched slots store here
+  W.csh = (2 * k) & 31;
+  W.mlo = k < 16 ? ~0u : 0u;
+  const bool isU = k <= 10;                // zero flag / exponent slots: decision D + k
+  W.hsh = isU ? 0 : 16;                    // else from D + 2e: sign +2, mantissa 22+i: +1-i
+  const int kslot = isU ? k : (k <= 21 ? 2 : 23 - k);
+  W.kk = h * tsz + k;
+  const uint4 nullrec = make_uint4((uint32_t)half, 0xAAAAAAAAu, 0xAAAAAAAAu, 0u);  // dummy row, no decisions
 
+  // Stores of chunk c (recorded states, whole bits words) are issued at the
+  // start of chunk c+1, BEFORE its loads: vmcnt counts in issue order, so
+  // waiting for chunk c+2's data then never waits for stores just issued.
+  int par = 0;                    // pre stage buffer of the current chunk
+  uint8_t* pdst = a.ds.pre;       // pending copy: HBM (4-aligned), bytes incl. align, stage offset
+  int pnb = 0, palign = 0, pstage = 0;
+  uint32_t po0 = 0, po1 = 0, po2 = 0;  // pending bits words m = k, k+32, k+64
+  int64_t pwb = 0;
+  int pwend = 0;
+  bool pfirst = false;
+  auto flush_pending = [&]() {
+    {
+      const uint8_t* const src = fixed + pstage;
+      const int nw = pnb >> 2;
+      for (int i = k; i < nw; i += 32)
+        if (i > 0 || palign == 0) reinterpret_cast<uint32_t*>(pdst)[i] = reinterpret_cast<const uint32_t*>(src)[i];
+      if (k < 4) {
+        const int hb = palign + k;  // head bytes of the first dword
+        if (palign && hb < 4 && hb < pnb) pdst[hb] = src[hb];
+        const int tb = (nw << 2) + k;  // tail bytes past the last whole dword
+        if (tb < pnb && (nw > 0 || palign == 0 || tb >= 4)) pdst[tb] = src[tb];
+      }
+    }
+    uint32_t* const bits = a.ds.bits + pwb;
+    if (k < pwend) {
+      if (k == 0 && pfirst) atomicOr(&bits[0], po0);
+      else bits[k] = po0;
+    }
+    if (k + 32 < pwend) bits[k + 32] = po1;
+    if (k + 64 < pwend) bits[k + 64] = po2;
+    pnb = 0;
+    pwend = 0;
+  };
+
+  uint64_t t_loop = 0, n_steps = 0;
+  const uint64_t t_all = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
   for (int j = 0; j < seg.nframes; j++) {
     const int f = seg.first_frame + j;
-    const int64_t sid = (int64_t)f * a.nslices + slice;
+    const int64_t sid = (int64_t)f * a.nslices + (live ? sl : 0);
     const int* dc = a.ds.dcount + sid * 3;
-    const int64_t gbase = a.ds.dbase[sid] + (grp ? dc[0] : 0);  // first decision of the chain
-    int64_t wbase = gbase >> 5;  // bits word held in stage[0]
-    bool first_word = true;      // stage[0] may share its word with another chain
-    int64_t run = 0;             // decisions so far in this frame's chain
+    const int64_t gbase = live ? a.ds.dbase[sid] + (grp ? dc[0] : 0) : 0;  // first decision of the chain
+    bool first_word = true;   // the chain's first bits word may be shared with another chain
+    uint32_t carry = 0;       // bits of the partial word at decision gbase + run
+    int64_t run = 0;          // decisions so far in this frame's chain
     for (int pl = p0; pl < p1; pl++) {
-      const int64_t nsym = (pl < 2 ? g.plane_sym_off[pl + 1] : g.nsym) - g.plane_sym_off[pl];
+      const int64_t nsym = live ? (pl < 2 ? g.plane_sym_off[pl + 1] : g.nsym) - g.plane_sym_off[pl] : 0;
       const uint4* rp = a.rec + (int64_t)f * a.frame_samples + g.sym_off + g.plane_sym_off[pl];
-      uint4 next = lane < nsym ? rp[lane] : make_uint4(0, 0, 0, 0);
-      for (int64_t base = 0; base < nsym; base += kWalkThreads) {
-        const uint4 mine = next;
-        if (base + kWalkThreads + lane < nsym) next = rp[base + kWalkThreads + lane];
-        const int cnt = (int)min((int64_t)kWalkThreads, nsym - base);
-        const bool valid = lane < cnt;
-        const int v = valid ? (int)(int16_t)(mine.x >> 16) : 0;
-        const int d0 = (int)(mine.w & 0xFFFu);
-        const int nd = valid ? decisions_of(v) : 0;
-        const int total = __builtin_amdgcn_readlane(d0 + nd, cnt - 1);
-        uint8_t* const pre = a.ds.pre + gbase + run;
+      const uint32_t* cp = a.cbits + ((int64_t)f * a.frame_chunks + g.chunk_off[pl]) * kChunkWords;
+      const int nch = (int)((nsym + kChunk - 1) / kChunk);
+      const int nchunks = max(__builtin_amdgcn_readlane(nch, 0), __builtin_amdgcn_readlane(nch, 32));
+      // a chunk's inputs: 2 records and the funnel's bits words per lane
+      struct In {
+        uint4 m0, m1;
+        uint32_t hd, w0, w0p, w1, w1p, w2, w2p;
+      };
+      auto load = [&](int c) -> In {
+        In x;
+        const int64_t b = (int64_t)c * kChunk;
+        x.m0 = rec_or_null(rp, b + k, nsym, nullrec);
+        x.m1 = rec_or_null(rp, b + 32 + k, nsym, nullrec);
+        const bool ok = c < nch;  // else read chunk 0 of a plane of the pair (valid memory), use zeros
+        const uint32_t* q = cp + (int64_t)(ok ? c : 0) * kChunkWords;  // word 1 + m: bits word m
+        auto ld = [&](int i, bool use) -> uint32_t {
+          uint32_t zero = 0u;
+          pin(zero);
+          return use ? q[min(i, kChunkWords - 1)] : zero;
+        };
+        x.hd = ld(0, ok);
+        x.w0 = ld(1 + k, ok);
+        x.w0p = ld(k, ok && k > 0);
+        x.w1 = ld(33 + k, ok);
+        x.w1p = ld(32 + k, ok);
+        x.w2 = ld(65 + k, ok && 65 + k < kChunkWords);
+        x.w2p = ld(64 + k, ok && 64 + k < kChunkWords);
+        return x;
+      };
+      flush_pending();
+      In nx = load(0);
+      for (int c = 0; c < nchunks; c++) {
+        In cx = nx;
+        // wait for chunk c's data NOW, while everything older is long done;
+        // after the stores and loads below, vmcnt would wait for those too
+        pin(cx.m0.x); pin(cx.m0.y); pin(cx.m0.z); pin(cx.m0.w);
+        pin(cx.m1.x); pin(cx.m1.y); pin(cx.m1.z); pin(cx.m1.w);
+        pin(cx.hd); pin(cx.w0); pin(cx.w0p); pin(cx.w1); pin(cx.w1p); pin(cx.w2); pin(cx.w2p);
+        flush_pending();                       // chunk c-1's stores, then ...
+        if (c + 1 < nchunks) nx = load(c + 1);  // ... chunk c+1's loads
+        const int cnt = (int)min((int64_t)kChunk, max((int64_t)0, nsym - (int64_t)c * kChunk));
+        const int total = (int)(cx.hd & ~kChunkLong);
+        const bool lng = __ballot((cx.hd & kChunkLong) != 0) != 0;
+        const int64_t pos0 = gbase + run;  // decision index of the chunk's first decision
 
-        // decision bits -> stage (LDS) -> whole words to the bits array
+        // decision bits: funnel-shift the chunk's words to their HBM place
         {
-          const int64_t pos0 = gbase + run;                 // decision index of the chunk's first decision
-          const int off0 = (int)(pos0 - (wbase << 5));      // < 32
-          if (valid) {
-            const uint64_t bs = decision_bits(v);
-            const int q = off0 + d0, w = q >> 5, sh = q & 31;
-            const uint64_t x = bs << sh;                    // nd + sh <= 33 + 31 bits
-            atomicOr(&stage[w], (uint32_t)x);
-            if (nd + sh > 32) atomicOr(&stage[w + 1], (uint32_t)(x >> 32));
-          }
-          __syncthreads();
-          const int wend = (off0 + total) >> 5;             // complete words
-          const uint32_t sw = stage[lane];
-          const uint32_t carry = stage[wend];
-          if (lane < wend) {
-            if (lane == 0 && first_word) atomicOr(&a.ds.bits[wbase], sw);
-            else a.ds.bits[wbase + lane] = sw;
-          }
-          if (lane + kWalkThreads < wend) a.ds.bits[wbase + lane + kWalkThreads] = stage[lane + kWalkThreads];
-          __syncthreads();
-          stage[lane] = lane == 0 ? carry : 0u;
-          if (lane < kStageWords - kWalkThreads) stage[lane + kWalkThreads] = 0u;
+          const int sh = (int)(pos0 & 31);
+          const int rs = (32 - sh) & 31;
+          uint32_t o0 = sh ? __builtin_amdgcn_alignbit(cx.w0, cx.w0p, rs) : cx.w0;
+          const uint32_t o1 = sh ? __builtin_amdgcn_alignbit(cx.w1, cx.w1p, rs) : cx.w1;
+          const uint32_t o2 = sh ? __builtin_amdgcn_alignbit(cx.w2, cx.w2p, rs) : cx.w2;
+          if (k == 0) o0 |= carry;
+          const int wend = (sh + total) >> 5;  // complete words
+          // the partial word wend -> carry (word m sits in lane m % 32 of its half, round m / 32)
+          const int wA = __builtin_amdgcn_readlane(wend, 0), wB = __builtin_amdgcn_readlane(wend, 32);
+          const uint32_t rA = (wA >> 5) == 0 ? o0 : (wA >> 5) == 1 ? o1 : o2;
+          const uint32_t rB = (wB >> 5) == 0 ? o0 : (wB >> 5) == 1 ? o1 : o2;
+          const uint32_t cA = __builtin_amdgcn_readlane(rA, wA & 31);
+          const uint32_t cB = __builtin_amdgcn_readlane(rB, 32 + (wB & 31));
+          const uint32_t ncarry = h ? cB : cA;
+          po0 = o0;
+          po1 = o1;
+          po2 = o2;
+          pwb = pos0 >> 5;
+          pwend = wend;
+          pfirst = first_word;
           if (wend > 0) first_word = false;
-          wbase += wend;
+          carry = ncarry;
         }
 
-        if (__ballot(v >= 1024 || v <= -1024)) {  // e >= 10 somewhere: one symbol at a time, no staging
-          __syncthreads();
-          for (int t = 0; t < cnt; t++) {
-            SymDec d;
-            d.row = (int)(__builtin_amdgcn_readlane(mine.x, t) & 0xFFFFu) / 32;
-            d.v = __builtin_amdgcn_readlane(v, t);
-            d.mag = d.v < 0 ? 0u - (unsigned)d.v : (unsigned)d.v;
-            d.e = d.v ? 31 - __builtin_clz(d.mag) : -1;
-            walk_long(tbl, a.ftab, d, lane, pre + __builtin_amdgcn_readlane(d0, t));
+        myrecs[k] = pick(k < cnt, cx.m0, nullrec);
+        myrecs[k + 32] = pick(k + 32 < cnt, cx.m1, nullrec);
+        if (k < 2) myrecs[kChunk + k] = nullrec;
+        __syncthreads();
+
+        if (lng) {  // e >= 10 somewhere: one symbol at a time, recorded straight to HBM
+          const int cmax = max(__builtin_amdgcn_readlane(cnt, 0), __builtin_amdgcn_readlane(cnt, 32));
+          for (int t = 0; t < cmax; t++) {
+            const uint4 r = myrecs[t];
+            if (t < cnt)
+              walk_long(mytbl, a.ftab, (int)(int16_t)(r.x >> 16), (int)(r.x & 0xFFFFu) + k, k,
+                        a.ds.pre + pos0 + (int)(r.w & 0xFFFu));
           }
           __syncthreads();
           run += total;
           continue;
         }
 
-        recs[lane] = mine;
-        const uint64_t same = __ballot(valid && (mine.w & kRecSame));
-        __syncthreads();
-
-        uint4 r0 = recs[0];
-        uint4 r1 = recs[1];
-        uint32_t ldsv = tbl[(int)(r0.x & 0xFFFFu) + W.k];
-        uint32_t ns = 0;
-        if (cnt == kWalkThreads) {
-          static_for<0, kWalkThreads>([&](auto tc) {
-            constexpr int T = decltype(tc)::value;
-            const uint4 r2 = recs[T + 2];  // two ahead (past the chunk: unused)
-            walk_step<true>(r0, r1, (same >> T) & 1, ldsv, ns, tbl, t3, pstage, dummy, W);
-            r0 = r1;
-            r1 = r2;
-          });
-        } else {
-          for (int t = 0; t < cnt; t++) {
-            const uint4 r2 = recs[t + 2];
-            walk_step<false>(r0, r1, (same >> t) & 1, ldsv, ns, tbl, t3, pstage, dummy, W);
-            r0 = r1;
-            r1 = r2;
-          }
+        const int align = (int)(pos0 & 3);  // pre stage byte i <-> HBM byte pos0 - align + i
+        const int pb = kLdsPre + (par * 2 + h) * kPreHalf;
+        const int kc = kslot + pb - kLdsPre + align;
+        W.dummy = pb - kLdsPre + kPreStage + 4 + k;
+        uint4 r0 = myrecs[0], r1 = myrecs[1];
+        uint32_t l0 = tbl[(int)(r0.x & 0xFFFFu) + W.kk];
+        uint32_t e1 = 0;
+        int addr_prev = (int)((fixed + kLdsPre + W.dummy) - tbl);  // no T-1 yet: a dummy byte
+        const uint64_t t0 = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+        static_for<0, kChunk>([&](auto tc) {
+          constexpr int T = decltype(tc)::value;
+          const uint4 r2 = myrecs[T + 2];  // two ahead
+          walk_step(fixed, tbl, r0, r1, e1, l0, addr_prev, kc, W);
+          r0 = r1;
+          r1 = r2;
+        });
+        tbl[addr_prev] = (uint8_t)e1;  // the chunk's last symbol
+        if (a.dbg) {
+          __builtin_amdgcn_s_waitcnt(0);
+          t_loop += __builtin_amdgcn_s_memtime() - t0;
+          n_steps += kChunk;
         }
+        // chunk c's recorded states go out with chunk c+1's stores
+        pdst = a.ds.pre + pos0 - align;
+        pnb = align + total;
+        palign = align;
+        pstage = pb;
+        par ^= 1;
         __syncthreads();
-        for (int i = lane; i < total; i += kWalkThreads) pre[i] = pstage[i];
         run += total;
       }
     }
     // the frame's last, partial bits word
-    if (lane == 0 && ((gbase + run) & 31)) atomicOr(&a.ds.bits[wbase], stage[0]);
-    __syncthreads();
-    for (int i = lane; i < kStageWords; i += kWalkThreads) stage[i] = 0;
-    __syncthreads();
+    if (k == 0 && ((gbase + run) & 31)) atomicOr(&a.ds.bits[(gbase + run) >> 5], carry);
   }
-  if (seg.save_states) {
+  flush_pending();
+  if (seg.save_states && live) {
     __syncthreads();
-    uint4* dst = reinterpret_cast<uint4*>(a.persist + (int64_t)slice * a.state_bytes + goff);
-    for (int64_t i = lane; i < n16; i += kWalkThreads) dst[i] = t4[i];
+    uint4* dst = reinterpret_cast<uint4*>(a.persist + (int64_t)sl * a.state_bytes + goff);
+    const uint4* t4 = reinterpret_cast<const uint4*>(mytbl);
+    for (int64_t i = k; i < n16; i += 32) dst[i] = t4[i];
+  }
+  if (a.dbg && lane == 0) {
+    a.dbg[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memtime() - t_all;
+    a.dbg[blockIdx.x * 4 + 1] = t_loop;
+    a.dbg[blockIdx.x * 4 + 2] = n_steps;
   }
 }
 
@@ -1318,10 +1470,10 @@ int launch_dcode(const CodeArgs& a, void* stream) {
 int64_t walk_lds_bytes(int64_t state_bytes) { return walk_lds_bytes_dev(state_bytes); }
 
 int launch_walk(const WalkArgs& a, int nsegs, void* stream) {
-  const size_t lds = (size_t)walk_lds_bytes_dev(a.state_bytes);
-  if ((int64_t)lds > kWalkLdsMax) return -1;
-  dim3 grid((unsigned)(nsegs * a.nslices * 2)), block(kWalkThreads);
-  hipLaunchKernelGGL(ffv1_walk, grid, block, lds, reinterpret_cast<hipStream_t>(stream), a);
+  if (walk_lds_bytes_dev(a.state_bytes) > kWalkLdsMax) return -1;
+  const size_t dyn = (size_t)(2 * (a.state_bytes / 2 + 32));  // the tables; the fixed part is static
+  dim3 grid((unsigned)(nsegs * ((a.nslices + 1) / 2) * 2)), block(kWalkThreads);
+  hipLaunchKernelGGL(ffv1_walk, grid, block, dyn, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
