@@ -752,21 +752,31 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_dcode(CodeArgs a) {
   const uint4* P = reinterpret_cast<const uint4*>(a.ds.pre + base);
   const uint32_t* B = a.ds.bits + (base >> 5);
   const int nmax = wave_max(n);
+  // blocks of 32 decisions (32 state bytes + one bits word), loaded two
+  // blocks ahead (streams are padded to 64 decisions: reads stay inside)
   const uint4 z4 = make_uint4(0, 0, 0, 0);
-  uint4 na = z4, nb = z4;
-  uint32_t nw = 0u;
+  uint4 na = z4, nb = z4, ma = z4, mb = z4;
+  uint32_t nw = 0u, mw = 0u;
   if (n > 0) {
     na = P[0];
-    nb = P[1];  // streams are padded to 64 decisions
+    nb = P[1];
     nw = B[0];
+  }
+  if (n > 32) {
+    ma = P[2];
+    mb = P[3];
+    mw = B[1];
   }
   for (int i = 0; i < nmax; i += 32) {
     const uint4 wa = na, wb = nb;
     const uint32_t bw = nw;
-    if (i + 32 < n) {  // next block (streams are padded to 64 decisions)
-      na = P[(i >> 4) + 2];
-      nb = P[(i >> 4) + 3];
-      nw = B[(i >> 5) + 1];
+    na = ma;
+    nb = mb;
+    nw = mw;
+    if (i + 64 < n) {
+      ma = P[(i >> 4) + 4];
+      mb = P[(i >> 4) + 5];
+      mw = B[(i >> 5) + 2];
     }
     if (i + 32 <= n)
       decide32<false>(L, wa, wb, bw, 32);
