@@ -222,6 +222,7 @@ struct ffv1hip_ctx {
   int64_t frame_samples = 0;  // symbols of one frame (each slice padded to 4)
   int64_t frame_chunks = 0;   // 64-sample walk chunks of one frame
   int max_ops = 0;
+  int nopsets = 1;         // op sets the header programs use (<= kOpSets)
   std::vector<SliceGeom> geom;
   // device buffers
   uint8_t* d_frames = nullptr;
@@ -246,6 +247,7 @@ struct ffv1hip_ctx {
   int64_t* d_dtotal = nullptr;   // [2] decisions of the batch (incl. alignment)
   int64_t* h_dtotal = nullptr;   // pinned readback of d_dtotal
   uint8_t* d_pre[2] = {nullptr, nullptr};    // [decision] state before the decision
+  uint8_t* d_scratch = nullptr;               // where idle walk chains write their stage
   uint32_t* d_bits[2] = {nullptr, nullptr};  // [decision / 32] decision bits
   int64_t dcap[2] = {0, 0};      // decisions d_pre/d_bits hold
   int buf = 0;                   // buffer set of the next batch
@@ -407,7 +409,9 @@ static void build_ops(ffv1hip_ctx* c) {
   const ffv1hip_params& p = c->P;
   c->ops.assign(size_t(2) * c->nslices * kMaxOps, Op{0, 0, 0, 0});
   c->nops.assign(size_t(2) * c->nslices, 0);
-  enum { kSetHdr = 0, kSetQ0 = 1, kSetKey = 6, kSetSlice = 7 };
+  c->nopsets = 1;
+  // the sets a v3 stream uses first: its coder then keeps only two per lane
+  enum { kSetKey = 0, kSetSlice = 1, kSetHdr = 2, kSetQ0 = 3 };
   for (int key = 0; key < 2; key++)
     for (int s = 0; s < c->nslices; s++) {
       OpList L;
@@ -447,6 +451,7 @@ static void build_ops(ffv1hip_ctx* c) {
         L.sym(kSetSlice, 1, p.sar_den, false);
       }
       const size_t sel = size_t(key) * c->nslices + s;
+      for (const Op& op : L.ops) c->nopsets = std::max(c->nopsets, int(op.set) + 1);
       c->nops[sel] = int(L.ops.size());
       std::memcpy(&c->ops[sel * kMaxOps], L.ops.data(), L.ops.size() * sizeof(Op));
     }
@@ -456,7 +461,7 @@ static void free_device(ffv1hip_ctx* c) {
   void* ptrs[] = {c->d_frames, c->d_qt, c->d_tabs, c->d_ops, c->d_nops, c->d_segs, c->d_keys,
                   c->d_slice_out, c->d_slice_bytes, c->d_packets, c->d_packet_size, c->d_persist,
                   c->d_tables, c->d_sym, c->d_keys2, c->d_cbits, c->d_dcount, c->d_dbase, c->d_dtotal, c->d_pre[0],
-                  c->d_pre[1], c->d_bits[0], c->d_bits[1], c->d_geom, c->d_slot_frames, c->d_status};
+                  c->d_pre[1], c->d_bits[0], c->d_bits[1], c->d_scratch, c->d_geom, c->d_slot_frames, c->d_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_dtotal) (void)hipHostFree(c->h_dtotal);
@@ -529,7 +534,8 @@ static int alloc_device(ffv1hip_ctx* c) {
     for (hipEvent_t& e : c->coded) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     // decision capacity: the worst case when it is small, else ~12 per symbol
     // (real content codes ~10); a batch that needs more grows the set
-    const int64_t align = int64_t(nb) * c->nslices * kStreamAlign;
+    HIP_TRY(hipMalloc(&c->d_scratch, 4096));
+    const int64_t align = int64_t(nb) * c->nslices * kStreamSlack;
     const int64_t worst = int64_t(nb) * c->frame_samples * c->wmax + align;
     const int64_t guess = int64_t(nb) * c->frame_samples * 12 + align;
     const int64_t cap = worst <= (int64_t(1) << 31) ? worst : std::min(worst, guess);
@@ -789,7 +795,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     if (timed(0, st, [&] { return launch_layout(d_dcount, n * c->nslices, d_dbase, c->d_dtotal + fb, st); }) < 0)
       return set_err(-5, "layout launch failed: %s", hipGetErrorString(hipGetLastError()));
     // decisions of this batch: the worst case fits without asking the device
-    int64_t need = int64_t(n) * c->frame_samples * c->wmax + int64_t(n) * c->nslices * kStreamAlign;
+    int64_t need = int64_t(n) * c->frame_samples * c->wmax + int64_t(n) * c->nslices * kStreamSlack;
     if (need > c->dcap[fb]) {
       HIP_TRY(hipMemcpyAsync(c->h_dtotal + fb, c->d_dtotal + fb, sizeof(int64_t), hipMemcpyDeviceToHost, st));
       HIP_TRY(hipStreamSynchronize(st));  // also: set fb's previous coder is done (waited above)
@@ -799,6 +805,15 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     }
     HIP_TRY(hipMemsetAsync(c->d_bits[fb], 0, size_t((need + 31) / 32) * 4, st));
     DecisionStream ds{d_dcount, d_dbase, c->d_pre[fb], c->d_bits[fb]};
+    BitsArgs ba{};
+    ba.cbits = sa.cbits;
+    ba.frame_chunks = c->frame_chunks;
+    ba.geom = c->d_geom;
+    ba.nslices = c->nslices;
+    ba.nframes = n;
+    ba.ds = ds;
+    if (timed(0, st, [&] { return launch_bits(ba, st); }) < 0)
+      return set_err(-5, "bits launch failed: %s", hipGetErrorString(hipGetLastError()));
     WalkArgs wa{};
     wa.rec = d_rec;
     wa.cbits = sa.cbits;
@@ -811,6 +826,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     wa.state_bytes = ca.state_bytes;
     wa.persist = c->d_persist;
     wa.ds = ds;
+    wa.scratch = c->d_scratch;
     // FFV1HIP_WALKDBG=1 (measurement hook): per-block cycle split to stderr
     static const bool walkdbg = std::getenv("FFV1HIP_WALKDBG") && std::atoi(std::getenv("FFV1HIP_WALKDBG"));
     uint64_t* d_dbg = nullptr;
@@ -828,10 +844,11 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       HIP_TRY(hipStreamSynchronize(st));
       HIP_TRY(hipFree(d_dbg));
       double all[2] = {0, 0}, loop[2] = {0, 0}, steps[2] = {0, 0};
-      for (int b = 0; b < nblk; b++) {
-        all[b & 1] += double(h[4 * b]);
-        loop[b & 1] += double(h[4 * b + 1]);
-        steps[b & 1] += double(h[4 * b + 2]);
+      for (int b = 0; b < nblk; b++) {  // luma chains are the first half of the grid
+        const int gi = b >= nblk / 2;
+        all[gi] += double(h[4 * b]);
+        loop[gi] += double(h[4 * b + 1]);
+        steps[gi] += double(h[4 * b + 2]);
       }
       for (int g = 0; g < 2; g++)
         std::fprintf(stderr, "walkdbg grp %d: blocks %d, memtime per block %.3g, loop share %.3f, memtime/step %.1f\n", g,
@@ -842,6 +859,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     HIP_TRY(hipEventRecord(c->walked[fb], st));
     HIP_TRY(hipStreamWaitEvent(cst, c->walked[fb], 0));
     ca.nframes = n;
+    ca.nopsets = c->nopsets;
     ca.ds = ds;
     if (timed(1, cst, [&] { return launch_dcode(ca, cst); }) < 0)
       return set_err(-5, "code launch failed: %s", hipGetErrorString(hipGetLastError()));

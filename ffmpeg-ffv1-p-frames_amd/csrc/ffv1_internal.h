@@ -84,9 +84,17 @@ constexpr uint32_t kRecSame = 0x80000000u;
 
 // Decision stream of one batch (frame-parallel mode).  Every (frame, slice)
 // stream's binary decisions, in coding order, start at decision index
-// dbase[frame][slice] (a multiple of 64); decision d has its adaptive state
-// as it stood before the decision in pre[d] and its value in bit d of
-// bits[] (bit d & 31 of word d >> 5).
+// dbase[frame][slice] (a multiple of 64): the luma chain's dcount[0]
+// decisions, then, from chroma_start(dcount[0]), the chroma chain's (Cb then
+// Cr).  Each chain is followed by kChainPad unused decisions: the states
+// walk writes a chunk's recorded bytes in whole 16-byte blocks, and the
+// blocks past a chain's last decision land there.  Decision d has s' (the
+// state it is coded with, folded with its bit, see ffv1_walk) in pre[d] and
+// its value in bit d of bits[] (bit d & 31 of word d >> 5).
+constexpr int kChainPad = 1536;
+__host__ __device__ inline int64_t chroma_start(int64_t dc0) { return ((dc0 + 63) & ~int64_t(63)) + kChainPad; }
+// decisions a stream takes beyond its own (alignment and the two pads)
+constexpr int64_t kStreamSlack = 2 * kChainPad + 2 * 64;
 struct DecisionStream {
   const int* dcount;          // [frame][slice][3] decisions per plane
   const int64_t* dbase;       // [frame][slice]
@@ -121,6 +129,7 @@ struct CodeArgs {
   int version;                // bitstream version (Golomb: v3 adds a 129/0 decision)
   int coded_bits;             // "bits" of encode_line (8 for <=8-bit)
   int nframes;                // decision-stream mode: frames of the batch
+  int nopsets;                // decision-stream mode: op sets the header programs use
   DecisionStream ds;
 };
 
@@ -142,7 +151,18 @@ struct WalkArgs {
   int64_t state_bytes;
   uint8_t* persist;           // [slice][state_bytes]
   DecisionStream ds;
+  uint8_t* scratch;           // >= 2 KiB: where idle chains write their stage
   uint64_t* dbg;              // optional [block][4] cycle counters (FFV1HIP_WALKDBG)
+};
+
+// Kernel 2b: the decision bits, from the chunks' packed words to their place
+// in the decision stream (one block per (frame, slice) stream).
+struct BitsArgs {
+  const uint32_t* cbits;      // [batch frame][frame_chunks][kChunkWords]
+  int64_t frame_chunks;
+  const SliceGeom* geom;
+  int nslices, nframes;
+  DecisionStream ds;
 };
 
 struct AssembleArgs {
@@ -162,6 +182,7 @@ int launch_code(const CodeArgs& a, void* stream);
 int launch_layout(const int* dcount, int nstreams, int64_t* dbase, int64_t* total, void* stream);
 int launch_walk(const WalkArgs& a, int nsegs, void* stream);
 int launch_dcode(const CodeArgs& a, void* stream);
+int launch_bits(const BitsArgs& a, void* stream);
 int64_t walk_lds_bytes(int64_t state_bytes);
 constexpr int64_t kWalkLdsMax = 64 * 1024;  // states walk: one plane group's table + T9 + staging in LDS
 constexpr int kStreamAlign = 64;            // decisions: every stream starts at a multiple

@@ -233,8 +233,8 @@ __device__ __forceinline__ void pin(uint32_t& v) { asm volatile("" : "+v"(v)); }
 struct Lane {
   int low, range;
   uint32_t r0, r1, r2, r3, r4, r5, r6, r7;  // states of the current context row (byte k = slot k)
-  int dc;              // digits in the LDS ring
   uint32_t* ring;      // this lane's ring row (LDS)
+  uint32_t* rp;        // ring head: the digits so far are ring[0 .. rp - ring)
 
   template <int D>
   __device__ __forceinline__ uint32_t& w() {
@@ -308,19 +308,19 @@ __device__ __forceinline__ Sink make_sink(uint8_t* out, int64_t cap) {
 // advances when a byte is really shifted out.
 __device__ __forceinline__ void renorm(Lane& L) {
   const bool need = L.range < 0x100;
-  L.ring[L.dc] = (uint32_t)L.low;
-  L.dc += need ? 1 : 0;
-  L.low = need ? ((L.low & 0xFF) << 8) : L.low;
+  *L.rp = (uint32_t)L.low;
+  L.rp += need ? 1 : 0;
+  L.low = need ? (int)__builtin_amdgcn_perm(0u, (uint32_t)L.low, 0x0c0c000cu) : L.low;  // (low & 0xFF) << 8
   L.range = need ? (L.range << 8) : L.range;
 }
 
 __device__ __forceinline__ void flush(Lane& L, Sink& S) {
-  for (int t = 0; t < L.dc; t++) S.digit((int)L.ring[t]);
-  L.dc = 0;
+  for (const uint32_t* p = L.ring; p < L.rp; p++) S.digit((int)*p);
+  L.rp = L.ring;
 }
 
 __device__ __forceinline__ void flush_if(Lane& L, Sink& S, int above) {
-  if (__ballot(L.dc > above)) flush(L, S);
+  if (__ballot((int)(L.rp - L.ring) > above)) flush(L, S);
 }
 
 __device__ __forceinline__ void rac_core(Lane& L, int s, int bit) {
@@ -516,10 +516,12 @@ constexpr int kCodeThreads = kWave;
 constexpr int kOpsetBytes = kOpSets * 32;
 
 // Key bit / in-band v0/v1 header / v3 slice header (per-lane op program).
+// os: this lane's op-set states (osb bytes); flush_at: the ring's flush
+// threshold before each op (<= 29 digits per op).
 __device__ __forceinline__ void run_header_ops(const CodeArgs& a, Lane& L, Sink& S, uint8_t* os, int key,
                                                int slice, bool live, const uint8_t* dtab,
-                                               const uint8_t* ftab) {
-  for (int i = 0; i < kOpsetBytes; i++) os[i] = 128;
+                                               const uint8_t* ftab, int osb, int flush_at) {
+  for (int i = 0; i < osb; i++) os[i] = 128;
   const int sel = key * a.nslices + slice;
   const int n = live ? a.nops[sel] : 0;
   const Op* ops = a.ops + (int64_t)sel * kMaxOps;
@@ -533,21 +535,21 @@ __device__ __forceinline__ void run_header_ops(const CodeArgs& a, Lane& L, Sink&
       else
         symbol_lds(L, st, op.value, op.kind == kOpSymS, t);
     }
-    flush_if(L, S, kHeaderFlushAt);
+    flush_if(L, S, flush_at);
   }
 }
 
 __device__ __forceinline__ void lane_init(Lane& L, uint32_t* ring) {
   L.low = 0;
   L.range = 0xFF00;
-  L.dc = 0;
   L.ring = ring;
+  L.rp = ring;
   L.r0 = L.r1 = L.r2 = L.r3 = L.r4 = L.r5 = L.r6 = L.r7 = 0;
 }
 
 // slice end: a 0 decision on state 129, then ff_rac_terminate
-__device__ __forceinline__ int64_t terminate(Lane& L, Sink& S, bool state129) {
-  flush_if(L, S, kRing - 4);
+__device__ __forceinline__ int64_t terminate(Lane& L, Sink& S, bool state129, int ring) {
+  flush_if(L, S, ring - 4);
   if (state129) {
     rac_core(L, 129, 0);
     renorm(L);
@@ -605,7 +607,7 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
   uint8_t* const out = a.slice_out + ((int64_t)(live ? f : 0) * a.nslices + slice) * a.slice_cap;
   Sink S = make_sink(out, live ? a.slice_cap : 0);  // idle lanes write nothing
 
-  run_header_ops(a, L, S, opsets + lane * kOpsetBytes, key, slice, live, dtab, ftab);
+  run_header_ops(a, L, S, opsets + lane * kOpsetBytes, key, slice, live, dtab, ftab, kOpsetBytes, kHeaderFlushAt);
 
   const SliceGeom& g = a.geom[slice];
   const int64_t nsym = live ? g.nsym : 0;
@@ -674,7 +676,7 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
   }
 
   if (live) {
-    const int64_t nbytes = terminate(L, S, true);
+    const int64_t nbytes = terminate(L, S, true, kRing);
     if (nbytes > a.slice_cap) atomicAdd(a.status, 1);
     a.slice_bytes[(int64_t)f * a.nslices + slice] = nbytes;
     if (a.j == seg.nframes - 1 && seg.save_states) {
@@ -686,12 +688,19 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
 
 // ---------------------------------------------------------------------------
 // Kernel 2, decision-stream form: one lane per (frame, slice) stream of the
-// batch.  ffv1_walk recorded every decision's state and bit, so what is
-// left is put_rac's arithmetic (rangecoder.h:90-102) and the renormalisation
-// (rangecoder.h:52-75), 32 decisions per step from 32 state bytes + one bit
-// word: no per-symbol structure, so no lane waits on another's exponent.
+// batch.  ffv1_walk recorded every decision's state and ffv1_bits its bit,
+// so what is left is put_rac's arithmetic (rangecoder.h:90-102) and the
+// renormalisation (rangecoder.h:52-75), 32 decisions per step from 32 state
+// bytes + one bit word: no per-symbol structure, so no lane waits on
+// another's exponent.  The ring is small (a flush check every 16 decisions)
+// so that a coder wave fits in the LDS the states walk leaves on a CU.
+constexpr int kDRing = 40;                   // renorm digits per lane before a flush
+constexpr int kDRingStride = kDRing + 1;
+constexpr int kDFlushAt = kDRing - 17;       // checked every 16 decisions
+
 template <bool TAIL>
-__device__ __forceinline__ void decide32(Lane& L, const uint4& wa, const uint4& wb, uint32_t bw, int rem) {
+__device__ __forceinline__ void decide32(Lane& L, Sink& S, const uint4& wa, const uint4& wb, uint32_t bw,
+                                         int rem) {
   static_for<0, 32>([&](auto jc) {
     constexpr int J = decltype(jc)::value;
     constexpr int SH = (J & 3) * 8;
@@ -704,9 +713,9 @@ __device__ __forceinline__ void decide32(Lane& L, const uint4& wa, const uint4& 
     else if constexpr (J < 24) w = wb.y;
     else if constexpr (J < 28) w = wb.z;
     else w = wb.w;
-    const unsigned sp = (w >> SH) & 0xFF;     // s' = bit ? state : 256 - state
-    const int m = -(int)((bw >> J) & 1u);     // all ones for a 1 decision
-    const unsigned c = (unsigned)~m & 255u;   // round-up term of a 0 decision
+    const unsigned sp = __builtin_amdgcn_ubfe(w, SH, 8);        // s' = bit ? state : 256 - state
+    const int m = __builtin_amdgcn_sbfe((int)bw, J, 1);         // all ones for a 1 decision
+    const unsigned c = (unsigned)~m & 255u;                     // round-up term of a 0 decision
     // put_rac: 1 -> range*s >> 8; 0 -> range - (range*s >> 8) = (range*(256-s) + 255) >> 8
     const int nr0 = (int)(__umul24((unsigned)L.range, sp) + c) >> 8;
     int nl = L.low + ((L.range - nr0) & m);
@@ -719,14 +728,20 @@ __device__ __forceinline__ void decide32(Lane& L, const uint4& wa, const uint4& 
     L.low = nl;
     L.range = nr;
     renorm(L);
+    if constexpr (J == 15) flush_if(L, S, kDFlushAt);
   });
+}
+
+__host__ __device__ constexpr size_t dcode_lds_bytes(int nopsets) {
+  return 1024 + (size_t)kCodeThreads * (nopsets * 32 + kDRingStride * 4);
 }
 
 __global__ __launch_bounds__(kCodeThreads) void ffv1_dcode(CodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int osb = a.nopsets * 32;
   uint8_t* const tabs = lds;
   uint8_t* const opsets = lds + 1024;
-  uint32_t* const ring = reinterpret_cast<uint32_t*>(opsets + kCodeThreads * kOpsetBytes);
+  uint32_t* const ring = reinterpret_cast<uint32_t*>(opsets + kCodeThreads * osb);
   for (int i = threadIdx.x; i < 1024; i += kCodeThreads) tabs[i] = a.tabs[i];
   __syncthreads();
   const int lane = threadIdx.x;
@@ -739,94 +754,104 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_dcode(CodeArgs a) {
   const int key = live ? a.keyflags[f] : 0;
 
   Lane L;
-  lane_init(L, ring + lane * kRingStride);
+  lane_init(L, ring + lane * kDRingStride);
   uint8_t* const out = a.slice_out + ((int64_t)f * a.nslices + slice) * a.slice_cap;
   Sink S = make_sink(out, live ? a.slice_cap : 0);
-  run_header_ops(a, L, S, opsets + lane * kOpsetBytes, key, slice, live, tabs, tabs + 512);
-  flush_if(L, S, kRing - 33);
+  run_header_ops(a, L, S, opsets + lane * osb, key, slice, live, tabs, tabs + 512, osb, kDRing - 30);
+  flush_if(L, S, kDFlushAt);
 
   const int64_t st = (int64_t)f * a.nslices + slice;
   const int* dc = a.ds.dcount + st * 3;
-  const int n = live ? dc[0] + dc[1] + dc[2] : 0;
   const int64_t base = live ? a.ds.dbase[st] : 0;  // multiple of kStreamAlign
-  const uint4* P = reinterpret_cast<const uint4*>(a.ds.pre + base);
-  const uint32_t* B = a.ds.bits + (base >> 5);
-  const int nmax = wave_max(n);
-  // blocks of 32 decisions (32 state bytes + one bits word), loaded two
-  // blocks ahead (streams are padded to 64 decisions: reads stay inside)
-  const uint4 z4 = make_uint4(0, 0, 0, 0);
-  uint4 na = z4, nb = z4, ma = z4, mb = z4;
-  uint32_t nw = 0u, mw = 0u;
-  if (n > 0) {
-    na = P[0];
-    nb = P[1];
-    nw = B[0];
-  }
-  if (n > 32) {
-    ma = P[2];
-    mb = P[3];
-    mw = B[1];
-  }
-  for (int i = 0; i < nmax; i += 32) {
-    const uint4 wa = na, wb = nb;
-    const uint32_t bw = nw;
-    na = ma;
-    nb = mb;
-    nw = mw;
-    if (i + 64 < n) {
-      ma = P[(i >> 4) + 4];
-      mb = P[(i >> 4) + 5];
-      mw = B[(i >> 5) + 2];
+  // the luma chain's decisions, then the chroma chain's at their own start
+  for (int part = 0; part < 2; part++) {
+    const int n = live ? (part ? dc[1] + dc[2] : dc[0]) : 0;
+    const int64_t pb = base + (part && live ? chroma_start(dc[0]) : 0);  // multiple of 64
+    const uint4* P = reinterpret_cast<const uint4*>(a.ds.pre + pb);
+    const uint32_t* B = a.ds.bits + (pb >> 5);
+    const int nmax = wave_max(n);
+    // blocks of 32 decisions (32 state bytes + one bits word), loaded two
+    // blocks ahead (parts are padded to 64 decisions: reads stay inside)
+    const uint4 z4 = make_uint4(0, 0, 0, 0);
+    uint4 na = z4, nb = z4, ma = z4, mb = z4;
+    uint32_t nw = 0u, mw = 0u;
+    if (n > 0) {
+      na = P[0];
+      nb = P[1];
+      nw = B[0];
     }
-    if (i + 32 <= n)
-      decide32<false>(L, wa, wb, bw, 32);
-    else if (i < n)
-      decide32<true>(L, wa, wb, bw, n - i);
-    flush_if(L, S, kRing - 33);  // <= 32 digits per block
+    if (n > 32) {
+      ma = P[2];
+      mb = P[3];
+      mw = B[1];
+    }
+    for (int i = 0; i < nmax; i += 32) {
+      const uint4 wa = na, wb = nb;
+      const uint32_t bw = nw;
+      na = ma;
+      nb = mb;
+      nw = mw;
+      if (i + 64 < n) {
+        ma = P[(i >> 4) + 4];
+        mb = P[(i >> 4) + 5];
+        mw = B[(i >> 5) + 2];
+      }
+      if (i + 32 <= n)
+        decide32<false>(L, S, wa, wb, bw, 32);
+      else if (i < n)
+        decide32<true>(L, S, wa, wb, bw, n - i);
+      flush_if(L, S, kDFlushAt);  // <= 16 digits per half block
+    }
   }
   if (live) {
-    const int64_t nbytes = terminate(L, S, true);
+    const int64_t nbytes = terminate(L, S, true, kDRing);
     if (nbytes > a.slice_cap) atomicAdd(a.status, 1);
     a.slice_bytes[st] = nbytes;
   }
 }
 
 // ---------------------------------------------------------------------------
-// Kernel 2a: context-state walk.  One wave per (segment, slice, plane group);
-// group 0 = the luma contexts, 1 = the chroma contexts Cb and Cr share
-// (ffv1enc.c:1194-1195): independent chains.  The group's [contexts][32]
-// states live in LDS.  Symbols are taken in chunks of 64: a prologue with
-// one symbol per lane computes decision counts, offsets (wave prefix sum),
-// decision bits and a per-symbol record (row, 2-bit slot codes, offset);
-// then the symbols are applied one per step, lane k < 32 owning slot k of
-// the symbol's row (put_symbol_inline, ffv1enc.c:185-231).  Each touched
-// lane records the state its decision is coded with at the decision's
-// index (LDS staging, copied out per chunk).
+// Kernel 2a: context-state walk.  One wave per (segment, slice pair, plane
+// group); group 0 = the luma contexts, 1 = the chroma contexts Cb and Cr
+// share (ffv1enc.c:1194-1195): independent chains.  Half h = lane / 32 walks
+// the chain of slice 2 * pair + h, lane k = lane % 32 owning slot k of the
+// current symbol's row (put_symbol_inline, ffv1enc.c:185-231), with its
+// group's [contexts][32] states in LDS.  A wave is issue-bound, so two
+// chains per instruction stream walk at nearly twice the rate of one; LDS
+// (one table per chain) caps chains per CU either way.
 //
-// Critical path per symbol: one LDS lookup, T3[code * 256 + state] (code 0/1
-// a decision bit, 2 no decision), plus a select: the next symbol's row
-// states are read from LDS a step ahead and, when it is the same row, taken
-// from the register just computed instead.
+// Every decision's s' (below) is recorded at the decision's index in the
+// stream.  Symbols come in chunks of 64 (ffv1_symbols' records, each with
+// the row, 2-bit slot codes and the decision offsets); a chunk's recorded
+// bytes are staged in LDS and go out, at the start of the next chunk, as
+// whole 16-byte blocks: the bytes before the chunk's first decision are
+// carried over from the previous chunk's stage, and the blocks past a
+// chain's last decision land in the chain's pad (kChainPad).
+//
+// Critical path per symbol: one LDS lookup, N[code][state] (code 0/1 a
+// decision bit, 2 no decision), plus a select: the next symbol's row states
+// are read from LDS a step ahead and, when it is the same row, taken from
+// the register just computed instead.
 constexpr int kWalkThreads = kWave;
 constexpr int kT3Bytes = 3 * 256;
-constexpr int kStageWords = 80;     // bits: >= (64 symbols * 33 bits + 31) / 32 + 1
-constexpr int kPreStage = 64 * 21;  // pre-states of one chunk of symbols with e <= 9
+constexpr int kChunk = 64;                   // symbols per chunk (the records' D is chunk-relative)
+constexpr int kPreStage = kChunk * 21;       // recorded bytes of a chunk of symbols with e <= 9
+constexpr int kRecSlots = kChunk + 3;        // + three read-ahead slots (null records)
+constexpr int kPreData = kPreStage + 16;     // a chain's stage: <= 15 bytes carried in, then the chunk
+constexpr int kPreHalf = kPreData + 32;      // + one dummy byte per slot
+constexpr int kCopyBlocks = 3;               // 16-byte blocks per lane that write a stage out
+static_assert(kCopyBlocks * 32 * 16 >= kPreData, "the copy-out covers the stage");
+static_assert(kCopyBlocks * 32 * 16 <= kChainPad, "the copy-out stays inside the chain and its pad");
+
+// LDS image of the walk: a fixed part (static, so every offset below is an
+// instruction immediate) and the two state tables (dynamic).
+constexpr int kLdsN = 0;                                      // u8 [3][256]: a slot's next state
+constexpr int kLdsS = kLdsN + kT3Bytes;                       // u8 [3][256]: the s' it records
+constexpr int kLdsRecs = kLdsS + kT3Bytes;                    // [2][kRecSlots] records
+constexpr int kLdsPre = kLdsRecs + 2 * kRecSlots * 16;        // [2][kPreHalf] recorded s'
+constexpr int kLdsFixed = kLdsPre + 2 * kPreHalf;
 
 int64_t walk_lds_bytes_dev(int64_t state_bytes);
-
-struct SymDec {  // one symbol, wave-uniform
-  int row, v, e;
-  unsigned mag;
-};
-
-__device__ __forceinline__ SymDec decode_sym(uint32_t sv) {
-  SymDec d;
-  d.row = (int)(sv >> 16);
-  d.v = (int16_t)(sv & 0xFFFF);
-  d.mag = d.v < 0 ? 0u - (unsigned)d.v : (unsigned)d.v;
-  d.e = d.v ? 31 - __builtin_clz(d.mag) : -1;
-  return d;
-}
 
 // Any exponent, one symbol: lane k < 32 of a half applies all decisions of
 // slot k in order (slot 10 takes e-8 exponent decisions beyond e = 9, slot
@@ -872,57 +897,57 @@ __device__ __forceinline__ void walk_long(uint8_t* tbl, const uint8_t* ftab, int
   tbl[row_off] = (uint8_t)st;
 }
 
-// Two chains per wave: half h = lane / 32 walks chain h of the block's pair
-// (two slices of one segment and plane group), lane k = lane % 32 owning
-// slot k of its chain's current row.  A wave is issue-bound, so two chains
-// per instruction stream walk at nearly twice the rate of one; LDS (one
-// table per chain) caps chains per CU either way.
-constexpr int kChunk = 64;                   // symbols per chunk (the records' D is chunk-relative)
-constexpr int kRecSlots = kChunk + 2;        // + two read-ahead slots (null records)
-constexpr int kPreHalf = (kPreStage + 4 + 32 + 15) & ~15;  // pre stage of a chain: +3 align slack, 32 dummies
-
-// LDS image of the walk: a fixed part (static, so every offset below is an
-// instruction immediate) and the two state tables (dynamic).
-constexpr int kLdsT3 = 0;                                     // u16 [3][256]: next | s' << 8
-constexpr int kLdsRecs = kLdsT3 + 2 * kT3Bytes;               // [2][kRecSlots] records
-constexpr int kLdsPre = kLdsRecs + 2 * kRecSlots * 16;        // [2 buffers][2][kPreHalf] recorded s'
-constexpr int kLdsFixed = kLdsPre + 4 * kPreHalf;
-
 // per-lane constants of the step
 struct WalkLane {
-  int csh, hsh, kc;   // code shift; D or D+2e; slot offset from it
+  int csh, hsh;       // code shift; D or D+2e
   uint32_t mlo;       // all ones for slots 0..15 (codes in the record's y word)
   int kk;             // k + this half's table base
-  int dummy;          // pre stage byte of untouched slots
+  int dummy;          // stage byte of untouched slots
 };
 
-// Symbol T: the lookup of T is issued first; T-1's table write, the read of
-// T+1's row and T's recorded state then fill the lookup's latency.  The row
-// read one symbol ahead misses T's write, so a symbol continuing its
-// predecessor's row takes the state from the register instead.
-// T3[code][state] = the state after the slot's decision (code 0/1 its bit,
-// 2 none) | s' << 8, s' = the recorded value: the state for a 1 decision,
-// 256 - state for a 0 one, so that put_rac's new range is
-// (range * s' + (bit ? 0 : 255)) >> 8.
-__device__ __forceinline__ void walk_step(uint8_t* fixed, uint8_t* tbl, const uint4& r0, const uint4& r1,
-                                          uint32_t& e1, uint32_t& l0, int& addr_prev, int kc,
-                                          const WalkLane& W) {
+// A symbol as lane k of its chain sees it.
+struct StepIn {
+  uint32_t code;  // the slot's decision: 0/1 its bit, 2 none
+  int pos;        // stage byte of the decision (the lane's dummy byte for none)
+  int addr;       // the slot's state byte in the tables
+  bool same;      // same row as the previous symbol
+};
+
+__device__ __forceinline__ StepIn derive(const uint4& r, const WalkLane& W, int kc) {
+  StepIn d;
+  d.code = __builtin_amdgcn_ubfe((r.y & W.mlo) | (r.z & ~W.mlo), W.csh, 2);  // bitwise: a select
+                                                                              // of members would go to scratch
+  const int pos = (int)__builtin_amdgcn_ubfe(r.w, W.hsh, 12) + kc;
+  d.pos = d.code == 2u ? W.dummy : pos;
+  d.addr = (int)(r.x & 0xFFFFu) + W.kk;
+  d.same = (int)r.w < 0;  // kRecSame
+  return d;
+}
+
+// Symbol T: the lookups of T are issued first; T-1's table and stage writes
+// and the read of T+1's row then fill their latency.  The row read one
+// symbol ahead misses T's write, so a symbol continuing its predecessor's
+// row takes the state from the register instead.
+// N[code][state] = the state after the slot's decision (code 0/1 its bit, 2
+// none); S[code][state] = s', the state for a 1 decision and 256 - state for
+// a 0 one, so that put_rac's new range is (range * s' + (bit ? 0 : 255)) >> 8.
+__device__ __forceinline__ void walk_step(uint8_t* fixed, uint8_t* tbl, const StepIn& d, int addr_next,
+                                          uint32_t& e1, uint32_t& s1, uint32_t& l0, int& addr_prev,
+                                          int& pos_prev) {
   uint32_t a1 = e1, a0 = l0;
   pin(a1);
   pin(a0);
-  const bool same = (int)r0.w < 0;  // kRecSame
-  const uint32_t st = same ? a1 : a0;  // low byte: the slot's state
-  const uint32_t code = (((r0.y & W.mlo) | (r0.z & ~W.mlo)) >> W.csh) & 3u;  // bitwise: a select
-                                                                              // of members would go to scratch
-  const uint32_t idx = __builtin_amdgcn_perm(code, st, 0x0c0c0400u);  // code << 8 | (st & 0xFF)
-  uint32_t ev = reinterpret_cast<const uint16_t*>(fixed + kLdsT3)[idx];
-  tbl[addr_prev] = (uint8_t)a1;                          // T-1 (lanes 32..63 repeat 0..31)
-  l0 = tbl[(int)(r1.x & 0xFFFFu) + W.kk];                // T+1's row, after every earlier write but T's
-  const int pos = (int)((r0.w >> W.hsh) & 0xFFFu) + kc;
-  addr_prev = (int)(r0.x & 0xFFFFu) + W.kk;
-  pin(ev);
-  fixed[kLdsPre + (code == 2u ? W.dummy : pos)] = (uint8_t)(ev >> 8);
-  e1 = ev;
+  const uint32_t st = d.same ? a1 : a0;
+  const uint32_t idx = (d.code << 8) | st;
+  const uint32_t n = fixed[kLdsN + idx];
+  const uint32_t s = fixed[kLdsS + idx];
+  tbl[addr_prev] = (uint8_t)a1;              // T-1's state
+  fixed[kLdsPre + pos_prev] = (uint8_t)s1;   // T-1's recorded s'
+  l0 = tbl[addr_next];                       // T+1's row, after every earlier write but T's
+  addr_prev = d.addr;
+  pos_prev = d.pos;
+  e1 = n;
+  s1 = s;
 }
 
 int64_t walk_lds_bytes_dev(int64_t state_bytes) { return kLdsFixed + 2 * (state_bytes / 2 + 32); }
@@ -950,13 +975,16 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   const int h = lane >> 5, k = lane & 31;
   for (int i = lane; i < kT3Bytes; i += kWalkThreads) {
     const int code = i >> 8, st = i & 255;
-    const int next = code < 2 ? a.ftab[i] : st;
-    const int sp = code == 1 ? st : 256 - st;  // (st = 0 never occurs)
-    reinterpret_cast<uint16_t*>(fixed + kLdsT3)[i] = (uint16_t)(next | ((sp & 0xFF) << 8));
+    fixed[kLdsN + i] = (uint8_t)(code < 2 ? a.ftab[i] : st);
+    fixed[kLdsS + i] = (uint8_t)(code == 1 ? st : 256 - st);  // (state 0 never occurs)
   }
-  const int grp = blockIdx.x & 1;
+  // every luma chain first: they are twice as long as the chroma ones, which
+  // then fill the CUs as the luma waves finish
+  const int nblk = gridDim.x / 2;
+  const int grp = (int)blockIdx.x >= nblk;
   const int npairs = (a.nslices + 1) / 2;
-  const int seg_i = (blockIdx.x >> 1) / npairs, pair = (blockIdx.x >> 1) % npairs;
+  const int bi = (int)blockIdx.x - grp * nblk;
+  const int seg_i = bi / npairs, pair = bi % npairs;
   const Segment seg = a.segs[seg_i];
   const int sl = 2 * pair + h;              // this half's slice
   const bool live = sl < a.nslices;
@@ -965,6 +993,8 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   if (grp && g.plane_sym_off[1] >= g.nsym) return;  // no chroma (uniform: geometry of a frame)
   uint8_t* const mytbl = tbl + h * tsz;
   uint4* const myrecs = reinterpret_cast<uint4*>(fixed + kLdsRecs) + h * kRecSlots;
+  uint8_t* const stage = fixed + kLdsPre + h * kPreHalf;
+  uint4* const stage4 = reinterpret_cast<uint4*>(stage);
   const int64_t n16 = half / 16;
   const int64_t goff = grp * half;
   {
@@ -987,40 +1017,25 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   W.hsh = isU ? 0 : 16;                    // else from D + 2e: sign +2, mantissa 22+i: +1-i
   const int kslot = isU ? k : (k <= 21 ? 2 : 23 - k);
   W.kk = h * tsz + k;
+  W.dummy = h * kPreHalf + kPreData + k;
   const uint4 nullrec = make_uint4((uint32_t)half, 0xAAAAAAAAu, 0xAAAAAAAAu, 0u);  // dummy row, no decisions
 
-  // Stores of chunk c (recorded states, whole bits words) are issued at the
-  // start of chunk c+1, BEFORE its loads: vmcnt counts in issue order, so
-  // waiting for chunk c+2's data then never waits for stores just issued.
-  int par = 0;                    // pre stage buffer of the current chunk
-  uint8_t* pdst = a.ds.pre;       // pending copy: HBM (4-aligned), bytes incl. align, stage offset
-  int pnb = 0, palign = 0, pstage = 0;
-  uint32_t po0 = 0, po1 = 0, po2 = 0;  // pending bits words m = k, k+32, k+64
-  int64_t pwb = 0;
-  int pwend = 0;
-  bool pfirst = false;
-  auto flush_pending = [&]() {
-    {
-      const uint8_t* const src = fixed + pstage;
-      const int nw = pnb >> 2;
-      for (int i = k; i < nw; i += 32)
-        if (i > 0 || palign == 0) reinterpret_cast<uint32_t*>(pdst)[i] = reinterpret_cast<const uint32_t*>(src)[i];
-      if (k < 4) {
-        const int hb = palign + k;  // head bytes of the first dword
-        if (palign && hb < 4 && hb < pnb) pdst[hb] = src[hb];
-        const int tb = (nw << 2) + k;  // tail bytes past the last whole dword
-        if (tb < pnb && (nw > 0 || palign == 0 || tb >= 4)) pdst[tb] = src[tb];
-      }
-    }
-    uint32_t* const bits = a.ds.bits + pwb;
-    if (k < pwend) {
-      if (k == 0 && pfirst) atomicOr(&bits[0], po0);
-      else bits[k] = po0;
-    }
-    if (k + 32 < pwend) bits[k + 32] = po1;
-    if (k + 64 < pwend) bits[k + 64] = po2;
-    pnb = 0;
-    pwend = 0;
+  // The stage of chunk c goes out at the start of chunk c+1, before its
+  // loads are issued: vmcnt counts in issue order, so waiting for chunk
+  // c+2's data then never waits for stores just issued.  LDS ops of a wave
+  // run in order, so the copy-out reads the stage before chunk c+1's steps
+  // write it.  Before the first chunk, and after a chunk recorded straight
+  // to HBM, the copy goes to the scratch area.
+  uint8_t* pdst = a.scratch;  // 16-aligned
+  int plast = 0;              // stage block holding the chunk's last bytes
+  auto copy_out = [&]() {
+    static_for<0, kCopyBlocks>([&](auto ic) {
+      constexpr int I = decltype(ic)::value;
+      const uint4 v = stage4[I * 32 + k];
+      reinterpret_cast<uint4*>(pdst)[I * 32 + k] = v;
+    });
+    const uint4 t = stage4[plast];  // the bytes before the next chunk's first decision
+    stage4[0] = t;
   };
 
   uint64_t t_loop = 0, n_steps = 0;
@@ -1029,43 +1044,31 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
     const int f = seg.first_frame + j;
     const int64_t sid = (int64_t)f * a.nslices + (live ? sl : 0);
     const int* dc = a.ds.dcount + sid * 3;
-    const int64_t gbase = live ? a.ds.dbase[sid] + (grp ? dc[0] : 0) : 0;  // first decision of the chain
-    bool first_word = true;   // the chain's first bits word may be shared with another chain
-    uint32_t carry = 0;       // bits of the partial word at decision gbase + run
-    int64_t run = 0;          // decisions so far in this frame's chain
+    const int64_t gbase = live ? a.ds.dbase[sid] + (grp ? chroma_start(dc[0]) : 0) : 0;  // chain start
+    int64_t run = 0;  // decisions so far in this frame's chain
     for (int pl = p0; pl < p1; pl++) {
       const int64_t nsym = live ? (pl < 2 ? g.plane_sym_off[pl + 1] : g.nsym) - g.plane_sym_off[pl] : 0;
       const uint4* rp = a.rec + (int64_t)f * a.frame_samples + g.sym_off + g.plane_sym_off[pl];
       const uint32_t* cp = a.cbits + ((int64_t)f * a.frame_chunks + g.chunk_off[pl]) * kChunkWords;
       const int nch = (int)((nsym + kChunk - 1) / kChunk);
       const int nchunks = max(__builtin_amdgcn_readlane(nch, 0), __builtin_amdgcn_readlane(nch, 32));
-      // a chunk's inputs: 2 records and the funnel's bits words per lane
+      // a chunk's inputs: 2 records per lane and the chunk header
       struct In {
         uint4 m0, m1;
-        uint32_t hd, w0, w0p, w1, w1p, w2, w2p;
+        uint32_t hd;
       };
       auto load = [&](int c) -> In {
         In x;
         const int64_t b = (int64_t)c * kChunk;
         x.m0 = rec_or_null(rp, b + k, nsym, nullrec);
         x.m1 = rec_or_null(rp, b + 32 + k, nsym, nullrec);
-        const bool ok = c < nch;  // else read chunk 0 of a plane of the pair (valid memory), use zeros
-        const uint32_t* q = cp + (int64_t)(ok ? c : 0) * kChunkWords;  // word 1 + m: bits word m
-        auto ld = [&](int i, bool use) -> uint32_t {
-          uint32_t zero = 0u;
-          pin(zero);
-          return use ? q[min(i, kChunkWords - 1)] : zero;
-        };
-        x.hd = ld(0, ok);
-        x.w0 = ld(1 + k, ok);
-        x.w0p = ld(k, ok && k > 0);
-        x.w1 = ld(33 + k, ok);
-        x.w1p = ld(32 + k, ok);
-        x.w2 = ld(65 + k, ok && 65 + k < kChunkWords);
-        x.w2p = ld(64 + k, ok && 64 + k < kChunkWords);
+        const bool ok = c < nch;  // else read chunk 0 of a plane of the pair (valid memory), use 0
+        uint32_t zero = 0u;
+        pin(zero);
+        const uint32_t hv = cp[(int64_t)(ok ? c : 0) * kChunkWords];
+        x.hd = ok ? hv : zero;
         return x;
       };
-      flush_pending();
       In nx = load(0);
       for (int c = 0; c < nchunks; c++) {
         In cx = nx;
@@ -1073,44 +1076,17 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
         // after the stores and loads below, vmcnt would wait for those too
         pin(cx.m0.x); pin(cx.m0.y); pin(cx.m0.z); pin(cx.m0.w);
         pin(cx.m1.x); pin(cx.m1.y); pin(cx.m1.z); pin(cx.m1.w);
-        pin(cx.hd); pin(cx.w0); pin(cx.w0p); pin(cx.w1); pin(cx.w1p); pin(cx.w2); pin(cx.w2p);
-        flush_pending();                       // chunk c-1's stores, then ...
+        pin(cx.hd);
+        copy_out();                             // chunk c-1's stage, then ...
         if (c + 1 < nchunks) nx = load(c + 1);  // ... chunk c+1's loads
         const int cnt = (int)min((int64_t)kChunk, max((int64_t)0, nsym - (int64_t)c * kChunk));
         const int total = (int)(cx.hd & ~kChunkLong);
         const bool lng = __ballot((cx.hd & kChunkLong) != 0) != 0;
         const int64_t pos0 = gbase + run;  // decision index of the chunk's first decision
-
-        // decision bits: funnel-shift the chunk's words to their HBM place
-        {
-          const int sh = (int)(pos0 & 31);
-          const int rs = (32 - sh) & 31;
-          uint32_t o0 = sh ? __builtin_amdgcn_alignbit(cx.w0, cx.w0p, rs) : cx.w0;
-          const uint32_t o1 = sh ? __builtin_amdgcn_alignbit(cx.w1, cx.w1p, rs) : cx.w1;
-          const uint32_t o2 = sh ? __builtin_amdgcn_alignbit(cx.w2, cx.w2p, rs) : cx.w2;
-          if (k == 0) o0 |= carry;
-          const int wend = (sh + total) >> 5;  // complete words
-          // the partial word wend -> carry (word m sits in lane m % 32 of its half, round m / 32)
-          const int wA = __builtin_amdgcn_readlane(wend, 0), wB = __builtin_amdgcn_readlane(wend, 32);
-          const uint32_t rA = (wA >> 5) == 0 ? o0 : (wA >> 5) == 1 ? o1 : o2;
-          const uint32_t rB = (wB >> 5) == 0 ? o0 : (wB >> 5) == 1 ? o1 : o2;
-          const uint32_t cA = __builtin_amdgcn_readlane(rA, wA & 31);
-          const uint32_t cB = __builtin_amdgcn_readlane(rB, 32 + (wB & 31));
-          const uint32_t ncarry = h ? cB : cA;
-          po0 = o0;
-          po1 = o1;
-          po2 = o2;
-          pwb = pos0 >> 5;
-          pwend = wend;
-          pfirst = first_word;
-          if (wend > 0) first_word = false;
-          carry = ncarry;
-        }
-
         myrecs[k] = pick(k < cnt, cx.m0, nullrec);
         myrecs[k + 32] = pick(k + 32 < cnt, cx.m1, nullrec);
-        if (k < 2) myrecs[kChunk + k] = nullrec;
-        __syncthreads();
+        if (k < kRecSlots - kChunk) myrecs[kChunk + k] = nullrec;
+        __builtin_amdgcn_wave_barrier();
 
         if (lng) {  // e >= 10 somewhere: one symbol at a time, recorded straight to HBM
           const int cmax = max(__builtin_amdgcn_readlane(cnt, 0), __builtin_amdgcn_readlane(cnt, 32));
@@ -1120,49 +1096,57 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
               walk_long(mytbl, a.ftab, (int)(int16_t)(r.x >> 16), (int)(r.x & 0xFFFFu) + k, k,
                         a.ds.pre + pos0 + (int)(r.w & 0xFFFu));
           }
-          __syncthreads();
+          // the next chunk's carried bytes: read back what was just written
+          __builtin_amdgcn_s_waitcnt(0);
+          const uint32_t* src = reinterpret_cast<const uint32_t*>(a.ds.pre + ((pos0 + total) & ~(int64_t)15));
+          uint4 tb;
+          tb.x = __hip_atomic_load(src + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          tb.y = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          tb.z = __hip_atomic_load(src + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          tb.w = __hip_atomic_load(src + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          stage4[0] = tb;
+          pdst = a.scratch;
+          plast = 0;
+          __builtin_amdgcn_wave_barrier();
           run += total;
           continue;
         }
 
-        const int align = (int)(pos0 & 3);  // pre stage byte i <-> HBM byte pos0 - align + i
-        const int pb = kLdsPre + (par * 2 + h) * kPreHalf;
-        const int kc = kslot + pb - kLdsPre + align;
-        W.dummy = pb - kLdsPre + kPreStage + 4 + k;
-        uint4 r0 = myrecs[0], r1 = myrecs[1];
-        uint32_t l0 = tbl[(int)(r0.x & 0xFFFFu) + W.kk];
-        uint32_t e1 = 0;
-        int addr_prev = (int)((fixed + kLdsPre + W.dummy) - tbl);  // no T-1 yet: a dummy byte
+        const int align = (int)(pos0 & 15);  // stage byte i <-> HBM byte pos0 - align + i
+        const int kc = kslot + h * kPreHalf + align;
+        StepIn d0 = derive(myrecs[0], W, kc), d1 = derive(myrecs[1], W, kc);
+        uint4 rn = myrecs[2];
+        uint32_t l0 = tbl[d0.addr];
+        uint32_t e1 = 0u, s1 = 0u;
+        int addr_prev = (int)((stage + kPreData + k) - tbl);  // no T-1 yet: the dummy byte
+        int pos_prev = W.dummy;
         const uint64_t t0 = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
         static_for<0, kChunk>([&](auto tc) {
           constexpr int T = decltype(tc)::value;
-          const uint4 r2 = myrecs[T + 2];  // two ahead
-          walk_step(fixed, tbl, r0, r1, e1, l0, addr_prev, kc, W);
-          r0 = r1;
-          r1 = r2;
+          walk_step(fixed, tbl, d0, d1.addr, e1, s1, l0, addr_prev, pos_prev);
+          const uint4 r3 = myrecs[T + 3];  // three ahead
+          __builtin_amdgcn_sched_barrier(0);  // keeps the read here, not sunk to its use a step later
+          d0 = d1;
+          d1 = derive(rn, W, kc);
+          rn = r3;
         });
         tbl[addr_prev] = (uint8_t)e1;  // the chunk's last symbol
+        fixed[kLdsPre + pos_prev] = (uint8_t)s1;
         if (a.dbg) {
           __builtin_amdgcn_s_waitcnt(0);
           t_loop += __builtin_amdgcn_s_memtime() - t0;
           n_steps += kChunk;
         }
-        // chunk c's recorded states go out with chunk c+1's stores
-        pdst = a.ds.pre + pos0 - align;
-        pnb = align + total;
-        palign = align;
-        pstage = pb;
-        par ^= 1;
-        __syncthreads();
+        pdst = live ? a.ds.pre + (pos0 & ~(int64_t)15) : a.scratch;
+        plast = (align + total) >> 4;
+        __builtin_amdgcn_wave_barrier();
         run += total;
       }
     }
-    // the frame's last, partial bits word
-    if (k == 0 && ((gbase + run) & 31)) atomicOr(&a.ds.bits[(gbase + run) >> 5], carry);
   }
-  flush_pending();
+  copy_out();
+  __builtin_amdgcn_wave_barrier();
   if (seg.save_states && live) {
-    __syncthreads();
     uint4* dst = reinterpret_cast<uint4*>(a.persist + (int64_t)sl * a.state_bytes + goff);
     const uint4* t4 = reinterpret_cast<const uint4*>(mytbl);
     for (int64_t i = k; i < n16; i += 32) dst[i] = t4[i];
@@ -1175,7 +1159,8 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
 }
 
 // Decision-stream layout: stream (frame, slice) i starts at the sum of the
-// earlier streams' decisions, each rounded up to kStreamAlign.
+// earlier streams' lengths: the luma chain, its pad, the chroma chain from
+// chroma_start, its pad (ffv1_internal.h, DecisionStream).
 constexpr int kLayoutThreads = 1024;
 __global__ __launch_bounds__(kLayoutThreads) void ffv1_layout(const int* dcount, int nstreams, int64_t* dbase,
                                                               int64_t* total) {
@@ -1184,8 +1169,8 @@ __global__ __launch_bounds__(kLayoutThreads) void ffv1_layout(const int* dcount,
   const int per = (nstreams + kLayoutThreads - 1) / kLayoutThreads;
   const int lo = min(t * per, nstreams), hi = min(lo + per, nstreams);
   auto len = [&](int i) -> int64_t {
-    const int64_t n = (int64_t)dcount[3 * i] + dcount[3 * i + 1] + dcount[3 * i + 2];
-    return (n + kStreamAlign - 1) / kStreamAlign * kStreamAlign;
+    const int64_t n = (int64_t)dcount[3 * i + 1] + dcount[3 * i + 2];
+    return chroma_start(dcount[3 * i]) + ((n + kStreamAlign - 1) / kStreamAlign * kStreamAlign) + kChainPad;
   };
   int64_t sum = 0;
   for (int i = lo; i < hi; i++) sum += len(i);
@@ -1203,6 +1188,89 @@ __global__ __launch_bounds__(kLayoutThreads) void ffv1_layout(const int* dcount,
     acc += len(i);
   }
   if (t == kLayoutThreads - 1) *total = part[t];
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 2c: the decision bits.  ffv1_symbols packed each chunk's bits in
+// coding order (word 1 + m = bits 32m .. 32m+31 of the chunk); one block
+// per (frame, slice) stream scans the chunks' decision counts in coding
+// order (luma, then the chroma chain from chroma_start) and funnel-shifts
+// every chunk's words to their place.  A wave takes a run of consecutive
+// chunks and carries the word a chunk shares with the next one in a
+// register; only the words shared with another wave's run are OR-ed in
+// (the array is zeroed first).
+constexpr int kBitsThreads = 256;
+constexpr int kBitsWaves = kBitsThreads / kWave;
+__global__ __launch_bounds__(kBitsThreads) void ffv1_bits(BitsArgs a) {
+  __shared__ int off[kBitsThreads];
+  __shared__ int tot[kBitsThreads];
+  __shared__ int wsum[kBitsWaves];
+  const int s = blockIdx.x, f = blockIdx.y;
+  const int t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
+  const SliceGeom& g = a.geom[s];
+  const int64_t sid = (int64_t)f * a.nslices + s;
+  const int* dc = a.ds.dcount + sid * 3;
+  const int64_t base = a.ds.dbase[sid];
+  const uint32_t* const fc = a.cbits + (int64_t)f * a.frame_chunks * kChunkWords;
+  int run = 0;  // stream-relative decision index of the next chunk
+  for (int p = 0; p < 3; p++) {
+    if (p == 1) run = (int)chroma_start(dc[0]);
+    const int64_t nsym = (p < 2 ? g.plane_sym_off[p + 1] : g.nsym) - g.plane_sym_off[p];
+    const int nch = (int)((nsym + kChunk - 1) / kChunk);
+    const uint32_t* const pc = fc + g.chunk_off[p] * kChunkWords;
+    for (int c0 = 0; c0 < nch; c0 += kBitsThreads) {
+      const int c = c0 + t;
+      const int n = c < nch ? (int)(pc[(int64_t)c * kChunkWords] & ~kChunkLong) : 0;
+      const int x = wave_incl_scan(n, lane);
+      if (lane == kWave - 1) wsum[wv] = x;
+      __syncthreads();
+      int before = 0, all = 0;
+      for (int w = 0; w < kBitsWaves; w++) {
+        before += w < wv ? wsum[w] : 0;
+        all += wsum[w];
+      }
+      off[t] = run + before + x - n;
+      tot[t] = n;
+      __syncthreads();
+      // this wave's run of chunks
+      const int cn = min(kBitsThreads, nch - c0);
+      const int per = (cn + kBitsWaves - 1) / kBitsWaves;
+      const int i0 = wv * per, i1 = min(cn, i0 + per);
+      uint32_t carry = 0u;  // the previous chunk's last, partial word (lane 0)
+      for (int i = i0; i < i1; i++) {
+        const uint32_t* const q = pc + (int64_t)(c0 + i) * kChunkWords;
+        const int64_t pos = base + __builtin_amdgcn_readfirstlane(off[i]);
+        const int total = __builtin_amdgcn_readfirstlane(tot[i]);
+        const int sh = (int)(pos & 31);
+        const int nw = (sh + total + 31) >> 5;
+        const bool partial = ((sh + total) & 31) != 0;
+        uint32_t* const dst = a.ds.bits + (pos >> 5);
+        uint32_t lastw = 0u;
+        for (int m0 = 0; m0 < nw; m0 += kWave) {
+          const int m = m0 + lane;
+          const uint32_t hi = m < nw ? q[1 + m] : 0u;
+          const uint32_t lo = m && m < nw ? q[m] : 0u;
+          uint32_t v = sh ? __builtin_amdgcn_alignbit(hi, lo, 32 - sh) : hi;
+          if (m == 0 && sh) v |= carry;  // zero for the run's first chunk
+          const bool shared_head = m == 0 && sh && i == i0;
+          const bool tail = m == nw - 1 && partial;
+          if (m < nw) {
+            if (tail && i + 1 < i1) {
+              // held for the next chunk of the run
+            } else if (shared_head || tail) {
+              atomicOr(&dst[m], v);
+            } else {
+              dst[m] = v;
+            }
+          }
+          if ((nw - 1) >= m0 && (nw - 1) < m0 + kWave) lastw = __builtin_amdgcn_readlane(v, (nw - 1) - m0);
+        }
+        carry = partial ? lastw : 0u;
+      }
+      run += all;
+      __syncthreads();
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1308,8 +1376,9 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
   lane_init(L, ring + lane * kRingStride);
   uint8_t* const out = a.slice_out + ((int64_t)(live ? f : 0) * a.nslices + slice) * a.slice_cap;
   Sink S = make_sink(out, live ? a.slice_cap : 0);  // idle lanes write nothing
-  run_header_ops(a, L, S, opsets + lane * kOpsetBytes, key, slice, live, tabs, tabs + 512);
-  const int64_t ac_bytes = terminate(L, S, a.version > 2);
+  run_header_ops(a, L, S, opsets + lane * kOpsetBytes, key, slice, live, tabs, tabs + 512, kOpsetBytes,
+                 kHeaderFlushAt);
+  const int64_t ac_bytes = terminate(L, S, a.version > 2, kRing);
   if (!live) return;
 
   BitSink b{0ull, 0, ac_bytes, out, a.slice_cap};
@@ -1473,7 +1542,7 @@ int launch_code(const CodeArgs& a, void* stream) {
 int launch_dcode(const CodeArgs& a, void* stream) {
   const int64_t streams = (int64_t)a.nframes * a.nslices;
   dim3 grid((unsigned)((streams + kCodeThreads - 1) / kCodeThreads)), block(kCodeThreads);
-  hipLaunchKernelGGL(ffv1_dcode, grid, block, code_lds_bytes(kCodeThreads), reinterpret_cast<hipStream_t>(stream), a);
+  hipLaunchKernelGGL(ffv1_dcode, grid, block, dcode_lds_bytes(a.nopsets), reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1484,6 +1553,12 @@ int launch_walk(const WalkArgs& a, int nsegs, void* stream) {
   const size_t dyn = (size_t)(2 * (a.state_bytes / 2 + 32));  // the tables; the fixed part is static
   dim3 grid((unsigned)(nsegs * ((a.nslices + 1) / 2) * 2)), block(kWalkThreads);
   hipLaunchKernelGGL(ffv1_walk, grid, block, dyn, reinterpret_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_bits(const BitsArgs& a, void* stream) {
+  hipLaunchKernelGGL(ffv1_bits, dim3(a.nslices, a.nframes), dim3(kBitsThreads), 0, reinterpret_cast<hipStream_t>(stream),
+                     a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

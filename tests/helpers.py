@@ -102,6 +102,8 @@ PARITY_STREAMS = [
     Stream("cif420_range_intra_v3", 352, 288, "yuv420p", 4, slices=4, gop_size=1),
     Stream("p10_gop4", 480, 270, "yuv420p10", 9, slices=4, gop_size=4, depth=10),
     Stream("p10_d2_gop5", 320, 180, "yuv420p10", 7, slices=6, gop_size=5, source="d2", depth=10),
+    # an odd slice count (3x3): the states walk pairs slices per wave, the last alone
+    Stream("p10_9slices", 360, 270, "yuv420p10", 5, slices=9, gop_size=3, source="d2", depth=10),
     Stream("p12_444", 256, 144, "yuv444p16", 5, slices=4, gop_size=3, bits_per_raw_sample=12,
            depth=16, chroma444=True),
     Stream("p16_444_wrap", 128, 96, "yuv444p16", 3, slices=4, gop_size=2, source="random"),
