@@ -960,11 +960,6 @@ __device__ __forceinline__ uint4 pick(bool c, uint4 a, uint4 b) {
   return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
 }
 
-// record i of a plane with n records, or the null record (reads a valid one)
-__device__ __forceinline__ uint4 rec_or_null(const uint4* rp, int64_t i, int64_t n, uint4 nul) {
-  const int64_t j = i < n ? i : 0;
-  return pick(i < n, rp[j], nul);
-}
 
 __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t fixed[kLdsFixed];
@@ -1057,16 +1052,15 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
         uint4 m0, m1;
         uint32_t hd;
       };
+      // raw loads (indices past the plane read record / chunk 0 of a plane of
+      // the pair: valid memory); what is past the plane is masked where the
+      // data is used, a chunk later: a select here would wait for the loads
       auto load = [&](int c) -> In {
         In x;
         const int64_t b = (int64_t)c * kChunk;
-        x.m0 = rec_or_null(rp, b + k, nsym, nullrec);
-        x.m1 = rec_or_null(rp, b + 32 + k, nsym, nullrec);
-        const bool ok = c < nch;  // else read chunk 0 of a plane of the pair (valid memory), use 0
-        uint32_t zero = 0u;
-        pin(zero);
-        const uint32_t hv = cp[(int64_t)(ok ? c : 0) * kChunkWords];
-        x.hd = ok ? hv : zero;
+        x.m0 = rp[b + k < nsym ? b + k : 0];
+        x.m1 = rp[b + 32 + k < nsym ? b + 32 + k : 0];
+        x.hd = cp[(int64_t)(c < nch ? c : 0) * kChunkWords];
         return x;
       };
       In nx = load(0);
@@ -1080,8 +1074,9 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
         copy_out();                             // chunk c-1's stage, then ...
         if (c + 1 < nchunks) nx = load(c + 1);  // ... chunk c+1's loads
         const int cnt = (int)min((int64_t)kChunk, max((int64_t)0, nsym - (int64_t)c * kChunk));
-        const int total = (int)(cx.hd & ~kChunkLong);
-        const bool lng = __ballot((cx.hd & kChunkLong) != 0) != 0;
+        const uint32_t hd = c < nch ? cx.hd : 0u;
+        const int total = (int)(hd & ~kChunkLong);
+        const bool lng = __ballot((hd & kChunkLong) != 0) != 0;
         const int64_t pos0 = gbase + run;  // decision index of the chunk's first decision
         myrecs[k] = pick(k < cnt, cx.m0, nullrec);
         myrecs[k + 32] = pick(k + 32 < cnt, cx.m1, nullrec);
