@@ -786,7 +786,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     HIP_TRY(hipMemcpyAsync(c->d_slot_frames, ident.data(), sizeof(int) * n, hipMemcpyHostToDevice, st));
     sa.frame_of_slot = c->d_slot_frames;
     sa.nslots = n;
-    sa.dcount = d_dcount;
+    sa.dcount = d_dcount;  // accumulated by the symbols blocks of each plane
+    HIP_TRY(hipMemsetAsync(d_dcount, 0, sizeof(int) * 3 * size_t(n) * c->nslices, st));
     sa.rec = d_rec;
     sa.cbits = c->d_cbits + size_t(fb) * kChunkWords * c->frame_chunks * c->max_batch;
     sa.frame_chunks = c->frame_chunks;
@@ -861,8 +862,33 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     ca.nframes = n;
     ca.nopsets = c->nopsets;
     ca.ds = ds;
+    // FFV1HIP_CODEDBG=1 (measurement hook): per-wave cycle split to stderr
+    static const bool codedbg = std::getenv("FFV1HIP_CODEDBG") && std::atoi(std::getenv("FFV1HIP_CODEDBG"));
+    const int nwaves = int((int64_t(n) * c->nslices + 63) / 64);
+    uint64_t* d_cdbg = nullptr;
+    if (codedbg) {
+      HIP_TRY(hipMalloc(&d_cdbg, sizeof(uint64_t) * 4 * nwaves));
+      HIP_TRY(hipMemsetAsync(d_cdbg, 0, sizeof(uint64_t) * 4 * nwaves, cst));
+      ca.dbg = d_cdbg;
+    }
     if (timed(1, cst, [&] { return launch_dcode(ca, cst); }) < 0)
       return set_err(-5, "code launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (codedbg) {
+      std::vector<uint64_t> h(size_t(4) * nwaves);
+      HIP_TRY(hipMemcpyAsync(h.data(), d_cdbg, h.size() * 8, hipMemcpyDeviceToHost, cst));
+      HIP_TRY(hipStreamSynchronize(cst));
+      HIP_TRY(hipFree(d_cdbg));
+      double all = 0, fl = 0, dec = 0, mx = 0, its = 0;
+      for (int w = 0; w < nwaves; w++) {
+        all += double(h[4 * w]);
+        fl += double(h[4 * w + 1]);
+        dec += double(h[4 * w + 2]);
+        its += double(h[4 * w + 3]);
+        mx = std::max(mx, double(h[4 * w]));
+      }
+      std::fprintf(stderr, "codedbg: waves %d, memtime per wave %.3g (max %.3g), flush share %.3f, memtime/decision %.1f, decisions per wave %.3g, flush iterations per wave %.3g, memtime per iteration %.1f\n",
+                   nwaves, all / nwaves, mx, fl / all, all / dec, dec / nwaves, its / nwaves, fl / its);
+    }
   } else {
     for (int j = 0; j < maxlen; j++) {
       sa.frame_of_slot = c->d_slot_frames + size_t(j) * nsegs;

@@ -131,6 +131,7 @@ struct CodeArgs {
   int nframes;                // decision-stream mode: frames of the batch
   int nopsets;                // decision-stream mode: op sets the header programs use
   DecisionStream ds;
+  uint64_t* dbg;              // optional [wave][4] cycle counters (FFV1HIP_CODEDBG)
 };
 
 // Kernel 2a: the context-state walk.  The adaptive states a slice's range

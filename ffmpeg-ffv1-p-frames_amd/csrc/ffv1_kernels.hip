@@ -52,6 +52,7 @@ __device__ __forceinline__ int fold_bits(int d, int bits) {
 // ---------------------------------------------------------------------------
 // Kernel 1: symbols.
 constexpr int kSymThreads = 256;
+constexpr int kSymSplit = 8;  // blocks per slice plane: the per-block loop is latency-bound
 
 // Range-coder decisions of one residual: put_symbol_inline (ffv1enc.c:185-231)
 // codes a zero flag, e+1 exponent decisions, e mantissa bits and a sign.
@@ -110,14 +111,11 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   __shared__ uint32_t cstage[kSymThreads / kWave][kChunkWords];  // a wave's chunk bits
   for (int i = threadIdx.x; i < 5 * 256; i += kSymThreads) qt[i] = a.qt[i];
   __syncthreads();
-  const int slice = blockIdx.x, slot = blockIdx.y, p = blockIdx.z;
+  // a plane of a slice is split into kSymSplit runs of whole 256-sample steps
+  const int slice = blockIdx.x, slot = blockIdx.y, p = blockIdx.z / kSymSplit, part = blockIdx.z % kSymSplit;
   const int f = a.frame_of_slot[slot];
-  if (f < 0) return;
-  int* const count = a.dcount ? a.dcount + ((int64_t)slot * a.nslices + slice) * 3 + p : nullptr;
-  if (p >= a.nplanes) {
-    if (count && threadIdx.x == 0) *count = 0;
-    return;
-  }
+  if (f < 0 || p >= a.nplanes) return;
+  int* const count = a.dcount ? a.dcount + ((int64_t)slot * a.nslices + slice) * 3 + p : nullptr;  // zeroed
   const SliceGeom& g = a.geom[slice];
   const int pw = g.pw[p], ph = g.ph[p], px = g.px[p], py = g.py[p];
   const uint8_t* base = a.frames + (int64_t)f * a.frame_bytes + a.plane_off[p];
@@ -135,10 +133,12 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
 
   int ndec = 0;
   const int64_t n = (int64_t)pw * ph;
+  const int64_t span = (n + kSymSplit * kSymThreads - 1) / (kSymSplit * kSymThreads) * kSymThreads;
+  const int64_t b0 = part * span, b1 = min(n, b0 + span);
   const int lane = threadIdx.x & (kWave - 1);
   uint4* const rec = a.rec ? a.rec + (int64_t)slot * a.frame_samples + g.sym_off + g.plane_sym_off[p] : nullptr;
   // whole waves per step: a wave's 64 consecutive samples are one walk chunk
-  for (int64_t base = 0; base < n; base += kSymThreads) {
+  for (int64_t base = b0; base < b1; base += kSymThreads) {
     const int64_t idx = base + threadIdx.x;
     const bool valid = idx < n;
     const int y = valid ? (int)(idx / pw) : 0, x = valid ? (int)(idx - (int64_t)y * pw) : 0;
@@ -201,14 +201,14 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
       out[idx] = ((uint32_t)(row0 + ctx) << 16) | (uint16_t)diff;
     }
   }
-  if (count) {
+  if (count && b0 < b1) {
     for (int o = 32; o > 0; o >>= 1) ndec += __shfl_xor(ndec, o);
     if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = ndec;
     __syncthreads();
     if (threadIdx.x == 0) {
       int t = 0;
       for (int w = 0; w < kSymThreads / kWave; w++) t += red[w];
-      *count = t;
+      atomicAdd(count, t);
     }
   }
 }
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
 // ops of a whole decision, and with 64 independent streams per wave some lane
 // renormalises on almost every decision anyway.
 constexpr int kRing = 96;        // renorm digits per lane held in LDS before a flush
-constexpr int kRingStride = kRing + 1;  // [lane][kRing + 1]: lanes at equal heads hit distinct banks
+constexpr int kRingStride = kRing + 5;  // [lane][kRing + 5]: odd, so lanes at equal heads hit distinct banks
 constexpr int kFlushAt = kRing - 69;    // checked every second symbol step (<= 34 digits per symbol)
 constexpr int kHeaderFlushAt = kRing - 30;  // per header op (host-checked |value| < 2^14: <= 29 digits)
 
@@ -251,37 +251,40 @@ struct Lane {
 };
 
 // Byte writer: renorm_encoder's outstanding-byte / 0xFF-run logic
-// (rangecoder.h:52-75) replayed over the recorded values of `low`.
+// (rangecoder.h:52-75) replayed over the recorded values of `low`, without
+// per-lane branches: every digit but the first and those of a 0xFF run
+// emits the outstanding byte (+1 on a carry), a run's fill bytes follow in
+// a rare wave-level loop.  Bytes gather in a dword; a full one is stored.
 struct Sink {
   uint8_t* out;
-  int64_t cap, opos;
-  uint32_t ow;
+  int64_t cap, opos;  // opos: bytes stored, a multiple of 4
+  uint32_t ow;        // bytes not yet stored, the oldest in the low byte
   int on, pending, run;
 
-  __device__ __forceinline__ void emit(int b) {
-    ow |= (uint32_t)(b & 0xFF) << (on << 3);
-    if (++on == 4) {
+  __device__ __forceinline__ void put(uint32_t b, bool en) {
+    ow |= en ? (b & 0xFFu) << (on << 3) : 0u;
+    on += en ? 1 : 0;
+    if (on == 4) {
       if (opos + 4 <= cap) *reinterpret_cast<uint32_t*>(out + opos) = ow;
       opos += 4;
       ow = 0;
       on = 0;
     }
   }
-  __device__ __forceinline__ void digit(int low) {
+  // one recorded `low` (act: this lane has it)
+  __device__ __forceinline__ void digit(int low, bool act) {
     const int qv = low >> 8;
-    if (pending < 0) {
-      pending = qv;
-    } else if (low > 0xFF00 && low < 0x10000) {
-      run++;
-    } else if (qv < 0x100) {
-      emit(pending);
-      for (; run; run--) emit(0xFF);
-      pending = qv;
-    } else {
-      emit(pending + 1);
-      for (; run; run--) emit(0x00);
-      pending = qv & 0xFF;
+    const bool first = pending < 0;
+    const bool isrun = !first && low > 0xFF00 && low < 0x10000;
+    const bool emit = act && !first && !isrun;
+    const int c = qv >> 8;  // carry into the outstanding byte
+    put((uint32_t)(pending + c), emit);
+    if (__ballot(emit && run > 0)) {  // a run of 0xFF digits ends: its bytes, 0xFF or 0x00 after a carry
+      const uint32_t fill = c ? 0x00u : 0xFFu;
+      for (int r = 0; __ballot(emit && r < run); r++) put(fill, emit && r < run);
     }
+    pending = act && (first || emit) ? (qv & 0xFF) : pending;
+    run = act && isrun ? run + 1 : (emit ? 0 : run);
   }
   // bytes so far (ff_rac_terminate's count once the terminate digits are in)
   __device__ __forceinline__ int64_t finish() {
@@ -314,8 +317,17 @@ __device__ __forceinline__ void renorm(Lane& L) {
   L.range = need ? (L.range << 8) : L.range;
 }
 
+// Every lane replays its ring, four entries read at a time (ring rows are 3
+// entries longer than the ring).
 __device__ __forceinline__ void flush(Lane& L, Sink& S) {
-  for (const uint32_t* p = L.ring; p < L.rp; p++) S.digit((int)*p);
+  const int n = (int)(L.rp - L.ring);
+  for (int t = 0; __ballot(t < n); t += 4) {
+    const uint32_t d0 = L.ring[t], d1 = L.ring[t + 1], d2 = L.ring[t + 2], d3 = L.ring[t + 3];
+    S.digit((int)d0, t < n);
+    S.digit((int)d1, t + 1 < n);
+    S.digit((int)d2, t + 2 < n);
+    S.digit((int)d3, t + 3 < n);
+  }
   L.rp = L.ring;
 }
 
@@ -695,12 +707,22 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
 // another's exponent.  The ring is small (a flush check every 16 decisions)
 // so that a coder wave fits in the LDS the states walk leaves on a CU.
 constexpr int kDRing = 40;                   // renorm digits per lane before a flush
-constexpr int kDRingStride = kDRing + 1;
+constexpr int kDRingStride = kDRing + 3;  // odd: lanes at equal heads hit distinct banks
 constexpr int kDFlushAt = kDRing - 17;       // checked every 16 decisions
+
+// flush_if, timed into *tf when tf is set (FFV1HIP_CODEDBG)
+__device__ __forceinline__ void flush_if_t(Lane& L, Sink& S, int above, uint64_t* tf) {
+  if (__ballot((int)(L.rp - L.ring) > above)) {
+    const uint64_t t0 = tf ? __builtin_amdgcn_s_memtime() : 0;
+    if (tf) tf[1] += wave_max((int)(L.rp - L.ring));
+    flush(L, S);
+    if (tf) tf[0] += __builtin_amdgcn_s_memtime() - t0;
+  }
+}
 
 template <bool TAIL>
 __device__ __forceinline__ void decide32(Lane& L, Sink& S, const uint4& wa, const uint4& wb, uint32_t bw,
-                                         int rem) {
+                                         int rem, uint64_t* tf) {
   static_for<0, 32>([&](auto jc) {
     constexpr int J = decltype(jc)::value;
     constexpr int SH = (J & 3) * 8;
@@ -728,7 +750,7 @@ __device__ __forceinline__ void decide32(Lane& L, Sink& S, const uint4& wa, cons
     L.low = nl;
     L.range = nr;
     renorm(L);
-    if constexpr (J == 15) flush_if(L, S, kDFlushAt);
+    if constexpr (J == 15) flush_if_t(L, S, kDFlushAt, tf);
   });
 }
 
@@ -763,6 +785,9 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_dcode(CodeArgs a) {
   const int64_t st = (int64_t)f * a.nslices + slice;
   const int* dc = a.ds.dcount + st * 3;
   const int64_t base = live ? a.ds.dbase[st] : 0;  // multiple of kStreamAlign
+  uint64_t tfl[2] = {0, 0}, ndec = 0;
+  uint64_t* const tf = a.dbg ? tfl : nullptr;
+  const uint64_t t_all = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
   // the luma chain's decisions, then the chroma chain's at their own start
   for (int part = 0; part < 2; part++) {
     const int n = live ? (part ? dc[1] + dc[2] : dc[0]) : 0;
@@ -797,11 +822,18 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_dcode(CodeArgs a) {
         mw = B[(i >> 5) + 2];
       }
       if (i + 32 <= n)
-        decide32<false>(L, S, wa, wb, bw, 32);
+        decide32<false>(L, S, wa, wb, bw, 32, tf);
       else if (i < n)
-        decide32<true>(L, S, wa, wb, bw, n - i);
-      flush_if(L, S, kDFlushAt);  // <= 16 digits per half block
+        decide32<true>(L, S, wa, wb, bw, n - i, tf);
+      flush_if_t(L, S, kDFlushAt, tf);  // <= 16 digits per half block
     }
+    ndec += nmax;
+  }
+  if (a.dbg && lane == 0) {
+    a.dbg[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memtime() - t_all;
+    a.dbg[blockIdx.x * 4 + 1] = tfl[0];
+    a.dbg[blockIdx.x * 4 + 2] = ndec;
+    a.dbg[blockIdx.x * 4 + 3] = tfl[1];
   }
   if (live) {
     const int64_t nbytes = terminate(L, S, true, kDRing);
@@ -1033,6 +1065,9 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
     stage4[0] = t;
   };
 
+  // the walk is the longer of the two pipelines it overlaps with (the coder
+  // of the previous batch): it wins the VALU arbitration on a shared SIMD
+  __builtin_amdgcn_s_setprio(2);
   uint64_t t_loop = 0, n_steps = 0;
   const uint64_t t_all = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
   for (int j = 0; j < seg.nframes; j++) {
@@ -1232,35 +1267,62 @@ __global__ __launch_bounds__(kBitsThreads) void ffv1_bits(BitsArgs a) {
       const int per = (cn + kBitsWaves - 1) / kBitsWaves;
       const int i0 = wv * per, i1 = min(cn, i0 + per);
       uint32_t carry = 0u;  // the previous chunk's last, partial word (lane 0)
-      for (int i = i0; i < i1; i++) {
-        const uint32_t* const q = pc + (int64_t)(c0 + i) * kChunkWords;
-        const int64_t pos = base + __builtin_amdgcn_readfirstlane(off[i]);
-        const int total = __builtin_amdgcn_readfirstlane(tot[i]);
+      // word m of chunk i: lo/hi = its words m-1 and m (zero outside)
+      auto word = [&](int i, int m, int64_t pos, int total, uint32_t hi, uint32_t lo, bool last_of_run,
+                      uint32_t& lastw) {
         const int sh = (int)(pos & 31);
         const int nw = (sh + total + 31) >> 5;
         const bool partial = ((sh + total) & 31) != 0;
         uint32_t* const dst = a.ds.bits + (pos >> 5);
-        uint32_t lastw = 0u;
-        for (int m0 = 0; m0 < nw; m0 += kWave) {
-          const int m = m0 + lane;
-          const uint32_t hi = m < nw ? q[1 + m] : 0u;
-          const uint32_t lo = m && m < nw ? q[m] : 0u;
-          uint32_t v = sh ? __builtin_amdgcn_alignbit(hi, lo, 32 - sh) : hi;
-          if (m == 0 && sh) v |= carry;  // zero for the run's first chunk
-          const bool shared_head = m == 0 && sh && i == i0;
-          const bool tail = m == nw - 1 && partial;
-          if (m < nw) {
-            if (tail && i + 1 < i1) {
-              // held for the next chunk of the run
-            } else if (shared_head || tail) {
-              atomicOr(&dst[m], v);
-            } else {
-              dst[m] = v;
-            }
+        uint32_t v = sh ? __builtin_amdgcn_alignbit(hi, lo, 32 - sh) : hi;
+        if (m == 0 && sh) v |= carry;  // zero for the run's first chunk
+        const bool shared_head = m == 0 && sh && i == i0;
+        const bool tail = m == nw - 1 && partial;
+        if (m < nw) {
+          if (tail && !last_of_run) {
+            // held for the next chunk of the run
+          } else if (shared_head || tail) {
+            atomicOr(&dst[m], v);
+          } else {
+            dst[m] = v;
           }
-          if ((nw - 1) >= m0 && (nw - 1) < m0 + kWave) lastw = __builtin_amdgcn_readlane(v, (nw - 1) - m0);
         }
-        carry = partial ? lastw : 0u;
+        const int lm = nw - 1;
+        if (lm >= (m & ~(kWave - 1)) && lm < (m & ~(kWave - 1)) + kWave)
+          lastw = __builtin_amdgcn_readlane(v, lm & (kWave - 1));
+      };
+      // four chunks' words in flight at a time; the carry then runs through them
+      for (int i = i0; i < i1; i += 4) {
+        uint32_t H[4], L[4];
+        int64_t P[4];
+        int T[4], NW[4];
+        static_for<0, 4>([&](auto kc) {
+          constexpr int K = decltype(kc)::value;
+          const bool ok = i + K < i1;
+          const int ii = ok ? i + K : i;
+          const uint32_t* const q = pc + (int64_t)(c0 + ii) * kChunkWords;
+          P[K] = base + __builtin_amdgcn_readfirstlane(off[ii]);
+          T[K] = ok ? __builtin_amdgcn_readfirstlane(tot[ii]) : 0;
+          NW[K] = ((int)(P[K] & 31) + T[K] + 31) >> 5;
+          H[K] = lane < NW[K] ? q[1 + lane] : 0u;
+          L[K] = lane && lane < NW[K] ? q[lane] : 0u;
+        });
+        static_for<0, 4>([&](auto kc) {
+          constexpr int K = decltype(kc)::value;
+          if (i + K < i1) {
+            const bool last = i + K + 1 == i1;
+            uint32_t lastw = 0u;
+            word(i + K, lane, P[K], T[K], H[K], L[K], last, lastw);
+            if (NW[K] > kWave) {  // long chunks (e >= 15 symbols): words 64..66
+              const uint32_t* const q = pc + (int64_t)(c0 + i + K) * kChunkWords;
+              const int m = kWave + lane;
+              const uint32_t hi = m < NW[K] ? q[1 + m] : 0u;
+              const uint32_t lo = m < NW[K] ? q[m] : 0u;
+              word(i + K, m, P[K], T[K], hi, lo, last, lastw);
+            }
+            carry = ((P[K] + T[K]) & 31) ? lastw : 0u;
+          }
+        });
       }
       run += all;
       __syncthreads();
@@ -1341,7 +1403,7 @@ __device__ __forceinline__ void vlc_put(BitSink& b, uint64_t& rec, int v, int bi
 __global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t tabs[1024];
   __shared__ __attribute__((aligned(16))) uint8_t opsets[kCodeThreads * kOpsetBytes];
-  __shared__ uint32_t ring[kRingStride * kWave];
+  __shared__ __attribute__((aligned(16))) uint32_t ring[kRingStride * kWave];
   for (int i = threadIdx.x; i < 1024; i += kCodeThreads) tabs[i] = a.tabs[i];
   __syncthreads();
   const int lane = threadIdx.x;
@@ -1522,7 +1584,7 @@ __global__ __launch_bounds__(kAsmThreads) void ffv1_assemble_packets(AssembleArg
 }  // namespace
 
 int launch_symbols(const SymbolArgs& a, void* stream) {
-  dim3 grid(a.nslices, a.nslots, a.dcount ? 3 : a.nplanes), block(kSymThreads);  // counts of absent planes: 0
+  dim3 grid(a.nslices, a.nslots, a.nplanes * kSymSplit), block(kSymThreads);
   hipLaunchKernelGGL(ffv1_symbols, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
