@@ -706,7 +706,7 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
 // bytes + one bit word: no per-symbol structure, so no lane waits on
 // another's exponent.  The ring is small (a flush check every 16 decisions)
 // so that a coder wave fits in the LDS the states walk leaves on a CU.
-constexpr int kDRing = 40;                   // renorm digits per lane before a flush
+constexpr int kDRing = 32;                   // renorm digits per lane before a flush
 constexpr int kDRingStride = kDRing + 3;  // odd: lanes at equal heads hit distinct banks
 constexpr int kDFlushAt = kDRing - 17;       // checked every 16 decisions
 
