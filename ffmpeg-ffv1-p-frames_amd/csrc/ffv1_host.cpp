@@ -263,7 +263,7 @@ struct ffv1hip_ctx {
   bool profiling = false;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> kev;  // [2 * launches]: start/stop per kernel launch
-  std::vector<int> kev_kind;    // per launch: 0 symbols, 1 code, 2 states, 3 assembly
+  std::vector<int> kev_kind;    // per launch: 0 symbols, 1 code, 2 states, 3 assembly, 4 layout, 5 bits
   int nkev = 0;
   int last_nsegs = 0;
 };
@@ -793,7 +793,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     sa.frame_chunks = c->frame_chunks;
     if (timed(0, st, [&] { return launch_symbols(sa, st); }) < 0)
       return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
-    if (timed(0, st, [&] { return launch_layout(d_dcount, n * c->nslices, d_dbase, c->d_dtotal + fb, st); }) < 0)
+    if (timed(4, st, [&] { return launch_layout(d_dcount, n * c->nslices, d_dbase, c->d_dtotal + fb, st); }) < 0)
       return set_err(-5, "layout launch failed: %s", hipGetErrorString(hipGetLastError()));
     // decisions of this batch: the worst case fits without asking the device
     int64_t need = int64_t(n) * c->frame_samples * c->wmax + int64_t(n) * c->nslices * kStreamSlack;
@@ -813,7 +813,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     ba.nslices = c->nslices;
     ba.nframes = n;
     ba.ds = ds;
-    if (timed(0, st, [&] { return launch_bits(ba, st); }) < 0)
+    if (timed(5, st, [&] { return launch_bits(ba, st); }) < 0)
       return set_err(-5, "bits launch failed: %s", hipGetErrorString(hipGetLastError()));
     WalkArgs wa{};
     wa.rec = d_rec;
@@ -1044,6 +1044,8 @@ int ffv1hip_last_kernel_stats(ffv1hip_ctx* c, ffv1hip_kernel_stats* out) {
       case 0: s.symbols_ms += ms; s.symbols_launches++; break;
       case 1: s.code_ms += ms; s.code_launches++; break;
       case 2: s.states_ms += ms; s.states_launches++; break;
+      case 4: s.layout_ms += ms; s.layout_launches++; break;
+      case 5: s.bits_ms += ms; s.bits_launches++; break;
       default: s.assemble_ms += ms; s.assemble_launches++; break;
     }
   }

@@ -88,9 +88,9 @@ constexpr uint32_t kRecSame = 0x80000000u;
 // decisions, then, from chroma_start(dcount[0]), the chroma chain's (Cb then
 // Cr).  Each chain is followed by kChainPad unused decisions: the states
 // walk writes a chunk's recorded bytes in whole 16-byte blocks, and the
-// blocks past a chain's last decision land there.  Decision d has s' (the
-// state it is coded with, folded with its bit, see ffv1_walk) in pre[d] and
-// its value in bit d of bits[] (bit d & 31 of word d >> 5).
+// blocks past a chain's last decision land there.  Decision d has the
+// adaptive state it is coded with in pre[d] and its value in bit d of
+// bits[] (bit d & 31 of word d >> 5).
 constexpr int kChainPad = 1536;
 __host__ __device__ inline int64_t chroma_start(int64_t dc0) { return ((dc0 + 63) & ~int64_t(63)) + kChainPad; }
 // decisions a stream takes beyond its own (alignment and the two pads)

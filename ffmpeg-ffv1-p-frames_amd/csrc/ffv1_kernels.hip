@@ -735,13 +735,14 @@ __device__ __forceinline__ void decide32(Lane& L, Sink& S, const uint4& wa, cons
     else if constexpr (J < 24) w = wb.y;
     else if constexpr (J < 28) w = wb.z;
     else w = wb.w;
-    const unsigned sp = __builtin_amdgcn_ubfe(w, SH, 8);        // s' = bit ? state : 256 - state
     const int m = __builtin_amdgcn_sbfe((int)bw, J, 1);         // all ones for a 1 decision
-    const unsigned c = (unsigned)~m & 255u;                     // round-up term of a 0 decision
-    // put_rac: 1 -> range*s >> 8; 0 -> range - (range*s >> 8) = (range*(256-s) + 255) >> 8
-    const int nr0 = (int)(__umul24((unsigned)L.range, sp) + c) >> 8;
-    int nl = L.low + ((L.range - nr0) & m);
-    int nr = nr0;
+    // put_rac (rangecoder.h:90-102): r1 = range * state >> 8; a 1 decision
+    // keeps r1 and adds range - r1 to low, a 0 decision keeps range - r1
+    const int r1 = (int)(__umul24((unsigned)L.range, (w >> SH) & 0xFFu) >> 8);
+    const int d = L.range - r1;
+    int nl = L.low + (d & m);
+    int nr;  // m ? r1 : d, one v_bfi (the compiler would make it a compare and two selects)
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(nr) : "v"(m), "v"(r1), "v"(d));
     if constexpr (TAIL) {
       const bool act = J < rem;
       nl = act ? nl : L.low;
@@ -852,7 +853,7 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_dcode(CodeArgs a) {
 // chains per instruction stream walk at nearly twice the rate of one; LDS
 // (one table per chain) caps chains per CU either way.
 //
-// Every decision's s' (below) is recorded at the decision's index in the
+// Every decision's adaptive state is recorded at the decision's index in the
 // stream.  Symbols come in chunks of 64 (ffv1_symbols' records, each with
 // the row, 2-bit slot codes and the decision offsets); a chunk's recorded
 // bytes are staged in LDS and go out, at the start of the next chunk, as
@@ -878,16 +879,15 @@ static_assert(kCopyBlocks * 32 * 16 <= kChainPad, "the copy-out stays inside the
 // LDS image of the walk: a fixed part (static, so every offset below is an
 // instruction immediate) and the two state tables (dynamic).
 constexpr int kLdsN = 0;                                      // u8 [3][256]: a slot's next state
-constexpr int kLdsS = kLdsN + kT3Bytes;                       // u8 [3][256]: the s' it records
-constexpr int kLdsRecs = kLdsS + kT3Bytes;                    // [2][kRecSlots] records
-constexpr int kLdsPre = kLdsRecs + 2 * kRecSlots * 16;        // [2][kPreHalf] recorded s'
+constexpr int kLdsRecs = kLdsN + kT3Bytes;                    // [2][kRecSlots] records
+constexpr int kLdsPre = kLdsRecs + 2 * kRecSlots * 16;        // [2][kPreHalf] recorded states
 constexpr int kLdsFixed = kLdsPre + 2 * kPreHalf;
 
 int64_t walk_lds_bytes_dev(int64_t state_bytes);
 
 // Any exponent, one symbol: lane k < 32 of a half applies all decisions of
 // slot k in order (slot 10 takes e-8 exponent decisions beyond e = 9, slot
-// 31 the mantissa bits >= 9, the sign goes to slot 21) and records s' for
+// 31 the mantissa bits >= 9, the sign goes to slot 21) and records the state for
 // each (see walk_step).  row_off: the slot's byte in the half's table.
 __device__ __forceinline__ void walk_long(uint8_t* tbl, const uint8_t* ftab, int v, int row_off, int k,
                                           uint8_t* pre) {
@@ -923,7 +923,7 @@ __device__ __forceinline__ void walk_long(uint8_t* tbl, const uint8_t* ftab, int
     else if (k <= 10) bit = di <= e;
     else if (k <= 21) bit = v < 0;
     else bit = (mag >> (2 * e + 1 - di)) & 1;
-    pre[di] = (uint8_t)(bit ? st : 256 - st);  // s', as walk_step records it
+    pre[di] = (uint8_t)st;  // the state it is coded with, as walk_step records it
     st = ftab[(bit << 8) | st];
   }
   tbl[row_off] = (uint8_t)st;
@@ -956,30 +956,26 @@ __device__ __forceinline__ StepIn derive(const uint4& r, const WalkLane& W, int 
   return d;
 }
 
-// Symbol T: the lookups of T are issued first; T-1's table and stage writes
-// and the read of T+1's row then fill their latency.  The row read one
-// symbol ahead misses T's write, so a symbol continuing its predecessor's
-// row takes the state from the register instead.
+// Symbol T: the lookup of T is issued first; T's recorded state, T-1's
+// table write and the read of T+1's row then fill its latency.  The row read
+// one symbol ahead misses T's write, so a symbol continuing its
+// predecessor's row takes the state from the register instead.
 // N[code][state] = the state after the slot's decision (code 0/1 its bit, 2
-// none); S[code][state] = s', the state for a 1 decision and 256 - state for
-// a 0 one, so that put_rac's new range is (range * s' + (bit ? 0 : 255)) >> 8.
+// none); the state before it is what the coder needs (put_rac's r1 = range *
+// state >> 8).
 __device__ __forceinline__ void walk_step(uint8_t* fixed, uint8_t* tbl, const StepIn& d, int addr_next,
-                                          uint32_t& e1, uint32_t& s1, uint32_t& l0, int& addr_prev,
-                                          int& pos_prev) {
+                                          uint32_t& e1, uint32_t& l0, int& addr_prev) {
   uint32_t a1 = e1, a0 = l0;
   pin(a1);
   pin(a0);
   const uint32_t st = d.same ? a1 : a0;
   const uint32_t idx = (d.code << 8) | st;
   const uint32_t n = fixed[kLdsN + idx];
-  const uint32_t s = fixed[kLdsS + idx];
+  fixed[kLdsPre + d.pos] = (uint8_t)st;      // T's recorded state
   tbl[addr_prev] = (uint8_t)a1;              // T-1's state
-  fixed[kLdsPre + pos_prev] = (uint8_t)s1;   // T-1's recorded s'
   l0 = tbl[addr_next];                       // T+1's row, after every earlier write but T's
   addr_prev = d.addr;
-  pos_prev = d.pos;
   e1 = n;
-  s1 = s;
 }
 
 int64_t walk_lds_bytes_dev(int64_t state_bytes) { return kLdsFixed + 2 * (state_bytes / 2 + 32); }
@@ -1003,7 +999,6 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   for (int i = lane; i < kT3Bytes; i += kWalkThreads) {
     const int code = i >> 8, st = i & 255;
     fixed[kLdsN + i] = (uint8_t)(code < 2 ? a.ftab[i] : st);
-    fixed[kLdsS + i] = (uint8_t)(code == 1 ? st : 256 - st);  // (state 0 never occurs)
   }
   // every luma chain first: they are twice as long as the chroma ones, which
   // then fill the CUs as the luma waves finish
@@ -1147,13 +1142,12 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
         StepIn d0 = derive(myrecs[0], W, kc), d1 = derive(myrecs[1], W, kc);
         uint4 rn = myrecs[2];
         uint32_t l0 = tbl[d0.addr];
-        uint32_t e1 = 0u, s1 = 0u;
+        uint32_t e1 = 0u;
         int addr_prev = (int)((stage + kPreData + k) - tbl);  // no T-1 yet: the dummy byte
-        int pos_prev = W.dummy;
         const uint64_t t0 = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
         static_for<0, kChunk>([&](auto tc) {
           constexpr int T = decltype(tc)::value;
-          walk_step(fixed, tbl, d0, d1.addr, e1, s1, l0, addr_prev, pos_prev);
+          walk_step(fixed, tbl, d0, d1.addr, e1, l0, addr_prev);
           const uint4 r3 = myrecs[T + 3];  // three ahead
           __builtin_amdgcn_sched_barrier(0);  // keeps the read here, not sunk to its use a step later
           d0 = d1;
@@ -1161,7 +1155,6 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
           rn = r3;
         });
         tbl[addr_prev] = (uint8_t)e1;  // the chunk's last symbol
-        fixed[kLdsPre + pos_prev] = (uint8_t)s1;
         if (a.dbg) {
           __builtin_amdgcn_s_waitcnt(0);
           t_loop += __builtin_amdgcn_s_memtime() - t0;

@@ -67,7 +67,9 @@ class KernelStats(ctypes.Structure):
                 ("assemble_ms", ctypes.c_float), ("symbols_launches", ctypes.c_int),
                 ("code_launches", ctypes.c_int), ("assemble_launches", ctypes.c_int),
                 ("frames_coded_per_launch_max", ctypes.c_int64), ("states_ms", ctypes.c_float),
-                ("states_launches", ctypes.c_int)]
+                ("states_launches", ctypes.c_int), ("layout_ms", ctypes.c_float),
+                ("bits_ms", ctypes.c_float), ("layout_launches", ctypes.c_int),
+                ("bits_launches", ctypes.c_int)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

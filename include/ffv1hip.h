@@ -133,16 +133,20 @@ int ffv1hip_last_kernel_ms(ffv1hip_ctx *ctx, float *encode_ms, float *assemble_m
 
 /* Per-kernel totals of every call since profiling was (re)enabled: summed
  * HIP-event durations (events on each kernel's own stream) and launch counts
- * of ffv1_symbols (prediction/context), ffv1_states (context-state walk,
- * frame-parallel mode), ffv1_code (range coder) and ffv1_assemble_packets.
- * Frame-parallel mode launches each once per call; the chained mode launches
- * symbols and code once per frame index of the GOP. */
+ * of ffv1_symbols (prediction/context), the states walk (ffv1_walk,
+ * frame-parallel mode), the range coder (ffv1_dcode; ffv1_code or
+ * ffv1_code_golomb in the chained mode), ffv1_assemble_packets, and in
+ * frame-parallel mode the decision layout (ffv1_layout) and decision bits
+ * (ffv1_bits).  Frame-parallel mode launches each once per call; the chained
+ * mode launches symbols and code once per frame index of the GOP. */
 typedef struct ffv1hip_kernel_stats {
     float symbols_ms, code_ms, assemble_ms;
     int symbols_launches, code_launches, assemble_launches;
     int64_t frames_coded_per_launch_max;   /* slice streams per coder launch / nslices */
     float states_ms;                       /* context-state walk (frame-parallel mode) */
     int states_launches;
+    float layout_ms, bits_ms;              /* frame-parallel mode */
+    int layout_launches, bits_launches;
 } ffv1hip_kernel_stats;
 int ffv1hip_last_kernel_stats(ffv1hip_ctx *ctx, ffv1hip_kernel_stats *out);
 
