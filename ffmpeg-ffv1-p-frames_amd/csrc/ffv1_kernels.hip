@@ -97,13 +97,20 @@ __device__ __forceinline__ void slot_codes(int v, uint32_t& c0, uint32_t& c1) {
   c1 = spread16(bm >> 16) | (spread16(nt >> 16) << 1);
 }
 
-__device__ __forceinline__ int wave_incl_scan(int x, int lane) {
-  for (int o = 1; o < kWave; o <<= 1) {
-    const int y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
+// Inclusive wave scan in DPP moves (no LDS round trips): within rows of 16
+// by row_shr 1, 2, 4, 8, then the row totals by row_bcast 15 / 31.
+__device__ __forceinline__ int wave_incl_scan(int x, int /*lane*/) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 into rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 into rows 2, 3
   return x;
 }
+
+// the previous lane's value (lane 0: 0), a DPP wave_shr:1
+__device__ __forceinline__ int wave_prev(int x) { return __builtin_amdgcn_update_dpp(0, x, 0x138, 0xf, 0xf, true); }
 
 __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   __shared__ int16_t qt[5 * 256];
@@ -173,7 +180,7 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
       const int d0 = incl - nd;
       const unsigned mag = diff < 0 ? 0u - (unsigned)diff : (unsigned)diff;
       const int e = diff ? 31 - __builtin_clz(mag) : 0;
-      const int prev = __shfl_up(raddr, 1);
+      const int prev = wave_prev(raddr);
       uint32_t c0, c1;
       slot_codes(diff, c0, c1);
       const uint32_t w = (uint32_t)d0 | ((uint32_t)(d0 + 2 * e) << 16) | (lane > 0 && prev == raddr ? kRecSame : 0u);
