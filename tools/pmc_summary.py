@@ -15,7 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    for k in ("ffv1_code_golomb", "ffv1_code", "ffv1_states", "ffv1_symbols", "ffv1_assemble_packets"):
+    for k in ("ffv1_code_golomb", "ffv1_dcode", "ffv1_code", "ffv1_walk", "ffv1_bits", "ffv1_layout", "ffv1_symbols",
+              "ffv1_assemble_packets"):
         if k in name:
             return k
     return name
@@ -51,12 +52,12 @@ def main(tag, frames_per_launch, config):
         "note": "per-launch means over the profiled bench run; FETCH_SIZE doubled (gfx950), WRITE_SIZE as is",
         "kernels": kernels,
         "rocprof_avg_ms": stats,
-        "encode_hbm_bytes_per_launch": kernels.get("ffv1_code", {}).get("hbm_bytes"),
+        "encode_hbm_bytes_per_launch": kernels.get("ffv1_dcode", {}).get("hbm_bytes"),
     }
     json.dump(out, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01", int(sys.argv[2]) if len(sys.argv) > 2 else 144,
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01", int(sys.argv[2]) if len(sys.argv) > 2 else 252,
          "3840x2160 yuv420p10")
