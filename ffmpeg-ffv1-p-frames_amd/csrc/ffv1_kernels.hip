@@ -51,8 +51,8 @@ __device__ __forceinline__ int fold_bits(int d, int bits) {
 
 // ---------------------------------------------------------------------------
 // Kernel 1: symbols.
-constexpr int kSymThreads = 256;
-constexpr int kSymSplit = 8;  // blocks per slice plane: the per-block loop is latency-bound
+constexpr int kSymThreads = 64;  // one wave per block: a wave slowed by a busy SIMD holds back no other
+constexpr int kSymSplit = 24;  // blocks per slice plane: the per-block loop is latency-bound
 
 // Range-coder decisions of one residual: put_symbol_inline (ffv1enc.c:185-231)
 // codes a zero flag, e+1 exponent decisions, e mantissa bits and a sign.
