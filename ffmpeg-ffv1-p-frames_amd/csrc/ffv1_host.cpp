@@ -253,6 +253,9 @@ struct ffv1hip_ctx {
   int buf = 0;                   // buffer set of the next batch
   hipStream_t code_stream = nullptr;  // ffv1_dcode + assembly, behind the states walk
   hipEvent_t walked[2] = {nullptr, nullptr};
+  hipStream_t bits_stream = nullptr;  // ffv1_bits, beside the states walk
+  hipEvent_t laid[2] = {nullptr, nullptr};    // set k's stream layout and zeroed bits are ready
+  hipEvent_t bitsed[2] = {nullptr, nullptr};  // set k's decision bits are in place
   hipEvent_t coded[2] = {nullptr, nullptr};  // the coder of the batch that last used set k is done
   SliceGeom* d_geom = nullptr;
   int* d_slot_frames = nullptr;  // [j][slot]
@@ -471,7 +474,12 @@ static void free_device(ffv1hip_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->code_stream) (void)hipStreamDestroy(c->code_stream);
+  if (c->bits_stream) (void)hipStreamDestroy(c->bits_stream);
   for (hipEvent_t& e : c->walked)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t& e : c->laid)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t& e : c->bitsed)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t& e : c->coded)
     if (e) (void)hipEventDestroy(e);
@@ -530,6 +538,9 @@ static int alloc_device(ffv1hip_ctx* c) {
     HIP_TRY(hipMalloc(&c->d_dtotal, 2 * sizeof(int64_t)));
     HIP_TRY(hipHostMalloc(&c->h_dtotal, 2 * sizeof(int64_t), hipHostMallocDefault));
     HIP_TRY(hipStreamCreateWithFlags(&c->code_stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&c->bits_stream, hipStreamNonBlocking));
+    for (hipEvent_t& e : c->laid) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (hipEvent_t& e : c->bitsed) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->walked) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->coded) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     // decision capacity: the worst case when it is small, else ~12 per symbol
@@ -813,8 +824,13 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     ba.nslices = c->nslices;
     ba.nframes = n;
     ba.ds = ds;
-    if (timed(5, st, [&] { return launch_bits(ba, st); }) < 0)
+    // the bits run beside the walk, on their own stream; the coder waits for both
+    hipStream_t const bst = serial ? st : c->bits_stream;
+    HIP_TRY(hipEventRecord(c->laid[fb], st));
+    HIP_TRY(hipStreamWaitEvent(bst, c->laid[fb], 0));
+    if (timed(5, bst, [&] { return launch_bits(ba, bst); }) < 0)
       return set_err(-5, "bits launch failed: %s", hipGetErrorString(hipGetLastError()));
+    HIP_TRY(hipEventRecord(c->bitsed[fb], bst));
     WalkArgs wa{};
     wa.rec = d_rec;
     wa.cbits = sa.cbits;
@@ -859,6 +875,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     // the next batch (on st) then overlaps this batch's coding
     HIP_TRY(hipEventRecord(c->walked[fb], st));
     HIP_TRY(hipStreamWaitEvent(cst, c->walked[fb], 0));
+    HIP_TRY(hipStreamWaitEvent(cst, c->bitsed[fb], 0));
     ca.nframes = n;
     ca.nopsets = c->nopsets;
     ca.ds = ds;
@@ -966,6 +983,7 @@ int ffv1hip_synchronize(ffv1hip_ctx* c) {
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (c->code_stream) HIP_TRY(hipStreamSynchronize(c->code_stream));
+  if (c->bits_stream) HIP_TRY(hipStreamSynchronize(c->bits_stream));
   return 0;
 }
 
