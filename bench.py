@@ -32,7 +32,7 @@ sys.path.insert(0, os.path.join(ROOT, "ffmpeg-ffv1-p-frames_amd"))
 W, H, PIX_FMT, SLICES, GOP = 3840, 2160, "yuv420p10", 64, 12
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 KERNEL = {"symbols": "ffv1_symbols", "layout": "ffv1_layout", "bits": "ffv1_bits", "states": "ffv1_walk",
-          "code": "ffv1_dcode", "assemble": "ffv1_assemble_packets"}
+          "code": "ffv1_dcode", "sink": "ffv1_sink", "assemble": "ffv1_assemble_packets"}
 PIN_MD5_24 = "08e3975d4d0f5f2e5c82cd4037764789"  # tests/golden/known_answers.json (config 3)
 
 
@@ -193,7 +193,7 @@ def main():
         bitexact = h.hexdigest() == PIN_MD5_24
 
     tot = stats[0]
-    names = ("symbols", "layout", "bits", "states", "code", "assemble")
+    names = ("symbols", "layout", "bits", "states", "code", "sink", "assemble")
     per_step = {k: tot[k + "_ms"] / args.steps for k in names}
     launches = {k: tot[k + "_launches"] // args.steps for k in names}
     code_ms = per_step["code"]
@@ -235,8 +235,8 @@ def main():
             },
             "bits_per_pixel": round(out_bytes * 8 / (B * W * H), 4),
             "bitexact_vs_reference_pin": bitexact,
-            # kernels of the two overlapped pipelines: symbols -> layout -> bits
-            # -> walk (batch k+1) beside dcode -> assemble (batch k)
+            # kernels of the overlapped pipelines: symbols -> layout -> walk
+            # (batch k+1), bits beside the walk, dcode -> sink -> assemble (batch k)
             "kernel_ms_per_step": dict(
                 **{KERNEL[k]: round(per_step[k], 3) for k in names},
                 launches={KERNEL[k]: launches[k] for k in names}),

@@ -211,6 +211,7 @@ struct ffv1hip_ctx {
   std::vector<Op> ops;     // [key][slice][kMaxOps]
   std::vector<int> nops;   // [key][slice]
   int64_t slice_cap = 0;
+  int64_t slice_stride = 0;  // bytes per slice slot of d_slice_out
   int64_t packet_stride = 0;
   int64_t frame_bytes = 0;  // host-layout batch buffer stride
   int64_t plane_bytes[3]{};
@@ -521,7 +522,7 @@ static int alloc_device(ffv1hip_ctx* c) {
   HIP_TRY(hipMemcpy(c->d_nops, c->nops.data(), c->nops.size() * sizeof(int), hipMemcpyHostToDevice));
   HIP_TRY(hipMalloc(&c->d_segs, sizeof(Segment) * (nb + 1)));
   HIP_TRY(hipMalloc(&c->d_keys, nb));
-  HIP_TRY(hipMalloc(&c->d_slice_out, size_t(c->slice_cap) * c->nslices * nb));
+  HIP_TRY(hipMalloc(&c->d_slice_out, size_t(c->slice_stride) * c->nslices * nb));
   HIP_TRY(hipMalloc(&c->d_slice_bytes, sizeof(int64_t) * c->nslices * nb));
   HIP_TRY(hipMalloc(&c->d_packets, size_t(c->packet_stride) * nb));
   HIP_TRY(hipMalloc(&c->d_packet_size, sizeof(int64_t) * nb));
@@ -644,6 +645,9 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
     const int64_t lds = walk_lds_bytes(int64_t(2) * c->contexts * 32);
     c->frames_mode = p.ac && lds <= kWalkLdsMax && !(mode && std::strcmp(mode, "chain") == 0);
     c->wmax = 2 * (p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample) + 1;
+    // the decision-stream coder writes a slice's digits (2 bytes each) where
+    // ffv1_sink then writes its bytes
+    c->slice_stride = c->frames_mode ? 2 * c->slice_cap : c->slice_cap;
   }
   int rc = alloc_device(c);
   if (rc < 0) {
@@ -764,6 +768,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   ca.persist = c->d_persist;
   ca.slice_out = c->d_slice_out;
   ca.slice_cap = c->slice_cap;
+  ca.slice_stride = c->slice_stride;
   ca.slice_bytes = c->d_slice_bytes;
   ca.status = c->d_status;
   ca.version = p.version;
@@ -890,6 +895,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     }
     if (timed(1, cst, [&] { return launch_dcode(ca, cst); }) < 0)
       return set_err(-5, "code launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (timed(6, cst, [&] { return launch_sink(ca, cst); }) < 0)
+      return set_err(-5, "sink launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (codedbg) {
       std::vector<uint64_t> h(size_t(4) * nwaves);
       HIP_TRY(hipMemcpyAsync(h.data(), d_cdbg, h.size() * 8, hipMemcpyDeviceToHost, cst));
@@ -921,6 +928,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   AssembleArgs b{};
   b.slice_out = c->d_slice_out;
   b.slice_cap = c->slice_cap;
+  b.slice_stride = c->slice_stride;
   b.slice_bytes = c->d_slice_bytes;
   b.packets = c->d_packets;
   b.packet_stride = c->packet_stride;
@@ -1064,6 +1072,7 @@ int ffv1hip_last_kernel_stats(ffv1hip_ctx* c, ffv1hip_kernel_stats* out) {
       case 2: s.states_ms += ms; s.states_launches++; break;
       case 4: s.layout_ms += ms; s.layout_launches++; break;
       case 5: s.bits_ms += ms; s.bits_launches++; break;
+      case 6: s.sink_ms += ms; s.sink_launches++; break;
       default: s.assemble_ms += ms; s.assemble_launches++; break;
     }
   }

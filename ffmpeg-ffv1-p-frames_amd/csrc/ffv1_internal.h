@@ -122,8 +122,9 @@ struct CodeArgs {
   int64_t state_bytes;        // 2 * contexts * 32
   uint8_t* tables;            // [chain][state_bytes] working context states (grid-padded)
   uint8_t* persist;           // [slice][state_bytes]
-  uint8_t* slice_out;         // [batch frame][slice][slice_cap]
-  int64_t slice_cap;
+  uint8_t* slice_out;         // [batch frame][slice][slice_stride]
+  int64_t slice_cap;          // byte budget of a slice
+  int64_t slice_stride;       // bytes per slice slot (decision-stream mode: 2 x slice_cap, for the digits)
   int64_t* slice_bytes;       // [batch frame][slice]
   int* status;                // [0] overflow count
   int version;                // bitstream version (Golomb: v3 adds a 129/0 decision)
@@ -169,6 +170,7 @@ struct BitsArgs {
 struct AssembleArgs {
   const uint8_t* slice_out;
   int64_t slice_cap;
+  int64_t slice_stride;
   const int64_t* slice_bytes;  // [frame][slice]
   uint8_t* packets;            // [frame] regions of packet_stride bytes
   int64_t packet_stride;
@@ -183,6 +185,7 @@ int launch_code(const CodeArgs& a, void* stream);
 int launch_layout(const int* dcount, int nstreams, int64_t* dbase, int64_t* total, void* stream);
 int launch_walk(const WalkArgs& a, int nsegs, void* stream);
 int launch_dcode(const CodeArgs& a, void* stream);
+int launch_sink(const CodeArgs& a, void* stream);
 int launch_bits(const BitsArgs& a, void* stream);
 int64_t walk_lds_bytes(int64_t state_bytes);
 constexpr int64_t kWalkLdsMax = 64 * 1024;  // states walk: one plane group's table + T9 + staging in LDS

@@ -278,11 +278,13 @@ struct Sink {
       on = 0;
     }
   }
-  // one recorded `low` (act: this lane has it)
-  __device__ __forceinline__ void digit(int low, bool act) {
-    const int qv = low >> 8;
+  // one recorded `low` (act: this lane has it), as qv = low >> 8 and whether
+  // its low byte is non-zero: low is in (0xFF00, 0x10000) iff qv is 0xFF and
+  // it is
+  __device__ __forceinline__ void digit(int low, bool act) { digit_q(low >> 8, (low & 0xFF) != 0, act); }
+  __device__ __forceinline__ void digit_q(int qv, bool lownz, bool act) {
     const bool first = pending < 0;
-    const bool isrun = !first && low > 0xFF00 && low < 0x10000;
+    const bool isrun = !first && qv == 0xFF && lownz;
     const bool emit = act && !first && !isrun;
     const int c = qv >> 8;  // carry into the outstanding byte
     put((uint32_t)(pending + c), emit);
@@ -338,7 +340,34 @@ __device__ __forceinline__ void flush(Lane& L, Sink& S) {
   L.rp = L.ring;
 }
 
-__device__ __forceinline__ void flush_if(Lane& L, Sink& S, int above) {
+// Digit writer (decision-stream coder): the ring's values of `low` go out
+// unreplayed, one u16 each, qv = low >> 8 | (low & 0xFF ? 0x200 : 0);
+// ffv1_sink then turns them into the slice's bytes.
+struct DigitSink {
+  uint16_t* out;
+  int n, cap;  // digits so far, capacity
+  __device__ __forceinline__ void put(uint32_t low, int t, bool act) {
+    const int i = n + t;
+    if (act && i < cap) out[i] = (uint16_t)((low >> 8) | ((low & 0xFFu) ? 0x200u : 0u));
+  }
+  __device__ __forceinline__ int64_t finish() { return n; }
+};
+
+__device__ __forceinline__ void flush(Lane& L, DigitSink& D) {
+  const int n = (int)(L.rp - L.ring);
+  for (int t = 0; __ballot(t < n); t += 4) {
+    const uint32_t d0 = L.ring[t], d1 = L.ring[t + 1], d2 = L.ring[t + 2], d3 = L.ring[t + 3];
+    D.put(d0, t, t < n);
+    D.put(d1, t + 1, t + 1 < n);
+    D.put(d2, t + 2, t + 2 < n);
+    D.put(d3, t + 3, t + 3 < n);
+  }
+  D.n += n;
+  L.rp = L.ring;
+}
+
+template <class SinkT>
+__device__ __forceinline__ void flush_if(Lane& L, SinkT& S, int above) {
   if (__ballot((int)(L.rp - L.ring) > above)) flush(L, S);
 }
 
@@ -537,7 +566,8 @@ constexpr int kOpsetBytes = kOpSets * 32;
 // Key bit / in-band v0/v1 header / v3 slice header (per-lane op program).
 // os: this lane's op-set states (osb bytes); flush_at: the ring's flush
 // threshold before each op (<= 29 digits per op).
-__device__ __forceinline__ void run_header_ops(const CodeArgs& a, Lane& L, Sink& S, uint8_t* os, int key,
+template <class SinkT>
+__device__ __forceinline__ void run_header_ops(const CodeArgs& a, Lane& L, SinkT& S, uint8_t* os, int key,
                                                int slice, bool live, const uint8_t* dtab,
                                                const uint8_t* ftab, int osb, int flush_at) {
   for (int i = 0; i < osb; i++) os[i] = 128;
@@ -567,7 +597,8 @@ __device__ __forceinline__ void lane_init(Lane& L, uint32_t* ring) {
 }
 
 // slice end: a 0 decision on state 129, then ff_rac_terminate
-__device__ __forceinline__ int64_t terminate(Lane& L, Sink& S, bool state129, int ring) {
+template <class SinkT>
+__device__ __forceinline__ int64_t terminate(Lane& L, SinkT& S, bool state129, int ring) {
   flush_if(L, S, ring - 4);
   if (state129) {
     rac_core(L, 129, 0);
@@ -623,7 +654,7 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
 
   Lane L;
   lane_init(L, ring + lane * kRingStride);
-  uint8_t* const out = a.slice_out + ((int64_t)(live ? f : 0) * a.nslices + slice) * a.slice_cap;
+  uint8_t* const out = a.slice_out + ((int64_t)(live ? f : 0) * a.nslices + slice) * a.slice_stride;
   Sink S = make_sink(out, live ? a.slice_cap : 0);  // idle lanes write nothing
 
   run_header_ops(a, L, S, opsets + lane * kOpsetBytes, key, slice, live, dtab, ftab, kOpsetBytes, kHeaderFlushAt);
@@ -718,18 +749,25 @@ constexpr int kDRingStride = kDRing + 3;  // odd: lanes at equal heads hit disti
 constexpr int kDFlushAt = kDRing - 17;       // checked every 16 decisions
 
 // flush_if, timed into *tf when tf is set (FFV1HIP_CODEDBG)
-__device__ __forceinline__ void flush_if_t(Lane& L, Sink& S, int above, uint64_t* tf) {
+// flush_if, timed (FFV1HIP_CODEDBG): cycles into tf, wave-max entries into ti
+struct FlushTimer {
+  bool on;
+  uint64_t tf, ti;
+};
+
+template <class SinkT>
+__device__ __forceinline__ void flush_if_t(Lane& L, SinkT& S, int above, FlushTimer& T) {
   if (__ballot((int)(L.rp - L.ring) > above)) {
-    const uint64_t t0 = tf ? __builtin_amdgcn_s_memtime() : 0;
-    if (tf) tf[1] += wave_max((int)(L.rp - L.ring));
+    const uint64_t t0 = T.on ? __builtin_amdgcn_s_memtime() : 0;
+    if (T.on) T.ti += wave_max((int)(L.rp - L.ring));
     flush(L, S);
-    if (tf) tf[0] += __builtin_amdgcn_s_memtime() - t0;
+    if (T.on) T.tf += __builtin_amdgcn_s_memtime() - t0;
   }
 }
 
-template <bool TAIL>
-__device__ __forceinline__ void decide32(Lane& L, Sink& S, const uint4& wa, const uint4& wb, uint32_t bw,
-                                         int rem, uint64_t* tf) {
+template <bool TAIL, class SinkT>
+__device__ __forceinline__ void decide32(Lane& L, SinkT& S, const uint4& wa, const uint4& wb, uint32_t bw,
+                                         int rem, FlushTimer& tf) {
   static_for<0, 32>([&](auto jc) {
     constexpr int J = decltype(jc)::value;
     constexpr int SH = (J & 3) * 8;
@@ -785,16 +823,18 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_dcode(CodeArgs a) {
 
   Lane L;
   lane_init(L, ring + lane * kDRingStride);
-  uint8_t* const out = a.slice_out + ((int64_t)f * a.nslices + slice) * a.slice_cap;
-  Sink S = make_sink(out, live ? a.slice_cap : 0);
+  // the stream's digits, in its slice_out slot (2 bytes per digit; ffv1_sink
+  // rewrites the slot with the bytes in place)
+  DigitSink S{reinterpret_cast<uint16_t*>(a.slice_out + ((int64_t)f * a.nslices + slice) * a.slice_stride), 0,
+              live ? (int)(a.slice_stride / 2) : 0};
   run_header_ops(a, L, S, opsets + lane * osb, key, slice, live, tabs, tabs + 512, osb, kDRing - 30);
   flush_if(L, S, kDFlushAt);
 
   const int64_t st = (int64_t)f * a.nslices + slice;
   const int* dc = a.ds.dcount + st * 3;
   const int64_t base = live ? a.ds.dbase[st] : 0;  // multiple of kStreamAlign
-  uint64_t tfl[2] = {0, 0}, ndec = 0;
-  uint64_t* const tf = a.dbg ? tfl : nullptr;
+  uint64_t ndec = 0;
+  FlushTimer tf{a.dbg != nullptr, 0, 0};
   const uint64_t t_all = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
   // the luma chain's decisions, then the chroma chain's at their own start
   for (int part = 0; part < 2; part++) {
@@ -839,13 +879,62 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_dcode(CodeArgs a) {
   }
   if (a.dbg && lane == 0) {
     a.dbg[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memtime() - t_all;
-    a.dbg[blockIdx.x * 4 + 1] = tfl[0];
+    a.dbg[blockIdx.x * 4 + 1] = tf.tf;
     a.dbg[blockIdx.x * 4 + 2] = ndec;
-    a.dbg[blockIdx.x * 4 + 3] = tfl[1];
+    a.dbg[blockIdx.x * 4 + 3] = tf.ti;
   }
   if (live) {
-    const int64_t nbytes = terminate(L, S, true, kDRing);
-    if (nbytes > a.slice_cap) atomicAdd(a.status, 1);
+    const int64_t ndig = terminate(L, S, true, kDRing);
+    if (ndig > a.slice_stride / 2) atomicAdd(a.status, 1);
+    a.slice_bytes[st] = ndig;  // digits, until ffv1_sink
+  }
+}
+
+// The byte writer of the decision-stream coder, one wave per (frame, slice)
+// stream.  renorm_encoder (rangecoder.h:52-75) emits, for every digit j but
+// the last non-run one and the 0xFF-run digits after it, the byte
+// (qv_j + c_j) & 0xFF, where c_j is the carry (qv_k >> 8) of the first
+// non-run digit k after j (a run digit: qv = 0xFF with a non-zero low byte,
+// never the first).  So 64 digits at a time are turned into bytes in
+// parallel; only the tail of a block, from its last non-run digit, waits for
+// the next block with a non-run digit.  The bytes go over the digits (byte i
+// never passes digit i, which sits at bytes 2i, 2i+1).
+constexpr int kSinkThreads = kWave;
+__global__ __launch_bounds__(kSinkThreads) void ffv1_sink(CodeArgs a) {
+  const int64_t st = blockIdx.x;
+  const int lane = threadIdx.x;
+  uint8_t* const out = a.slice_out + st * a.slice_stride;
+  const uint16_t* const din = reinterpret_cast<const uint16_t*>(out);
+  const int n = (int)a.slice_bytes[st];  // digits
+  const int cap = (int)a.slice_cap;
+  int pend = -1;       // the last non-run digit so far: its byte and its run's wait for a carry
+  uint32_t pqv = 0u;   // its qv
+  uint32_t nx = lane < n ? din[lane] : 0u;
+  for (int b = 0; b * kWave < n; b++) {
+    const int j = b * kWave + lane;
+    const uint32_t d = nx;
+    nx = j + kWave < n ? din[j + kWave] : 0u;  // the next block, in flight
+    const uint32_t qv = d & 0x1FFu;
+    const bool nonrun = j < n && !(j > 0 && qv == 0xFFu && (d & 0x200u));
+    const uint64_t m = __ballot(nonrun);
+    if (!m) continue;  // a run goes on
+    __builtin_amdgcn_wave_barrier();  // every lane has read its digit before any byte lands
+    const int first = __builtin_ctzll(m), last = 63 - __builtin_clzll(m);
+    const uint32_t c0 = __builtin_amdgcn_readlane(qv >> 8, first);
+    if (pend >= 0) {  // the waiting byte and its run: 0xFF, or 0x00 after a carry
+      const int end = b * kWave + first;
+      for (int i = pend + lane; i < end; i += kWave)
+        if (i < cap) out[i] = (uint8_t)(i == pend ? (pqv + c0) & 0xFFu : (0xFFu + c0) & 0xFFu);
+    }
+    const uint64_t after = lane < 63 ? m & (~0ull << (lane + 1)) : 0ull;
+    const uint32_t ck = __shfl(qv >> 8, after ? __builtin_ctzll(after) : 0);
+    if (lane >= first && lane < last && j < cap) out[j] = (uint8_t)((qv + ck) & 0xFFu);
+    pend = b * kWave + last;
+    pqv = __builtin_amdgcn_readlane(qv, last);
+  }
+  if (lane == 0) {
+    const int nbytes = pend < 0 ? 0 : pend;
+    if (nbytes > cap) atomicAdd(a.status, 1);
     a.slice_bytes[st] = nbytes;
   }
 }
@@ -1431,7 +1520,7 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
   // state 129 and ff_rac_terminate (ffv1enc.c:1173-1183)
   Lane L;
   lane_init(L, ring + lane * kRingStride);
-  uint8_t* const out = a.slice_out + ((int64_t)(live ? f : 0) * a.nslices + slice) * a.slice_cap;
+  uint8_t* const out = a.slice_out + ((int64_t)(live ? f : 0) * a.nslices + slice) * a.slice_stride;
   Sink S = make_sink(out, live ? a.slice_cap : 0);  // idle lanes write nothing
   run_header_ops(a, L, S, opsets + lane * kOpsetBytes, key, slice, live, tabs, tabs + 512, kOpsetBytes,
                  kHeaderFlushAt);
@@ -1552,7 +1641,7 @@ __global__ __launch_bounds__(kAsmThreads) void ffv1_assemble_packets(AssembleArg
   const int64_t n = sb[s];
   const bool has_size = s > 0 || a.version > 2;
   const int64_t body = n + (has_size ? 3 : 0) + (a.ec ? 1 : 0);  // bytes covered by the CRC
-  const uint8_t* src = a.slice_out + ((int64_t)f * a.nslices + s) * a.slice_cap;
+  const uint8_t* src = a.slice_out + ((int64_t)f * a.nslices + s) * a.slice_stride;
   uint8_t* dst = a.packets + (int64_t)f * a.packet_stride + off;
 
   auto body_byte = [&](int64_t i) -> uint32_t {
@@ -1622,6 +1711,13 @@ int launch_bits(const BitsArgs& a, void* stream) {
 int launch_layout(const int* dcount, int nstreams, int64_t* dbase, int64_t* total, void* stream) {
   hipLaunchKernelGGL(ffv1_layout, dim3(1), dim3(kLayoutThreads), 0, reinterpret_cast<hipStream_t>(stream), dcount,
                      nstreams, dbase, total);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_sink(const CodeArgs& a, void* stream) {
+  const int64_t streams = (int64_t)a.nframes * a.nslices;
+  dim3 grid((unsigned)streams), block(kSinkThreads);
+  hipLaunchKernelGGL(ffv1_sink, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -69,7 +69,8 @@ class KernelStats(ctypes.Structure):
                 ("frames_coded_per_launch_max", ctypes.c_int64), ("states_ms", ctypes.c_float),
                 ("states_launches", ctypes.c_int), ("layout_ms", ctypes.c_float),
                 ("bits_ms", ctypes.c_float), ("layout_launches", ctypes.c_int),
-                ("bits_launches", ctypes.c_int)]
+                ("bits_launches", ctypes.c_int), ("sink_ms", ctypes.c_float),
+                ("sink_launches", ctypes.c_int)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

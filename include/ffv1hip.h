@@ -137,7 +137,7 @@ int ffv1hip_last_kernel_ms(ffv1hip_ctx *ctx, float *encode_ms, float *assemble_m
  * frame-parallel mode), the range coder (ffv1_dcode; ffv1_code or
  * ffv1_code_golomb in the chained mode), ffv1_assemble_packets, and in
  * frame-parallel mode the decision layout (ffv1_layout) and decision bits
- * (ffv1_bits).  Frame-parallel mode launches each once per call; the chained
+ * (ffv1_bits) and the coder's byte writer (ffv1_sink).  Frame-parallel mode launches each once per call; the chained
  * mode launches symbols and code once per frame index of the GOP. */
 typedef struct ffv1hip_kernel_stats {
     float symbols_ms, code_ms, assemble_ms;
@@ -147,6 +147,8 @@ typedef struct ffv1hip_kernel_stats {
     int states_launches;
     float layout_ms, bits_ms;              /* frame-parallel mode */
     int layout_launches, bits_launches;
+    float sink_ms;                         /* frame-parallel mode: the coder's byte writer (ffv1_sink) */
+    int sink_launches;
 } ffv1hip_kernel_stats;
 int ffv1hip_last_kernel_stats(ffv1hip_ctx *ctx, ffv1hip_kernel_stats *out);
 
