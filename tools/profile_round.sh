@@ -10,7 +10,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/prof_$TAG
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-BENCH="$R/bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+BENCH="$R/bench.py --warmup 1 --no-cpu-baseline"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 $BENCH > $O/kt.log 2>&1 || exit 1
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o fetch --output-format csv -- python3 $BENCH > $O/fetch.log 2>&1 || exit 2
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $O/write -o write --output-format csv -- python3 $BENCH > $O/write.log 2>&1 || exit 3
