@@ -111,7 +111,7 @@ def load_traffic(frames_per_step):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)  # the two pipelines fill and drain once per run
+    ap.add_argument("--steps", type=int, default=20)  # the pipelines fill and drain once per run
     ap.add_argument("--warmup", type=int, default=1)
     # 21 GOPs = 252 frames per batch: 252 coder waves (one per frame of each
     # slice) fit the CUs beside the states walk of the next batch
