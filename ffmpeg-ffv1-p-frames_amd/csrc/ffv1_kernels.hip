@@ -765,9 +765,17 @@ __device__ __forceinline__ void flush_if_t(Lane& L, SinkT& S, int above, FlushTi
   }
 }
 
-template <bool TAIL, class SinkT>
+// the first rem state bytes of a 16-byte block (rem may be <= 0 or >= 16)
+__device__ __forceinline__ uint32_t tail_word(uint32_t w, int rem) {
+  return rem >= 4 ? w : rem <= 0 ? 0u : (w & ((1u << (8 * rem)) - 1u));
+}
+__device__ __forceinline__ uint4 tail_mask(const uint4& v, int rem) {
+  return make_uint4(tail_word(v.x, rem), tail_word(v.y, rem - 4), tail_word(v.z, rem - 8), tail_word(v.w, rem - 12));
+}
+
+template <class SinkT>
 __device__ __forceinline__ void decide32(Lane& L, SinkT& S, const uint4& wa, const uint4& wb, uint32_t bw,
-                                         int rem, FlushTimer& tf) {
+                                         FlushTimer& tf) {
   static_for<0, 32>([&](auto jc) {
     constexpr int J = decltype(jc)::value;
     constexpr int SH = (J & 3) * 8;
@@ -788,11 +796,6 @@ __device__ __forceinline__ void decide32(Lane& L, SinkT& S, const uint4& wa, con
     int nl = L.low + (d & m);
     int nr;  // m ? r1 : d, one v_bfi (the compiler would make it a compare and two selects)
     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(nr) : "v"(m), "v"(r1), "v"(d));
-    if constexpr (TAIL) {
-      const bool act = J < rem;
-      nl = act ? nl : L.low;
-      nr = act ? nr : L.range;
-    }
     L.low = nl;
     L.range = nr;
     renorm(L);
@@ -859,8 +862,8 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_dcode(CodeArgs a) {
       mw = B[1];
     }
     for (int i = 0; i < nmax; i += 32) {
-      const uint4 wa = na, wb = nb;
-      const uint32_t bw = nw;
+      uint4 wa = na, wb = nb;
+      uint32_t bw = nw;
       na = ma;
       nb = mb;
       nw = mw;
@@ -869,10 +872,17 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_dcode(CodeArgs a) {
         mb = P[(i >> 4) + 5];
         mw = B[(i >> 5) + 2];
       }
-      if (i + 32 <= n)
-        decide32<false>(L, S, wa, wb, bw, 32, tf);
-      else if (i < n)
-        decide32<true>(L, S, wa, wb, bw, n - i, tf);
+      // the tail: a state-0 decision of bit 0 leaves low and range as they
+      // are (r1 = 0, range - r1 = range), so the bytes past the end are
+      // zeroed and the same code runs (one copy of it: the I-cache is shared
+      // with the walker on the CU)
+      const int rem = n - i;
+      if (rem < 32) {
+        wa = tail_mask(wa, rem);
+        wb = tail_mask(wb, rem - 16);
+        bw = rem > 0 ? bw & ((1u << rem) - 1u) : 0u;
+      }
+      decide32(L, S, wa, wb, bw, tf);
       flush_if_t(L, S, kDFlushAt, tf);  // <= 16 digits per half block
     }
     ndec += nmax;
