@@ -51,8 +51,12 @@ __device__ __forceinline__ int fold_bits(int d, int bits) {
 
 // ---------------------------------------------------------------------------
 // Kernel 1: symbols.
-constexpr int kSymThreads = 64;  // one wave per block: a wave slowed by a busy SIMD holds back no other
-constexpr int kSymSplit = 24;  // blocks per slice plane: the per-block loop is latency-bound
+#ifndef FFV1_SYM_THREADS
+#define FFV1_SYM_THREADS 64
+#define FFV1_SYM_SPLIT 24
+#endif
+constexpr int kSymThreads = FFV1_SYM_THREADS;  // one wave per block: a wave slowed by a busy SIMD holds back no other
+constexpr int kSymSplit = FFV1_SYM_SPLIT;  // blocks per slice plane: the per-block loop is latency-bound
 
 // Range-coder decisions of one residual: put_symbol_inline (ffv1enc.c:185-231)
 // codes a zero flag, e+1 exponent decisions, e mantissa bits and a sign.
@@ -112,6 +116,7 @@ __device__ __forceinline__ int wave_incl_scan(int x, int /*lane*/) {
 // the previous lane's value (lane 0: 0), a DPP wave_shr:1
 __device__ __forceinline__ int wave_prev(int x) { return __builtin_amdgcn_update_dpp(0, x, 0x138, 0xf, 0xf, true); }
 
+template <int SB>  // stored sample bytes, 1 or 2
 __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   __shared__ int16_t qt[5 * 256];
   __shared__ int red[kSymThreads / kWave];
@@ -130,12 +135,14 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   uint32_t* out = a.sym + (int64_t)slot * a.frame_samples + g.sym_off + g.plane_sym_off[p];
   const int row0 = p ? a.contexts : 0;  // plane context 1 rows follow plane 0's
 
-  auto load = [&](int x, int y) -> int {  // sample of the slice plane, as int16 (ffv1enc.c:390-407)
+  // sample of the slice plane as int16 (ffv1enc.c:390-407), at in-plane
+  // coordinates: every load is unconditional, so the loads of a step are
+  // issued back to back and waited for once
+  const int sh = a.packed_at_lsb ? 0 : a.msb_shift;
+  auto load = [&](int x, int y) -> int {
     const uint8_t* r = base + (int64_t)(py + y) * stride;
-    if (a.sample_bytes == 1) return r[px + x];
-    unsigned v = reinterpret_cast<const uint16_t*>(r)[px + x];
-    if (!a.packed_at_lsb) v >>= a.msb_shift;
-    return (int16_t)v;
+    if constexpr (SB == 1) return r[px + x];
+    else return (int16_t)(reinterpret_cast<const uint16_t*>(r)[px + x] >> sh);
   };
 
   int ndec = 0;
@@ -144,24 +151,43 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   const int64_t b0 = part * span, b1 = min(n, b0 + span);
   const int lane = threadIdx.x & (kWave - 1);
   uint4* const rec = a.rec ? a.rec + (int64_t)slot * a.frame_samples + g.sym_off + g.plane_sym_off[p] : nullptr;
+  // the plane's chunk headers (read once: a reload inside the loop would
+  // wait for the record stores)
+  uint32_t* const cbase = rec ? a.cbits + ((int64_t)slot * a.frame_chunks + g.chunk_off[p]) * kChunkWords : nullptr;
+  // the lane's sample, stepped along the plane without a division per step
+  int cy = (int)((b0 + threadIdx.x) / pw), cx = (int)((b0 + threadIdx.x) - (int64_t)cy * pw);
   // whole waves per step: a wave's 64 consecutive samples are one walk chunk
   for (int64_t base = b0; base < b1; base += kSymThreads) {
     const int64_t idx = base + threadIdx.x;
     const bool valid = idx < n;
-    const int y = valid ? (int)(idx / pw) : 0, x = valid ? (int)(idx - (int64_t)y * pw) : 0;
+    const int y = valid ? cy : 0, x = valid ? cx : 0;
+    cx += kSymThreads;
+    while (cx >= pw) {
+      cx -= pw;
+      cy++;
+    }
     // neighbourhood as the zeroed two/three-row ring exposes it:
     // rows above the slice read 0; L(x=0) = T; LT(x=0) = sample two rows up
     // in column 0; RT past the right edge = T; LL(x=0) = 0, LL(x=1) = T(0).
+    const int ym1 = y ? y - 1 : 0, ym2 = y >= 2 ? y - 2 : 0;
+    const int xm1 = x ? x - 1 : 0, xp1 = x + 1 < pw ? x + 1 : x;
     const int X = load(x, y);
-    const int T = y ? load(x, y - 1) : 0;
-    const int T0 = y ? load(0, y - 1) : 0;
-    const int L = x ? load(x - 1, y) : T0;
-    const int LT = x ? (y ? load(x - 1, y - 1) : 0) : (y >= 2 ? load(0, y - 2) : 0);
-    const int RT = x + 1 < pw ? (y ? load(x + 1, y - 1) : 0) : T;
+    const int rT = load(x, ym1), rT0 = load(0, ym1), rL = load(xm1, y);
+    const int rLT = load(xm1, ym1), rLT0 = load(0, ym2), rRT = load(xp1, ym1);
+    int rLL = 0, rTT = 0;
+    if (a.model1) {
+      rLL = load(x >= 2 ? x - 2 : 0, y);
+      rTT = load(x, ym2);
+    }
+    const int T = y ? rT : 0;
+    const int T0 = y ? rT0 : 0;
+    const int L = x ? rL : T0;
+    const int LT = x ? (y ? rLT : 0) : (y >= 2 ? rLT0 : 0);
+    const int RT = x + 1 < pw ? (y ? rRT : 0) : T;
     int ctx = qt[(L - LT) & 0xFF] + qt[256 + ((LT - T) & 0xFF)] + qt[512 + ((T - RT) & 0xFF)];
     if (a.model1) {
-      const int LL = x >= 2 ? load(x - 2, y) : (x == 1 ? T0 : 0);
-      const int TT = y >= 2 ? load(x, y - 2) : 0;
+      const int LL = x >= 2 ? rLL : (x == 1 ? T0 : 0);
+      const int TT = y >= 2 ? rTT : 0;
       ctx += qt[768 + ((LL - L) & 0xFF)] + qt[1024 + ((TT - T) & 0xFF)];
     }
     int diff = X - median3(L, L + T - LT, T);
@@ -199,8 +225,7 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
         const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
         const bool lng = __ballot(valid && (diff >= 1024 || diff <= -1024)) != 0;
         if (lane == 0) cs[0] = (uint32_t)total | (lng ? kChunkLong : 0u);
-        uint32_t* const dst = a.cbits + ((int64_t)slot * a.frame_chunks + g.chunk_off[p] + (base + wv * kWave) / kWave) *
-                                            kChunkWords;
+        uint32_t* const dst = cbase + ((base + wv * kWave) / kWave) * kChunkWords;
         dst[lane] = cs[lane];
         if (lane < kChunkWords - kWave) dst[kWave + lane] = cs[kWave + lane];
       }
@@ -1684,7 +1709,10 @@ __global__ __launch_bounds__(kAsmThreads) void ffv1_assemble_packets(AssembleArg
 
 int launch_symbols(const SymbolArgs& a, void* stream) {
   dim3 grid(a.nslices, a.nslots, a.nplanes * kSymSplit), block(kSymThreads);
-  hipLaunchKernelGGL(ffv1_symbols, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
+  if (a.sample_bytes == 1)
+    hipLaunchKernelGGL(ffv1_symbols<1>, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
+  else
+    hipLaunchKernelGGL(ffv1_symbols<2>, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
