@@ -830,7 +830,9 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     ba.nframes = n;
     ba.ds = ds;
     // the bits run beside the walk, on their own stream; the coder waits for both
-    hipStream_t const bst = serial ? st : c->bits_stream;
+    // FFV1HIP_BITS_INLINE=1 (measurement hook): the bits kernel before the walk, on its stream
+    static const bool bits_inline = std::getenv("FFV1HIP_BITS_INLINE") && std::atoi(std::getenv("FFV1HIP_BITS_INLINE"));
+    hipStream_t const bst = serial || bits_inline ? st : c->bits_stream;
     HIP_TRY(hipEventRecord(c->laid[fb], st));
     HIP_TRY(hipStreamWaitEvent(bst, c->laid[fb], 0));
     if (timed(5, bst, [&] { return launch_bits(ba, bst); }) < 0)

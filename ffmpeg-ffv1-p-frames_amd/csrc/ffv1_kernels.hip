@@ -1194,6 +1194,10 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   // the walk is the longer of the two pipelines it overlaps with (the coder
   // of the previous batch): it wins the VALU arbitration on a shared SIMD
   __builtin_amdgcn_s_setprio(2);
+#ifdef FFV1_WALK_FAT
+  // the whole register file of a SIMD: no other wave shares this one's SIMD
+  asm volatile("" ::: "v255", "a255");
+#endif
   uint64_t t_loop = 0, n_steps = 0;
   const uint64_t t_all = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
   for (int j = 0; j < seg.nframes; j++) {
@@ -1689,10 +1693,27 @@ __global__ __launch_bounds__(kAsmThreads) void ffv1_assemble_packets(AssembleArg
   for (int64_t i = t; i < body; i += kAsmThreads) dst[i] = (uint8_t)body_byte(i);
 
   if (a.ec) {
-    const int64_t chunk = (body + kAsmThreads - 1) / kAsmThreads;
+    // a thread's run of the body: whole 16-byte blocks of the slice bytes
+    // (slots are 256-aligned) read as vectors, then the few trailing bytes
+    const int64_t chunk = ((body + kAsmThreads - 1) / kAsmThreads + 15) & ~(int64_t)15;
     const int64_t b0 = min((int64_t)t * chunk, body), b1 = min(b0 + chunk, body);
     uint32_t crc = 0;
-    for (int64_t i = b0; i < b1; i++) crc = (crc << 8) ^ crc_tab[(crc >> 24) ^ body_byte(i)];
+    auto crc_word = [&](uint32_t w) {
+      crc = (crc << 8) ^ crc_tab[(crc >> 24) ^ (w & 0xFFu)];
+      crc = (crc << 8) ^ crc_tab[(crc >> 24) ^ ((w >> 8) & 0xFFu)];
+      crc = (crc << 8) ^ crc_tab[(crc >> 24) ^ ((w >> 16) & 0xFFu)];
+      crc = (crc << 8) ^ crc_tab[(crc >> 24) ^ (w >> 24)];
+    };
+    int64_t i = b0;
+    const int64_t vend = min(b1, n);
+    for (; i + 16 <= vend; i += 16) {
+      const uint4 v = *reinterpret_cast<const uint4*>(src + i);
+      crc_word(v.x);
+      crc_word(v.y);
+      crc_word(v.z);
+      crc_word(v.w);
+    }
+    for (; i < b1; i++) crc = (crc << 8) ^ crc_tab[(crc >> 24) ^ body_byte(i)];
     __syncthreads();
     crc_part[t] = (b1 > b0) ? gf2_mulmod(crc, xpow8(body - b1, pw)) : 0u;
     __syncthreads();
