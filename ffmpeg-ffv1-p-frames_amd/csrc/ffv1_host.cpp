@@ -1106,3 +1106,263 @@ int ffv1hip_set_slice_states(ffv1hip_ctx* c, const uint8_t* buf, int64_t size) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Decoder: the FFV1 decoder's AVCodec callbacks (ffv1dec.c decode_init :1007,
+// decode_frame :896-1005, decode_end) for the streams this library encodes
+// (version 3, range coder, context model 0).  Host work is the reference
+// decoder's own host work: the key bit and the slice chain read backwards
+// from the packet end (ffv1dec.c:931-989); the slices decode on the GPU.
+struct ffv1hip_dec {
+  ffv1hip_params P{};
+  int device = 0;
+  int nslices = 0;
+  int contexts = 0;
+  int64_t state_bytes = 0;
+  int64_t frame_bytes = 0;
+  int64_t plane_off[3]{};
+  int plane_w[3]{};
+  int row_cap = 0;
+  bool have_states = false;
+  std::vector<SliceGeom> geom;
+  uint8_t* d_persist = nullptr;
+  SliceGeom* d_geom = nullptr;
+  int16_t* d_qt = nullptr;
+  uint8_t* d_ftab = nullptr;
+  int* d_status = nullptr;
+  hipStream_t stream = nullptr;
+};
+
+static void dec_free(ffv1hip_dec* d) {
+  (void)hipFree(d->d_persist);
+  (void)hipFree(d->d_geom);
+  (void)hipFree(d->d_qt);
+  (void)hipFree(d->d_ftab);
+  (void)hipFree(d->d_status);
+  if (d->stream) (void)hipStreamDestroy(d->stream);
+}
+
+extern "C" {
+
+ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* extradata, int extradata_size,
+                                int device, int* err) {
+  auto fail = [&](int code) -> ffv1hip_dec* {
+    if (err) *err = code;
+    return nullptr;
+  };
+  if (!params) return fail(set_err(-22, "invalid arguments"));
+  const ffv1hip_params& p = *params;
+  if (p.version != 3 || p.ac == 0 || p.context_model != 0 || p.num_h_slices * p.num_v_slices > 256 ||
+      p.bits_per_raw_sample < 8 || p.bits_per_raw_sample > 16 || p.width <= 0 || p.height <= 0 ||
+      p.num_h_slices <= 0 || p.num_v_slices <= 0)
+    return fail(set_err(-38, "GPU decoder: version 3, range coder, context model 0 only"));
+  // The stream's extradata must be the one these parameters produce
+  // (read_extradata, ffv1dec.c:509-631, would derive the same parameters).
+  ffv1hip_ctx tmp;
+  tmp.P = p;
+  tmp.contexts = contexts_of(p.context_model);
+  tmp.dflt = default_tables();
+  tmp.frame = p.ac == 2 ? custom_tables(tmp.dflt) : tmp.dflt;
+  quant_set(tmp.qt, p.context_model, p.bits_per_raw_sample);
+  build_extradata(&tmp);
+  if (!extradata || extradata_size != int(tmp.extradata.size()) ||
+      std::memcmp(extradata, tmp.extradata.data(), tmp.extradata.size()) != 0)
+    return fail(set_err(FFV1HIP_AVERROR_INVALIDDATA, "extradata does not match the parameters"));
+  ffv1hip_dec* d = new ffv1hip_dec();
+  d->P = p;
+  d->device = device;
+  d->nslices = p.num_h_slices * p.num_v_slices;
+  d->contexts = tmp.contexts;
+  d->state_bytes = int64_t(2) * d->contexts * 32;
+  const int cw = p.chroma_planes ? -((-p.width) >> p.chroma_h_shift) : 0;
+  const int ch = p.chroma_planes ? -((-p.height) >> p.chroma_v_shift) : 0;
+  const int64_t pb0 = int64_t(p.width) * p.height * p.sample_bytes, pb1 = int64_t(cw) * ch * p.sample_bytes;
+  d->plane_off[0] = 0;
+  d->plane_off[1] = pb0;
+  d->plane_off[2] = pb0 + pb1;
+  d->plane_w[0] = p.width;
+  d->plane_w[1] = d->plane_w[2] = cw;
+  d->frame_bytes = (pb0 + 2 * pb1 + 255) & ~int64_t(255);
+  d->geom.resize(d->nslices);
+  for (int s = 0; s < d->nslices; s++) {  // ffv1.c:117-145, ffv1dec.c:361-474
+    SliceGeom& g = d->geom[s];
+    std::memset(&g, 0, sizeof(g));
+    const int sx = s % p.num_h_slices, sy = s / p.num_h_slices;
+    const int x0 = int(int64_t(p.width) * sx / p.num_h_slices);
+    const int y0 = int(int64_t(p.height) * sy / p.num_v_slices);
+    g.px[0] = x0;
+    g.py[0] = y0;
+    g.pw[0] = int(int64_t(p.width) * (sx + 1) / p.num_h_slices) - x0;
+    g.ph[0] = int(int64_t(p.height) * (sy + 1) / p.num_v_slices) - y0;
+    for (int k = 1; k < 3; k++) {
+      g.pw[k] = p.chroma_planes ? -((-g.pw[0]) >> p.chroma_h_shift) : 0;
+      g.ph[k] = p.chroma_planes ? -((-g.ph[0]) >> p.chroma_v_shift) : 0;
+      g.px[k] = x0 >> p.chroma_h_shift;
+      g.py[k] = y0 >> p.chroma_v_shift;
+    }
+    d->row_cap = std::max(d->row_cap, g.pw[0]);
+  }
+  d->row_cap = (d->row_cap + 7) & ~7;
+  if (decode_lds_bytes(d->state_bytes, d->row_cap) > 64 * 1024) {
+    delete d;
+    return fail(set_err(-38, "GPU decoder: slice too wide for the LDS row buffer"));
+  }
+  auto init = [&]() -> int {
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    HIP_TRY(hipMalloc(&d->d_persist, d->state_bytes * d->nslices));
+    HIP_TRY(hipMalloc(&d->d_geom, sizeof(SliceGeom) * d->nslices));
+    HIP_TRY(hipMalloc(&d->d_qt, sizeof(int16_t) * 3 * 256));
+    HIP_TRY(hipMalloc(&d->d_ftab, 512));
+    HIP_TRY(hipMalloc(&d->d_status, sizeof(int) * 4));
+    HIP_TRY(hipMemcpy(d->d_geom, d->geom.data(), sizeof(SliceGeom) * d->nslices, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d->d_qt, tmp.qt, sizeof(int16_t) * 3 * 256, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d->d_ftab, tmp.frame.to0, 256, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d->d_ftab + 256, tmp.frame.to1, 256, hipMemcpyHostToDevice));
+    return 0;
+  };
+  int rc = init();
+  if (rc < 0) {
+    dec_free(d);
+    delete d;
+    return fail(rc);
+  }
+  if (err) *err = 0;
+  return d;
+}
+
+void ffv1hip_dec_destroy(ffv1hip_dec* d) {
+  if (!d) return;
+  (void)hipSetDevice(d->device);
+  dec_free(d);
+  delete d;
+}
+
+int ffv1hip_decode(ffv1hip_dec* d, const uint8_t* packets, const int64_t* sizes, int n_frames,
+                   void* const* planes, const int* strides, int* key_flags) {
+  if (!d || !packets || !sizes || n_frames < 0 || (n_frames && (!planes || !strides)))
+    return set_err(-22, "null argument");
+  if (n_frames == 0) return 0;
+  const ffv1hip_params& p = d->P;
+  const int ns = d->nslices;
+  const int trailer = 3 + (p.ec ? 5 : 0);
+  std::vector<uint8_t> keys(n_frames);
+  std::vector<int64_t> starts(size_t(n_frames) * ns), ends(size_t(n_frames) * ns);
+  int64_t total = 0;
+  for (int f = 0; f < n_frames; f++) {
+    const uint8_t* pk = packets + total;
+    const int64_t size = sizes[f];
+    if (size < 2) return set_err(FFV1HIP_AVERROR_INVALIDDATA, "frame %d: packet too small", f);
+    // key bit: the first decision with state 128 from range 0xFF00 (ffv1dec.c:931)
+    keys[f] = ((pk[0] << 8) | pk[1]) >= 0x7F80;
+    // the slice chain, from the packet end (ffv1dec.c:948-989)
+    const uint8_t* q = pk + size;
+    for (int i = ns - 1; i >= 0; i--) {
+      if (q - pk < trailer) return set_err(FFV1HIP_AVERROR_INVALIDDATA, "frame %d: slice %d trailer", f, i);
+      const int64_t v = ((int64_t(q[-trailer]) << 16) | (q[-trailer + 1] << 8) | q[-trailer + 2]) + trailer;
+      if (v > q - pk) return set_err(FFV1HIP_AVERROR_INVALIDDATA, "frame %d: slice %d size", f, i);
+      ends[size_t(f) * ns + i] = (q - packets);
+      q -= v;
+      starts[size_t(f) * ns + i] = (q - packets);
+      if (p.ec && crc32_msb(q, size_t(v)) != 0)
+        return set_err(FFV1HIP_AVERROR_INVALIDDATA, "frame %d: slice %d CRC mismatch", f, i);
+    }
+    if (q != pk) return set_err(FFV1HIP_AVERROR_INVALIDDATA, "frame %d: %d slices do not span the packet", f, ns);
+    total += size;
+  }
+  if (!keys[0] && !d->have_states)
+    return set_err(FFV1HIP_AVERROR_INVALIDDATA, "stream does not start with a keyframe");
+  std::vector<Segment> segs;
+  for (int f = 0; f < n_frames; f++) {
+    if (f == 0 || keys[f]) segs.push_back(Segment{f, 0, f == 0 && !keys[0], 0});
+    segs.back().nframes++;
+  }
+  segs.back().save_states = 1;
+  HIP_TRY(hipSetDevice(d->device));
+  uint8_t* d_pk = nullptr;
+  int64_t* d_se = nullptr;
+  uint8_t* d_keys = nullptr;
+  Segment* d_segs = nullptr;
+  uint8_t* d_out = nullptr;
+  auto run = [&]() -> int {
+    const size_t nse = size_t(n_frames) * ns;
+    HIP_TRY(hipMalloc(&d_pk, size_t(total) + 64));
+    HIP_TRY(hipMalloc(&d_se, 2 * nse * sizeof(int64_t)));
+    HIP_TRY(hipMalloc(&d_keys, size_t(n_frames)));
+    HIP_TRY(hipMalloc(&d_segs, segs.size() * sizeof(Segment)));
+    HIP_TRY(hipMalloc(&d_out, size_t(d->frame_bytes) * n_frames));
+    HIP_TRY(hipMemsetAsync(d_pk + total, 0, 64, d->stream));
+    // samples no slice codes (odd chroma offsets, ffv1enc.c:1186-1188) read as 0
+    HIP_TRY(hipMemsetAsync(d_out, 0, size_t(d->frame_bytes) * n_frames, d->stream));
+    HIP_TRY(hipMemcpyAsync(d_pk, packets, size_t(total), hipMemcpyHostToDevice, d->stream));
+    HIP_TRY(hipMemcpyAsync(d_se, starts.data(), nse * sizeof(int64_t), hipMemcpyHostToDevice, d->stream));
+    HIP_TRY(hipMemcpyAsync(d_se + nse, ends.data(), nse * sizeof(int64_t), hipMemcpyHostToDevice, d->stream));
+    HIP_TRY(hipMemcpyAsync(d_keys, keys.data(), size_t(n_frames), hipMemcpyHostToDevice, d->stream));
+    HIP_TRY(hipMemcpyAsync(d_segs, segs.data(), segs.size() * sizeof(Segment), hipMemcpyHostToDevice, d->stream));
+    HIP_TRY(hipMemsetAsync(d->d_status, 0, sizeof(int) * 4, d->stream));
+    DecodeArgs a{};
+    a.pkts = d_pk;
+    a.slice_start = d_se;
+    a.slice_end = d_se + nse;
+    a.keyflags = d_keys;
+    a.segs = d_segs;
+    a.geom = d->d_geom;
+    a.nslices = ns;
+    a.nplanes = p.chroma_planes ? 3 : 1;
+    a.qt = d->d_qt;
+    a.ftab = d->d_ftab;
+    a.state_bytes = d->state_bytes;
+    a.persist = d->d_persist;
+    a.out = d_out;
+    a.frame_bytes = d->frame_bytes;
+    for (int k = 0; k < 3; k++) {
+      a.plane_off[k] = d->plane_off[k];
+      a.plane_w[k] = d->plane_w[k];
+    }
+    a.sample_bytes = p.sample_bytes;
+    a.packed_at_lsb = p.packed_at_lsb;
+    a.msb_shift = 16 - p.bits_per_raw_sample;
+    a.coded_bits = p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample;
+    a.width = p.width;
+    a.height = p.height;
+    a.num_h = p.num_h_slices;
+    a.num_v = p.num_v_slices;
+    a.context_model = p.context_model;
+    a.row_cap = d->row_cap;
+    a.status = d->d_status;
+    if (launch_decode(a, int(segs.size()), d->stream) < 0)
+      return set_err(-5, "ffv1_decode_slices launch failed: %s", hipGetErrorString(hipGetLastError()));
+    int status = 0;
+    HIP_TRY(hipMemcpyAsync(&status, d->d_status, sizeof(int), hipMemcpyDeviceToHost, d->stream));
+    HIP_TRY(hipStreamSynchronize(d->stream));
+    if (status) return set_err(FFV1HIP_AVERROR_INVALIDDATA, "%d slice(s) with a bad key bit or slice header", status);
+    const int np = p.chroma_planes ? 3 : 1;
+    for (int f = 0; f < n_frames; f++)
+      for (int k = 0; k < np; k++) {
+        const int rows = k ? -((-p.height) >> p.chroma_v_shift) : p.height;
+        const int wb = d->plane_w[k] * p.sample_bytes;
+        HIP_TRY(hipMemcpy2DAsync(planes[3 * f + k], strides[3 * f + k],
+                                 d_out + int64_t(f) * d->frame_bytes + d->plane_off[k], wb, wb, rows,
+                                 hipMemcpyDeviceToHost, d->stream));
+      }
+    HIP_TRY(hipStreamSynchronize(d->stream));
+    return 0;
+  };
+  int rc = run();
+  (void)hipFree(d_pk);
+  (void)hipFree(d_se);
+  (void)hipFree(d_keys);
+  (void)hipFree(d_segs);
+  (void)hipFree(d_out);
+  if (rc < 0) return rc;
+  d->have_states = true;
+  if (key_flags)
+    for (int f = 0; f < n_frames; f++) key_flags[f] = keys[f];
+  return 0;
+}
+
+void ffv1hip_dec_reset(ffv1hip_dec* d) {
+  if (d) d->have_states = false;
+}
+
+}  // extern "C"

@@ -180,6 +180,32 @@ struct AssembleArgs {
   int ec;
 };
 
+// Decoder (ffv1_decode.hip): one workgroup per (segment, slice) chain of a
+// batch of packets, range coder, context model 0, version 3.
+struct DecodeArgs {
+  const uint8_t* pkts;         // packets back to back, 8-byte aligned, >= 64 bytes of pad
+  const int64_t* slice_start;  // [frame][slice] byte offset of the slice in pkts
+  const int64_t* slice_end;    // [frame][slice] end of the slice's bytes (trailer included)
+  const uint8_t* keyflags;     // [frame]
+  const Segment* segs;
+  const SliceGeom* geom;
+  int nslices, nplanes;
+  const int16_t* qt;           // [3][256]
+  const uint8_t* ftab;         // frame transition table: to0[256] | to1[256]
+  int64_t state_bytes;         // 2 * contexts * 32
+  uint8_t* persist;            // [slice][state_bytes]: the chain carried across calls
+  uint8_t* out;                // [frame] regions of frame_bytes, planes tightly packed
+  int64_t frame_bytes;
+  int64_t plane_off[3];
+  int plane_w[3];
+  int sample_bytes, packed_at_lsb, msb_shift, coded_bits;
+  int width, height, num_h, num_v, context_model;
+  int row_cap;                 // widest slice plane (samples)
+  int* status;                 // [0] slices whose key bit or header disagrees
+};
+int launch_decode(const DecodeArgs& a, int nsegs, void* stream);
+int64_t decode_lds_bytes(int64_t state_bytes, int row_cap);
+
 int launch_symbols(const SymbolArgs& a, void* stream);
 int launch_code(const CodeArgs& a, void* stream);
 int launch_layout(const int* dcount, int nstreams, int64_t* dbase, int64_t* total, void* stream);

@@ -6,7 +6,9 @@ assembly) runs as HIP kernels in ``lib/libffv1hip.so``; this package is the
 host mirror of the reference's AVCodec interface over that C-ABI.
 """
 from .encoder import (AVCodecContext, AVPacket, FFV1Encoder, FFV1Error, HipEncoder, Options,
-                      Params, configure, load_library, EXPORTED_SYMBOLS, AVERROR_INVALIDDATA)
+                      Params, configure, load_library, EXPORTED_SYMBOLS, AVERROR_INVALIDDATA,
+                      HipDecoder)
 
 __all__ = ["AVCodecContext", "AVPacket", "FFV1Encoder", "FFV1Error", "HipEncoder", "Options",
-           "Params", "configure", "load_library", "EXPORTED_SYMBOLS", "AVERROR_INVALIDDATA"]
+           "Params", "configure", "load_library", "EXPORTED_SYMBOLS", "AVERROR_INVALIDDATA",
+           "HipDecoder"]

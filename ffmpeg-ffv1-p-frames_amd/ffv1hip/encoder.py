@@ -59,6 +59,7 @@ EXPORTED_SYMBOLS = (
     "ffv1hip_get_slice_states", "ffv1hip_set_slice_states", "ffv1hip_last_error",
     "ffv1hip_abi_version", "ffv1hip_set_profiling", "ffv1hip_last_kernel_ms",
     "ffv1hip_last_kernel_stats", "ffv1hip_synchronize",
+    "ffv1hip_dec_create", "ffv1hip_dec_destroy", "ffv1hip_decode", "ffv1hip_dec_reset",
 )
 
 
@@ -122,6 +123,14 @@ def load_library():
     L.ffv1hip_last_kernel_ms.restype = ctypes.c_int
     L.ffv1hip_last_kernel_stats.argtypes = [vp, P(KernelStats)]
     L.ffv1hip_last_kernel_stats.restype = ctypes.c_int
+    L.ffv1hip_dec_create.argtypes = [P(Params), u8p, ctypes.c_int, ctypes.c_int, P(ctypes.c_int)]
+    L.ffv1hip_dec_create.restype = vp
+    L.ffv1hip_dec_destroy.argtypes = [vp]
+    L.ffv1hip_dec_destroy.restype = None
+    L.ffv1hip_decode.argtypes = [vp, u8p, P(i64), ctypes.c_int, P(vp), P(ctypes.c_int), P(ctypes.c_int)]
+    L.ffv1hip_decode.restype = ctypes.c_int
+    L.ffv1hip_dec_reset.argtypes = [vp]
+    L.ffv1hip_dec_reset.restype = None
     L.ffv1hip_abi_version.argtypes = []
     L.ffv1hip_abi_version.restype = ctypes.c_int
     _lib = L
@@ -374,3 +383,54 @@ class FFV1Encoder:
             self._enc.close()
             self._enc = None
         return 0
+
+
+class HipDecoder:
+    """Owner of one ``ffv1hip_dec``: ff_ffv1_decoder's decode_frame on the GPU
+    (ffv1dec.c:896-1005) for version-3 range-coded streams, context model 0.
+    Context states carry across :meth:`decode` calls like the encoder's."""
+
+    def __init__(self, params: Params, extradata: bytes, device: int = 0):
+        L = load_library()
+        self.params = params
+        err = ctypes.c_int(0)
+        ex = np.frombuffer(bytes(extradata) or b"\0", np.uint8).copy()
+        self._h = L.ffv1hip_dec_create(ctypes.byref(params), _u8p(ex), len(extradata), device,
+                                       ctypes.byref(err))
+        if not self._h:
+            raise FFV1Error(err.value, "ffv1hip_dec_create")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().ffv1hip_dec_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def reset(self):
+        load_library().ffv1hip_dec_reset(self._h)
+
+    def decode(self, packets: Sequence[bytes]) -> List[Tuple[List[np.ndarray], bool]]:
+        """Decode packets in order; returns (planes, key) per frame, planes as
+        2-D uint8/uint16 arrays in the encoder's input layout."""
+        L = load_library()
+        n = len(packets)
+        if n == 0:
+            return []
+        buf = np.frombuffer(b"".join(packets), np.uint8).copy()
+        sizes = (ctypes.c_int64 * n)(*[len(pk) for pk in packets])
+        dt = np.uint8 if self.params.sample_bytes == 1 else np.uint16
+        shapes = self.params.plane_shapes()
+        frames = [[np.zeros(shp, dt) for shp in shapes] for _ in range(n)]
+        ptrs = (ctypes.c_void_p * (3 * n))()
+        strides = (ctypes.c_int * (3 * n))()
+        for i, fr in enumerate(frames):
+            for k in range(3):
+                a = fr[min(k, len(fr) - 1)]
+                ptrs[3 * i + k] = a.ctypes.data
+                strides[3 * i + k] = a.strides[0]
+        keys = (ctypes.c_int * n)()
+        rc = L.ffv1hip_decode(self._h, _u8p(buf), sizes, n, ptrs, strides, keys)
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_decode")
+        return [(frames[i], bool(keys[i])) for i in range(n)]

@@ -152,6 +152,30 @@ typedef struct ffv1hip_kernel_stats {
 } ffv1hip_kernel_stats;
 int ffv1hip_last_kernel_stats(ffv1hip_ctx *ctx, ffv1hip_kernel_stats *out);
 
+/* Decoder: the AVCodec callbacks of ff_ffv1_decoder (ffv1dec.c decode_init
+ * :1007, decode_frame :896-1005, decode_end) for the streams this library
+ * encodes: version 3, range coder, context model 0 (the on-device lossless
+ * self-check).  ffv1hip_dec_create takes the stream's parameters and its
+ * extradata, which must be the one those parameters produce (what
+ * read_extradata, ffv1dec.c:509-631, would parse); otherwise
+ * FFV1HIP_AVERROR_INVALIDDATA.  Unsupported parameters give -ENOSYS. */
+typedef struct ffv1hip_dec ffv1hip_dec;
+ffv1hip_dec *ffv1hip_dec_create(const ffv1hip_params *params,
+                                const uint8_t *extradata, int extradata_size,
+                                int device, int *err);
+void ffv1hip_dec_destroy(ffv1hip_dec *dec);
+/* decode_frame over a batch: packets back to back in HOST memory (sizes[i]
+ * bytes each); plane p of frame i goes to planes[3*i + p] with row stride
+ * strides[3*i + p] (the encoder's input layout).  The key bit and the slice
+ * chain (3-byte sizes, CRC-32 when ec) are checked on the host as in
+ * ffv1dec.c:931-989; every (GOP segment, slice) chain decodes on the GPU.
+ * Context states carry across calls like the encoder's.  key_flags may be
+ * NULL. */
+int ffv1hip_decode(ffv1hip_dec *dec, const uint8_t *packets,
+                   const int64_t *sizes, int n_frames, void *const *planes,
+                   const int *strides, int *key_flags);
+/* Forget the carried states: the next frame must be a keyframe. */
+void ffv1hip_dec_reset(ffv1hip_dec *dec);
 /* Last error message (thread-local) and the ABI version. */
 const char *ffv1hip_last_error(void);
 int ffv1hip_abi_version(void);
