@@ -119,6 +119,8 @@ def main():
     ap.add_argument("--data", choices=("d1", "d2"), default="d1")
     ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-decode-check", action="store_true",
+                    help="skip decoding the last step's packets with the GPU decoder")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -192,6 +194,24 @@ def main():
             h.update(p)
         bitexact = h.hexdigest() == PIN_MD5_24
 
+    # on-device lossless self-check (outside the timed region): the GPU
+    # decoder (ffv1_decode_slices) decodes the last step's packets
+    decode = None
+    if not args.no_decode_check:
+        from ffv1hip import HipDecoder
+        dec = HipDecoder(params, enc.extradata(), local_rank)
+        td = time.perf_counter()
+        got = dec.decode([p for p, _ in pkts])
+        td = time.perf_counter() - td
+        dec.close()
+        lossless = all(k == key and all(np.array_equal(a, b) for a, b in zip(planes, f))
+                       for (planes, k), (_, key), f in zip(got, pkts, frames))
+        del got
+        decode = {"frames": B, "lossless": lossless, "seconds": round(td, 3),
+                  "mpix_s": round(B * W * H / td / 1e6, 2),
+                  "note": "ffv1hip_decode incl. H2D of the packets and D2H of the frames"}
+        log(f"[rank {rank}] GPU decode self-check: {B} frames in {td:.2f}s, lossless={lossless}")
+
     tot = stats[0]
     names = ("symbols", "layout", "bits", "states", "code", "sink", "assemble")
     per_step = {k: tot[k + "_ms"] / args.steps for k in names}
@@ -252,6 +272,7 @@ def main():
                 "avg_launch_ms": round(code_ms_per_launch, 3),
             },
             "cpu_baseline": cpu,
+            "decode_selfcheck": decode,
         }
         print(json.dumps(res), flush=True)
     if dist:

@@ -52,37 +52,33 @@ __device__ inline void rac_refill(RacDec& c, const uint64_t* w) {
   c.ptr++;
 }
 
-// get_rac (rangecoder.h:117-147)
-__device__ inline int rac_get(RacDec& c, uint8_t* st, const uint8_t* to0, const uint8_t* to1,
-                              const uint64_t* w) {
+// get_rac (rangecoder.h:117-147), branch-free: the transition pair of the
+// state (tt[s] = to0[s] | to1[s] << 8) is read beside the range arithmetic,
+// so a decision waits on two LDS reads (state, pair) rather than three.
+__device__ inline int rac_get(RacDec& c, uint8_t* st, const uint16_t* tt, const uint64_t* w) {
   const uint32_t s = *st;
+  const uint32_t pair = tt[s];
   const uint32_t r1 = (c.range * s) >> 8;
-  c.range -= r1;
-  int bit;
-  if (c.low < c.range) {
-    *st = to0[s];
-    bit = 0;
-  } else {
-    c.low -= c.range;
-    c.range = r1;
-    *st = to1[s];
-    bit = 1;
-  }
+  const uint32_t rr = c.range - r1;
+  const int bit = c.low >= rr;
+  c.low -= bit ? rr : 0u;
+  c.range = bit ? r1 : rr;
+  *st = uint8_t(bit ? pair >> 8 : pair);
   if (c.range < 0x100) rac_refill(c, w);
   return bit;
 }
 
 // get_symbol_inline (ffv1dec.c:44-66)
-__device__ inline int rac_symbol(RacDec& c, uint8_t* st, int is_signed, const uint8_t* to0,
-                                 const uint8_t* to1, const uint64_t* w) {
-  if (rac_get(c, st, to0, to1, w)) return 0;
+__device__ inline int rac_symbol(RacDec& c, uint8_t* st, int is_signed, const uint16_t* tt,
+                                 const uint64_t* w) {
+  if (rac_get(c, st, tt, w)) return 0;
   int e = 0;
-  while (rac_get(c, st + 1 + (e < 9 ? e : 9), to0, to1, w)) {
+  while (rac_get(c, st + 1 + (e < 9 ? e : 9), tt, w)) {
     if (++e > 31) return 0;
   }
   int a = 1;
-  for (int i = e - 1; i >= 0; i--) a = 2 * a + rac_get(c, st + 22 + (i < 9 ? i : 9), to0, to1, w);
-  if (is_signed && rac_get(c, st + 11 + (e < 10 ? e : 10), to0, to1, w)) return -a;
+  for (int i = e - 1; i >= 0; i--) a = 2 * a + rac_get(c, st + 22 + (i < 9 ? i : 9), tt, w);
+  if (is_signed && rac_get(c, st + 11 + (e < 10 ? e : 10), tt, w)) return -a;
   return a;
 }
 
@@ -94,16 +90,15 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
   extern __shared__ __align__(16) uint8_t lds[];
   const int s = blockIdx.x, seg = blockIdx.y, lane = threadIdx.x;
   const Segment sg = a.segs[seg];
-  const SliceGeom g = a.geom[s];
+  const SliceGeom* g = a.geom + s;  // read through the pointer: a by-value copy indexed by plane spills
   uint8_t* states = lds;                                         // [2][contexts][32]
-  uint8_t* to0 = lds + a.state_bytes;                            // [256]
-  uint8_t* to1 = to0 + 256;                                      // [256]
-  uint8_t* hdr = to1 + 256;                                      // [32] slice-header states
+  uint16_t* tt = reinterpret_cast<uint16_t*>(lds + a.state_bytes);  // [256] to0 | to1 << 8
+  uint8_t* hdr = lds + a.state_bytes + 512;                      // [32] slice-header states
   int16_t* qt = reinterpret_cast<int16_t*>(hdr + 32);            // [3][256]
   int16_t* ring = qt + 3 * 256;                                  // [2][row_cap]
   __shared__ int bad;
   const uint64_t* pkw = reinterpret_cast<const uint64_t*>(a.pkts);
-  for (int i = lane; i < 512; i += kDecThreads) to0[i] = a.ftab[i];
+  for (int i = lane; i < 256; i += kDecThreads) tt[i] = uint16_t(a.ftab[i] | (a.ftab[256 + i] << 8));
   for (int i = lane; i < 3 * 256; i += kDecThreads) qt[i] = a.qt[i];
   if (lane == 0) bad = 0;
   const int mask = (1 << a.coded_bits) - 1;
@@ -127,22 +122,22 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
       int ok = 1;
       if (s == 0) {  // the key bit, state 128 (ffv1dec.c:931-933)
         hdr[0] = 128;
-        ok &= rac_get(c, hdr, to0, to1, pkw) == key;
+        ok &= rac_get(c, hdr, tt, pkw) == key;
       }
       // decode_slice_header (ffv1dec.c:169-215), checked against the grid
       for (int i = 0; i < 32; i++) hdr[i] = 128;
-      const int sx = rac_symbol(c, hdr, 0, to0, to1, pkw);
-      const int sy = rac_symbol(c, hdr, 0, to0, to1, pkw);
-      const int sw = rac_symbol(c, hdr, 0, to0, to1, pkw);
-      const int sh = rac_symbol(c, hdr, 0, to0, to1, pkw);
+      const int sx = rac_symbol(c, hdr, 0, tt, pkw);
+      const int sy = rac_symbol(c, hdr, 0, tt, pkw);
+      const int sw = rac_symbol(c, hdr, 0, tt, pkw);
+      const int sh = rac_symbol(c, hdr, 0, tt, pkw);
       const int x0 = int(int64_t(sx) * a.width / a.num_h), y0 = int(int64_t(sy) * a.height / a.num_v);
       const int x1 = int(int64_t(sx + sw + 1) * a.width / a.num_h);
       const int y1 = int(int64_t(sy + sh + 1) * a.height / a.num_v);
-      ok &= x0 == g.px[0] && y0 == g.py[0] && x1 - x0 == g.pw[0] && y1 - y0 == g.ph[0];
-      for (int i = 0; i < 2; i++) ok &= rac_symbol(c, hdr, 0, to0, to1, pkw) == a.context_model;
-      (void)rac_symbol(c, hdr, 0, to0, to1, pkw);  // picture structure
-      (void)rac_symbol(c, hdr, 0, to0, to1, pkw);  // sample aspect ratio
-      (void)rac_symbol(c, hdr, 0, to0, to1, pkw);
+      ok &= x0 == g->px[0] && y0 == g->py[0] && x1 - x0 == g->pw[0] && y1 - y0 == g->ph[0];
+      for (int i = 0; i < 2; i++) ok &= rac_symbol(c, hdr, 0, tt, pkw) == a.context_model;
+      (void)rac_symbol(c, hdr, 0, tt, pkw);  // picture structure
+      (void)rac_symbol(c, hdr, 0, tt, pkw);  // sample aspect ratio
+      (void)rac_symbol(c, hdr, 0, tt, pkw);
       if (!ok) {
         bad = 1;
         atomicAdd(&a.status[0], 1);
@@ -153,44 +148,47 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
     for (int p = 0; p < planes; p++) {
       for (int i = lane; i < 2 * a.row_cap; i += kDecThreads) ring[i] = 0;
       __syncthreads();
-      if (lane == 0) {
-        // decode_plane / decode_line (ffv1dec.c:42-117, :248-280): the
-        // same zeroed-ring neighbourhood as the encoder's encode_plane
-        uint8_t* pst = states + (p ? a.state_bytes / 2 : 0);
-        const int w = g.pw[p], h = g.ph[p];
-        const int16_t* q0 = qt;
-        const int16_t* q1 = qt + 256;
-        const int16_t* q2 = qt + 512;
-        uint8_t* obase = a.out + int64_t(f) * a.frame_bytes + a.plane_off[p];
-        for (int y = 0; y < h; y++) {
-          int16_t* cur = ring + (y & 1) * a.row_cap;        // holds row y-2 until written
-          const int16_t* up = ring + ((y + 1) & 1) * a.row_cap;
+      // decode_plane / decode_line (ffv1dec.c:42-117, :248-280): the same
+      // zeroed-ring neighbourhood as the encoder's encode_plane.  Lane 0
+      // decodes a row into LDS; the wave then stores it (coalesced), so the
+      // serial loop issues no global stores.
+      uint8_t* pst = states + (p ? a.state_bytes / 2 : 0);
+      const int w = g->pw[p], h = g->ph[p];
+      const int64_t poff = p == 0 ? a.plane_off[0] : (p == 1 ? a.plane_off[1] : a.plane_off[2]);
+      const int pw = p == 0 ? a.plane_w[0] : (p == 1 ? a.plane_w[1] : a.plane_w[2]);
+      uint8_t* obase = a.out + int64_t(f) * a.frame_bytes + poff;
+      const int16_t* q0 = qt;
+      const int16_t* q1 = qt + 256;
+      const int16_t* q2 = qt + 512;
+      for (int y = 0; y < h; y++) {
+        int16_t* cur = ring + (y & 1) * a.row_cap;  // holds row y-2 until written
+        const int16_t* up = ring + ((y + 1) & 1) * a.row_cap;
+        if (lane == 0) {
           int T = up[0];
           int L = T;
           int LT = cur[0];  // two rows up, column 0
-          const int64_t orow = int64_t(g.py[p] + y) * a.plane_w[p] + g.px[p];
           for (int x = 0; x < w; x++) {
             const int RT = x + 1 < w ? up[x + 1] : T;
-            int ctx = q0[(L - LT) & 0xFF] + q1[(LT - T) & 0xFF] + q2[(T - RT) & 0xFF];
+            const int ctx = q0[(L - LT) & 0xFF] + q1[(LT - T) & 0xFF] + q2[(T - RT) & 0xFF];
             const int pred = median3(L, L + T - LT, T);
-            int diff;
-            if (ctx < 0) {
-              diff = -rac_symbol(c, pst + (-ctx) * 32, 1, to0, to1, pkw);
-            } else {
-              diff = rac_symbol(c, pst + ctx * 32, 1, to0, to1, pkw);
-            }
+            const int diff = ctx < 0 ? -rac_symbol(c, pst + (-ctx) * 32, 1, tt, pkw)
+                                     : rac_symbol(c, pst + ctx * 32, 1, tt, pkw);
             const int16_t v = int16_t((pred + diff) & mask);
             cur[x] = v;
-            const uint32_t u = uint16_t(v);
-            if (a.sample_bytes == 1) {
-              obase[orow + x] = uint8_t(u);
-            } else {
-              reinterpret_cast<uint16_t*>(obase)[orow + x] =
-                  uint16_t(a.packed_at_lsb ? u : (u << a.msb_shift));
-            }
             LT = T;
             T = RT;
             L = v;
+          }
+        }
+        __syncthreads();
+        const int64_t orow = int64_t(g->py[p] + y) * pw + g->px[p];
+        if (a.sample_bytes == 1) {
+          for (int x = lane; x < w; x += kDecThreads) obase[orow + x] = uint8_t(cur[x]);
+        } else {
+          uint16_t* o16 = reinterpret_cast<uint16_t*>(obase) + orow;
+          for (int x = lane; x < w; x += kDecThreads) {
+            const uint32_t u = uint16_t(cur[x]);
+            o16[x] = uint16_t(a.packed_at_lsb ? u : (u << a.msb_shift));
           }
         }
       }

@@ -8,7 +8,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ffv1hip.h"
@@ -186,6 +189,23 @@ uint32_t crc32_msb(const uint8_t* p, size_t n) {
     crc ^= uint32_t(p[i]) << 24;
     for (int k = 0; k < 8; k++) crc = (crc & 0x80000000u) ? (crc << 1) ^ 0x04C11DB7u : (crc << 1);
   }
+  return crc;
+}
+
+// Table-driven form of crc32_msb (av_crc with AV_CRC_32_IEEE,
+// libavutil/crc.c:356-380), for the decoder's slice checks.
+uint32_t crc32_msb_fast(const uint8_t* p, size_t n) {
+  static const std::vector<uint32_t> tab = [] {
+    std::vector<uint32_t> t(256);
+    for (uint32_t i = 0; i < 256; i++) {
+      uint32_t c = i << 24;
+      for (int k = 0; k < 8; k++) c = (c & 0x80000000u) ? (c << 1) ^ 0x04C11DB7u : (c << 1);
+      t[i] = c;
+    }
+    return t;
+  }();
+  uint32_t crc = 0;
+  for (size_t i = 0; i < n; i++) crc = (crc << 8) ^ tab[(crc >> 24) ^ p[i]];
   return crc;
 }
 
@@ -1264,11 +1284,23 @@ int ffv1hip_decode(ffv1hip_dec* d, const uint8_t* packets, const int64_t* sizes,
       ends[size_t(f) * ns + i] = (q - packets);
       q -= v;
       starts[size_t(f) * ns + i] = (q - packets);
-      if (p.ec && crc32_msb(q, size_t(v)) != 0)
-        return set_err(FFV1HIP_AVERROR_INVALIDDATA, "frame %d: slice %d CRC mismatch", f, i);
     }
     if (q != pk) return set_err(FFV1HIP_AVERROR_INVALIDDATA, "frame %d: %d slices do not span the packet", f, ns);
     total += size;
+  }
+  if (p.ec) {  // slice CRCs (ffv1dec.c:964): residue 0, checked on host threads
+    const size_t nse = size_t(n_frames) * ns;
+    std::atomic<int64_t> bad{-1};
+    const int nt = int(std::max<size_t>(1, std::min<size_t>({nse, 16, std::thread::hardware_concurrency()})));
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; t++)
+      pool.emplace_back([&, t] {
+        for (size_t k = size_t(t); k < nse; k += size_t(nt))
+          if (crc32_msb_fast(packets + starts[k], size_t(ends[k] - starts[k])) != 0) bad = int64_t(k);
+      });
+    for (auto& th : pool) th.join();
+    if (bad >= 0)
+      return set_err(FFV1HIP_AVERROR_INVALIDDATA, "frame %d: slice %d CRC mismatch", int(bad / ns), int(bad % ns));
   }
   if (!keys[0] && !d->have_states)
     return set_err(FFV1HIP_AVERROR_INVALIDDATA, "stream does not start with a keyframe");
