@@ -1114,6 +1114,14 @@ int64_t ffv1hip_get_slice_states(ffv1hip_ctx* c, uint8_t* buf, int64_t cap) {
   return n;
 }
 
+int ffv1hip_set_picture_number(ffv1hip_ctx* c, int64_t picture_number) {
+  if (!c || picture_number < 0) return set_err(-22, "invalid arguments");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());
+  c->picture_number = picture_number;
+  return 0;
+}
+
 int ffv1hip_set_slice_states(ffv1hip_ctx* c, const uint8_t* buf, int64_t size) {
   if (!c || !buf) return set_err(-22, "null argument");
   const int64_t n = int64_t(2) * c->contexts * 32 * c->nslices;

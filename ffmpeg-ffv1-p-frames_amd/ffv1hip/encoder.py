@@ -60,6 +60,7 @@ EXPORTED_SYMBOLS = (
     "ffv1hip_abi_version", "ffv1hip_set_profiling", "ffv1hip_last_kernel_ms",
     "ffv1hip_last_kernel_stats", "ffv1hip_synchronize",
     "ffv1hip_dec_create", "ffv1hip_dec_destroy", "ffv1hip_decode", "ffv1hip_dec_reset",
+    "ffv1hip_set_picture_number",
 )
 
 
@@ -115,6 +116,8 @@ def load_library():
     L.ffv1hip_get_slice_states.restype = i64
     L.ffv1hip_set_slice_states.argtypes = [vp, u8p, i64]
     L.ffv1hip_set_slice_states.restype = ctypes.c_int
+    L.ffv1hip_set_picture_number.argtypes = [vp, i64]
+    L.ffv1hip_set_picture_number.restype = ctypes.c_int
     L.ffv1hip_last_error.argtypes = []
     L.ffv1hip_last_error.restype = ctypes.c_char_p
     L.ffv1hip_set_profiling.argtypes = [vp, ctypes.c_int]
@@ -267,6 +270,29 @@ class HipEncoder:
         stride = ctypes.c_int64()
         L.ffv1hip_device_packets(self._h, ctypes.byref(d_p), ctypes.byref(stride), ctypes.byref(d_s))
         return d_p.value, stride.value, d_s.value
+
+    def get_slice_states(self) -> np.ndarray:
+        """The P-frame carry after the last frame encoded: [slice][2][contexts][32]."""
+        L = load_library()
+        n = L.ffv1hip_get_slice_states(self._h, None, 0)
+        if n < 0:
+            raise FFV1Error(n, "ffv1hip_get_slice_states")
+        buf = np.zeros(n, np.uint8)
+        rc = L.ffv1hip_get_slice_states(self._h, _u8p(buf), n)
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_get_slice_states")
+        return buf
+
+    def set_slice_states(self, buf: np.ndarray, picture_number: int):
+        """Continue another encoder's stream at `picture_number` from its states."""
+        L = load_library()
+        buf = np.ascontiguousarray(buf, np.uint8)
+        rc = L.ffv1hip_set_slice_states(self._h, _u8p(buf), buf.size)
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_set_slice_states")
+        rc = L.ffv1hip_set_picture_number(self._h, picture_number)
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_set_picture_number")
 
     def set_profiling(self, on: bool = True):
         rc = load_library().ffv1hip_set_profiling(self._h, int(on))

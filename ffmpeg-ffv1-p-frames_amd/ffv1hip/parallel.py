@@ -11,6 +11,8 @@ from __future__ import annotations
 
 from typing import Callable, Dict, List, Sequence, Tuple
 
+import numpy as np
+
 
 def gop_ranges(n_frames: int, gop: int) -> List[Tuple[int, int]]:
     """[start, end) frame ranges of the GOPs of an n-frame stream."""
@@ -51,3 +53,72 @@ def gather_packets(local: Dict[int, Tuple[bytes, bool]], n_frames: int, dist, ra
     for o in objs:
         merged.update(o)
     return [merged[i] for i in range(n_frames)]
+
+
+# ---------------------------------------------------------------------------
+# The within-GOP exchange step (SURVEY §8e): when a stream has fewer GOPs than
+# ranks (or GOPs too long to balance), frames are split into contiguous
+# ranges and a range that starts inside a GOP continues the P-frame chain of
+# the rank before it.  The only state crossing ranks is the per-slice
+# context-state snapshot after the previous range's last frame
+# (2 x contexts x 32 bytes per slice: 2.73 MB for 64 slices, context model
+# 0), sent point-to-point (RCCL over xGMI on GPUs, gloo on CPU).
+
+def contiguous_ranges(n_frames: int, world: int) -> List[Tuple[int, int]]:
+    """[lo, hi) frame range of every rank: contiguous, sizes differ by <= 1."""
+    base, extra = divmod(n_frames, world)
+    out, lo = [], 0
+    for r in range(world):
+        hi = lo + base + (1 if r < extra else 0)
+        out.append((lo, hi))
+        lo = hi
+    return out
+
+
+def _is_key(i: int, gop: int) -> bool:
+    return gop == 0 or i % gop == 0  # ffv1enc.c:1299
+
+
+def encode_exchanged(encoder_factory: Callable[[], object], frames: Callable[[int], Sequence],
+                     n_frames: int, gop: int, dist, rank: int, world: int,
+                     to_tensor: Callable, from_tensor: Callable,
+                     state_bytes: int) -> Dict[int, Tuple[bytes, bool]]:
+    """Encode this rank's contiguous range.
+
+    The part of the range from its first keyframe on (the body) is
+    independent and is encoded first; its final states go to rank+1 when
+    rank+1's range starts inside a GOP.  The head (the frames before the
+    first keyframe) waits for rank-1's states, then continues that chain in
+    a second encoder placed at the right picture number.  Encoders need
+    ``encode``, ``get_slice_states`` and ``set_slice_states(buf, pn)``;
+    ``to_tensor``/``from_tensor`` move a state blob to and from the
+    communication device."""
+    if n_frames < world:
+        raise ValueError("the exchange step needs at least one frame per rank")
+    ranges = contiguous_ranges(n_frames, world)
+    lo, hi = ranges[rank]
+    out: Dict[int, Tuple[bytes, bool]] = {}
+    first_key = next((i for i in range(lo, hi) if _is_key(i, gop)), hi)
+    send_next = rank + 1 < world and not _is_key(ranges[rank + 1][0], gop)
+
+    def send(states):
+        dist.send(to_tensor(states), dst=rank + 1)
+
+    last_states = None
+    if first_key < hi:  # body: independent of the other ranks
+        enc = encoder_factory()
+        for i, p in zip(range(first_key, hi), enc.encode([frames(i) for i in range(first_key, hi)])):
+            out[i] = p
+        last_states = enc.get_slice_states()
+        if send_next:
+            send(last_states)
+    if lo < first_key:  # head: continue rank-1's chain
+        buf = to_tensor(np.zeros(state_bytes, np.uint8))
+        dist.recv(buf, src=rank - 1)
+        enc = encoder_factory()
+        enc.set_slice_states(from_tensor(buf), lo)
+        for i, p in zip(range(lo, first_key), enc.encode([frames(i) for i in range(lo, first_key)])):
+            out[i] = p
+        if first_key == hi and send_next:  # no keyframe in the range: pass the chain on
+            send(enc.get_slice_states())
+    return out

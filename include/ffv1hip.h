@@ -123,6 +123,11 @@ void ffv1hip_reset(ffv1hip_ctx *ctx);
 int64_t ffv1hip_get_slice_states(ffv1hip_ctx *ctx, uint8_t *buf, int64_t cap);
 int     ffv1hip_set_slice_states(ffv1hip_ctx *ctx, const uint8_t *buf,
                                  int64_t size);
+/* Resume a stream mid-GOP (the multi-GPU exchange step): the picture number
+ * of the next frame, which places the keyframes (ffv1enc.c:1299).  With
+ * ffv1hip_set_slice_states a second context continues another's P-frame
+ * chain bit-exactly. */
+int     ffv1hip_set_picture_number(ffv1hip_ctx *ctx, int64_t picture_number);
 
 /* Kernel timing: when enabled, HIP events are recorded on the launch stream
  * around each kernel of every call; ffv1hip_last_kernel_ms synchronises and

@@ -1094,6 +1094,36 @@ int64_t ffv1o_enc_frame(ffv1o_enc *e, const uint8_t *const planes[3],
     return pos;
 }
 
+/* The P-frame carry of every slice (PlaneContext.state, ffv1.h:72):
+ * [slice][plane_ctx 0..1][context][32] bytes, range coder only; and the
+ * picture number that places keyframes (ffv1enc.c:1299).  Used to resume a
+ * stream mid-GOP in another encoder (the multi-rank exchange step). */
+int64_t ffv1o_enc_get_states(const ffv1o_enc *e, uint8_t *buf, int64_t cap)
+{
+    int64_t per = (int64_t)e->contexts * 32, n = 2 * per * e->nslices;
+    if (!buf)
+        return n;
+    if (cap < n)
+        return -1;
+    for (int i = 0; i < e->nslices; i++)
+        for (int p = 0; p < 2; p++)
+            memcpy(buf + (2 * (int64_t)i + p) * per, e->sl[i].ps[p].rac, (size_t)per);
+    return n;
+}
+
+int ffv1o_enc_set_states(ffv1o_enc *e, const uint8_t *buf, int64_t size,
+                         int64_t picture_number)
+{
+    int64_t per = (int64_t)e->contexts * 32;
+    if (size != 2 * per * e->nslices)
+        return -1;
+    for (int i = 0; i < e->nslices; i++)
+        for (int p = 0; p < 2; p++)
+            memcpy(e->sl[i].ps[p].rac, buf + (2 * (int64_t)i + p) * per, (size_t)per);
+    e->picture_number = picture_number;
+    return 0;
+}
+
 int ffv1o_enc_last_slice_bytes(const ffv1o_enc *e, int *bytes, int n)
 {
     for (int i = 0; i < n && i < e->nslices; i++)

@@ -77,6 +77,9 @@ int64_t    ffv1o_enc_frame(ffv1o_enc *e, const uint8_t *const planes[3],
                            const int strides[3], uint8_t *out, int64_t cap,
                            int *key);
 /* Per-slice byte counts of the last frame (before the trailer). */
+int64_t    ffv1o_enc_get_states(const ffv1o_enc *e, uint8_t *buf, int64_t cap);
+int        ffv1o_enc_set_states(ffv1o_enc *e, const uint8_t *buf, int64_t size,
+                                int64_t picture_number);
 int        ffv1o_enc_last_slice_bytes(const ffv1o_enc *e, int *bytes, int n);
 
 /* Symbols of one slice in coding order: (context << 16) | (uint16)diff, the

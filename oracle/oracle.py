@@ -53,6 +53,11 @@ def lib():
         L.ffv1o_enc_frame.argtypes = [ctypes.c_void_p, P(u8p), P(ctypes.c_int), u8p, ctypes.c_int64, P(ctypes.c_int)]
         L.ffv1o_enc_frame.restype = ctypes.c_int64
         L.ffv1o_enc_last_slice_bytes.argtypes = [ctypes.c_void_p, P(ctypes.c_int), ctypes.c_int]
+        L.ffv1o_enc_get_states.argtypes = [ctypes.c_void_p, P(ctypes.c_uint8), ctypes.c_int64]
+        L.ffv1o_enc_get_states.restype = ctypes.c_int64
+        L.ffv1o_enc_set_states.argtypes = [ctypes.c_void_p, P(ctypes.c_uint8), ctypes.c_int64,
+                                           ctypes.c_int64]
+        L.ffv1o_enc_set_states.restype = ctypes.c_int
         L.ffv1o_slice_symbols.argtypes = [P(Config), P(u8p), P(ctypes.c_int), ctypes.c_int, P(ctypes.c_int32), ctypes.c_int64]
         L.ffv1o_slice_symbols.restype = ctypes.c_int64
         L.ffv1o_dec_new.argtypes = [P(Config), u8p, ctypes.c_int]
@@ -136,6 +141,17 @@ class Encoder:
         if n < 0:
             raise RuntimeError(f"ffv1o_enc_frame: {n}")
         return out[:n].tobytes(), bool(key.value)
+
+    def get_slice_states(self) -> np.ndarray:
+        n = lib().ffv1o_enc_get_states(self._h, None, 0)
+        buf = np.zeros(n, np.uint8)
+        lib().ffv1o_enc_get_states(self._h, _u8p(buf), n)
+        return buf
+
+    def set_slice_states(self, buf: np.ndarray, picture_number: int):
+        buf = np.ascontiguousarray(buf, np.uint8)
+        if lib().ffv1o_enc_set_states(self._h, _u8p(buf), buf.size, picture_number) < 0:
+            raise ValueError("state blob size")
 
     def last_slice_bytes(self):
         n = self.cfg.num_h_slices * self.cfg.num_v_slices

@@ -125,3 +125,25 @@ def test_8k_grid16_lossless_roundtrip():
         assert k == key
         for a, b in zip(planes, f):
             np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("split", [2, 5])
+def test_state_forwarding_between_contexts(split):
+    """The multi-GPU exchange step through the C-ABI: a second context resumes
+    the P-frame chain mid-GOP from the first's slice states
+    (ffv1hip_get_slice_states -> ffv1hip_set_slice_states +
+    ffv1hip_set_picture_number) and the packets equal one context's."""
+    from ffv1hip import HipEncoder
+    s = Stream("fwd", 320, 180, "yuv420p10", 9, slices=6, gop_size=12, source="d2", depth=10)
+    frames = list(s.frames())
+    _, ref = hip_encode(s, frames, batch=9)
+    a = HipEncoder(hip_params(s), 0, 9)
+    head = a.encode(frames[:split])
+    st = a.get_slice_states()
+    a.close()
+    b = HipEncoder(hip_params(s), 0, 9)
+    b.set_slice_states(st, split)
+    tail = b.encode(frames[split:])
+    b.close()
+    assert head + tail == ref
+    assert [k for _, k in head + tail] == [True] + [False] * 8

@@ -86,3 +86,74 @@ def test_gop_sharded_gloo_world2_matches_single_process():
     ref = enc.encode(frames)
     assert [k for _, k in got] == [i % GOP == 0 for i in range(N)]
     assert got == ref
+
+
+# --- the within-GOP exchange step: contiguous ranges + state forwarding ----
+
+def _oracle_encoder_gop(gop):
+    from oracle import oracle
+
+    class Enc:
+        def __init__(self):
+            self.e = oracle.Encoder(oracle.configure(W, H, "yuv420p10", slices=4, coder=1,
+                                                     gop_size=gop))
+
+        def encode(self, frames):
+            return [self.e.encode(f) for f in frames]
+
+        def get_slice_states(self):
+            return self.e.get_slice_states()
+
+        def set_slice_states(self, buf, pn):
+            self.e.set_slice_states(buf, pn)
+
+    return Enc
+
+
+def _xworker(rank, world, port, q, gop):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "ffmpeg-ffv1-p-frames_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from ffv1hip import parallel
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    frames = _frames()
+    factory = _oracle_encoder_gop(gop)
+    state_bytes = factory().get_slice_states().size
+    local = parallel.encode_exchanged(factory, lambda i: frames[i], N, gop, dist, rank, world,
+                                      to_tensor=lambda a: torch.from_numpy(np.array(a, np.uint8)),
+                                      from_tensor=lambda t: t.numpy(), state_bytes=state_bytes)
+    got = parallel.gather_packets(local, N, dist, rank, world)
+    if rank == 0:
+        q.put(got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_contiguous_ranges_partition():
+    from ffv1hip import parallel
+    for n, w in [(11, 2), (11, 3), (24, 8), (8, 8)]:
+        r = parallel.contiguous_ranges(n, w)
+        assert r[0][0] == 0 and r[-1][1] == n
+        assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
+        assert max(e - s for s, e in r) - min(e - s for s, e in r) <= 1
+
+
+@pytest.mark.parametrize("world,gop", [(2, 12), (2, 4), (3, 12), (3, 5)])
+def test_exchange_step_gloo_matches_single_process(world, gop):
+    """A GOP split across ranks continues bit-exactly from the forwarded states."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_xworker, args=(r, world, port, q, gop)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    frames = _frames()
+    ref = _oracle_encoder_gop(gop)().encode(frames)
+    assert [k for _, k in got] == [i % gop == 0 for i in range(N)]
+    assert got == ref
