@@ -30,6 +30,42 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ffmpeg-ffv1-p-frames_amd"))
 
 W, H, PIX_FMT, SLICES, GOP = 3840, 2160, "yuv420p10", 64, 12
+# --config: c3 is the metric's workload (BASELINE configs[2]); the others are
+# the remaining BASELINE configs on one GPU, checked by the GPU decoder's
+# lossless round trip (and c2 also by the reference's MD5 pin).
+CONFIGS = {
+    "c3": dict(W=3840, H=2160, PIX_FMT="yuv420p10", SLICES=64, GOP=12, BPR=0, DEPTH=10, C444=False,
+               GRID=False, GOPS=21, PIN=("08e3975d4d0f5f2e5c82cd4037764789", 24),
+               metric="Mpixels/s encoded (bit-exact) 4K yuv420p10 FFV1 P-frames",
+               workload="4K 3840x2160 yuv420p10le, coder=1 (range, custom table), slices=64, keyint=12 P-frames"),
+    "c2": dict(W=1920, H=1080, PIX_FMT="yuv420p", SLICES=24, GOP=1, BPR=0, DEPTH=8, C444=False,
+               GRID=False, GOPS=480, PIN=("58e800634d515e024a515ba618f24dc3", 50),
+               metric="Mpixels/s encoded (bit-exact) 1080p yuv420p FFV1 intra",
+               workload="1080p 1920x1080 yuv420p, coder=1 (range, custom table), slices=24, intra-only"),
+    "c4": dict(W=3840, H=2160, PIX_FMT="yuv444p16", SLICES=64, GOP=12, BPR=12, DEPTH=16, C444=True,
+               GRID=False, GOPS=12, PIN=None,
+               metric="Mpixels/s encoded (lossless) 4K yuv444p12 FFV1 P-frames",
+               workload="4K 3840x2160 yuv444p16le + bits_per_raw_sample=12, coder=1, slices=64, keyint=12 P-frames"),
+    "c5": dict(W=7680, H=4320, PIX_FMT="yuv420p10", SLICES=256, GOP=12, BPR=0, DEPTH=10, C444=False,
+               GRID=True, GOPS=6, PIN=None,
+               metric="Mpixels/s encoded (lossless) 8K yuv420p10 FFV1 P-frames",
+               workload="8K 7680x4320 yuv420p10le, coder=1, slices=256 (16x16 grid), keyint=12 P-frames"),
+}
+CFG = CONFIGS["c3"]
+BPR, DEPTH, C444, GRID = 0, 10, False, False
+
+
+def select_config(name):
+    global W, H, PIX_FMT, SLICES, GOP, BPR, DEPTH, C444, GRID, CFG
+    CFG = CONFIGS[name]
+    W, H, PIX_FMT, SLICES, GOP = CFG["W"], CFG["H"], CFG["PIX_FMT"], CFG["SLICES"], CFG["GOP"]
+    BPR, DEPTH, C444, GRID = CFG["BPR"], CFG["DEPTH"], CFG["C444"], CFG["GRID"]
+
+
+def hip_configure():
+    from ffv1hip import configure
+    return configure(W, H, PIX_FMT, slices=SLICES, coder=1, gop_size=GOP, bits_per_raw_sample=BPR,
+                     allow_large_grid=GRID)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 KERNEL = {"symbols": "ffv1_symbols", "layout": "ffv1_layout", "bits": "ffv1_bits", "states": "ffv1_walk",
           "code": "ffv1_dcode", "sink": "ffv1_sink", "assemble": "ffv1_assemble_packets"}
@@ -43,9 +79,9 @@ def log(*a):
 def make_frames(n, data):
     from ffv1hip import synth
     if data == "d1":
-        gen = synth.videogen_frames(W, H, n, depth=10)
+        gen = synth.videogen_frames(W, H, n, depth=DEPTH, chroma444=C444)
     else:
-        gen = synth.d2_frames(W, H, n, depth=10)
+        gen = synth.d2_frames(W, H, n, depth=DEPTH, chroma444=C444)
     return [f for f in gen]
 
 
@@ -66,7 +102,12 @@ def cpu_baseline(frames, threads):
     """
     sys.path.insert(0, ROOT)
     from oracle import oracle
-    cfg = oracle.configure(W, H, PIX_FMT, slices=SLICES, coder=1, gop_size=GOP)
+    if GRID:
+        cfg = oracle.configure(W, H, PIX_FMT, slices=0, coder=1, gop_size=GOP)
+        cfg.num_h_slices, cfg.num_v_slices = 16, 16
+    else:
+        cfg = oracle.configure(W, H, PIX_FMT, slices=SLICES, coder=1, gop_size=GOP,
+                               bits_per_raw_sample=BPR)
     sample = frames[:3]
 
     def one():
@@ -88,7 +129,7 @@ def cpu_baseline(frames, threads):
     multi = threads * len(sample) * W * H / (t1 - t0) / 1e6
     return {
         "value": round(multi, 3), "unit": "Mpixels/s", "cores": threads, "kind": "port",
-        "sample": f"{threads} threads x 3 frames (1 key + 2 P, one GOP each) of the same 4K 10-bit "
+        "sample": f"{threads} threads x 3 frames (one GOP each) of the same {W}x{H} {PIX_FMT} "
                   f"clip, oracle/ffv1_oracle.c, GOP-sharded",
         "single_thread": {"value": round(single, 3), "cores": 1, "sample": "3 frames"},
     }
@@ -115,13 +156,19 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     # 21 GOPs = 252 frames per batch: 252 coder waves (one per frame of each
     # slice) fit the CUs beside the states walk of the next batch
-    ap.add_argument("--gops", type=int, default=21, help="GOPs (x12 frames) per rank per step")
+    ap.add_argument("--gops", type=int, default=0,
+                    help="GOPs per rank per step (default: 21 for c3, see CONFIGS)")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c3",
+                    help="BASELINE config: c3 (the metric's, default), c2, c4, c5")
     ap.add_argument("--data", choices=("d1", "d2"), default="d1")
     ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-decode-check", action="store_true",
                     help="skip decoding the last step's packets with the GPU decoder")
     args = ap.parse_args()
+    select_config(args.config)
+    if args.gops <= 0:
+        args.gops = CFG["GOPS"]
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -137,12 +184,12 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     B = args.gops * GOP
-    params = configure(W, H, PIX_FMT, slices=SLICES, coder=1, gop_size=GOP)
+    params = hip_configure()
     shapes = params.plane_shapes()
-    plane_bytes = [h * w * 2 for h, w in shapes]
+    plane_bytes = [h * w * params.sample_bytes for h, w in shapes]
     frame_bytes = (sum(plane_bytes) + 255) // 256 * 256
     offs = [0, plane_bytes[0], plane_bytes[0] + plane_bytes[1]]
-    strides = [shapes[0][1] * 2, shapes[1][1] * 2, shapes[2][1] * 2]
+    strides = [shapes[k][1] * params.sample_bytes for k in range(3)]
 
     t0 = time.perf_counter()
     frames = make_frames(B, args.data)
@@ -188,11 +235,12 @@ def main():
     pkts = enc.fetch(B)
     out_bytes = sum(len(p) for p, _ in pkts)
     bitexact = None
-    if args.data == "d1" and B >= 24:
+    pin = CFG["PIN"]
+    if args.data == "d1" and pin and B >= pin[1]:
         h = hashlib.md5()
-        for p, _ in pkts[:24]:
+        for p, _ in pkts[:pin[1]]:
             h.update(p)
-        bitexact = h.hexdigest() == PIN_MD5_24
+        bitexact = h.hexdigest() == pin[0]
 
     # on-device lossless self-check (outside the timed region): the GPU
     # decoder (ffv1_decode_slices) decodes the last step's packets
@@ -235,7 +283,7 @@ def main():
     mpix = args.steps * B * W * H * world / elapsed / 1e6
     if rank == 0:
         res = {
-            "metric": "Mpixels/s encoded (bit-exact) 4K yuv420p10 FFV1 P-frames",
+            "metric": CFG["metric"],
             "value": round(mpix, 2),
             "unit": "Mpixels/s",
             "n_gpus": world,
@@ -245,10 +293,10 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u16",
-            "data": f"synthetic ({'tests/videogen clip widened to 10 bit' if args.data == 'd1' else 'D2 seeded noisy clip'}), HBM-resident",
+            "dtype": "u8" if params.sample_bytes == 1 else "u16",
+            "data": f"synthetic ({f'tests/videogen clip at {DEPTH} bit' if args.data == 'd1' else 'D2 seeded noisy clip'}), HBM-resident",
             "config": {
-                "workload": "4K 3840x2160 yuv420p10le, coder=1 (range, custom table), slices=64, keyint=12 P-frames",
+                "workload": CFG["workload"],
                 "frames_per_step_per_gpu": B,
                 "gops_per_step_per_gpu": args.gops,
                 "parallelism": f"gop-sharded x{world}",

@@ -1131,12 +1131,15 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
     const int code = i >> 8, st = i & 255;
     fixed[kLdsN + i] = (uint8_t)(code < 2 ? a.ftab[i] : st);
   }
-  // every luma chain first: they are twice as long as the chroma ones, which
-  // then fill the CUs as the luma waves finish
+  // the longer plane group's chains first (luma at 4:2:0, twice as long as
+  // chroma; chroma at 4:4:4, where Cb and Cr make one chain twice luma's);
+  // the shorter ones then fill the CUs as those waves finish
   const int nblk = gridDim.x / 2;
-  const int grp = (int)blockIdx.x >= nblk;
+  const SliceGeom& g0 = a.geom[0];
+  const bool chroma_first = 2 * (int64_t)g0.pw[1] * g0.ph[1] > (int64_t)g0.pw[0] * g0.ph[0];
+  const int grp = ((int)blockIdx.x >= nblk) != chroma_first;
   const int npairs = (a.nslices + 1) / 2;
-  const int bi = (int)blockIdx.x - grp * nblk;
+  const int bi = (int)blockIdx.x - ((int)blockIdx.x >= nblk ? nblk : 0);
   const int seg_i = bi / npairs, pair = bi % npairs;
   const Segment seg = a.segs[seg_i];
   const int sl = 2 * pair + h;              // this half's slice
@@ -1253,7 +1256,7 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
           for (int t = 0; t < cmax; t++) {
             const uint4 r = myrecs[t];
             if (t < cnt)
-              walk_long(mytbl, a.ftab, (int)(int16_t)(r.x >> 16), (int)(r.x & 0xFFFFu) + k, k,
+              walk_long(mytbl, fixed + kLdsN, (int)(int16_t)(r.x >> 16), (int)(r.x & 0xFFFFu) + k, k,
                         a.ds.pre + pos0 + (int)(r.w & 0xFFFu));
           }
           // the next chunk's carried bytes: read back what was just written
