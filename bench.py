@@ -242,10 +242,10 @@ def main():
             h.update(p)
         bitexact = h.hexdigest() == pin[0]
 
-    # on-device lossless self-check (outside the timed region): the GPU
-    # decoder (ffv1_decode_slices) decodes the last step's packets
+    # on-device lossless self-check (outside the timed region, rank 0): the
+    # GPU decoder (ffv1_decode_slices) decodes the last step's packets
     decode = None
-    if not args.no_decode_check:
+    if not args.no_decode_check and rank == 0:
         from ffv1hip import HipDecoder
         dec = HipDecoder(params, enc.extradata(), local_rank)
         td = time.perf_counter()

@@ -1018,10 +1018,9 @@ int64_t walk_lds_bytes_dev(int64_t state_bytes);
 
 // Any exponent, one symbol: lane k < 32 of a half applies all decisions of
 // slot k in order (slot 10 takes e-8 exponent decisions beyond e = 9, slot
-// 31 the mantissa bits >= 9, the sign goes to slot 21) and records the state for
-// each (see walk_step).  row_off: the slot's byte in the half's table.
-__device__ __forceinline__ void walk_long(uint8_t* tbl, const uint8_t* ftab, int v, int row_off, int k,
-                                          uint8_t* pre) {
+// 31 the mantissa bits >= 9, the sign goes to slot 21) to its state st,
+// records the state for each (see walk_step) and returns the new state.
+__device__ __forceinline__ int walk_long(int st, const uint8_t* ftab, int v, int k, uint8_t* pre) {
   const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
   const int e = v ? 31 - __builtin_clz(mag) : -1;
   int n = 0, d0 = 0;  // decisions of this slot: indices d0 .. d0+n-1
@@ -1045,8 +1044,6 @@ __device__ __forceinline__ void walk_long(uint8_t* tbl, const uint8_t* ftab, int
     n = e >= 10 ? e - 9 : 0;
     d0 = e + 2;
   }
-  if (!n) return;
-  int st = tbl[row_off];
   for (int j = 0; j < n; j++) {
     const int di = d0 + j;
     int bit;
@@ -1057,7 +1054,7 @@ __device__ __forceinline__ void walk_long(uint8_t* tbl, const uint8_t* ftab, int
     pre[di] = (uint8_t)st;  // the state it is coded with, as walk_step records it
     st = ftab[(bit << 8) | st];
   }
-  tbl[row_off] = (uint8_t)st;
+  return st;
 }
 
 // per-lane constants of the step
@@ -1253,11 +1250,21 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
 
         if (lng) {  // e >= 10 somewhere: one symbol at a time, recorded straight to HBM
           const int cmax = max(__builtin_amdgcn_readlane(cnt, 0), __builtin_amdgcn_readlane(cnt, 32));
+          // the next symbol's row is read before this symbol's write (a symbol
+          // on its predecessor's row takes the state from the register), so a
+          // symbol waits on its transition lookups only
+          uint4 r = myrecs[0];
+          int st = mytbl[(int)(r.x & 0xFFFFu) + k];
           for (int t = 0; t < cmax; t++) {
-            const uint4 r = myrecs[t];
-            if (t < cnt)
-              walk_long(mytbl, fixed + kLdsN, (int)(int16_t)(r.x >> 16), (int)(r.x & 0xFFFFu) + k, k,
-                        a.ds.pre + pos0 + (int)(r.w & 0xFFFu));
+            const uint4 rn = myrecs[t + 1];
+            const int stn = mytbl[(int)(rn.x & 0xFFFFu) + k];
+            if (t < cnt) {
+              st = walk_long(st, fixed + kLdsN, (int)(int16_t)(r.x >> 16), k,
+                             a.ds.pre + pos0 + (int)(r.w & 0xFFFu));
+              mytbl[(int)(r.x & 0xFFFFu) + k] = (uint8_t)st;
+            }
+            st = (int)rn.w < 0 ? st : stn;
+            r = rn;
           }
           // the next chunk's carried bytes: read back what was just written
           __builtin_amdgcn_s_waitcnt(0);
