@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    for k in ("ffv1_code_golomb", "ffv1_dcode", "ffv1_code", "ffv1_walk", "ffv1_bits", "ffv1_layout", "ffv1_symbols",
+    for k in ("ffv1_decode_slices", "ffv1_code_golomb", "ffv1_dcode", "ffv1_code", "ffv1_walk", "ffv1_bits", "ffv1_layout", "ffv1_symbols",
               "ffv1_sink", "ffv1_assemble_packets"):
         if k in name:
             return k
