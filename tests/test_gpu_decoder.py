@@ -107,3 +107,29 @@ def test_hip_encode_decode_4k_p10_roundtrip():
         for a, b in zip(planes, frames[i]):
             np.testing.assert_array_equal(a, b, err_msg=f"frame {i}")
     dec.close()
+
+
+@pytest.mark.parametrize("shape", ["8k_grid16", "1080p_intra_8bit", "4k_444p12"])
+def test_hip_encode_decode_roundtrip_baseline_shapes(shape):
+    """The other BASELINE configs at full frame size: HIP encode -> HIP decode
+    returns the input (8K has no reference bitstream; this is its check)."""
+    from ffv1hip import HipDecoder, HipEncoder
+    s = {
+        "8k_grid16": Stream("8k", 7680, 4320, "yuv420p10", 3, slices=256, gop_size=2, source="d2",
+                            depth=10, allow_large_grid=True, extra={"grid": (16, 16)}),
+        "1080p_intra_8bit": Stream("c2", 1920, 1080, "yuv420p", 3, slices=24, gop_size=1),
+        "4k_444p12": Stream("c4", 3840, 2160, "yuv444p16", 3, slices=64, gop_size=12,
+                            bits_per_raw_sample=12, depth=16, chroma444=True),
+    }[shape]
+    frames = list(s.frames())
+    enc = HipEncoder(hip_params(s), 0, len(frames))
+    ex = enc.extradata()
+    pkts = enc.encode(frames)
+    enc.close()
+    dec = HipDecoder(hip_params(s), ex, 0)
+    got = dec.decode([p for p, _ in pkts])
+    dec.close()
+    for i, ((planes, k), (_, key)) in enumerate(zip(got, pkts)):
+        assert k == key
+        for a, b in zip(planes, frames[i]):
+            np.testing.assert_array_equal(a, b, err_msg=f"frame {i}")
