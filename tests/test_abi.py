@@ -96,3 +96,35 @@ def test_unsupported_parameters_are_refused():
     with pytest.raises(FFV1Error) as e:
         HipEncoder(p, 0, 1)
     assert e.value.code == -38
+
+
+def test_decoder_contract_checks_before_the_gpu():
+    """ffv1hip_dec_create refuses what the GPU decoder does not decode
+    (-ENOSYS) and extradata the parameters would not produce
+    (AVERROR_INVALIDDATA) on the host, before any HIP call."""
+    from ffv1hip import AVERROR_INVALIDDATA, FFV1Error, HipDecoder, configure
+    from oracle import oracle
+    p = configure(352, 288, "yuv420p10", coder=1, slices=4)
+    ex = oracle.Encoder(oracle.configure(352, 288, "yuv420p10", coder=1, slices=4)).extradata()
+    for field, value in (("context_model", 1), ("ac", 0), ("version", 1)):
+        q = configure(352, 288, "yuv420p10", coder=1, slices=4)
+        setattr(q, field, value)
+        with pytest.raises(FFV1Error) as e:
+            HipDecoder(q, ex, 0)
+        assert e.value.code == -38, field
+    with pytest.raises(FFV1Error) as e:
+        HipDecoder(p, ex[:-1] + bytes([ex[-1] ^ 0x5A]), 0)
+    assert e.value.code == AVERROR_INVALIDDATA
+
+
+def test_decoder_no_silent_cpu_fallback_without_gpu():
+    import torch
+    from ffv1hip import FFV1Error, HipDecoder, configure
+    from oracle import oracle
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    p = configure(352, 288, "yuv420p10", coder=1, slices=4)
+    ex = oracle.Encoder(oracle.configure(352, 288, "yuv420p10", coder=1, slices=4)).extradata()
+    with pytest.raises(FFV1Error) as e:
+        HipDecoder(p, ex, 0)
+    assert e.value.code == -5
