@@ -30,7 +30,7 @@ def per_kernel(path, counter):
     return {k: statistics.mean(v) for k, v in vals.items()}
 
 
-def main(tag, frames_per_launch, config):
+def main(tag, frames_per_launch, config, out_name="pmc_traffic.json"):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
@@ -54,10 +54,11 @@ def main(tag, frames_per_launch, config):
         "rocprof_avg_ms": stats,
         "encode_hbm_bytes_per_launch": kernels.get("ffv1_dcode", {}).get("hbm_bytes"),
     }
-    json.dump(out, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(dst, out_name), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
     main(sys.argv[1] if len(sys.argv) > 1 else "r01", int(sys.argv[2]) if len(sys.argv) > 2 else 252,
-         "3840x2160 yuv420p10")
+         sys.argv[3] if len(sys.argv) > 3 else "3840x2160 yuv420p10",
+         sys.argv[4] if len(sys.argv) > 4 else "pmc_traffic.json")
