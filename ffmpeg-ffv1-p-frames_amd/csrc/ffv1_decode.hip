@@ -171,8 +171,9 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
             const int RT = x + 1 < w ? up[x + 1] : T;
             const int ctx = q0[(L - LT) & 0xFF] + q1[(LT - T) & 0xFF] + q2[(T - RT) & 0xFF];
             const int pred = median3(L, L + T - LT, T);
-            const int diff = ctx < 0 ? -rac_symbol(c, pst + (-ctx) * 32, 1, tt, pkw)
-                                     : rac_symbol(c, pst + ctx * 32, 1, tt, pkw);
+            // one call site: the symbol decoder is the kernel's hot code
+            const int sym = rac_symbol(c, pst + (ctx < 0 ? -ctx : ctx) * 32, 1, tt, pkw);
+            const int diff = ctx < 0 ? -sym : sym;
             const int16_t v = int16_t((pred + diff) & mask);
             cur[x] = v;
             LT = T;
