@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
     if (key) {  // ff_ffv1_clear_slice_state on keyframes (ffv1dec.c:261-263)
       for (int64_t i = lane; i < words; i += kDecThreads) st4[i] = 0x80808080u;
     } else if (j == 0) {  // continue the previous call's chain
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(a.persist + int64_t(s) * a.state_bytes);
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(a.persist_in + int64_t(s) * a.state_bytes);
       for (int64_t i = lane; i < words; i += kDecThreads) st4[i] = src[i];
     }
     __syncthreads();
@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
   }
   if (sg.save_states) {
     const uint32_t* st4 = reinterpret_cast<const uint32_t*>(states);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(a.persist + int64_t(s) * a.state_bytes);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(a.persist_out + int64_t(s) * a.state_bytes);
     for (int64_t i = lane; i < a.state_bytes / 4; i += kDecThreads) dst[i] = st4[i];
   }
 }

@@ -257,7 +257,11 @@ struct ffv1hip_ctx {
   int64_t* d_slice_bytes = nullptr;
   uint8_t* d_packets = nullptr;
   int64_t* d_packet_size = nullptr;
-  uint8_t* d_persist = nullptr;
+  // the P-frame carry, [slice][2][contexts][32], double-buffered: a batch
+  // reads d_persist[pcur] and writes d_persist[pcur ^ 1] (its segments may
+  // load and save the same slice in one launch, in any block order)
+  uint8_t* d_persist[2] = {nullptr, nullptr};
+  int pcur = 0;
   uint8_t* d_tables = nullptr;   // [slot][slice][2][contexts][32]
   uint32_t* d_sym = nullptr;     // [slot][frame_samples]; frames mode: walk records (uint4), 2 x [batch frame][frame_samples]
   // frames mode, two buffer sets: the walk of batch k+1 runs while batch k codes
@@ -280,8 +284,27 @@ struct ffv1hip_ctx {
   hipEvent_t coded[2] = {nullptr, nullptr};  // the coder of the batch that last used set k is done
   SliceGeom* d_geom = nullptr;
   int* d_slot_frames = nullptr;  // [j][slot]
-  int* d_status = nullptr;
+  int* d_status = nullptr;       // [set][4]: [0] slices over budget, [1] most bytes one needed
   hipStream_t stream = nullptr;
+  // ordering between calls: the next batch's launch stream waits for `dep`
+  // (the previous batch's last use of the buffers it rewrites first), and
+  // ffv1hip_synchronize waits for `done` (the previous batch's last kernel)
+  hipEvent_t dep_ev = nullptr, done_ev = nullptr;
+  bool dep_valid = false;
+  // the last batch, kept so that a slice over the byte budget can be
+  // encoded again with a larger budget (ffv1hip_fetch)
+  struct LastBatch {
+    bool valid = false;
+    const uint8_t* frames = nullptr;
+    int64_t frame_bytes = 0;
+    int64_t plane_off[3]{};
+    int plane_stride[3]{};
+    int n = 0;
+    hipStream_t st = nullptr;
+    int64_t pn0 = 0;
+    bool have0 = false;
+    int pcur0 = 0, buf0 = 0, status_set = 0;
+  } last;
   int last_n = 0;
   std::vector<int> last_keys;
   bool profiling = false;
@@ -483,8 +506,8 @@ static void build_ops(ffv1hip_ctx* c) {
 
 static void free_device(ffv1hip_ctx* c) {
   void* ptrs[] = {c->d_frames, c->d_qt, c->d_tabs, c->d_ops, c->d_nops, c->d_segs, c->d_keys,
-                  c->d_slice_out, c->d_slice_bytes, c->d_packets, c->d_packet_size, c->d_persist,
-                  c->d_tables, c->d_sym, c->d_keys2, c->d_cbits, c->d_dcount, c->d_dbase, c->d_dtotal, c->d_pre[0],
+                  c->d_slice_out, c->d_slice_bytes, c->d_packets, c->d_packet_size, c->d_persist[0],
+                  c->d_persist[1], c->d_tables, c->d_sym, c->d_keys2, c->d_cbits, c->d_dcount, c->d_dbase, c->d_dtotal, c->d_pre[0],
                   c->d_pre[1], c->d_bits[0], c->d_bits[1], c->d_scratch, c->d_geom, c->d_slot_frames, c->d_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -493,6 +516,8 @@ static void free_device(ffv1hip_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t& e : c->kev)
     if (e) (void)hipEventDestroy(e);
+  if (c->dep_ev) (void)hipEventDestroy(c->dep_ev);
+  if (c->done_ev) (void)hipEventDestroy(c->done_ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->code_stream) (void)hipStreamDestroy(c->code_stream);
   if (c->bits_stream) (void)hipStreamDestroy(c->bits_stream);
@@ -547,7 +572,12 @@ static int alloc_device(ffv1hip_ctx* c) {
   HIP_TRY(hipMalloc(&c->d_packets, size_t(c->packet_stride) * nb));
   HIP_TRY(hipMalloc(&c->d_packet_size, sizeof(int64_t) * nb));
   const size_t state_bytes = size_t(2) * c->contexts * 32;
-  HIP_TRY(hipMalloc(&c->d_persist, state_bytes * c->nslices));
+  for (uint8_t*& pb : c->d_persist) {
+    HIP_TRY(hipMalloc(&pb, state_bytes * c->nslices));
+    HIP_TRY(hipMemset(pb, 128, state_bytes * c->nslices));
+  }
+  HIP_TRY(hipEventCreateWithFlags(&c->dep_ev, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming));
   // the coder grid is padded to whole waves and idle lanes touch their own table
   if (c->frames_mode) {
     // double-buffered: the states walk of batch k+1 runs while batch k codes
@@ -581,8 +611,8 @@ static int alloc_device(ffv1hip_ctx* c) {
   HIP_TRY(hipMalloc(&c->d_geom, sizeof(SliceGeom) * c->nslices));
   HIP_TRY(hipMemcpy(c->d_geom, c->geom.data(), sizeof(SliceGeom) * c->nslices, hipMemcpyHostToDevice));
   HIP_TRY(hipMalloc(&c->d_slot_frames, sizeof(int) * size_t(c->max_slots) * (nb + 1)));
-  HIP_TRY(hipMalloc(&c->d_status, sizeof(int) * 4));
-  HIP_TRY(hipMemset(c->d_status, 0, sizeof(int) * 4));
+  HIP_TRY(hipMalloc(&c->d_status, sizeof(int) * 8));
+  HIP_TRY(hipMemset(c->d_status, 0, sizeof(int) * 8));
   return 0;
 }
 
@@ -650,6 +680,10 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
   // Slice byte budget: 4 bytes per coded sample (+4 KiB); real content codes
   // below 2 bytes per 16-bit sample.  Exceeding it reports -ENOSPC.
   c->slice_cap = ((max_nsym * 4 + 4096) + 255) & ~int64_t(255);
+  // FFV1HIP_SLICE_CAP (test hook): a small starting budget, to exercise the
+  // re-encode with a larger one (ffv1hip_fetch)
+  if (const char* e = std::getenv("FFV1HIP_SLICE_CAP"))
+    c->slice_cap = (std::max<int64_t>(256, std::atoll(e)) + 255) & ~int64_t(255);
   c->packet_stride = ((c->slice_cap + 16) * c->nslices + 255) & ~int64_t(255);
   // frame slots (segments) per call: one per GOP touched by the batch
   c->max_slots = p.gop_size > 1 ? std::min(max_batch_frames, (max_batch_frames + p.gop_size - 2) / p.gop_size + 1)
@@ -722,6 +756,25 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     return set_err(-22, "P-frame without preceding keyframe state");
   segs.front().load_states = !keys[0];
   segs.back().save_states = 1;
+  const int nsegs = int(segs.size());
+  if (nsegs > c->max_slots) return set_err(-22, "batch spans %d GOPs (max %d)", nsegs, c->max_slots);
+  // what to restore if this batch has to be encoded again (ffv1hip_fetch)
+  c->last.valid = true;
+  c->last.frames = d_frames;
+  c->last.frame_bytes = frame_bytes;
+  for (int k = 0; k < 3; k++) {
+    c->last.plane_off[k] = plane_off[k];
+    c->last.plane_stride[k] = plane_stride[k];
+  }
+  c->last.n = n;
+  c->last.st = st;
+  c->last.pn0 = c->picture_number;
+  c->last.have0 = c->have_states;
+  c->last.pcur0 = c->pcur;
+  c->last.buf0 = c->buf;
+  // the previous batch (possibly on another stream) is done with what this
+  // one rewrites first: segments, slot lists, keyflags, the persist buffer
+  if (c->dep_valid) HIP_TRY(hipStreamWaitEvent(st, c->dep_ev, 0));
   // frames mode: the coder stream may still be on the previous batch, so the
   // buffers it reads alternate between two sets; set fb was last read by the
   // coder of batch k-2, which must be done before this batch rewrites it
@@ -734,8 +787,6 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   HIP_TRY(hipMemcpyAsync(d_keys, keys.data(), n, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(c->d_segs, segs.data(), segs.size() * sizeof(Segment), hipMemcpyHostToDevice, st));
 
-  const int nsegs = int(segs.size());
-  if (nsegs > c->max_slots) return set_err(-22, "batch spans %d GOPs (max %d)", nsegs, c->max_slots);
   int maxlen = 0;
   for (const Segment& g : segs) maxlen = std::max(maxlen, g.nframes);
   std::vector<int> slot_frames(size_t(maxlen) * nsegs, -1);
@@ -785,12 +836,17 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   ca.tabs = c->d_tabs;
   ca.state_bytes = int64_t(2) * c->contexts * 32;
   ca.tables = c->d_tables;
-  ca.persist = c->d_persist;
+  ca.persist_in = c->d_persist[c->pcur];
+  ca.persist_out = c->d_persist[c->pcur ^ 1];
+  // overflow report of this batch (per buffer set: the coder of the
+  // previous batch may still write the other one)
+  const int sset = c->frames_mode ? fb : 0;
+  c->last.status_set = sset;
+  ca.status = c->d_status + 4 * sset;
   ca.slice_out = c->d_slice_out;
   ca.slice_cap = c->slice_cap;
   ca.slice_stride = c->slice_stride;
   ca.slice_bytes = c->d_slice_bytes;
-  ca.status = c->d_status;
   ca.version = p.version;
   ca.coded_bits = p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample;
 
@@ -868,7 +924,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     wa.segs = c->d_segs;
     wa.ftab = c->d_tabs + 512;
     wa.state_bytes = ca.state_bytes;
-    wa.persist = c->d_persist;
+    wa.persist_in = ca.persist_in;
+    wa.persist_out = ca.persist_out;
     wa.ds = ds;
     wa.scratch = c->d_scratch;
     // FFV1HIP_WALKDBG=1 (measurement hook): per-block cycle split to stderr
@@ -910,6 +967,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     static const bool codedbg = std::getenv("FFV1HIP_CODEDBG") && std::atoi(std::getenv("FFV1HIP_CODEDBG"));
     const int nwaves = int((int64_t(n) * c->nslices + 63) / 64);
     uint64_t* d_cdbg = nullptr;
+    HIP_TRY(hipMemsetAsync(ca.status, 0, sizeof(int) * 4, cst));
     if (codedbg) {
       HIP_TRY(hipMalloc(&d_cdbg, sizeof(uint64_t) * 4 * nwaves));
       HIP_TRY(hipMemsetAsync(d_cdbg, 0, sizeof(uint64_t) * 4 * nwaves, cst));
@@ -936,6 +994,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
                    nwaves, all / nwaves, mx, fl / all, all / dec, dec / nwaves, its / nwaves, fl / its);
     }
   } else {
+    HIP_TRY(hipMemsetAsync(ca.status, 0, sizeof(int) * 4, st));
     for (int j = 0; j < maxlen; j++) {
       sa.frame_of_slot = c->d_slot_frames + size_t(j) * nsegs;
       if (timed(0, st, [&] { return launch_symbols(sa, st); }) < 0)
@@ -965,6 +1024,10 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     HIP_TRY(hipEventRecord(c->coded[fb], cst));
     c->buf ^= 1;
   }
+  HIP_TRY(hipEventRecord(c->dep_ev, st));  // frames mode: after the states walk
+  HIP_TRY(hipEventRecord(c->done_ev, cst));
+  c->dep_valid = true;
+  c->pcur ^= 1;
 
   c->picture_number += n;
   c->have_states = true;
@@ -982,15 +1045,49 @@ int ffv1hip_encode_device(ffv1hip_ctx* c, const void* d_frames, int64_t frame_by
                    n_frames, stream ? reinterpret_cast<hipStream_t>(stream) : c->stream);
 }
 
+// A slice went over the byte budget: the reference would still have coded
+// it (its buffer is ~w*h*140 bytes, ffv1enc.c:1232), so the last batch is
+// rolled back (picture number, P-frame carry, buffer set) and encoded again
+// with a budget sized from what the slice needed.  The batch's input frames
+// must still be where the call found them.
+static int grow_slice_budget(ffv1hip_ctx* c, int64_t needed) {
+  const int64_t cap = ((needed + needed / 4 + 4096) + 255) & ~int64_t(255);
+  if (cap <= c->slice_cap) return set_err(-28, "slice byte budget %lld not enough", (long long)c->slice_cap);
+  HIP_TRY(hipDeviceSynchronize());
+  if (c->d_slice_out) HIP_TRY(hipFree(c->d_slice_out));
+  if (c->d_packets) HIP_TRY(hipFree(c->d_packets));
+  c->d_slice_out = nullptr;
+  c->d_packets = nullptr;
+  c->slice_cap = cap;
+  c->slice_stride = c->frames_mode ? 2 * cap : cap;
+  c->packet_stride = ((cap + 16) * c->nslices + 255) & ~int64_t(255);
+  if (hipMalloc(&c->d_slice_out, size_t(c->slice_stride) * c->nslices * c->max_batch) != hipSuccess ||
+      hipMalloc(&c->d_packets, size_t(c->packet_stride) * c->max_batch) != hipSuccess)
+    return set_err(-12, "slice buffers for a %lld-byte budget", (long long)cap);
+  return 0;
+}
+
 int ffv1hip_fetch(ffv1hip_ctx* c, uint8_t* out, int64_t out_cap, int64_t* sizes, int* key_flags) {
   if (!c) return set_err(-22, "null ctx");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipDeviceSynchronize());
-  int status[4];
-  HIP_TRY(hipMemcpy(status, c->d_status, sizeof(status), hipMemcpyDeviceToHost));
-  if (status[0]) {  // counted since the last fetch
-    HIP_TRY(hipMemset(c->d_status, 0, sizeof(status)));
-    return set_err(-28, "%d slices exceeded the slice byte budget", status[0]);
+  for (int attempt = 0;; attempt++) {
+    int status[4];
+    HIP_TRY(hipMemcpy(status, c->d_status + 4 * c->last.status_set, sizeof(status), hipMemcpyDeviceToHost));
+    if (!status[0]) break;
+    if (attempt >= 2 || !c->last.valid)
+      return set_err(-28, "%d slices exceeded the slice byte budget", status[0]);
+    const ffv1hip_ctx::LastBatch L = c->last;
+    c->picture_number = L.pn0;
+    c->have_states = L.have0;
+    c->pcur = L.pcur0;
+    c->buf = L.buf0;
+    c->dep_valid = false;  // synchronised above
+    int rc = grow_slice_budget(c, status[1]);
+    if (rc < 0) return rc;
+    rc = run_batch(c, L.frames, L.frame_bytes, L.plane_off, L.plane_stride, L.n, L.st);
+    if (rc < 0) return rc;
+    HIP_TRY(hipDeviceSynchronize());
   }
   const int n = c->last_n;
   std::vector<int64_t> sz(n);
@@ -1011,6 +1108,7 @@ int ffv1hip_fetch(ffv1hip_ctx* c, uint8_t* out, int64_t out_cap, int64_t* sizes,
 int ffv1hip_synchronize(ffv1hip_ctx* c) {
   if (!c) return set_err(-22, "null ctx");
   HIP_TRY(hipSetDevice(c->device));
+  if (c->dep_valid) HIP_TRY(hipEventSynchronize(c->done_ev));  // also a caller-given launch stream
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (c->code_stream) HIP_TRY(hipStreamSynchronize(c->code_stream));
   if (c->bits_stream) HIP_TRY(hipStreamSynchronize(c->bits_stream));
@@ -1110,7 +1208,7 @@ int64_t ffv1hip_get_slice_states(ffv1hip_ctx* c, uint8_t* buf, int64_t cap) {
   if (cap < n) return set_err(-22, "buffer too small");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(buf, c->d_persist, n, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(buf, c->d_persist[c->pcur], n, hipMemcpyDeviceToHost));
   return n;
 }
 
@@ -1128,7 +1226,7 @@ int ffv1hip_set_slice_states(ffv1hip_ctx* c, const uint8_t* buf, int64_t size) {
   if (size != n) return set_err(-22, "state blob is %lld bytes, expected %lld", (long long)size, (long long)n);
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(c->d_persist, buf, n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(c->d_persist[c->pcur], buf, n, hipMemcpyHostToDevice));
   c->have_states = true;
   return 0;
 }
@@ -1153,7 +1251,8 @@ struct ffv1hip_dec {
   int row_cap = 0;
   bool have_states = false;
   std::vector<SliceGeom> geom;
-  uint8_t* d_persist = nullptr;
+  uint8_t* d_persist[2] = {nullptr, nullptr};  // read [pcur], written [pcur ^ 1]
+  int pcur = 0;
   SliceGeom* d_geom = nullptr;
   int16_t* d_qt = nullptr;
   uint8_t* d_ftab = nullptr;
@@ -1162,7 +1261,8 @@ struct ffv1hip_dec {
 };
 
 static void dec_free(ffv1hip_dec* d) {
-  (void)hipFree(d->d_persist);
+  (void)hipFree(d->d_persist[0]);
+  (void)hipFree(d->d_persist[1]);
   (void)hipFree(d->d_geom);
   (void)hipFree(d->d_qt);
   (void)hipFree(d->d_ftab);
@@ -1238,7 +1338,8 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
   auto init = [&]() -> int {
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
-    HIP_TRY(hipMalloc(&d->d_persist, d->state_bytes * d->nslices));
+    HIP_TRY(hipMalloc(&d->d_persist[0], d->state_bytes * d->nslices));
+    HIP_TRY(hipMalloc(&d->d_persist[1], d->state_bytes * d->nslices));
     HIP_TRY(hipMalloc(&d->d_geom, sizeof(SliceGeom) * d->nslices));
     HIP_TRY(hipMalloc(&d->d_qt, sizeof(int16_t) * 3 * 256));
     HIP_TRY(hipMalloc(&d->d_ftab, 512));
@@ -1352,7 +1453,8 @@ int ffv1hip_decode(ffv1hip_dec* d, const uint8_t* packets, const int64_t* sizes,
     a.qt = d->d_qt;
     a.ftab = d->d_ftab;
     a.state_bytes = d->state_bytes;
-    a.persist = d->d_persist;
+    a.persist_in = d->d_persist[d->pcur];
+    a.persist_out = d->d_persist[d->pcur ^ 1];
     a.out = d_out;
     a.frame_bytes = d->frame_bytes;
     for (int k = 0; k < 3; k++) {
@@ -1395,6 +1497,7 @@ int ffv1hip_decode(ffv1hip_dec* d, const uint8_t* packets, const int64_t* sizes,
   (void)hipFree(d_segs);
   (void)hipFree(d_out);
   if (rc < 0) return rc;
+  d->pcur ^= 1;
   d->have_states = true;
   if (key_flags)
     for (int f = 0; f < n_frames; f++) key_flags[f] = keys[f];

@@ -121,12 +121,13 @@ struct CodeArgs {
   const uint8_t* tabs;        // [default to0|to1][frame to0|to1]
   int64_t state_bytes;        // 2 * contexts * 32
   uint8_t* tables;            // [chain][state_bytes] working context states (grid-padded)
-  uint8_t* persist;           // [slice][state_bytes]
+  const uint8_t* persist_in;  // [slice][state_bytes]: the carry the batch starts from
+  uint8_t* persist_out;       // [slice][state_bytes]: the carry it leaves (the other buffer)
   uint8_t* slice_out;         // [batch frame][slice][slice_stride]
   int64_t slice_cap;          // byte budget of a slice
   int64_t slice_stride;       // bytes per slice slot (decision-stream mode: 2 x slice_cap, for the digits)
   int64_t* slice_bytes;       // [batch frame][slice]
-  int* status;                // [0] overflow count
+  int* status;                // [0] slices over the byte budget, [1] most bytes a slice needed
   int version;                // bitstream version (Golomb: v3 adds a 129/0 decision)
   int coded_bits;             // "bits" of encode_line (8 for <=8-bit)
   int nframes;                // decision-stream mode: frames of the batch
@@ -151,7 +152,8 @@ struct WalkArgs {
   const Segment* segs;
   const uint8_t* ftab;        // frame transition table [bit][state]
   int64_t state_bytes;
-  uint8_t* persist;           // [slice][state_bytes]
+  const uint8_t* persist_in;  // [slice][state_bytes]
+  uint8_t* persist_out;       // [slice][state_bytes]
   DecisionStream ds;
   uint8_t* scratch;           // >= 2 KiB: where idle chains write their stage
   uint64_t* dbg;              // optional [block][4] cycle counters (FFV1HIP_WALKDBG)
@@ -193,7 +195,8 @@ struct DecodeArgs {
   const int16_t* qt;           // [3][256]
   const uint8_t* ftab;         // frame transition table: to0[256] | to1[256]
   int64_t state_bytes;         // 2 * contexts * 32
-  uint8_t* persist;            // [slice][state_bytes]: the chain carried across calls
+  const uint8_t* persist_in;   // [slice][state_bytes]: the chain carried across calls
+  uint8_t* persist_out;        // (two buffers: a launch never reads what it writes)
   uint8_t* out;                // [frame] regions of frame_bytes, planes tightly packed
   int64_t frame_bytes;
   int64_t plane_off[3];

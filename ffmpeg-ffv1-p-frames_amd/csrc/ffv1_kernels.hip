@@ -669,7 +669,7 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
   // context states: continue, or reset at a keyframe (ff_ffv1_clear_slice_state)
   if (live) {
     if (a.j == 0 && seg.load_states) {
-      const uint4* src = reinterpret_cast<const uint4*>(a.persist + (int64_t)slice * a.state_bytes);
+      const uint4* src = reinterpret_cast<const uint4*>(a.persist_in + (int64_t)slice * a.state_bytes);
       for (int64_t i = 0; i < a.state_bytes / 16; i++) reinterpret_cast<uint4*>(table)[i] = src[i];
     } else if (key) {
       const uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
@@ -752,10 +752,13 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
 
   if (live) {
     const int64_t nbytes = terminate(L, S, true, kRing);
-    if (nbytes > a.slice_cap) atomicAdd(a.status, 1);
-    a.slice_bytes[(int64_t)f * a.nslices + slice] = nbytes;
+    if (nbytes > a.slice_cap) {
+      atomicAdd(a.status, 1);
+      atomicMax(a.status + 1, (int)nbytes);
+    }
+    a.slice_bytes[(int64_t)f * a.nslices + slice] = min(nbytes, a.slice_cap);  // never past the slot
     if (a.j == seg.nframes - 1 && seg.save_states) {
-      uint4* dst = reinterpret_cast<uint4*>(a.persist + (int64_t)slice * a.state_bytes);
+      uint4* dst = reinterpret_cast<uint4*>(a.persist_out + (int64_t)slice * a.state_bytes);
       for (int64_t i = 0; i < a.state_bytes / 16; i++) dst[i] = reinterpret_cast<const uint4*>(table)[i];
     }
   }
@@ -920,8 +923,11 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_dcode(CodeArgs a) {
   }
   if (live) {
     const int64_t ndig = terminate(L, S, true, kDRing);
-    if (ndig > a.slice_stride / 2) atomicAdd(a.status, 1);
-    a.slice_bytes[st] = ndig;  // digits, until ffv1_sink
+    if (ndig > a.slice_stride / 2) {
+      atomicAdd(a.status, 1);
+      atomicMax(a.status + 1, (int)ndig);
+    }
+    a.slice_bytes[st] = min(ndig, a.slice_stride / 2);  // digits, until ffv1_sink; never past the slot
   }
 }
 
@@ -1153,7 +1159,7 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   {
     uint4* const t4 = reinterpret_cast<uint4*>(mytbl);
     if (seg.load_states && live) {
-      const uint4* src = reinterpret_cast<const uint4*>(a.persist + (int64_t)sl * a.state_bytes + goff);
+      const uint4* src = reinterpret_cast<const uint4*>(a.persist_in + (int64_t)sl * a.state_bytes + goff);
       for (int64_t i = k; i < n16; i += 32) t4[i] = src[i];
     } else {  // the segment starts at a keyframe (ff_ffv1_clear_slice_state)
       const uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
@@ -1315,7 +1321,7 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   copy_out();
   __builtin_amdgcn_wave_barrier();
   if (seg.save_states && live) {
-    uint4* dst = reinterpret_cast<uint4*>(a.persist + (int64_t)sl * a.state_bytes + goff);
+    uint4* dst = reinterpret_cast<uint4*>(a.persist_out + (int64_t)sl * a.state_bytes + goff);
     const uint4* t4 = reinterpret_cast<const uint4*>(mytbl);
     for (int64_t i = k; i < n16; i += 32) dst[i] = t4[i];
   }
@@ -1558,7 +1564,7 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
 
   if (live) {
     if (a.j == 0 && seg.load_states) {
-      const uint64_t* src = reinterpret_cast<const uint64_t*>(a.persist + (int64_t)slice * a.state_bytes);
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(a.persist_in + (int64_t)slice * a.state_bytes);
       for (int64_t i = 0; i < nrec; i++) table[i] = src[i];
     } else if (key) {
       for (int64_t i = 0; i < nrec; i++) table[i] = kVlcInit;  // ff_ffv1_clear_slice_state
@@ -1622,10 +1628,13 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
   }
   b.flush();
   const int64_t nbytes = b.pos;
-  if (nbytes > a.slice_cap) atomicAdd(a.status, 1);
-  a.slice_bytes[(int64_t)f * a.nslices + slice] = nbytes;
+  if (nbytes > a.slice_cap) {
+    atomicAdd(a.status, 1);
+    atomicMax(a.status + 1, (int)nbytes);
+  }
+  a.slice_bytes[(int64_t)f * a.nslices + slice] = min(nbytes, a.slice_cap);  // never past the slot
   if (a.j == seg.nframes - 1 && seg.save_states) {
-    uint64_t* dst = reinterpret_cast<uint64_t*>(a.persist + (int64_t)slice * a.state_bytes);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(a.persist_out + (int64_t)slice * a.state_bytes);
     for (int64_t i = 0; i < nrec; i++) dst[i] = table[i];
   }
 }

@@ -356,10 +356,16 @@ class AVCodecContext:
 class FFV1Encoder:
     """Mirror of ff_ffv1_encoder (ffv1enc.c:1415-1444), name "ffv1_hip".
 
-    ``encode2`` follows AV_CODEC_CAP_DELAY: frames are queued and encoded in
-    batches of ``batch`` on the GPU; a ``None`` frame drains the queue.  It
-    returns the list of packets made available by this call (the "got_packet"
-    outputs), in order, each with pts = dts = the frame's pts.
+    ``encode2(frame, pts)`` is AVCodec.encode2 (avcodec.h:3642-3643) under
+    AV_CODEC_CAP_DELAY, driven the way avcodec_encode_video2 drives it
+    (utils.c:1922-1990): each call hands over one frame (``None`` = flush)
+    and returns at most one packet (``got_packet``), or ``None``.  Frames
+    are queued and encoded on the GPU ``batch`` at a time, so the first
+    packet comes out with the batch-th frame and the encoder then returns
+    one packet per call; a ``None`` frame encodes what is queued and the
+    caller keeps flushing until ``None`` comes back (ffmpeg.c:1699-1776).
+    Every packet carries pts = dts = its frame's pts and the KEY flag
+    (ffv1enc.c:1365-1370).
     """
 
     name = "ffv1_hip"
@@ -370,12 +376,16 @@ class FFV1Encoder:
                 "yuv420p16", "yuv422p16", "yuv444p16", "gray16")
 
     def __init__(self, batch: int = 12, device: int = 0):
+        if batch < 1:
+            raise ValueError("batch must be >= 1")
         self.batch = batch
         self.device = device
         self.avctx: Optional[AVCodecContext] = None
         self.params: Optional[Params] = None
         self._enc: Optional[HipEncoder] = None
-        self._queue: List[Tuple[List[np.ndarray], int]] = []
+        self._queue: List[Tuple[List[np.ndarray], int]] = []   # frames not yet encoded
+        self._ready: List[AVPacket] = []                        # packets not yet returned
+        self._frames_in = 0
 
     def init(self, avctx: AVCodecContext) -> int:
         self.avctx = avctx
@@ -387,27 +397,31 @@ class FFV1Encoder:
         avctx.extradata = self._enc.extradata()
         return 0
 
-    def encode2(self, frame: Optional[Sequence[np.ndarray]], pts: Optional[int] = None) -> List[AVPacket]:
+    def encode2(self, frame: Optional[Sequence[np.ndarray]], pts: Optional[int] = None) -> Optional[AVPacket]:
+        if self._enc is None:
+            raise FFV1Error(-22, "encode2 before init")
         if frame is not None:
             self._queue.append(([np.ascontiguousarray(p) for p in frame],
-                                pts if pts is not None else self._enc.picture_number + len(self._queue)))
-            if len(self._queue) < self.batch:
-                return []
-        return self._drain()
+                                pts if pts is not None else self._frames_in))
+            self._frames_in += 1
+            if len(self._queue) == self.batch:
+                self._encode_queue()
+        elif self._queue:
+            self._encode_queue()
+        return self._ready.pop(0) if self._ready else None
 
-    def _drain(self) -> List[AVPacket]:
-        if not self._queue:
-            return []
+    def _encode_queue(self) -> None:
         frames = [f for f, _ in self._queue]
         pts = [p for _, p in self._queue]
         self._queue = []
         out = self._enc.encode(frames)
-        return [AVPacket(d, t, t, k) for (d, k), t in zip(out, pts)]
+        self._ready += [AVPacket(d, t, t, k) for (d, k), t in zip(out, pts)]
 
     def close(self) -> int:
         if self._enc is not None:
             self._enc.close()
             self._enc = None
+        self._queue, self._ready = [], []
         return 0
 
 

@@ -35,6 +35,7 @@ def encode_shard(encoder_factory: Callable[[], object], frames: Callable[[int], 
     for start, end in ranges:
         enc = encoder_factory()
         pk = enc.encode([frames(i) for i in range(start, end)])
+        _close(enc)
         for i, p in zip(range(start, end), pk):
             out[i] = p
     return out
@@ -112,6 +113,8 @@ def encode_exchanged(encoder_factory: Callable[[], object], frames: Callable[[in
         last_states = enc.get_slice_states()
         if send_next:
             send(last_states)
+        _close(enc)  # one encoder's device buffers at a time
+        enc = None
     if lo < first_key:  # head: continue rank-1's chain
         buf = to_tensor(np.zeros(state_bytes, np.uint8))
         dist.recv(buf, src=rank - 1)
@@ -121,4 +124,11 @@ def encode_exchanged(encoder_factory: Callable[[], object], frames: Callable[[in
             out[i] = p
         if first_key == hi and send_next:  # no keyframe in the range: pass the chain on
             send(enc.get_slice_states())
+        _close(enc)
     return out
+
+
+def _close(enc):
+    close = getattr(enc, "close", None)
+    if close is not None:
+        close()

@@ -716,8 +716,10 @@ ffv1o_enc *ffv1o_enc_new(const ffv1o_config *cfg)
         slice_rects(cfg, i, &s->x0, &s->y0, &s->w, &s->h);
         if ((int64_t)s->w * s->h > maxw)
             maxw = (int64_t)s->w * s->h;
-        /* generous per-slice budget: header + <=35 bytes per sample line */
-        s->cap = 4096 + (int64_t)s->w * s->h * 6 + (int64_t)s->w * 35 * 2;
+        /* the reference's slice buffer: pkt->size / slice_count of a packet
+         * of AV_INPUT_BUFFER_MIN_SIZE + w*h*140 bytes (ffv1enc.c:1232-1233,
+         * 1317-1322); malloc'd pages are only touched as far as used */
+        s->cap = (16384 + (int64_t)cfg->width * cfg->height * 140) / e->nslices;
         s->buf = malloc(s->cap);
         for (int p = 0; p < 2; p++) {
             s->ps[p].rac = malloc((size_t)e->contexts * 32);

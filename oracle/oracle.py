@@ -134,7 +134,7 @@ class Encoder:
         arr, strides = _plane_ptrs(planes)
         cap = 1 << 20
         for p in planes:
-            cap += p.nbytes * 2
+            cap += p.nbytes * 20  # <= 33 decisions (bytes) per 16-bit sample
         out = np.empty(cap, np.uint8)
         key = ctypes.c_int()
         n = lib().ffv1o_enc_frame(self._h, arr, strides, _u8p(out), cap, ctypes.byref(key))

@@ -1,0 +1,112 @@
+"""The N>1 path with the HIP encoder: GOP sharding and the exchange step
+under torch.distributed, several processes on cuda:0 (gloo for the
+messages; the driver's 8-GPU bench uses one process per GPU over RCCL).
+
+Both must reproduce the reference's own config-3 stream: 24 frames of 4K
+yuv420p10, 64 slices, g=12, MD5 08e3975d... (tests/golden/known_answers.json),
+i.e. sharding and state forwarding change nothing in the bitstream
+(GOP independence ffv1enc.c:1171-1172; the P-frame carry ffv1enc.c:1299).
+"""
+import hashlib
+import os
+import socket
+import sys
+
+import pytest
+
+from helpers import load_golden
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+W, H, N, GOP = 3840, 2160, 24, 12
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _pin():
+    return next(p for p in load_golden("known_answers.json")["streams"]
+                if p["name"] == "config3_4k_yuv420p10_coder1_slices64_g12")
+
+
+class _Enc:
+    """HipEncoder with the interface parallel.py expects."""
+
+    def __init__(self):
+        from ffv1hip import HipEncoder, configure
+        self.e = HipEncoder(configure(W, H, "yuv420p10", slices=64, coder=1, gop_size=GOP), 0, GOP)
+
+    def encode(self, frames):
+        out = []
+        for i in range(0, len(frames), GOP):
+            out += self.e.encode(frames[i:i + GOP])
+        return out
+
+    def get_slice_states(self):
+        return self.e.get_slice_states()
+
+    def set_slice_states(self, buf, pn):
+        self.e.set_slice_states(buf, pn)
+
+    def close(self):
+        self.e.close()
+
+
+def _worker(mode, rank, world, port, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "ffmpeg-ffv1-p-frames_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from ffv1hip import parallel, synth
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        frames = list(synth.videogen_frames(W, H, N, depth=10))
+        if mode == "shard":
+            mine = parallel.shard_gops(N, GOP, world, rank)
+            local = parallel.encode_shard(_Enc, lambda i: frames[i], mine)
+        else:
+            e = _Enc()
+            state_bytes = e.get_slice_states().size
+            e.close()
+            local = parallel.encode_exchanged(
+                _Enc, lambda i: frames[i], N, GOP, dist, rank, world,
+                to_tensor=lambda a: torch.from_numpy(np.array(a, np.uint8)),
+                from_tensor=lambda t: t.numpy(), state_bytes=state_bytes)
+        got = parallel.gather_packets(local, N, dist, rank, world)
+        if rank == 0:
+            h = hashlib.md5()
+            for p, _ in got:
+                h.update(p)
+            q.put((h.hexdigest(), [k for _, k in got]))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode,world", [("shard", 2), ("exchange", 3)])
+def test_hip_multiprocess_stream_matches_reference_pin(mode, world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(mode, r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        digest, keys = q.get(timeout=240)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.exitcode is None:
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs)
+    assert keys == [i % GOP == 0 for i in range(N)]
+    assert digest == _pin()["stream_md5"]

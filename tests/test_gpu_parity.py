@@ -147,3 +147,88 @@ def test_state_forwarding_between_contexts(split):
     b.close()
     assert head + tail == ref
     assert [k for _, k in head + tail] == [True] + [False] * 8
+
+
+def test_batch_ending_in_one_frame_segment():
+    """A batch that starts mid-GOP (its first segment loads the carried
+    states) and ends with a one-frame segment (which saves them): load and
+    save of one slice in one launch go to different buffers."""
+    from ffv1hip import HipEncoder
+    s = Stream("seg1", 320, 180, "yuv420p10", 11, slices=6, gop_size=4, source="d2", depth=10)
+    frames = list(s.frames())
+    _, _, ref = oracle_encode(s, frames)
+    enc = HipEncoder(hip_params(s), 0, 5)
+    got = []
+    for a, b in [(0, 2), (2, 5), (5, 9), (9, 11)]:  # [2,3]+[4], [5,6,7]+[8], [9,10]
+        got += enc.encode(frames[a:b])
+    enc.close()
+    assert got == ref
+
+
+@pytest.mark.parametrize("coder", ["frames", "chain"])
+def test_slice_budget_overflow_reencodes(coder, monkeypatch):
+    """A slice over the byte budget is encoded again with a larger budget
+    (the reference codes it: its buffer is ~w*h*140 bytes, ffv1enc.c:1232),
+    with the P-frame carry rolled back: the stream equals the oracle's."""
+    monkeypatch.setenv("FFV1HIP_SLICE_CAP", "512")
+    if coder == "chain":
+        monkeypatch.setenv("FFV1HIP_CODER", "chain")
+    s = PARITY_STREAMS[1]
+    frames = list(s.frames())
+    _, _, ref = oracle_encode(s, frames)
+    _, got = hip_encode(s, frames, batch=3)
+    assert got == ref
+
+
+@pytest.mark.parametrize("pix_fmt,bpr,nframes", [("yuv444p16", 12, 2), ("yuv444p16", 0, 1)])
+def test_full_entropy_noise_c4_shape(pix_fmt, bpr, nframes):
+    """Full-entropy noise at the config-4 shape (4K 4:4:4, 64 slices): the
+    most bytes per sample the path produces; equal to the oracle."""
+    import numpy as np
+    s = Stream("noise", 3840, 2160, pix_fmt, nframes, slices=64, gop_size=12, bits_per_raw_sample=bpr)
+    rng = np.random.default_rng(7)
+    shift = 16 - bpr if bpr else 0
+    frames = [[np.ascontiguousarray((rng.integers(0, 1 << (16 - shift), size=(2160, 3840)) << shift)
+                                    .astype(np.uint16)) for _ in range(3)] for _ in range(nframes)]
+    _, _, ref = oracle_encode(s, frames)
+    _, got = hip_encode(s, frames, batch=nframes)
+    assert [len(p) for p, _ in got] == [len(p) for p, _ in ref]
+    assert got == ref
+
+
+@pytest.mark.parametrize("batch", [12, 5])
+def test_avcodec_mirror_c3_known_answer(batch):
+    """FFV1Encoder's init / encode2 / encode2(NULL) / close (the AVCodec
+    callbacks of ff_ffv1_encoder, ffv1enc.c:1415-1444, driven the way
+    avcodec_encode_video2 drives them, utils.c:1922-1990) with
+    AV_CODEC_CAP_DELAY batching: the reference's config-3 stream, each
+    packet's pts/dts the frame's, KEY on every 12th."""
+    from ffv1hip import AVCodecContext, FFV1Encoder
+    pin = _pinned("config3_4k_yuv420p10_coder1_slices64_g12")
+    s = Stream("c3", 3840, 2160, "yuv420p10", pin["frames"], slices=64, gop_size=12, depth=10)
+    avctx = AVCodecContext(3840, 2160, "yuv420p10", gop_size=12, slices=64, coder=1)
+    enc = FFV1Encoder(batch=batch)
+    assert enc.init(avctx) == 0
+    assert md5(avctx.extradata).startswith(pin["extradata_md5_prefix"])
+    pkts, got = [], []
+    for i, f in enumerate(s.frames()):
+        pk = enc.encode2(f, pts=1000 + i)  # at most one packet per call
+        got.append(pk is not None)
+        if pk is not None:
+            pkts.append(pk)
+    while True:  # flush: NULL frames until no packet comes back
+        pk = enc.encode2(None)
+        if pk is None:
+            break
+        pkts.append(pk)
+    assert enc.close() == 0
+    assert len(pkts) == pin["frames"]
+    n = pin["frames"]
+    assert got == [i >= batch - 1 for i in range(n)]  # the delay: batch - 1 frames
+    assert [p.pts for p in pkts] == [1000 + i for i in range(len(pkts))]
+    assert [p.dts for p in pkts] == [p.pts for p in pkts]
+    assert [p.key for p in pkts] == [i % 12 == 0 for i in range(len(pkts))]
+    h = hashlib.md5()
+    for p in pkts:
+        h.update(p.data)
+    assert h.hexdigest() == pin["stream_md5"]
