@@ -27,6 +27,11 @@ def _synth():
         L.ffv1syn_clip_free.argtypes = [ctypes.c_void_p]
         L.ffv1syn_clip_next.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8)]
         L.ffv1syn_clip_next.restype = ctypes.c_int
+        L.ffv1syn_roto_new.argtypes = [ctypes.POINTER(ctypes.c_uint8), ctypes.c_int, ctypes.c_int]
+        L.ffv1syn_roto_new.restype = ctypes.c_void_p
+        L.ffv1syn_roto_free.argtypes = [ctypes.c_void_p]
+        L.ffv1syn_roto_next.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8)]
+        L.ffv1syn_roto_next.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -55,6 +60,38 @@ class VideogenClip:
         return [y, u, v]
 
 
+class RotozoomClip:
+    """The reference's "vsynth2" clip (tests/rotozoom.c), yuv420p u8 frames.
+
+    ``pnm`` is the 256x256 RGB24 source picture as a binary PPM (the
+    reference keeps it as tests/reference.pnm; a copy is a test fixture under
+    tests/golden/).
+    """
+
+    def __init__(self, pnm: bytes, width: int = 352, height: int = 288):
+        if len(pnm) < 15 + 256 * 256 * 3:
+            raise ValueError("rotozoom needs a 256x256 binary PPM")
+        self.w, self.h = width, height
+        self._src = np.frombuffer(pnm, np.uint8)[15:15 + 256 * 256 * 3].copy()
+        self._h = _synth().ffv1syn_roto_new(
+            self._src.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), width, height)
+        if not self._h:
+            raise ValueError("rotozoom needs even dimensions")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _synth().ffv1syn_roto_free(self._h)
+            self._h = None
+
+    def next_yuv420p(self):
+        n = self.w * self.h
+        buf = np.empty(n * 3 // 2, np.uint8)
+        _synth().ffv1syn_roto_next(self._h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+        return [buf[:n].reshape(self.h, self.w),
+                buf[n:n + n // 4].reshape(self.h // 2, self.w // 2),
+                buf[n + n // 4:].reshape(self.h // 2, self.w // 2)]
+
+
 def widen(planes, depth: int):
     """u8 planes -> u16 planes holding v << (depth - 8) (swscale shiftonly)."""
     return [np.ascontiguousarray(p.astype(np.uint16) << (depth - 8)) for p in planes]
@@ -66,6 +103,33 @@ def upsample_444(planes):
     h, w = y.shape
     up = lambda c: np.ascontiguousarray(np.repeat(np.repeat(c, 2, 0), 2, 1)[:h, :w])
     return [y, up(u), up(v)]
+
+
+def upsample_422(planes):
+    """yuv420p -> yuv422p by row repetition (swscale SWS_POINT: chroma row y>>1)."""
+    y, u, v = planes
+    h = y.shape[0]
+    return [y] + [np.ascontiguousarray(np.repeat(c, 2, 0)[:h]) for c in (u, v)]
+
+
+def convert(planes, pix_fmt: str):
+    """yuv420p u8 -> ``pix_fmt`` as the FATE vsynth tests convert their input
+    (``-sws_flags neighbor+bitexact``, tests/fate/vcodec.mak:116-124):
+    point-sampled chroma (libswscale/utils.c:344-359 with the default chroma
+    positions of :284-291 gives source index i>>1) and the depth change of the
+    15/19-bit intermediates (v << 7 >> 5, v << 11 >> 3: ``v << (depth - 8)``).
+    """
+    table = {"yuv420p": (None, 8), "yuv420p10": (None, 10), "yuv420p16": (None, 16),
+             "yuv422p": (upsample_422, 8), "yuv422p10": (upsample_422, 10),
+             "yuv422p16": (upsample_422, 16), "yuv444p": (upsample_444, 8),
+             "yuv444p10": (upsample_444, 10), "yuv444p16": (upsample_444, 16)}
+    if pix_fmt not in table:
+        raise ValueError(f"no FATE conversion to {pix_fmt}")
+    up, depth = table[pix_fmt]
+    f = up(planes) if up else list(planes)
+    if depth > 8:
+        f = widen(f, depth)
+    return [np.ascontiguousarray(p) for p in f]
 
 
 def videogen_frames(width: int, height: int, n: int, depth: int = 8, chroma444: bool = False):
