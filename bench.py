@@ -10,9 +10,14 @@ made resident in HBM before timing.
 
 A "step" = one pass of the encoder over a batch of --gops GOPs (12 frames
 each) already in HBM: slice coding + packet assembly, packets left in HBM.
-Multi-GPU: one process per GPU, each encodes its own GOPs (GOPs are
-independent: keyframes reset every context state), no data-path collective;
-value = all frames of all ranks / max-over-ranks time.
+Multi-GPU: one process per GPU over ONE clip of N x gops GOPs: rank r encodes
+GOPs r, r+N, r+2N, ... (GOPs are independent: keyframes reset every context
+state, ffv1enc.c:1171-1172), no data-path collective; value = all frames of
+all ranks / max-over-ranks time.  After the timed steps the per-GOP packet
+digests are gathered on rank 0 (a digest of the first 21 GOPs that does not
+depend on N), the packets of the pinned frames are gathered from the ranks
+that own them and checked against the reference's MD5, and every rank
+decodes its own packets with the GPU decoder.
 """
 from __future__ import annotations
 
@@ -76,12 +81,13 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_frames(n, data):
+def make_frames(n_total, data, keep):
+    """The frames i < n_total of the clip with keep(i) (the others skipped)."""
     from ffv1hip import synth
     if data == "d1":
-        gen = synth.videogen_frames(W, H, n, depth=DEPTH, chroma444=C444)
+        gen = synth.videogen_frames(W, H, n_total, depth=DEPTH, chroma444=C444, keep=keep)
     else:
-        gen = synth.d2_frames(W, H, n, depth=DEPTH, chroma444=C444)
+        gen = synth.d2_frames(W, H, n_total, depth=DEPTH, chroma444=C444, keep=keep)
     return [f for f in gen]
 
 
@@ -93,12 +99,24 @@ def pack_batch(frames, frame_bytes):
     return buf
 
 
+def cpu_threads():
+    """The host cores this process may use: the affinity mask, capped at the
+    box's CPU share for one GPU (OMP_NUM_THREADS, 16 on the GPU boxes)."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(avail, share) if share > 0 else avail)
+
+
 def cpu_baseline(frames, threads):
     """The CPU oracle (a port of the reference encoder, oracle/) on host cores.
 
-    Bounded sample: GOP-sharded threads, each encoding the first 3 frames
-    (1 key + 2 P) of the batch with its own encoder, plus a 1-thread run of
-    the same 3 frames.  ctypes drops the GIL, so threads run in parallel.
+    GOP-sharded, the strongest CPU configuration: each worker
+    thread encodes one whole GOP of the batch (1 key + 11 P frames) with its
+    own encoder; ctypes drops the GIL, so the threads run in parallel.  Plus a
+    one-thread run of one GOP.  Bounded sample: one GOP per thread.
     """
     sys.path.insert(0, ROOT)
     from oracle import oracle
@@ -108,44 +126,49 @@ def cpu_baseline(frames, threads):
     else:
         cfg = oracle.configure(W, H, PIX_FMT, slices=SLICES, coder=1, gop_size=GOP,
                                bits_per_raw_sample=BPR)
-    sample = frames[:3]
+    per = max(GOP, 1)
+    ngops = len(frames) // per
+    threads = max(1, min(threads, ngops))
 
-    def one():
+    def one(g):
         enc = oracle.Encoder(cfg)
-        for f in sample:
+        for f in frames[g * per:(g + 1) * per]:
             enc.encode(f)
 
     t0 = time.perf_counter()
-    one()
-    t1 = time.perf_counter()
-    single = len(sample) * W * H / (t1 - t0) / 1e6
-    ths = [threading.Thread(target=one) for _ in range(threads)]
+    one(0)
+    single = per * W * H / (time.perf_counter() - t0) / 1e6
+    ths = [threading.Thread(target=one, args=(g,)) for g in range(threads)]
     t0 = time.perf_counter()
     for t in ths:
         t.start()
     for t in ths:
         t.join()
-    t1 = time.perf_counter()
-    multi = threads * len(sample) * W * H / (t1 - t0) / 1e6
+    multi = threads * per * W * H / (time.perf_counter() - t0) / 1e6
     return {
         "value": round(multi, 3), "unit": "Mpixels/s", "cores": threads, "kind": "port",
-        "sample": f"{threads} threads x 3 frames (one GOP each) of the same {W}x{H} {PIX_FMT} "
+        "sample": f"{threads} threads x 1 GOP ({per} frames) each of the same {W}x{H} {PIX_FMT} "
                   f"clip, oracle/ffv1_oracle.c, GOP-sharded",
-        "single_thread": {"value": round(single, 3), "cores": 1, "sample": "3 frames"},
+        "host_cpus": os.cpu_count(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+        "single_thread": {"value": round(single, 3), "cores": 1, "sample": f"1 GOP ({per} frames)"},
+        "port_vs_reference": "the port runs at ~0.6x the reference ffmpeg single-threaded on the "
+                             "same 8-core host (12 vs 20.1 Mpix/s, BASELINE.md / DESIGN.md)",
     }
 
 
-def load_traffic(frames_per_step):
-    """HBM bytes per launch of ffv1_encode_slices from the committed PMC profile."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
-        return None
-    try:
-        d = json.load(open(path))
+def load_traffic(frames_per_step, kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC profile of the
+    same configuration and batch (profiles/pmc_traffic*.json), else None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json"))):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
         if d.get("frames_per_launch") == frames_per_step and d.get("config") == f"{W}x{H} {PIX_FMT}":
-            return d.get("encode_hbm_bytes_per_launch")
-    except Exception:
-        return None
+            k = d.get("kernels", {}).get(kernel)
+            if k:
+                return k.get("hbm_bytes")
     return None
 
 
@@ -161,7 +184,8 @@ def main():
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c3",
                     help="BASELINE config: c3 (the metric's, default), c2, c4, c5")
     ap.add_argument("--data", choices=("d1", "d2"), default="d1")
-    ap.add_argument("--cpu-threads", type=int, default=8)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (default: this process's cores, capped at OMP_NUM_THREADS)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-decode-check", action="store_true",
                     help="skip decoding the last step's packets with the GPU decoder")
@@ -177,11 +201,19 @@ def main():
     import torch
     from ffv1hip import HipEncoder, configure
 
+    # FFV1_BENCH_ONE_DEVICE=1 (rehearsal on a one-GPU box): every rank on
+    # device 0, gloo instead of RCCL for the barrier / max / gather
+    one_dev = os.environ.get("FFV1_BENCH_ONE_DEVICE") == "1"
+    if one_dev:
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if one_dev:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     B = args.gops * GOP
     params = hip_configure()
@@ -191,16 +223,19 @@ def main():
     offs = [0, plane_bytes[0], plane_bytes[0] + plane_bytes[1]]
     strides = [shapes[k][1] * params.sample_bytes for k in range(3)]
 
+    # one clip of world x gops GOPs; this rank's are GOPs rank, rank+world, ...
+    my_gops = [rank + world * j for j in range(args.gops)]
     t0 = time.perf_counter()
-    frames = make_frames(B, args.data)
+    frames = make_frames(world * B, args.data, keep=lambda i: (i // GOP) % world == rank)
+    assert len(frames) == B
     host = pack_batch(frames, frame_bytes)
     d_frames = torch.from_numpy(host).to(f"cuda:{local_rank}")
     del host
     torch.cuda.synchronize()
-    log(f"[rank {rank}] {B} frames generated and resident in HBM in {time.perf_counter() - t0:.1f}s")
+    log(f"[rank {rank}] {B} frames (GOPs {my_gops[0]}, {my_gops[0] + world}, ...) generated and "
+        f"resident in HBM in {time.perf_counter() - t0:.1f}s")
 
     enc = HipEncoder(params, device=local_rank, max_batch=B)
-    enc.set_profiling(True)
 
     def step():
         enc.encode_device(d_frames.data_ptr(), frame_bytes, offs, strides, B)
@@ -224,28 +259,53 @@ def main():
     enc.synchronize()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    stats = [enc.last_kernel_stats()]
+    stats = enc.last_kernel_stats()
     if dist:
         dist.barrier()
-        t = torch.tensor([elapsed], device=f"cuda:{local_rank}", dtype=torch.float64)
+        t = torch.tensor([elapsed], device="cpu" if one_dev else f"cuda:{local_rank}", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # packets of the last step (outside the timed region): size + bit-exactness
+    # packets of the last step (outside the timed region): this rank's GOPs
     pkts = enc.fetch(B)
     out_bytes = sum(len(p) for p, _ in pkts)
-    bitexact = None
-    pin = CFG["PIN"]
-    if args.data == "d1" and pin and B >= pin[1]:
+    gop_digest = {}
+    for j, g in enumerate(my_gops):
         h = hashlib.md5()
-        for p, _ in pkts[:pin[1]]:
+        for p, _ in pkts[j * GOP:(j + 1) * GOP]:
+            h.update(p)
+        gop_digest[g] = (h.hexdigest(), sum(len(p) for p, _ in pkts[j * GOP:(j + 1) * GOP]))
+    pin = CFG["PIN"]
+    pin_gops = set(range((pin[1] + GOP - 1) // GOP)) if (pin and args.data == "d1") else set()
+    pin_pkts = {g: [p for p, _ in pkts[j * GOP:(j + 1) * GOP]] for j, g in enumerate(my_gops)
+                if g in pin_gops}
+    if dist:
+        # the exchange after the encode: per-GOP digests from every rank, and
+        # the packets of the pinned frames from the ranks that own them
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (gop_digest, out_bytes, pin_pkts))
+    else:
+        gathered = [(gop_digest, out_bytes, pin_pkts)]
+    all_digest, all_pins, total_out = {}, {}, 0
+    for d, ob, pp in gathered:
+        all_digest.update(d)
+        all_pins.update(pp)
+        total_out += ob
+    bitexact = None
+    if pin_gops and all(g in all_pins for g in pin_gops):
+        h = hashlib.md5()
+        stream = [p for g in sorted(pin_gops) for p in all_pins[g]][:pin[1]]
+        for p in stream:
             h.update(p)
         bitexact = h.hexdigest() == pin[0]
+    n_all = len(all_digest)
+    first = min(n_all, CFG["GOPS"])
+    digest_first = hashlib.md5("".join(all_digest[g][0] for g in range(first)).encode()).hexdigest()
 
-    # on-device lossless self-check (outside the timed region, rank 0): the
-    # GPU decoder (ffv1_decode_slices) decodes the last step's packets
+    # on-device lossless self-check (outside the timed region, every rank on
+    # its own packets): the GPU decoder (ffv1_decode_slices)
     decode = None
-    if not args.no_decode_check and rank == 0:
+    if not args.no_decode_check:
         from ffv1hip import HipDecoder
         dec = HipDecoder(params, enc.extradata(), local_rank)
         td = time.perf_counter()
@@ -255,30 +315,35 @@ def main():
         lossless = all(k == key and all(np.array_equal(a, b) for a, b in zip(planes, f))
                        for (planes, k), (_, key), f in zip(got, pkts, frames))
         del got
-        decode = {"frames": B, "lossless": lossless, "seconds": round(td, 3),
-                  "mpix_s": round(B * W * H / td / 1e6, 2),
-                  "note": "ffv1hip_decode incl. H2D of the packets and D2H of the frames"}
+        if dist:
+            t = torch.tensor([1 if lossless else 0], device="cpu" if one_dev else f"cuda:{local_rank}",
+                             dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            lossless = bool(t.item())
+        decode = {"frames": B * world, "lossless": lossless, "seconds": round(td, 3),
+                  "mpix_s_per_gpu": round(B * W * H / td / 1e6, 2),
+                  "note": "ffv1hip_decode on every rank of its own packets, incl. H2D of the "
+                          "packets and D2H of the frames"}
         log(f"[rank {rank}] GPU decode self-check: {B} frames in {td:.2f}s, lossless={lossless}")
 
-    tot = stats[0]
     names = ("symbols", "layout", "bits", "states", "code", "sink", "assemble")
-    per_step = {k: tot[k + "_ms"] / args.steps for k in names}
-    launches = {k: tot[k + "_launches"] // args.steps for k in names}
-    code_ms = per_step["code"]
-    n_code = launches["code"]
+    per_step = {k: stats[k + "_ms"] / args.steps for k in names}
+    launches = {k: stats[k + "_launches"] // args.steps for k in names}
+    # Dominant kernel: the longest per step of the two serial chains, the
+    # states walk (ffv1_walk) and the range coder (ffv1_dcode): each is ONE
+    # launch per step over every frame of the batch.  Algorithmic bytes per
+    # launch: the input planes of the batch (3.0 B per luma
+    # pixel at 4:2:0 10 bit) + the packet bytes it produces.
+    dom = max(("states", "code"), key=lambda k: per_step[k] / max(launches[k], 1))
+    n_dom = max(launches[dom], 1)
     in_bytes = B * sum(plane_bytes)
-    # Dominant kernel: ffv1_dcode.  Frame-parallel mode: ONE launch per step
-    # codes every (frame, slice) stream of the batch.  Algorithmic bytes per
-    # launch: the input planes of the frames it codes (3.0 B
-    # per luma pixel at 4:2:0 10 bit) + the packet bytes they produce.
-    algo_per_launch = (in_bytes + out_bytes) / n_code
-    code_ms_per_launch = code_ms / n_code
-    achieved = algo_per_launch / (code_ms_per_launch * 1e-3) / 1e9
+    algo_per_launch = (in_bytes + out_bytes) / n_dom
+    ms_per_launch = per_step[dom] / n_dom
+    achieved = algo_per_launch / (ms_per_launch * 1e-3) / 1e9
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        ncpu = min(args.cpu_threads, os.cpu_count() or 1)
-        cpu = cpu_baseline(frames, ncpu)
+        cpu = cpu_baseline(frames, args.cpu_threads or cpu_threads())
 
     mpix = args.steps * B * W * H * world / elapsed / 1e6
     if rank == 0:
@@ -299,10 +364,13 @@ def main():
                 "workload": CFG["workload"],
                 "frames_per_step_per_gpu": B,
                 "gops_per_step_per_gpu": args.gops,
-                "parallelism": f"gop-sharded x{world}",
+                "parallelism": f"gop-sharded x{world} (rank r: GOPs r, r+{world}, ... of one clip)",
             },
-            "bits_per_pixel": round(out_bytes * 8 / (B * W * H), 4),
+            "bits_per_pixel": round(total_out * 8 / (B * world * W * H), 4),
             "bitexact_vs_reference_pin": bitexact,
+            "gop_digest": {"gops": n_all, f"first_{first}_gops_md5": digest_first,
+                           "note": "md5 over the per-GOP packet md5s in GOP order: the same for "
+                                   "every --gpus N (GOP bytes do not depend on the rank)"},
             # kernels of the overlapped pipelines: symbols -> layout -> walk
             # (batch k+1), bits beside the walk, dcode -> sink -> assemble (batch k)
             "kernel_ms_per_step": dict(
@@ -310,14 +378,14 @@ def main():
                 launches={KERNEL[k]: launches[k] for k in names}),
             "roofline": {
                 "bound": "hbm",
-                "kernel": "ffv1_dcode",
+                "kernel": KERNEL[dom],
                 "achieved": round(achieved, 3),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
-                "traffic": load_traffic(B),
+                "traffic": load_traffic(B, KERNEL[dom]),
                 "algorithmic_bytes_per_launch": int(algo_per_launch),
-                "avg_launch_ms": round(code_ms_per_launch, 3),
+                "avg_launch_ms": round(ms_per_launch, 3),
             },
             "cpu_baseline": cpu,
             "decode_selfcheck": decode,

@@ -313,6 +313,15 @@ struct ffv1hip_ctx {
   std::vector<int> kev_kind;    // per launch: 0 symbols, 1 code, 2 states, 3 assembly, 4 layout, 5 bits
   int nkev = 0;
   int last_nsegs = 0;
+  // ffv1hip_encode2 (AV_CODEC_CAP_DELAY): frames queued in d_frames slots
+  // 0..q_pts.size()-1, and encoded packets not yet handed out
+  std::vector<int64_t> q_pts;
+  struct Ready {
+    std::vector<uint8_t> data;
+    std::vector<int64_t> off, size, pts;
+    std::vector<int> key;
+    size_t next = 0;
+  } ready;
 };
 
 extern "C" {
@@ -1152,6 +1161,86 @@ int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides
       if (sizes) sizes[base + i] = local_sizes[i];
       used += local_sizes[i];
     }
+  }
+  return 0;
+}
+
+// The queued frames as one batch: encode, fetch the packets into `ready`.
+static int encode_queue(ffv1hip_ctx* c) {
+  const int n = int(c->q_pts.size());
+  const ffv1hip_params& p = c->P;
+  const int cw = -((-p.width) >> p.chroma_h_shift);
+  int64_t off[3] = {0, c->plane_bytes[0], c->plane_bytes[0] + c->plane_bytes[1]};
+  int pst[3] = {p.width * p.sample_bytes, cw * p.sample_bytes, cw * p.sample_bytes};
+  int rc = run_batch(c, c->d_frames, c->frame_bytes, off, pst, n, c->stream);
+  if (rc < 0) return rc;
+  std::vector<int64_t> sz(n);
+  std::vector<int> keys(n);
+  rc = ffv1hip_fetch(c, nullptr, 0, sz.data(), keys.data());  // sizes (and any budget re-encode)
+  if (rc < 0) return rc;
+  int64_t total = 0;
+  for (int64_t v : sz) total += v;
+  ffv1hip_ctx::Ready& R = c->ready;
+  R.data.resize(size_t(total));
+  rc = ffv1hip_fetch(c, R.data.data(), total, nullptr, nullptr);
+  if (rc < 0) return rc;
+  R.off.assign(n, 0);
+  for (int i = 1; i < n; i++) R.off[i] = R.off[i - 1] + sz[i - 1];
+  R.size.assign(sz.begin(), sz.end());
+  R.key.assign(keys.begin(), keys.end());
+  R.pts = c->q_pts;
+  R.next = 0;
+  c->q_pts.clear();
+  return 0;
+}
+
+int ffv1hip_encode2(ffv1hip_ctx* c, const void* const planes[3], const int strides[3], int64_t pts,
+                    uint8_t* out, int64_t out_cap, int64_t* size, int64_t* pts_out, int* key, int* got_packet) {
+  if (!c || !got_packet) return set_err(-22, "null argument");
+  *got_packet = 0;
+  HIP_TRY(hipSetDevice(c->device));
+  ffv1hip_ctx::Ready& R = c->ready;
+  if (planes) {
+    if (!strides) return set_err(-22, "null strides");
+    // the frame is copied into the next batch slot (the caller keeps
+    // ownership: it may reuse the buffer once the call returns)
+    const ffv1hip_params& p = c->P;
+    const int np = p.chroma_planes ? 3 : 1;
+    const int cw = -((-p.width) >> p.chroma_h_shift), ch = -((-p.height) >> p.chroma_v_shift);
+    const int64_t off[3] = {0, c->plane_bytes[0], c->plane_bytes[0] + c->plane_bytes[1]};
+    const int pst[3] = {p.width * p.sample_bytes, cw * p.sample_bytes, cw * p.sample_bytes};
+    const int64_t slot = int64_t(c->q_pts.size());
+    for (int k = 0; k < np; k++) {
+      if (!planes[k]) return set_err(-22, "null plane %d", k);
+      HIP_TRY(hipMemcpy2D(c->d_frames + slot * c->frame_bytes + off[k], pst[k], planes[k], strides[k], pst[k],
+                          k ? ch : p.height, hipMemcpyHostToDevice));
+    }
+    c->q_pts.push_back(pts);
+    // a full queue is encoded once the packets of the previous batch are out
+    if (int(c->q_pts.size()) == c->max_batch && R.next >= R.size.size()) {
+      const int rc = encode_queue(c);
+      if (rc < 0) return rc;
+    }
+  } else if (R.next >= R.size.size() && !c->q_pts.empty()) {  // flush: what is queued
+    const int rc = encode_queue(c);
+    if (rc < 0) return rc;
+  }
+  if (R.next >= R.size.size()) return 0;
+  const size_t i = R.next;
+  if (out) {
+    if (R.size[i] > out_cap) return set_err(-22, "packet of %lld bytes, buffer %lld", (long long)R.size[i],
+                                            (long long)out_cap);
+    std::memcpy(out, R.data.data() + R.off[i], size_t(R.size[i]));
+  }
+  if (size) *size = R.size[i];
+  if (pts_out) *pts_out = R.pts[i];
+  if (key) *key = R.key[i];
+  *got_packet = 1;
+  R.next++;
+  // the queue filled while packets were still being handed out
+  if (R.next >= R.size.size() && int(c->q_pts.size()) == c->max_batch) {
+    const int rc = encode_queue(c);
+    if (rc < 0) return rc;
   }
   return 0;
 }

@@ -86,11 +86,10 @@ void ffv1syn_clip_free(ffv1syn_clip *c)
     }
 }
 
-static void render(ffv1syn_clip *c)
+static void init_objects(ffv1syn_clip *c)
 {
-    const int num = c->frame, w = c->w, h = c->h;
-    if (num == 0)
-        for (int i = 0; i < 10; i++) {
+    const int w = c->w, h = c->h;
+    for (int i = 0; i < 10; i++) {
             vg_obj *o = &c->obj[i];
             o->x = vg_rand(&c->seed, w);
             o->y = vg_rand(&c->seed, h);
@@ -99,7 +98,23 @@ static void render(ffv1syn_clip *c)
             o->r = vg_rand(&c->seed, 256);
             o->g = vg_rand(&c->seed, 256);
             o->b = vg_rand(&c->seed, 256);
-        }
+    }
+}
+
+/* the objects' random walk after frame c->frame is drawn */
+static void move_objects(ffv1syn_clip *c)
+{
+    for (int i = 0; i < 10; i++) {
+        c->obj[i].x += (int)vg_rand(&c->seed, 21) - 10;
+        c->obj[i].y += (int)vg_rand(&c->seed, 21) - 10;
+    }
+}
+
+static void render(ffv1syn_clip *c)
+{
+    const int num = c->frame, w = c->w, h = c->h;
+    if (num == 0)
+        init_objects(c);
 
     /* panning gradient background */
     const int dx = vg_cos(num * 256 / 50) * 35;
@@ -134,9 +149,8 @@ static void render(ffv1syn_clip *c)
                 int b = o->b + vg_rand(&s, 50);
                 vg_plot(c, x + o->x, y + o->y, r, g, b);
             }
-        o->x += (int)vg_rand(&c->seed, 21) - 10;
-        o->y += (int)vg_rand(&c->seed, 21) - 10;
     }
+    move_objects(c);
 }
 
 /* BT.601 8-bit fixed point (FIX(x) = x * 256 rounded), 2x2 chroma average */
@@ -282,6 +296,16 @@ int ffv1syn_roto_next(ffv1syn_roto *r, uint8_t *out)
     rgb_to_yuv420(r->rgb, w, h, out, out + n, out + n + n / 4);
     r->frame++;
     return num;
+}
+
+/* Advance past the next frame without drawing it (the clip's only state
+ * across frames is the objects' random walk). */
+void ffv1syn_clip_skip(ffv1syn_clip *c)
+{
+    if (c->frame == 0)
+        init_objects(c);
+    move_objects(c);
+    c->frame++;
 }
 
 /* u8 -> u16 little-endian, v << shift (shift = depth - 8). */

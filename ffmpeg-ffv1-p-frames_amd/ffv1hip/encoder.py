@@ -60,7 +60,7 @@ EXPORTED_SYMBOLS = (
     "ffv1hip_abi_version", "ffv1hip_set_profiling", "ffv1hip_last_kernel_ms",
     "ffv1hip_last_kernel_stats", "ffv1hip_synchronize",
     "ffv1hip_dec_create", "ffv1hip_dec_destroy", "ffv1hip_decode", "ffv1hip_dec_reset",
-    "ffv1hip_set_picture_number",
+    "ffv1hip_set_picture_number", "ffv1hip_encode2",
 )
 
 
@@ -100,6 +100,9 @@ def load_library():
     L.ffv1hip_max_packet_size.restype = i64
     L.ffv1hip_encode.argtypes = [vp, P(vp), P(ctypes.c_int), ctypes.c_int, u8p, i64, P(i64), P(ctypes.c_int)]
     L.ffv1hip_encode.restype = ctypes.c_int
+    L.ffv1hip_encode2.argtypes = [vp, P(vp), P(ctypes.c_int), i64, u8p, i64, P(i64), P(i64),
+                                  P(ctypes.c_int), P(ctypes.c_int)]
+    L.ffv1hip_encode2.restype = ctypes.c_int
     L.ffv1hip_encode_device.argtypes = [vp, vp, i64, P(i64), P(ctypes.c_int), ctypes.c_int, vp]
     L.ffv1hip_encode_device.restype = ctypes.c_int
     L.ffv1hip_fetch.argtypes = [vp, u8p, i64, P(i64), P(ctypes.c_int)]
@@ -359,13 +362,14 @@ class FFV1Encoder:
     ``encode2(frame, pts)`` is AVCodec.encode2 (avcodec.h:3642-3643) under
     AV_CODEC_CAP_DELAY, driven the way avcodec_encode_video2 drives it
     (utils.c:1922-1990): each call hands over one frame (``None`` = flush)
-    and returns at most one packet (``got_packet``), or ``None``.  Frames
-    are queued and encoded on the GPU ``batch`` at a time, so the first
-    packet comes out with the batch-th frame and the encoder then returns
-    one packet per call; a ``None`` frame encodes what is queued and the
-    caller keeps flushing until ``None`` comes back (ffmpeg.c:1699-1776).
-    Every packet carries pts = dts = its frame's pts and the KEY flag
-    (ffv1enc.c:1365-1370).
+    and returns at most one packet (``got_packet``), or ``None``.  The
+    queueing is the library's (``ffv1hip_encode2``, the entry point an
+    AVCodec shim's encode2 forwards to): frames are encoded
+    on the GPU ``batch`` at a time, so the first packet comes out with the
+    batch-th frame and the encoder then returns one packet per call; a
+    ``None`` frame encodes what is queued and the caller keeps flushing until
+    ``None`` comes back (ffmpeg.c:1699-1776).  Every packet carries pts = dts
+    = its frame's pts and the KEY flag (ffv1enc.c:1365-1370).
     """
 
     name = "ffv1_hip"
@@ -383,9 +387,8 @@ class FFV1Encoder:
         self.avctx: Optional[AVCodecContext] = None
         self.params: Optional[Params] = None
         self._enc: Optional[HipEncoder] = None
-        self._queue: List[Tuple[List[np.ndarray], int]] = []   # frames not yet encoded
-        self._ready: List[AVPacket] = []                        # packets not yet returned
         self._frames_in = 0
+        self._out = None
 
     def init(self, avctx: AVCodecContext) -> int:
         self.avctx = avctx
@@ -395,33 +398,42 @@ class FFV1Encoder:
                                 avctx.allow_large_grid)
         self._enc = HipEncoder(self.params, self.device, self.batch)
         avctx.extradata = self._enc.extradata()
+        self._out = np.empty(self._enc.max_packet_size(), np.uint8)
         return 0
 
     def encode2(self, frame: Optional[Sequence[np.ndarray]], pts: Optional[int] = None) -> Optional[AVPacket]:
         if self._enc is None:
             raise FFV1Error(-22, "encode2 before init")
+        L = load_library()
+        ptrs = (ctypes.c_void_p * 3)()
+        strides = (ctypes.c_int * 3)()
+        keep = []
         if frame is not None:
-            self._queue.append(([np.ascontiguousarray(p) for p in frame],
-                                pts if pts is not None else self._frames_in))
+            np_planes = 3 if self.params.chroma_planes else 1
+            for k in range(3):
+                a = np.ascontiguousarray(frame[min(k, np_planes - 1)])
+                keep.append(a)
+                ptrs[k] = a.ctypes.data
+                strides[k] = a.strides[0]
+            if pts is None:
+                pts = self._frames_in
             self._frames_in += 1
-            if len(self._queue) == self.batch:
-                self._encode_queue()
-        elif self._queue:
-            self._encode_queue()
-        return self._ready.pop(0) if self._ready else None
-
-    def _encode_queue(self) -> None:
-        frames = [f for f, _ in self._queue]
-        pts = [p for _, p in self._queue]
-        self._queue = []
-        out = self._enc.encode(frames)
-        self._ready += [AVPacket(d, t, t, k) for (d, k), t in zip(out, pts)]
+        size, pts_out = ctypes.c_int64(), ctypes.c_int64()
+        key, got = ctypes.c_int(), ctypes.c_int()
+        rc = L.ffv1hip_encode2(self._enc._h, ptrs if frame is not None else None,
+                               strides if frame is not None else None, pts or 0, _u8p(self._out),
+                               self._out.size, ctypes.byref(size), ctypes.byref(pts_out),
+                               ctypes.byref(key), ctypes.byref(got))
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_encode2")
+        if not got.value:
+            return None
+        return AVPacket(self._out[:size.value].tobytes(), pts_out.value, pts_out.value, bool(key.value))
 
     def close(self) -> int:
         if self._enc is not None:
             self._enc.close()
             self._enc = None
-        self._queue, self._ready = [], []
         return 0
 
 

@@ -27,6 +27,7 @@ def _synth():
         L.ffv1syn_clip_free.argtypes = [ctypes.c_void_p]
         L.ffv1syn_clip_next.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8)]
         L.ffv1syn_clip_next.restype = ctypes.c_int
+        L.ffv1syn_clip_skip.argtypes = [ctypes.c_void_p]
         L.ffv1syn_roto_new.argtypes = [ctypes.POINTER(ctypes.c_uint8), ctypes.c_int, ctypes.c_int]
         L.ffv1syn_roto_new.restype = ctypes.c_void_p
         L.ffv1syn_roto_free.argtypes = [ctypes.c_void_p]
@@ -58,6 +59,11 @@ class VideogenClip:
         u = buf[n:n + n // 4].reshape(self.h // 2, self.w // 2)
         v = buf[n + n // 4:].reshape(self.h // 2, self.w // 2)
         return [y, u, v]
+
+    def skip(self, n: int = 1):
+        """Advance past n frames without drawing them."""
+        for _ in range(n):
+            _synth().ffv1syn_clip_skip(self._h)
 
 
 class RotozoomClip:
@@ -132,9 +138,15 @@ def convert(planes, pix_fmt: str):
     return [np.ascontiguousarray(p) for p in f]
 
 
-def videogen_frames(width: int, height: int, n: int, depth: int = 8, chroma444: bool = False):
+def videogen_frames(width: int, height: int, n: int, depth: int = 8, chroma444: bool = False,
+                    keep=None):
+    """n frames of the D1 clip; with ``keep`` (frame index -> bool) only the
+    kept frames are drawn and yielded, the others skipped."""
     clip = VideogenClip(width, height)
-    for _ in range(n):
+    for i in range(n):
+        if keep is not None and not keep(i):
+            clip.skip()
+            continue
         f = clip.next_yuv420p()
         if chroma444:
             f = upsample_444(f)
@@ -144,12 +156,13 @@ def videogen_frames(width: int, height: int, n: int, depth: int = 8, chroma444: 
 
 
 def d2_frames(width: int, height: int, n: int, depth: int = 10, chroma444: bool = False,
-              seed: int = 20261015):
+              seed: int = 20261015, keep=None):
     """SURVEY.md 8d "D2": smooth moving field + uniform noise, LSB-active.
 
     Y = clip(512 + 300 sin((x+8t)/97) cos((y-5t)/61) + U{-8..8}, 0, 1023)
     cb = 512 + 200 sin((x2+4t)/53); U = clip(cb + U{-4..4}); V = clip(1023-cb+U{-4..4})
-    Amplitudes scale by 2^(depth-10); samples are u16 (LSB aligned).
+    Amplitudes scale by 2^(depth-10); samples are u16 (LSB aligned).  With
+    ``keep``, skipped frames still draw their noise (the RNG stream is shared).
     """
     rng = np.random.Generator(np.random.PCG64(seed))
     scale = 2.0 ** (depth - 10)
@@ -160,10 +173,15 @@ def d2_frames(width: int, height: int, n: int, depth: int = 10, chroma444: bool 
     xs = np.arange(width, dtype=np.float64)[None, :]
     xc = np.arange(cw, dtype=np.float64)[None, :]
     for t in range(n):
+        ny = rng.integers(-8, 9, size=(height, width))
+        nu = rng.integers(-4, 5, size=(chh, cw))
+        nv = rng.integers(-4, 5, size=(chh, cw))
+        if keep is not None and not keep(t):
+            continue
         base = 512 + 300 * np.sin((xs + 8 * t) / 97) * np.cos((ys - 5 * t) / 61)
-        Y = np.rint(base * scale) + rng.integers(-8, 9, size=(height, width)) * scale
+        Y = np.rint(base * scale) + ny * scale
         cb = (512 + 200 * np.sin((xc + 4 * t) / 53)) * scale
         cb = np.broadcast_to(cb, (chh, cw))
-        U = np.rint(cb) + rng.integers(-4, 5, size=(chh, cw)) * scale
-        V = np.rint(maxv - cb) + rng.integers(-4, 5, size=(chh, cw)) * scale
+        U = np.rint(cb) + nu * scale
+        V = np.rint(maxv - cb) + nv * scale
         yield [np.ascontiguousarray(np.clip(p, 0, maxv).astype(np.uint16)) for p in (Y, U, V)]

@@ -89,6 +89,23 @@ int ffv1hip_encode(ffv1hip_ctx *ctx, const void *const *planes,
                    const int *strides, int n_frames, uint8_t *out,
                    int64_t out_cap, int64_t *sizes, int *key_flags);
 
+/* AVCodec.encode2 under AV_CODEC_CAP_DELAY, one frame per call the way
+ * avcodec_encode_video2 drives it (libavcodec/utils.c:1922-1990; the
+ * callback signature avcodec.h:3642-3643).  planes/strides: the frame's
+ * planes in HOST memory (copied before the call returns), or planes == NULL
+ * to flush (ffmpeg.c:1699-1776 passes NULL frames until no packet comes
+ * back).  Frames queue up to the context's max_batch_frames and are encoded
+ * together; each call then hands out at most one packet in input order, so
+ * the first packet comes with frame max_batch_frames (the encoder's delay is
+ * max_batch_frames - 1 frames).  A returned packet has pts = dts = its
+ * frame's pts and the key flag (ffv1enc.c:1365-1370).  out must hold
+ * ffv1hip_max_packet_size bytes.  *got_packet = 1 when a packet was
+ * written. */
+int ffv1hip_encode2(ffv1hip_ctx *ctx, const void *const planes[3],
+                    const int strides[3], int64_t pts, uint8_t *out,
+                    int64_t out_cap, int64_t *size, int64_t *pts_out,
+                    int *key, int *got_packet);
+
 /* Device-resident variant: frames already in HBM at d_frames + i*frame_bytes
  * with plane p at byte offset plane_offset[p] and row stride plane_stride[p].
  * The frames are read on `stream` (a hipStream_t, may be NULL: the context's
