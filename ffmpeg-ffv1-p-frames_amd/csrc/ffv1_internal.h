@@ -45,11 +45,13 @@ struct SliceGeom {
 };
 
 // Per walk chunk (64 consecutive samples of a plane), written by ffv1_symbols:
-// word 0 = the chunk's decisions | kChunkLong (a |diff| >= 1024 in it), words
+// word 0 = the chunk's decisions | kChunkLong / kChunkMulti flags, words
 // 1.. = the decision bits in coding order (bit d in word 1 + d / 32), then a
 // zero word.
 constexpr int kChunkWords = 68;
-constexpr uint32_t kChunkLong = 0x80000000u;
+constexpr uint32_t kChunkLong = 0x80000000u;   // a symbol with e >= 12 (|diff| >= 4096)
+constexpr uint32_t kChunkMulti = 0x40000000u;  // a symbol with e = 10 or 11 (slot 10 / 31 repeat)
+constexpr uint32_t kChunkFlags = kChunkLong | kChunkMulti;
 
 // Kernel 1: prediction + context + fold for every sample of a set of frames.
 struct SymbolArgs {
@@ -76,11 +78,15 @@ struct SymbolArgs {
 // A plane is walked in chunks of 64 consecutive samples (one per lane).
 //   x: row * 32 inside the plane group's table (bits 0..15) | (int16)diff << 16
 //   y, z: two bits per slot (slots 0..15, 16..31): 0/1 the slot's decision
-//         bit, 2 no decision (only for |diff| < 1024; see walk_long)
+//         bit, 2 no decision, 3 several decisions (slot 10 at e >= 10, slot
+//         31 at e >= 11: the walk derives them from diff); e <= 11 only, the
+//         chunks with a larger exponent take walk_long
 //   w: D | (D + 2e) << 16, D = the symbol's first decision counted from the
 //      start of its chunk; bit 31: same row as the previous sample of the
 //      chunk
+//   bit 30: same row as the sample two back in the chunk
 constexpr uint32_t kRecSame = 0x80000000u;
+constexpr uint32_t kRecSame2 = 0x40000000u;
 
 // Decision stream of one batch (frame-parallel mode).  Every (frame, slice)
 // stream's binary decisions, in coding order, start at decision index
@@ -91,7 +97,7 @@ constexpr uint32_t kRecSame = 0x80000000u;
 // blocks past a chain's last decision land there.  Decision d has the
 // adaptive state it is coded with in pre[d] and its value in bit d of
 // bits[] (bit d & 31 of word d >> 5).
-constexpr int kChainPad = 1536;
+constexpr int kChainPad = 2048;
 __host__ __device__ inline int64_t chroma_start(int64_t dc0) { return ((dc0 + 63) & ~int64_t(63)) + kChainPad; }
 // decisions a stream takes beyond its own (alignment and the two pads)
 constexpr int64_t kStreamSlack = 2 * kChainPad + 2 * 64;

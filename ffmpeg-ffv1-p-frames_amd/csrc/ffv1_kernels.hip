@@ -28,6 +28,7 @@
 //                  3-byte size, 0x00 and the slice CRC-32 computed chunk-
 //                  parallel and combined in GF(2) (ffv1enc.c:1326-1354).
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include <type_traits>
 
@@ -93,6 +94,24 @@ __device__ __forceinline__ uint32_t spread16(uint32_t x) {
 __device__ __forceinline__ void slot_codes(int v, uint32_t& c0, uint32_t& c1) {
   const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
   const int e = v ? 31 - __builtin_clz(mag) : -1;
+  if (e >= 10) {
+    // e = 10, 11: slots 1..9 a one each, slot 10 the ones of i = 9..e-1 and
+    // the terminating zero (code 3), sign in slot 21, mantissa bits 0..8 in
+    // slots 22..30, bits 9..e-1 in slot 31 (one: its bit; two: code 3)
+    const uint32_t pres = 0x7FFu & ~1u;  // slots 1..10
+    const uint32_t lo9 = mag & 0x1FFu;
+    uint32_t cc0 = spread16(pres & 0x3FEu) | (spread16(~pres & 0xFFFFu) << 1);  // 1s in 1..9, none elsewhere but 10
+    cc0 = (cc0 & ~(3u << 20)) | (3u << 20);                                       // slot 10: several
+    cc0 &= ~3u;                                                                   // slot 0: 0 (nonzero)
+    uint32_t hi = (uint32_t)(v < 0) << 5 | (lo9 << 6);  // slot 21 (bit 5 of the high half), 22..30
+    uint32_t pr = (1u << 5) | (0x1FFu << 6);
+    uint32_t cc1 = spread16(hi) | (spread16(~pr & 0xFFFFu) << 1);
+    const uint32_t c31 = e == 10 ? ((mag >> 9) & 1u) : 3u;
+    cc1 = (cc1 & ~(3u << 30)) | (c31 << 30);
+    c0 = cc0;
+    c1 = cc1;
+    return;
+  }
   const uint32_t lo = v ? (1u << e) - 1u : 0u;  // e ones
   const uint32_t tm = v ? (1u | (((2u << e) - 1u) << 1) | (1u << (11 + e)) | (lo << 22)) : 1u;
   const uint32_t bm = v ? ((lo << 1) | ((uint32_t)(v < 0) << (11 + e)) | ((mag & lo) << 22)) : 1u;
@@ -207,9 +226,11 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
       const unsigned mag = diff < 0 ? 0u - (unsigned)diff : (unsigned)diff;
       const int e = diff ? 31 - __builtin_clz(mag) : 0;
       const int prev = wave_prev(raddr);
+      const int prev2 = wave_prev(prev);
       uint32_t c0, c1;
       slot_codes(diff, c0, c1);
-      const uint32_t w = (uint32_t)d0 | ((uint32_t)(d0 + 2 * e) << 16) | (lane > 0 && prev == raddr ? kRecSame : 0u);
+      const uint32_t w = (uint32_t)d0 | ((uint32_t)(d0 + 2 * e) << 16) | (lane > 0 && prev == raddr ? kRecSame : 0u) |
+                         (lane > 1 && prev2 == raddr ? kRecSame2 : 0u);
       if (valid) rec[idx] = make_uint4((uint32_t)raddr | ((uint32_t)(uint16_t)diff << 16), c0, c1, w);
       // the chunk's decision bits, packed in coding order, and its header
       const int wv = threadIdx.x / kWave;
@@ -223,8 +244,9 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
           if ((uint32_t)(x >> 32)) atomicOr(&cs[2 + (d0 >> 5)], (uint32_t)(x >> 32));
         }
         const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
-        const bool lng = __ballot(valid && (diff >= 1024 || diff <= -1024)) != 0;
-        if (lane == 0) cs[0] = (uint32_t)total | (lng ? kChunkLong : 0u);
+        const bool lng = __ballot(valid && (diff >= 4096 || diff <= -4096)) != 0;
+        const bool mul = __ballot(valid && (diff >= 1024 || diff <= -1024)) != 0;
+        if (lane == 0) cs[0] = (uint32_t)total | (lng ? kChunkLong : 0u) | (mul ? kChunkMulti : 0u);
         uint32_t* const dst = cbase + ((base + wv * kWave) / kWave) * kChunkWords;
         dst[lane] = cs[lane];
         if (lane < kChunkWords - kWave) dst[kWave + lane] = cs[kWave + lane];
@@ -262,11 +284,15 @@ constexpr int kHeaderFlushAt = kRing - 30;  // per header op (host-checked |valu
 // exec-masked block behind a branch, which costs more than the lookups.
 __device__ __forceinline__ void pin(uint32_t& v) { asm volatile("" : "+v"(v)); }
 
+// LDS-typed pointer (address space 3): ring arithmetic stays 32-bit LDS
+// addressing, with no generic-pointer conversions on the per-decision path
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
 struct Lane {
   int low, range;
   uint32_t r0, r1, r2, r3, r4, r5, r6, r7;  // states of the current context row (byte k = slot k)
-  uint32_t* ring;      // this lane's ring row (LDS)
-  uint32_t* rp;        // ring head: the digits so far are ring[0 .. rp - ring)
+  lds_u32* ring;       // this lane's ring row (LDS)
+  lds_u32* rp;         // ring head: the digits so far are ring[0 .. rp - ring)
 
   template <int D>
   __device__ __forceinline__ uint32_t& w() {
@@ -343,12 +369,16 @@ __device__ __forceinline__ Sink make_sink(uint8_t* out, int64_t cap) {
 // Renormalisation (range < 0x100 needs at most one shift after a decision):
 // the value of `low` is always written at the ring head and the head only
 // advances when a byte is really shifted out.
+// One byte-permute selector does both shifts: (x & 0xFF) << 8 when a byte is
+// shifted out (range < 0x100, so that is range << 8 too), x as it is
+// otherwise.
 __device__ __forceinline__ void renorm(Lane& L) {
   const bool need = L.range < 0x100;
   *L.rp = (uint32_t)L.low;
   L.rp += need ? 1 : 0;
-  L.low = need ? (int)__builtin_amdgcn_perm(0u, (uint32_t)L.low, 0x0c0c000cu) : L.low;  // (low & 0xFF) << 8
-  L.range = need ? (L.range << 8) : L.range;
+  const uint32_t sel = need ? 0x0c0c000cu : 0x03020100u;
+  L.low = (int)__builtin_amdgcn_perm(0u, (uint32_t)L.low, sel);
+  L.range = (int)__builtin_amdgcn_perm(0u, (uint32_t)L.range, sel);
 }
 
 // Every lane replays its ring, four entries read at a time (ring rows are 3
@@ -616,8 +646,8 @@ __device__ __forceinline__ void run_header_ops(const CodeArgs& a, Lane& L, SinkT
 __device__ __forceinline__ void lane_init(Lane& L, uint32_t* ring) {
   L.low = 0;
   L.range = 0xFF00;
-  L.ring = ring;
-  L.rp = ring;
+  L.ring = (lds_u32*)ring;
+  L.rp = L.ring;
   L.r0 = L.r1 = L.r2 = L.r3 = L.r4 = L.r5 = L.r6 = L.r7 = 0;
 }
 
@@ -1003,13 +1033,13 @@ __global__ __launch_bounds__(kSinkThreads) void ffv1_sink(CodeArgs a) {
 // are read from LDS a step ahead and, when it is the same row, taken from
 // the register just computed instead.
 constexpr int kWalkThreads = kWave;
-constexpr int kT3Bytes = 3 * 256;
+constexpr int kT3Bytes = 4 * 256;  // N[code][state]: code 0/1 the bit, 2 none, 3 several (fixed up)
 constexpr int kChunk = 64;                   // symbols per chunk (the records' D is chunk-relative)
-constexpr int kPreStage = kChunk * 21;       // recorded bytes of a chunk of symbols with e <= 9
+constexpr int kPreStage = kChunk * 25;       // recorded bytes of a chunk of symbols with e <= 11
 constexpr int kRecSlots = kChunk + 3;        // + three read-ahead slots (null records)
 constexpr int kPreData = kPreStage + 16;     // a chain's stage: <= 15 bytes carried in, then the chunk
 constexpr int kPreHalf = kPreData + 32;      // + one dummy byte per slot
-constexpr int kCopyBlocks = 3;               // 16-byte blocks per lane that write a stage out
+constexpr int kCopyBlocks = 4;               // 16-byte blocks per lane that write a stage out
 static_assert(kCopyBlocks * 32 * 16 >= kPreData, "the copy-out covers the stage");
 static_assert(kCopyBlocks * 32 * 16 <= kChainPad, "the copy-out stays inside the chain and its pad");
 
@@ -1077,6 +1107,7 @@ struct StepIn {
   int pos;        // stage byte of the decision (the lane's dummy byte for none)
   int addr;       // the slot's state byte in the tables
   bool same;      // same row as the previous symbol
+  bool same2;     // same row as the symbol two back (and not the previous one's)
 };
 
 __device__ __forceinline__ StepIn derive(const uint4& r, const WalkLane& W, int kc) {
@@ -1087,29 +1118,57 @@ __device__ __forceinline__ StepIn derive(const uint4& r, const WalkLane& W, int 
   d.pos = d.code == 2u ? W.dummy : pos;
   d.addr = (int)(r.x & 0xFFFFu) + W.kk;
   d.same = (int)r.w < 0;  // kRecSame
+  d.same2 = (r.w & kRecSame2) != 0u;
   return d;
 }
 
 // Symbol T: the lookup of T is issued first; T's recorded state, T-1's
-// table write and the read of T+1's row then fill its latency.  The row read
-// one symbol ahead misses T's write, so a symbol continuing its
-// predecessor's row takes the state from the register instead.
+// table write and the read of T+2's row then fill its latency.  The row of
+// T+2 is read two symbols ahead, so it misses the writes of T and T+1: a
+// symbol continuing its predecessor's row takes that state from the register
+// (e1), one on the row of the symbol two back takes that one's (e2).  The
+// step's critical path is then one LDS lookup and two selects.
 // N[code][state] = the state after the slot's decision (code 0/1 its bit, 2
 // none); the state before it is what the coder needs (put_rac's r1 = range *
 // state >> 8).
-__device__ __forceinline__ void walk_step(uint8_t* fixed, uint8_t* tbl, const StepIn& d, int addr_next,
-                                          uint32_t& e1, uint32_t& l0, int& addr_prev) {
-  uint32_t a1 = e1, a0 = l0;
+__device__ __forceinline__ void walk_step(uint8_t* fixed, uint8_t* tbl, const StepIn& d, int addr_next2,
+                                          uint32_t& e1, uint32_t& e2, uint32_t& l0, uint32_t& l1,
+                                          int& addr_prev, uint32_t& st_out) {
+  uint32_t a1 = e1, a2 = e2, a0 = l0;
   pin(a1);
+  pin(a2);
   pin(a0);
-  const uint32_t st = d.same ? a1 : a0;
+  const uint32_t st = d.same ? a1 : (d.same2 ? a2 : a0);
   const uint32_t idx = (d.code << 8) | st;
   const uint32_t n = fixed[kLdsN + idx];
   fixed[kLdsPre + d.pos] = (uint8_t)st;      // T's recorded state
   tbl[addr_prev] = (uint8_t)a1;              // T-1's state
-  l0 = tbl[addr_next];                       // T+1's row, after every earlier write but T's
+  l0 = l1;
+  l1 = tbl[addr_next2];                      // T+2's row, after every earlier write but T's and T+1's
   addr_prev = d.addr;
+  e2 = a1;
   e1 = n;
+  st_out = st;
+}
+
+// A lane whose slot codes several decisions for symbol T (code 3: slot 10
+// at e = 10, 11; slot 31 at e = 11, put_symbol_inline's min(i, 9) slots,
+// ffv1enc.c:199-220): walk_step recorded st at pos and left the state; here
+// the slot's decisions are applied in order from st, each state recorded at
+// its decision (slot 10: D+10, D+11, ..; slot 31: D+e+2 .. D+2e-8, where pos
+// is the last), and the state after them returned.
+__device__ __noinline__ uint32_t walk_multi(uint8_t* fixed, uint32_t st, int v, int k, int pos, bool act) {
+  const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
+  const int e = 31 - __builtin_clz(mag | 1u);
+  const int n = !act ? 0 : k == 10 ? e - 8 : e - 9;
+  const int first = k == 10 ? pos : pos - (e - 10);
+  uint32_t x = st;
+  for (int j = 0; j < n; j++) {
+    const int bit = k == 10 ? (j < e - 9) : (int)((mag >> (e - 1 - j)) & 1u);
+    fixed[kLdsPre + first + j] = (uint8_t)x;
+    x = fixed[kLdsN + (bit << 8) + x];
+  }
+  return act ? x : 0u;
 }
 
 int64_t walk_lds_bytes_dev(int64_t state_bytes) { return kLdsFixed + 2 * (state_bytes / 2 + 32); }
@@ -1246,15 +1305,16 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
         if (c + 1 < nchunks) nx = load(c + 1);  // ... chunk c+1's loads
         const int cnt = (int)min((int64_t)kChunk, max((int64_t)0, nsym - (int64_t)c * kChunk));
         const uint32_t hd = c < nch ? cx.hd : 0u;
-        const int total = (int)(hd & ~kChunkLong);
+        const int total = (int)(hd & ~kChunkFlags);
         const bool lng = __ballot((hd & kChunkLong) != 0) != 0;
+        const bool mul = __ballot((hd & kChunkMulti) != 0) != 0;
         const int64_t pos0 = gbase + run;  // decision index of the chunk's first decision
         myrecs[k] = pick(k < cnt, cx.m0, nullrec);
         myrecs[k + 32] = pick(k + 32 < cnt, cx.m1, nullrec);
         if (k < kRecSlots - kChunk) myrecs[kChunk + k] = nullrec;
         __builtin_amdgcn_wave_barrier();
 
-        if (lng) {  // e >= 10 somewhere: one symbol at a time, recorded straight to HBM
+        if (lng) {  // e >= 12 somewhere: one symbol at a time, recorded straight to HBM
           const int cmax = max(__builtin_amdgcn_readlane(cnt, 0), __builtin_amdgcn_readlane(cnt, 32));
           // the next symbol's row is read before this symbol's write (a symbol
           // on its predecessor's row takes the state from the register), so a
@@ -1292,19 +1352,35 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
         const int kc = kslot + h * kPreHalf + align;
         StepIn d0 = derive(myrecs[0], W, kc), d1 = derive(myrecs[1], W, kc);
         uint4 rn = myrecs[2];
-        uint32_t l0 = tbl[d0.addr];
-        uint32_t e1 = 0u;
+        uint32_t l0 = tbl[d0.addr], l1 = tbl[d1.addr];
+        uint32_t e1 = 0u, e2 = 0u, st = 0u;
         int addr_prev = (int)((stage + kPreData + k) - tbl);  // no T-1 yet: the dummy byte
         const uint64_t t0 = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
-        static_for<0, kChunk>([&](auto tc) {
-          constexpr int T = decltype(tc)::value;
-          walk_step(fixed, tbl, d0, d1.addr, e1, l0, addr_prev);
-          const uint4 r3 = myrecs[T + 3];  // three ahead
-          __builtin_amdgcn_sched_barrier(0);  // keeps the read here, not sunk to its use a step later
-          d0 = d1;
-          d1 = derive(rn, W, kc);
-          rn = r3;
-        });
+        if (!mul) {
+          static_for<0, kChunk>([&](auto tc) {
+            constexpr int T = decltype(tc)::value;
+            walk_step(fixed, tbl, d0, (int)(rn.x & 0xFFFFu) + W.kk, e1, e2, l0, l1, addr_prev, st);
+            const uint4 r3 = myrecs[T + 3];  // three ahead
+            __builtin_amdgcn_sched_barrier(0);  // keeps the read here, not sunk to its use a step later
+            d0 = d1;
+            d1 = derive(rn, W, kc);
+            rn = r3;
+          });
+        } else {  // a symbol with e = 10 or 11 in the chunk: the same steps, checked for code 3
+          static_for<0, kChunk>([&](auto tc) {
+            constexpr int T = decltype(tc)::value;
+            walk_step(fixed, tbl, d0, (int)(rn.x & 0xFFFFu) + W.kk, e1, e2, l0, l1, addr_prev, st);
+            const uint4 r3 = myrecs[T + 3];
+            __builtin_amdgcn_sched_barrier(0);
+            if (__ballot(d0.code == 3u)) {  // rare: the slot's decisions one after the other
+              const int v = (int)(int16_t)(myrecs[T].x >> 16);
+              e1 = walk_multi(fixed, st, v, k, d0.pos, d0.code == 3u) | (d0.code == 3u ? 0u : e1);
+            }
+            d0 = d1;
+            d1 = derive(rn, W, kc);
+            rn = r3;
+          });
+        }
         tbl[addr_prev] = (uint8_t)e1;  // the chunk's last symbol
         if (a.dbg) {
           __builtin_amdgcn_s_waitcnt(0);
@@ -1394,7 +1470,7 @@ __global__ __launch_bounds__(kBitsThreads) void ffv1_bits(BitsArgs a) {
     const uint32_t* const pc = fc + g.chunk_off[p] * kChunkWords;
     for (int c0 = 0; c0 < nch; c0 += kBitsThreads) {
       const int c = c0 + t;
-      const int n = c < nch ? (int)(pc[(int64_t)c * kChunkWords] & ~kChunkLong) : 0;
+      const int n = c < nch ? (int)(pc[(int64_t)c * kChunkWords] & ~kChunkFlags) : 0;
       const int x = wave_incl_scan(n, lane);
       if (lane == kWave - 1) wsum[wv] = x;
       __syncthreads();
@@ -1774,7 +1850,11 @@ int64_t walk_lds_bytes(int64_t state_bytes) { return walk_lds_bytes_dev(state_by
 
 int launch_walk(const WalkArgs& a, int nsegs, void* stream) {
   if (walk_lds_bytes_dev(a.state_bytes) > kWalkLdsMax) return -1;
-  const size_t dyn = (size_t)(2 * (a.state_bytes / 2 + 32));  // the tables; the fixed part is static
+  size_t dyn = (size_t)(2 * (a.state_bytes / 2 + 32));  // the tables; the fixed part is static
+  // FFV1HIP_WALK_LDS_PAD (measurement hook): extra LDS per walk wave, to
+  // run the walk at a lower occupancy
+  static const long pad = std::getenv("FFV1HIP_WALK_LDS_PAD") ? std::atol(std::getenv("FFV1HIP_WALK_LDS_PAD")) : 0;
+  dyn += (size_t)pad;
   dim3 grid((unsigned)(nsegs * ((a.nslices + 1) / 2) * 2)), block(kWalkThreads);
   hipLaunchKernelGGL(ffv1_walk, grid, block, dyn, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
