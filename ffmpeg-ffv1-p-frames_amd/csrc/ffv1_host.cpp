@@ -274,6 +274,7 @@ struct ffv1hip_ctx {
   uint8_t* d_pre[2] = {nullptr, nullptr};    // [decision] state before the decision
   uint8_t* d_scratch = nullptr;               // where idle walk chains write their stage
   uint32_t* d_bits[2] = {nullptr, nullptr};  // [decision / 32] decision bits
+  uint8_t* d_opsets = nullptr;   // [coder lane][kOpSets * 32] header op states of the coder
   int64_t dcap[2] = {0, 0};      // decisions d_pre/d_bits hold
   int buf = 0;                   // buffer set of the next batch
   hipStream_t code_stream = nullptr;  // ffv1_dcode + assembly, behind the states walk
@@ -517,7 +518,7 @@ static void free_device(ffv1hip_ctx* c) {
   void* ptrs[] = {c->d_frames, c->d_qt, c->d_tabs, c->d_ops, c->d_nops, c->d_segs, c->d_keys,
                   c->d_slice_out, c->d_slice_bytes, c->d_packets, c->d_packet_size, c->d_persist[0],
                   c->d_persist[1], c->d_tables, c->d_sym, c->d_keys2, c->d_cbits, c->d_dcount, c->d_dbase, c->d_dtotal, c->d_pre[0],
-                  c->d_pre[1], c->d_bits[0], c->d_bits[1], c->d_scratch, c->d_geom, c->d_slot_frames, c->d_status};
+                  c->d_pre[1], c->d_bits[0], c->d_bits[1], c->d_scratch, c->d_opsets, c->d_geom, c->d_slot_frames, c->d_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_dtotal) (void)hipHostFree(c->h_dtotal);
@@ -606,6 +607,7 @@ static int alloc_device(ffv1hip_ctx* c) {
     // decision capacity: the worst case when it is small, else ~12 per symbol
     // (real content codes ~10); a batch that needs more grows the set
     HIP_TRY(hipMalloc(&c->d_scratch, 4096));
+    HIP_TRY(hipMalloc(&c->d_opsets, (size_t(nb) * c->nslices + 64) * kOpSets * 32));  // + a wave of padding lanes
     const int64_t align = int64_t(nb) * c->nslices * kStreamSlack;
     const int64_t worst = int64_t(nb) * c->frame_samples * c->wmax + align;
     const int64_t guess = int64_t(nb) * c->frame_samples * 12 + align;
@@ -937,6 +939,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     wa.persist_out = ca.persist_out;
     wa.ds = ds;
     wa.scratch = c->d_scratch;
+    static const bool force_multi = std::getenv("FFV1HIP_FORCE_MULTI") && std::atoi(std::getenv("FFV1HIP_FORCE_MULTI"));
+    wa.force_multi = force_multi;
     // FFV1HIP_WALKDBG=1 (measurement hook): per-block cycle split to stderr
     static const bool walkdbg = std::getenv("FFV1HIP_WALKDBG") && std::atoi(std::getenv("FFV1HIP_WALKDBG"));
     uint64_t* d_dbg = nullptr;
@@ -971,6 +975,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     HIP_TRY(hipStreamWaitEvent(cst, c->bitsed[fb], 0));
     ca.nframes = n;
     ca.nopsets = c->nopsets;
+    ca.opsets = c->d_opsets;
     ca.ds = ds;
     // FFV1HIP_CODEDBG=1 (measurement hook): per-wave cycle split to stderr
     static const bool codedbg = std::getenv("FFV1HIP_CODEDBG") && std::atoi(std::getenv("FFV1HIP_CODEDBG"));

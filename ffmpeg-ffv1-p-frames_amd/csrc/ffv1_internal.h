@@ -47,8 +47,8 @@ struct SliceGeom {
 // Per walk chunk (64 consecutive samples of a plane), written by ffv1_symbols:
 // word 0 = the chunk's decisions | kChunkLong / kChunkMulti flags, words
 // 1.. = the decision bits in coding order (bit d in word 1 + d / 32), then a
-// zero word.
-constexpr int kChunkWords = 68;
+// zero word; words 68, 69 = which of the 64 symbols have e = 10 or 11.
+constexpr int kChunkWords = 70;  // header, 66 bit words + a zero word, the 64-bit multi-symbol mask
 constexpr uint32_t kChunkLong = 0x80000000u;   // a symbol with e >= 12 (|diff| >= 4096)
 constexpr uint32_t kChunkMulti = 0x40000000u;  // a symbol with e = 10 or 11 (slot 10 / 31 repeat)
 constexpr uint32_t kChunkFlags = kChunkLong | kChunkMulti;
@@ -140,6 +140,7 @@ struct CodeArgs {
   int nopsets;                // decision-stream mode: op sets the header programs use
   DecisionStream ds;
   uint64_t* dbg;              // optional [wave][4] cycle counters (FFV1HIP_CODEDBG)
+  uint8_t* opsets;            // decision-stream mode: [stream][nopsets * 32] header op states
 };
 
 // Kernel 2a: the context-state walk.  The adaptive states a slice's range
@@ -163,6 +164,7 @@ struct WalkArgs {
   DecisionStream ds;
   uint8_t* scratch;           // >= 2 KiB: where idle chains write their stage
   uint64_t* dbg;              // optional [block][4] cycle counters (FFV1HIP_WALKDBG)
+  int force_multi;            // measurement hook: every chunk on the checked (multi) step
 };
 
 // Kernel 2b: the decision bits, from the chunks' packed words to their place

@@ -229,8 +229,10 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
       const int prev2 = wave_prev(prev);
       uint32_t c0, c1;
       slot_codes(diff, c0, c1);
+      // e = 10, 11: the composed N rows of slots 10 and 31 (ffv1_walk)
+      const uint32_t mrows = e >= 10 && e <= 11 ? (((e == 11 ? 3u : 6u) << 12) | (((mag >> 9) & 3u) << 28)) : 0u;
       const uint32_t w = (uint32_t)d0 | ((uint32_t)(d0 + 2 * e) << 16) | (lane > 0 && prev == raddr ? kRecSame : 0u) |
-                         (lane > 1 && prev2 == raddr ? kRecSame2 : 0u);
+                         (lane > 1 && prev2 == raddr ? kRecSame2 : 0u) | mrows;
       if (valid) rec[idx] = make_uint4((uint32_t)raddr | ((uint32_t)(uint16_t)diff << 16), c0, c1, w);
       // the chunk's decision bits, packed in coding order, and its header
       const int wv = threadIdx.x / kWave;
@@ -245,8 +247,9 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
         }
         const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
         const bool lng = __ballot(valid && (diff >= 4096 || diff <= -4096)) != 0;
-        const bool mul = __ballot(valid && (diff >= 1024 || diff <= -1024)) != 0;
-        if (lane == 0) cs[0] = (uint32_t)total | (lng ? kChunkLong : 0u) | (mul ? kChunkMulti : 0u);
+        const uint64_t mm = __ballot(valid && (diff >= 1024 || diff <= -1024) && diff < 4096 && diff > -4096);
+        if (lane == 0) cs[0] = (uint32_t)total | (lng ? kChunkLong : 0u) | (mm ? kChunkMulti : 0u);
+        if (lane < 2) cs[kChunkWords - 2 + lane] = (uint32_t)(mm >> (32 * lane));
         uint32_t* const dst = cbase + ((base + wv * kWave) / kWave) * kChunkWords;
         dst[lane] = cs[lane];
         if (lane < kChunkWords - kWave) dst[kWave + lane] = cs[kWave + lane];
@@ -861,18 +864,19 @@ __device__ __forceinline__ void decide32(Lane& L, SinkT& S, const uint4& wa, con
   });
 }
 
-__host__ __device__ constexpr size_t dcode_lds_bytes(int nopsets) {
-  return 1024 + (size_t)kCodeThreads * (nopsets * 32 + kDRingStride * 4);
+// The header ops keep their states in global memory and read their
+// transition tables from there (a few dozen decisions per stream): the
+// coder's LDS is its rings only, so that it fits beside three states-walk
+// waves on a CU.
+__host__ __device__ constexpr size_t dcode_lds_bytes(int /*nopsets*/) {
+  return (size_t)kCodeThreads * kDRingStride * 4;
 }
 
 __global__ __launch_bounds__(kCodeThreads) void ffv1_dcode(CodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int osb = a.nopsets * 32;
-  uint8_t* const tabs = lds;
-  uint8_t* const opsets = lds + 1024;
-  uint32_t* const ring = reinterpret_cast<uint32_t*>(opsets + kCodeThreads * osb);
-  for (int i = threadIdx.x; i < 1024; i += kCodeThreads) tabs[i] = a.tabs[i];
-  __syncthreads();
+  const uint8_t* const tabs = a.tabs;
+  uint32_t* const ring = reinterpret_cast<uint32_t*>(lds);
   const int lane = threadIdx.x;
   // slice-major: the lanes of a wave code one slice of consecutive frames,
   // streams of similar length
@@ -888,7 +892,8 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_dcode(CodeArgs a) {
   // rewrites the slot with the bytes in place)
   DigitSink S{reinterpret_cast<uint16_t*>(a.slice_out + ((int64_t)f * a.nslices + slice) * a.slice_stride), 0,
               live ? (int)(a.slice_stride / 2) : 0};
-  run_header_ops(a, L, S, opsets + lane * osb, key, slice, live, tabs, tabs + 512, osb, kDRing - 30);
+  // every lane its own op states, the padding lanes of the last wave included
+  run_header_ops(a, L, S, a.opsets + c * osb, key, slice, live, tabs, tabs + 512, osb, kDRing - 30);
   flush_if(L, S, kDFlushAt);
 
   const int64_t st = (int64_t)f * a.nslices + slice;
@@ -1033,7 +1038,12 @@ __global__ __launch_bounds__(kSinkThreads) void ffv1_sink(CodeArgs a) {
 // are read from LDS a step ahead and, when it is the same row, taken from
 // the register just computed instead.
 constexpr int kWalkThreads = kWave;
-constexpr int kT3Bytes = 4 * 256;  // N[code][state]: code 0/1 the bit, 2 none, 3 several (fixed up)
+// N[row][state]: rows 0/1 a decision of that bit, 2 none, and the composed
+// rows of the slots with several decisions (put_symbol_inline's min(i, 9)
+// slots at e = 10, 11): 3 = N0.N1.N1 (slot 10, e = 11), 4..7 = N[b9].N[b10]
+// (slot 31 at e = 11, row 4 + 2 b10 + b9; row 6 = N0.N1 is also slot 10 at
+// e = 10)
+constexpr int kT3Bytes = 8 * 256;
 constexpr int kChunk = 64;                   // symbols per chunk (the records' D is chunk-relative)
 constexpr int kPreStage = kChunk * 25;       // recorded bytes of a chunk of symbols with e <= 11
 constexpr int kRecSlots = kChunk + 3;        // + three read-ahead slots (null records)
@@ -1099,6 +1109,7 @@ struct WalkLane {
   uint32_t mlo;       // all ones for slots 0..15 (codes in the record's y word)
   int kk;             // k + this half's table base
   int dummy;          // stage byte of untouched slots
+  int msh, mwd, mbase;  // slots 10 / 31: where the record keeps the composed row (code 3)
 };
 
 // A symbol as lane k of its chain sees it.
@@ -1119,6 +1130,16 @@ __device__ __forceinline__ StepIn derive(const uint4& r, const WalkLane& W, int 
   d.addr = (int)(r.x & 0xFFFFu) + W.kk;
   d.same = (int)r.w < 0;  // kRecSame
   d.same2 = (r.w & kRecSame2) != 0u;
+  return d;
+}
+
+// In a chunk with e = 10, 11 symbols: code 3 (the slot's several decisions)
+// becomes the slot's composed N row, kept in the record (ffv1_symbols), so
+// the state chain stays one lookup per symbol.
+__device__ __forceinline__ StepIn derive_m(const uint4& r, const WalkLane& W, int kc) {
+  StepIn d = derive(r, W, kc);
+  const uint32_t rowm = __builtin_amdgcn_ubfe(r.w, W.msh, W.mwd) + W.mbase;
+  d.code = d.code == 3u ? rowm : d.code;
   return d;
 }
 
@@ -1151,24 +1172,36 @@ __device__ __forceinline__ void walk_step(uint8_t* fixed, uint8_t* tbl, const St
   st_out = st;
 }
 
-// A lane whose slot codes several decisions for symbol T (code 3: slot 10
-// at e = 10, 11; slot 31 at e = 11, put_symbol_inline's min(i, 9) slots,
-// ffv1enc.c:199-220): walk_step recorded st at pos and left the state; here
-// the slot's decisions are applied in order from st, each state recorded at
-// its decision (slot 10: D+10, D+11, ..; slot 31: D+e+2 .. D+2e-8, where pos
-// is the last), and the state after them returned.
-__device__ __noinline__ uint32_t walk_multi(uint8_t* fixed, uint32_t st, int v, int k, int pos, bool act) {
-  const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
-  const int e = 31 - __builtin_clz(mag | 1u);
-  const int n = !act ? 0 : k == 10 ? e - 8 : e - 9;
-  const int first = k == 10 ? pos : pos - (e - 10);
-  uint32_t x = st;
-  for (int j = 0; j < n; j++) {
-    const int bit = k == 10 ? (j < e - 9) : (int)((mag >> (e - 1 - j)) & 1u);
-    fixed[kLdsPre + first + j] = (uint8_t)x;
-    x = fixed[kLdsN + (bit << 8) + x];
+// After a chunk with e = 10, 11 symbols: the states the step did not record.
+// The step recorded the state before the slot's first decision at pos (slot
+// 10: D+10; slot 31: D+2e-8, its LAST decision, e = 11) and advanced the
+// chain with the composed row; here, from that state x0, the states before
+// the slot's later decisions: slot 10: N1(x0) at D+11 and, at e = 11,
+// N1.N1(x0) at D+12; slot 31: x0 at D+13 and N[b10](x0) at D+14
+// (put_symbol_inline, ffv1enc.c:199-220).  Lane k of a half takes its
+// chain's symbols k and k + 32 (hm: the half's mask), all at once.
+__device__ __forceinline__ void walk_multi_fill(uint8_t* fixed, const uint4* myrecs, uint64_t hm, int k, int base,
+                                                int dummy) {
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    const int t = k + 32 * i;
+    const bool act = (hm >> t) & 1u;
+    const uint4 r = myrecs[t];
+    const int v = (int)(int16_t)(r.x >> 16);
+    const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
+    const bool e11 = mag >= 2048u;
+    const int p10 = base + (int)(r.w & 0xFFFu) + 10;
+    const int p31 = base + (int)((r.w >> 16) & 0xFFFu) - 8;
+    const uint32_t x10 = fixed[kLdsPre + (act ? p10 : dummy)];
+    const uint32_t x31 = fixed[kLdsPre + (act ? p31 : dummy)];
+    const uint32_t a1 = fixed[kLdsN + 256 + x10];                     // N1
+    const uint32_t a2 = fixed[kLdsN + 7 * 256 + x10];                 // N1.N1
+    const uint32_t b1 = fixed[kLdsN + (((mag >> 10) & 1u) << 8) + x31];  // N[b10]
+    fixed[kLdsPre + (act ? p10 + 1 : dummy)] = (uint8_t)a1;
+    fixed[kLdsPre + (act && e11 ? p10 + 2 : dummy)] = (uint8_t)a2;
+    fixed[kLdsPre + (act && e11 ? p31 - 1 : dummy)] = (uint8_t)x31;
+    fixed[kLdsPre + (act && e11 ? p31 : dummy)] = (uint8_t)b1;
   }
-  return act ? x : 0u;
 }
 
 int64_t walk_lds_bytes_dev(int64_t state_bytes) { return kLdsFixed + 2 * (state_bytes / 2 + 32); }
@@ -1190,8 +1223,21 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   const int lane = threadIdx.x;
   const int h = lane >> 5, k = lane & 31;
   for (int i = lane; i < kT3Bytes; i += kWalkThreads) {
-    const int code = i >> 8, st = i & 255;
-    fixed[kLdsN + i] = (uint8_t)(code < 2 ? a.ftab[i] : st);
+    const int row = i >> 8, st = i & 255;
+    const uint8_t* const t0 = a.ftab;
+    const uint8_t* const t1 = a.ftab + 256;
+    int v;
+    switch (row) {
+      case 0: v = t0[st]; break;
+      case 1: v = t1[st]; break;
+      case 2: v = st; break;
+      case 3: v = t0[t1[t1[st]]]; break;
+      case 4: v = t0[t0[st]]; break;
+      case 5: v = t1[t0[st]]; break;
+      case 6: v = t0[t1[st]]; break;
+      default: v = t1[t1[st]]; break;
+    }
+    fixed[kLdsN + i] = (uint8_t)v;
   }
   // the longer plane group's chains first (luma at 4:2:0, twice as long as
   // chroma; chroma at 4:4:4, where Cb and Cr make one chain twice luma's);
@@ -1236,6 +1282,9 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   const int kslot = isU ? k : (k <= 21 ? 2 : 23 - k);
   W.kk = h * tsz + k;
   W.dummy = h * kPreHalf + kPreData + k;
+  W.msh = k == 31 ? 28 : 12;
+  W.mwd = k == 31 ? 2 : 3;
+  W.mbase = k == 31 ? 4 : 0;
   const uint4 nullrec = make_uint4((uint32_t)half, 0xAAAAAAAAu, 0xAAAAAAAAu, 0u);  // dummy row, no decisions
 
   // The stage of chunk c goes out at the start of chunk c+1, before its
@@ -1280,7 +1329,7 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
       // a chunk's inputs: 2 records per lane and the chunk header
       struct In {
         uint4 m0, m1;
-        uint32_t hd;
+        uint32_t hd, mlo, mhi;  // header, multi-symbol mask
       };
       // raw loads (indices past the plane read record / chunk 0 of a plane of
       // the pair: valid memory); what is past the plane is masked where the
@@ -1290,7 +1339,10 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
         const int64_t b = (int64_t)c * kChunk;
         x.m0 = rp[b + k < nsym ? b + k : 0];
         x.m1 = rp[b + 32 + k < nsym ? b + 32 + k : 0];
-        x.hd = cp[(int64_t)(c < nch ? c : 0) * kChunkWords];
+        const uint32_t* const ch = cp + (int64_t)(c < nch ? c : 0) * kChunkWords;
+        x.hd = ch[0];
+        x.mlo = ch[kChunkWords - 2];
+        x.mhi = ch[kChunkWords - 1];
         return x;
       };
       In nx = load(0);
@@ -1301,13 +1353,19 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
         pin(cx.m0.x); pin(cx.m0.y); pin(cx.m0.z); pin(cx.m0.w);
         pin(cx.m1.x); pin(cx.m1.y); pin(cx.m1.z); pin(cx.m1.w);
         pin(cx.hd);
+        pin(cx.mlo);
+        pin(cx.mhi);
         copy_out();                             // chunk c-1's stage, then ...
         if (c + 1 < nchunks) nx = load(c + 1);  // ... chunk c+1's loads
         const int cnt = (int)min((int64_t)kChunk, max((int64_t)0, nsym - (int64_t)c * kChunk));
         const uint32_t hd = c < nch ? cx.hd : 0u;
         const int total = (int)(hd & ~kChunkFlags);
         const bool lng = __ballot((hd & kChunkLong) != 0) != 0;
-        const bool mul = __ballot((hd & kChunkMulti) != 0) != 0;
+        // the symbols with e = 10, 11 of either chain: a wave-uniform mask
+        const uint32_t mlo = c < nch ? cx.mlo : 0u, mhi = c < nch ? cx.mhi : 0u;
+        const uint64_t msk = ((uint64_t)(__builtin_amdgcn_readlane(mhi, 0) | __builtin_amdgcn_readlane(mhi, 32)) << 32) |
+                             (uint64_t)(__builtin_amdgcn_readlane(mlo, 0) | __builtin_amdgcn_readlane(mlo, 32));
+        const bool mul = msk != 0 || a.force_multi;
         const int64_t pos0 = gbase + run;  // decision index of the chunk's first decision
         myrecs[k] = pick(k < cnt, cx.m0, nullrec);
         myrecs[k + 32] = pick(k + 32 < cnt, cx.m1, nullrec);
@@ -1366,20 +1424,19 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
             d1 = derive(rn, W, kc);
             rn = r3;
           });
-        } else {  // a symbol with e = 10 or 11 in the chunk: the same steps, checked for code 3
+        } else {  // a symbol with e = 10 or 11 in the chunk: composed rows, then the fill
+          StepIn m0 = derive_m(myrecs[0], W, kc), m1 = derive_m(myrecs[1], W, kc);
           static_for<0, kChunk>([&](auto tc) {
             constexpr int T = decltype(tc)::value;
-            walk_step(fixed, tbl, d0, (int)(rn.x & 0xFFFFu) + W.kk, e1, e2, l0, l1, addr_prev, st);
+            walk_step(fixed, tbl, m0, (int)(rn.x & 0xFFFFu) + W.kk, e1, e2, l0, l1, addr_prev, st);
             const uint4 r3 = myrecs[T + 3];
             __builtin_amdgcn_sched_barrier(0);
-            if (__ballot(d0.code == 3u)) {  // rare: the slot's decisions one after the other
-              const int v = (int)(int16_t)(myrecs[T].x >> 16);
-              e1 = walk_multi(fixed, st, v, k, d0.pos, d0.code == 3u) | (d0.code == 3u ? 0u : e1);
-            }
-            d0 = d1;
-            d1 = derive(rn, W, kc);
+            m0 = m1;
+            m1 = derive_m(rn, W, kc);
             rn = r3;
           });
+          const uint64_t hm = c < nch ? ((uint64_t)cx.mhi << 32) | cx.mlo : 0ull;  // this half's chain
+          walk_multi_fill(fixed, myrecs, hm, k, h * kPreHalf + align, W.dummy);
         }
         tbl[addr_prev] = (uint8_t)e1;  // the chunk's last symbol
         if (a.dbg) {
