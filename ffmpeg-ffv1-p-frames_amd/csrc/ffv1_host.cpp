@@ -591,9 +591,11 @@ static int alloc_device(ffv1hip_ctx* c) {
   // the coder grid is padded to whole waves and idle lanes touch their own table
   if (c->frames_mode) {
     // double-buffered: the states walk of batch k+1 runs while batch k codes
-    HIP_TRY(hipMalloc(&c->d_sym, 2 * sizeof(uint4) * size_t(c->frame_samples) * nb));  // walk records
+    // the walk records and chunk bits: one set (the next batch's symbols run
+    // after this batch's walk on the same stream, and wait for its bits)
+    HIP_TRY(hipMalloc(&c->d_sym, sizeof(uint4) * size_t(c->frame_samples) * nb));
     HIP_TRY(hipMalloc(&c->d_keys2, 2 * size_t(nb)));
-    HIP_TRY(hipMalloc(&c->d_cbits, 2 * sizeof(uint32_t) * kChunkWords * size_t(c->frame_chunks) * nb));
+    HIP_TRY(hipMalloc(&c->d_cbits, sizeof(uint32_t) * kChunkWords * size_t(c->frame_chunks) * nb));
     HIP_TRY(hipMalloc(&c->d_dcount, 2 * sizeof(int) * 3 * size_t(nb) * c->nslices));
     HIP_TRY(hipMalloc(&c->d_dbase, 2 * sizeof(int64_t) * size_t(nb) * c->nslices));
     HIP_TRY(hipMalloc(&c->d_dtotal, 2 * sizeof(int64_t)));
@@ -688,9 +690,12 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
     max_nsym = std::max(max_nsym, n);
   }
   c->frame_samples = off;
-  // Slice byte budget: 4 bytes per coded sample (+4 KiB); real content codes
-  // below 2 bytes per 16-bit sample.  Exceeding it reports -ENOSPC.
-  c->slice_cap = ((max_nsym * 4 + 4096) + 255) & ~int64_t(255);
+  // Slice byte budget: (bits + 4) / 8 bytes per coded sample (+4 KiB), above
+  // what full-entropy noise codes to (~1.1 B per 8-bit, ~2.1 B per 16-bit
+  // sample); a slice over it is encoded again with a budget sized from what
+  // it needed (ffv1hip_fetch), as the reference codes any slice within its
+  // w*h*140-byte packet (ffv1enc.c:1232).
+  c->slice_cap = ((max_nsym * (std::max(8, p.bits_per_raw_sample) + 4) / 8 + 4096) + 255) & ~int64_t(255);
   // FFV1HIP_SLICE_CAP (test hook): a small starting budget, to exercise the
   // re-encode with a larger one (ffv1hip_fetch)
   if (const char* e = std::getenv("FFV1HIP_SLICE_CAP"))
@@ -826,8 +831,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   sa.model1 = p.context_model;
   sa.qt = c->d_qt;
   uint32_t* const d_sym = c->frames_mode ? nullptr : c->d_sym;
-  uint4* const d_rec =
-      c->frames_mode ? reinterpret_cast<uint4*>(c->d_sym) + size_t(fb) * c->frame_samples * c->max_batch : nullptr;
+  uint4* const d_rec = c->frames_mode ? reinterpret_cast<uint4*>(c->d_sym) : nullptr;
   int* const d_dcount = c->frames_mode ? c->d_dcount + size_t(fb) * 3 * c->max_batch * c->nslices : nullptr;
   int64_t* const d_dbase = c->frames_mode ? c->d_dbase + size_t(fb) * c->max_batch * c->nslices : nullptr;
   sa.sym = d_sym;
@@ -892,7 +896,9 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     sa.dcount = d_dcount;  // accumulated by the symbols blocks of each plane
     HIP_TRY(hipMemsetAsync(d_dcount, 0, sizeof(int) * 3 * size_t(n) * c->nslices, st));
     sa.rec = d_rec;
-    sa.cbits = c->d_cbits + size_t(fb) * kChunkWords * c->frame_chunks * c->max_batch;
+    sa.cbits = c->d_cbits;
+    // the previous batch's bits kernel (its own stream) has read the chunk bits
+    HIP_TRY(hipStreamWaitEvent(st, c->bitsed[fb ^ 1], 0));
     sa.frame_chunks = c->frame_chunks;
     if (timed(0, st, [&] { return launch_symbols(sa, st); }) < 0)
       return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
