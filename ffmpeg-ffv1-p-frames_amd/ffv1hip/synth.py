@@ -118,6 +118,50 @@ def upsample_422(planes):
     return [y] + [np.ascontiguousarray(np.repeat(c, 2, 0)[:h]) for c in (u, v)]
 
 
+def _trunc_div(a: int, b: int) -> int:
+    q = abs(a) // abs(b)
+    return q if (a < 0) == (b < 0) else -q
+
+
+def _yuv2rgb_lut():
+    """The 32-bpp tables of ff_yuv2rgb_c_init_tables (libswscale/yuv2rgb.c:
+    765-842, 959-983) for limited-range input, the default BT.601 matrix
+    (ff_yuv2rgb_coeffs[SWS_CS_DEFAULT], :49-61; vf_scale.c:227-248) and unit
+    contrast / saturation: a luma curve ``ytab`` and the per-U / per-V index
+    offsets of fill_table / fill_gv_table (:728-751)."""
+    crv, cbu, cgu, cgv = 104597, 132201, -25675, -53279
+    cy = (1 << 16) * 255 // 219
+    oy = 16 << 16
+    crv, cbu, cgu, cgv = [_trunc_div(c * (1 << 16) + 0x8000, cy) for c in (crv, cbu, cgu, cgv)]
+    yb = -(384 << 16) - 512 * cy - oy
+    i = np.arange(2048, dtype=np.int64)
+    ytab = np.clip((yb + i * cy + 0x8000) >> 16, 0, 255).astype(np.uint8)
+    v = np.arange(256, dtype=np.int64)
+    return (ytab, 838 - (crv >> 9) + ((v * crv) >> 16), 838 - (cbu >> 9) + ((v * cbu) >> 16),
+            838 - (cgu >> 9) + ((v * cgu) >> 16), -(cgv >> 9) + ((v * cgv) >> 16))
+
+
+def yuv420p_to_bgr0(planes):
+    """yuv420p u8 -> bgr0 as ``-sws_flags neighbor+bitexact`` converts it:
+    BGR0 is scaled as BGRA (libswscale/utils.c:1031-1039); the even width
+    keeps half-resolution chroma (:1275-1291, 1362-1363) so each chroma
+    sample covers a 2x2 block (point filter, :344-358), and every output
+    pixel is three table reads (output.c yuv2rgb_write / yuv2rgb.c
+    yuv2rgb_c_32: R = r[Y], G = g[Y], B = b[Y]).  The padding byte is the
+    tables' alpha, 255; FFV1 does not code it."""
+    ytab, r_off, b_off, gu_off, gv_off = _yuv2rgb_lut()
+    y, u, v = [np.asarray(p).astype(np.int64) for p in planes]
+    h, w = y.shape
+    u = u[np.arange(h) >> 1][:, np.arange(w) >> 1]
+    v = v[np.arange(h) >> 1][:, np.arange(w) >> 1]
+    out = np.empty((h, w, 4), np.uint8)
+    out[..., 0] = ytab[y + b_off[u]]
+    out[..., 1] = ytab[y + gu_off[u] + gv_off[v]]
+    out[..., 2] = ytab[y + r_off[v]]
+    out[..., 3] = 255
+    return [out.reshape(h, 4 * w)]
+
+
 def convert(planes, pix_fmt: str):
     """yuv420p u8 -> ``pix_fmt`` as the FATE vsynth tests convert their input
     (``-sws_flags neighbor+bitexact``, tests/fate/vcodec.mak:116-124):
@@ -129,6 +173,8 @@ def convert(planes, pix_fmt: str):
              "yuv422p": (upsample_422, 8), "yuv422p10": (upsample_422, 10),
              "yuv422p16": (upsample_422, 16), "yuv444p": (upsample_444, 8),
              "yuv444p10": (upsample_444, 10), "yuv444p16": (upsample_444, 16)}
+    if pix_fmt == "bgr0":
+        return yuv420p_to_bgr0(planes)
     if pix_fmt not in table:
         raise ValueError(f"no FATE conversion to {pix_fmt}")
     up, depth = table[pix_fmt]

@@ -524,10 +524,12 @@ static const uint8_t CUSTOM_STT[256] = {
 
 typedef struct pixfmt_info {
     const char *name;
-    int planes;        /* 1 gray, 3 yuv */
+    int planes;        /* 1 gray, 3 yuv / rgb */
     int hs, vs;
     int depth;         /* nominal depth of the storage format */
-    int family;        /* 9, 10, 16 or 8: which switch group it enters */
+    int family;        /* 9, 10, 16 or 8: which switch group it enters;
+                          32 packed RGB32 (ffv1enc.c:780-792), 100 + bits
+                          planar GBR (:793-814) */
 } pixfmt_info;
 
 static const pixfmt_info PIXFMTS[] = {
@@ -541,6 +543,9 @@ static const pixfmt_info PIXFMTS[] = {
     {"yuv444p10", 3, 0, 0, 10, 10},
     {"yuv420p16", 3, 1, 1, 16, 16}, {"yuv422p16", 3, 1, 0, 16, 16},
     {"yuv444p16", 3, 0, 0, 16, 16}, {"gray16", 1, 0, 0, 16, 16},
+    {"bgr0", 3, 0, 0, 8, 32},       {"0rgb32", 3, 0, 0, 8, 32},
+    {"gbrp9", 3, 0, 0, 9, 109},     {"gbrp10", 3, 0, 0, 10, 110},
+    {"gbrp12", 3, 0, 0, 12, 112},   {"gbrp14", 3, 0, 0, 14, 114},
 };
 
 int ffv1o_configure(ffv1o_config *cfg, int width, int height,
@@ -594,14 +599,28 @@ int ffv1o_configure(ffv1o_config *cfg, int width, int height,
 
     /* pix_fmt switch, ffv1enc.c:720-820 */
     int bits = 0, packed = 0;
+    if (pf->family == 32) { /* AV_PIX_FMT_0RGB32 (= bgr0 in memory), :787-792 */
+        bits = bits_per_raw_sample ? bits_per_raw_sample : 8;
+        if (bits != 8)
+            return AVERR_ENOSYS;
+    } else if (pf->family > 100) { /* GBRP9..14, :793-814 */
+        bits = bits_per_raw_sample ? bits_per_raw_sample : pf->family - 100;
+        packed = 1;
+        if (version < 1)
+            version = 1;
+        if (ac == 0)
+            ac = 2;
+    }
     if (pf->family == 9 && !bits_per_raw_sample)
         bits = 9;
-    if (pf->family == 9 || pf->family == 10) {
+    if (pf->family == 32 || pf->family > 100)
+        ; /* RGB: set above */
+    else if (pf->family == 9 || pf->family == 10) {
         packed = 1;
         if (!bits_per_raw_sample && !bits)
             bits = 10;
     }
-    if (pf->family >= 9) {
+    if (pf->family >= 9 && pf->family <= 16) {
         if (!bits_per_raw_sample && !bits)
             bits = 16;
         else if (!bits)
@@ -624,7 +643,8 @@ int ffv1o_configure(ffv1o_config *cfg, int width, int height,
     cfg->transparency = 0;
     cfg->bits_per_raw_sample = bits;
     cfg->packed_at_lsb = packed;
-    cfg->sample_bytes = pf->depth > 8 ? 2 : 1;
+    cfg->sample_bytes = pf->family == 32 ? 4 : pf->depth > 8 ? 2 : 1;
+    cfg->colorspace = pf->family == 32 || pf->family > 100;
     cfg->version = version;
     cfg->ac = ac;
     cfg->ec = ec;
@@ -699,7 +719,12 @@ ffv1o_enc *ffv1o_enc_new(const ffv1o_config *cfg)
     e->cfg = *cfg;
     build_quant_set(e->qt, cfg->context_model, cfg->bits_per_raw_sample);
     e->contexts = context_count_of(cfg->context_model);
-    e->coded_bits = cfg->bits_per_raw_sample <= 8 ? 8 : cfg->bits_per_raw_sample;
+    /* encode_line's bits: RGB samples after the RCT carry one bit more
+     * (encode_rgb_frame, ffv1enc.c:460-466: 9 for 8-bit) */
+    if (cfg->colorspace)
+        e->coded_bits = cfg->bits_per_raw_sample <= 8 ? 9 : cfg->bits_per_raw_sample + 1;
+    else
+        e->coded_bits = cfg->bits_per_raw_sample <= 8 ? 8 : cfg->bits_per_raw_sample;
     rc_default_tables(&e->dflt);
     if (cfg->ac == 2) {
         memcpy(e->stt, CUSTOM_STT, 256);
@@ -726,7 +751,7 @@ ffv1o_enc *ffv1o_enc_new(const ffv1o_config *cfg)
             s->ps[p].vlc = malloc((size_t)e->contexts * sizeof(vlc_ctx));
         }
     }
-    e->scratch = malloc((size_t)maxw * sizeof(int16_t) + 16);
+    e->scratch = malloc(3 * (size_t)maxw * sizeof(int16_t) + 16);
     return e;
 }
 
@@ -780,7 +805,7 @@ int ffv1o_enc_extradata(ffv1o_enc *e, uint8_t *buf, int cap)
     if (cfg->ac == 2)
         for (int i = 1; i < 256; i++)
             rc_put_symbol(&c, st, e->stt[i] - e->dflt.to1[i], 1);
-    rc_put_symbol(&c, st, 0, 0); /* colorspace YUV */
+    rc_put_symbol(&c, st, cfg->colorspace, 0);
     rc_put_symbol(&c, st, cfg->bits_per_raw_sample, 0);
     rc_put(&c, &st[0], cfg->chroma_planes);
     rc_put_symbol(&c, st, cfg->chroma_h_shift, 0);
@@ -820,7 +845,7 @@ static void put_v01_header(const ffv1o_enc *e, rc_enc *c)
     if (cfg->ac == 2)
         for (int i = 1; i < 256; i++)
             rc_put_symbol(c, st, e->stt[i] - c->t->to1[i], 1);
-    rc_put_symbol(c, st, 0, 0);
+    rc_put_symbol(c, st, cfg->colorspace, 0);
     if (cfg->version > 0)
         rc_put_symbol(c, st, cfg->bits_per_raw_sample, 0);
     rc_put(c, &st[0], cfg->chroma_planes);
@@ -915,69 +940,136 @@ static void sample_symbol(const int16_t qt[5][256], int model1, int bits,
     *diff_out = fold_residual(diff, bits);
 }
 
-/* encode_plane/encode_line for the range coder */
-static void code_plane_rac(ffv1o_enc *e, rc_enc *c, plane_state *ps,
-                           const int16_t *P, int w, int h)
+/* encode_line for the range coder: row y of slice plane P (w wide) */
+static void code_row_rac(ffv1o_enc *e, rc_enc *c, plane_state *ps,
+                         const int16_t *P, int w, int y)
 {
     int model1 = e->cfg.context_model;
-    for (int y = 0; y < h; y++)
-        for (int x = 0; x < w; x++) {
-            taps t;
-            int ctx, diff;
-            get_taps(P, w, x, y, &t);
-            sample_symbol(e->qt, model1, e->coded_bits, &t, &ctx, &diff);
-            rc_put_symbol(c, ps->rac + (int64_t)ctx * 32, diff, 1);
-        }
+    for (int x = 0; x < w; x++) {
+        taps t;
+        int ctx, diff;
+        get_taps(P, w, x, y, &t);
+        sample_symbol(e->qt, model1, e->coded_bits, &t, &ctx, &diff);
+        rc_put_symbol(c, ps->rac + (int64_t)ctx * 32, diff, 1);
+    }
 }
 
-/* encode_plane/encode_line for Golomb-Rice incl. run mode
- * (ffv1enc.c:306-370) */
-static void code_plane_golomb(ffv1o_enc *e, bitw *b, plane_state *ps,
-                              const int16_t *P, int w, int h)
+/* encode_line for Golomb-Rice incl. run mode (ffv1enc.c:306-370); the run
+ * index persists across the lines of a plane (YCbCr: encode_plane resets it,
+ * :379) or of the whole slice (RGB: encode_rgb_frame, :423) */
+static void code_row_golomb(ffv1o_enc *e, bitw *b, plane_state *ps,
+                            const int16_t *P, int w, int y, int *run_index_io)
 {
     int model1 = e->cfg.context_model;
     int bits = e->coded_bits;
+    int run_index = *run_index_io;
+    int run_count = 0, run_mode = 0;
+    for (int x = 0; x < w; x++) {
+        taps t;
+        int ctx, diff;
+        get_taps(P, w, x, y, &t);
+        sample_symbol(e->qt, model1, bits, &t, &ctx, &diff);
+        if (ctx == 0)
+            run_mode = 1;
+        if (run_mode) {
+            if (diff) {
+                while (run_count >= 1 << log2_run[run_index]) {
+                    run_count -= 1 << log2_run[run_index];
+                    run_index++;
+                    bw_put(b, 1, 1);
+                }
+                bw_put(b, 1 + log2_run[run_index], run_count);
+                if (run_index)
+                    run_index--;
+                run_count = 0;
+                run_mode = 0;
+                if (diff > 0)
+                    diff--;
+            } else {
+                run_count++;
+            }
+        }
+        if (!run_mode)
+            vlc_put(b, &ps->vlc[ctx], diff, bits);
+    }
+    if (run_mode) {
+        while (run_count >= 1 << log2_run[run_index]) {
+            run_count -= 1 << log2_run[run_index];
+            run_index++;
+            bw_put(b, 1, 1);
+        }
+        if (run_count)
+            bw_put(b, 1, 1);
+    }
+    *run_index_io = run_index;
+}
+
+static void code_plane(ffv1o_enc *e, void *coder, int golomb, plane_state *ps,
+                       const int16_t *P, int w, int h)
+{
     int run_index = 0;
     for (int y = 0; y < h; y++) {
-        int run_count = 0, run_mode = 0;
-        for (int x = 0; x < w; x++) {
-            taps t;
-            int ctx, diff;
-            get_taps(P, w, x, y, &t);
-            sample_symbol(e->qt, model1, bits, &t, &ctx, &diff);
-            if (ctx == 0)
-                run_mode = 1;
-            if (run_mode) {
-                if (diff) {
-                    while (run_count >= 1 << log2_run[run_index]) {
-                        run_count -= 1 << log2_run[run_index];
-                        run_index++;
-                        bw_put(b, 1, 1);
-                    }
-                    bw_put(b, 1 + log2_run[run_index], run_count);
-                    if (run_index)
-                        run_index--;
-                    run_count = 0;
-                    run_mode = 0;
-                    if (diff > 0)
-                        diff--;
-                } else {
-                    run_count++;
-                }
-            }
-            if (!run_mode)
-                vlc_put(b, &ps->vlc[ctx], diff, bits);
-        }
-        if (run_mode) {
-            while (run_count >= 1 << log2_run[run_index]) {
-                run_count -= 1 << log2_run[run_index];
-                run_index++;
-                bw_put(b, 1, 1);
-            }
-            if (run_count)
-                bw_put(b, 1, 1);
-        }
+        if (golomb)
+            code_row_golomb(e, (bitw *)coder, ps, P, w, y, &run_index);
+        else
+            code_row_rac(e, (rc_enc *)coder, ps, P, w, y);
     }
+}
+
+/* The RCT of encode_rgb_frame (ffv1enc.c:430-458, v3: both coefficients 1):
+ * pixel (x, y) of the slice as the three coded samples G', B', R'.  bgr0 is
+ * one packed plane (B, G, R, X bytes); gbrp is three u16 planes whose first
+ * is read as "b", second as "g", third as "r", as the reference does. */
+static void rct_sample(const ffv1o_config *cfg, const uint8_t *const planes[3],
+                       const int strides[3], int x, int y, int out[3])
+{
+    int b, g, r;
+    int bits = cfg->bits_per_raw_sample;
+    if (cfg->sample_bytes == 4) {
+        const uint8_t *px = planes[0] + (int64_t)y * strides[0] + 4 * (int64_t)x;
+        b = px[0];
+        g = px[1];
+        r = px[2];
+    } else {
+        const uint8_t *q0 = planes[0] + (int64_t)y * strides[0] + 2 * (int64_t)x;
+        const uint8_t *q1 = planes[1] + (int64_t)y * strides[1] + 2 * (int64_t)x;
+        const uint8_t *q2 = planes[2] + (int64_t)y * strides[2] + 2 * (int64_t)x;
+        b = q0[0] | (q0[1] << 8);
+        g = q1[0] | (q1[1] << 8);
+        r = q2[0] | (q2[1] << 8);
+    }
+    b -= g;
+    r -= g;
+    g += (b + r) >> 2;
+    out[0] = g;
+    out[1] = b + (1 << bits);
+    out[2] = r + (1 << bits);
+}
+
+/* encode_rgb_frame (ffv1enc.c:413-473): the lines of G', B', R' interleaved
+ * (row y of each plane in turn), plane contexts 0, 1, 1; one run index for
+ * the whole slice. */
+static void code_rgb_slice(ffv1o_enc *e, slice_ctx *s, const uint8_t *const planes[3],
+                           const int strides[3], void *coder, int golomb)
+{
+    int64_t n = (int64_t)s->w * s->h;
+    int16_t *P[3] = {e->scratch, e->scratch + n, e->scratch + 2 * n};
+    for (int y = 0; y < s->h; y++)
+        for (int x = 0; x < s->w; x++) {
+            int v[3];
+            rct_sample(&e->cfg, planes, strides, s->x0 + x, s->y0 + y, v);
+            for (int p = 0; p < 3; p++)
+                P[p][(int64_t)y * s->w + x] = (int16_t)v[p];
+        }
+    int run_index = 0;
+    for (int y = 0; y < s->h; y++)
+        for (int p = 0; p < 3; p++) {
+            plane_state *ps = &s->ps[(p + 1) / 2];
+            if (golomb)
+                code_row_golomb(e, (bitw *)coder, ps, P[p], s->w, y, &run_index);
+            else
+                code_row_rac(e, (rc_enc *)coder, ps, P[p], s->w, y);
+        }
 }
 
 static void reset_slice_states(ffv1o_enc *e, slice_ctx *s)
@@ -1009,12 +1101,17 @@ static void for_each_plane(ffv1o_enc *e, slice_ctx *s,
             y0 = s->y0 >> cfg->chroma_v_shift;
         }
         load_plane(cfg, planes[p], strides[p], x0, y0, w, h, e->scratch);
-        plane_state *ps = &s->ps[p ? 1 : 0];
-        if (golomb)
-            code_plane_golomb(e, (bitw *)coder, ps, e->scratch, w, h);
-        else
-            code_plane_rac(e, (rc_enc *)coder, ps, e->scratch, w, h);
+        code_plane(e, coder, golomb, &s->ps[p ? 1 : 0], e->scratch, w, h);
     }
+}
+
+static void code_slice_planes(ffv1o_enc *e, slice_ctx *s, const uint8_t *const planes[3],
+                              const int strides[3], void *coder, int golomb)
+{
+    if (e->cfg.colorspace)
+        code_rgb_slice(e, s, planes, strides, coder, golomb);
+    else
+        for_each_plane(e, s, planes, strides, coder, golomb);
 }
 
 int64_t ffv1o_enc_frame(ffv1o_enc *e, const uint8_t *const planes[3],
@@ -1054,11 +1151,11 @@ int64_t ffv1o_enc_frame(ffv1o_enc *e, const uint8_t *const planes[3],
             if (cfg->version > 2 || (s->x0 == 0 && s->y0 == 0))
                 ac_bytes = rc_finish(&c);
             bw_init(&b, s->buf + ac_bytes, s->cap - ac_bytes);
-            for_each_plane(e, s, planes, strides, &b, 1);
+            code_slice_planes(e, s, planes, strides, &b, 1);
             s->bytes = ac_bytes + bw_bytes(&b);
             s->error = b.overflow || c.overflow;
         } else {
-            for_each_plane(e, s, planes, strides, &c, 0);
+            code_slice_planes(e, s, planes, strides, &c, 0);
             uint8_t st = 129;
             rc_put(&c, &st, 0);
             s->bytes = rc_finish(&c);
@@ -1181,7 +1278,7 @@ typedef struct dslice {
 
 struct ffv1o_dec {
     ffv1o_config cfg;
-    int version, micro_version, ac, ec, bits, chroma_planes, hs, vs;
+    int version, micro_version, ac, ec, bits, chroma_planes, hs, vs, colorspace;
     int num_h, num_v;
     int16_t qsets[2][5][256];
     int ctx_count[2];
@@ -1243,7 +1340,7 @@ ffv1o_dec *ffv1o_dec_new(const ffv1o_config *cfg, const uint8_t *ex, int exn)
     d->frame_tab = d->dflt;
     d->version = cfg->version;
     d->num_h = d->num_v = 1;
-    d->scratch = malloc((size_t)cfg->width * cfg->height * sizeof(int16_t) + 16);
+    d->scratch = malloc(3 * (size_t)cfg->width * cfg->height * sizeof(int16_t) + 16);
     if (exn > 0) { /* read_extra_header, ffv1dec.c:517-636 */
         if (ffv1o_crc32(0, ex, exn) != 0)
             goto fail;
@@ -1260,7 +1357,8 @@ ffv1o_dec *ffv1o_dec_new(const ffv1o_config *cfg, const uint8_t *ex, int exn)
                 d->stt[i] = (uint8_t)(rc_get_symbol(&c, st, 1) + d->dflt.to1[i]);
             rc_custom_tables(&d->frame_tab, &d->dflt, d->stt);
         }
-        if (rc_get_symbol(&c, st, 0) != 0) /* colorspace */
+        d->colorspace = rc_get_symbol(&c, st, 0);
+        if (d->colorspace > 1)
             goto fail;
         d->bits = rc_get_symbol(&c, st, 0);
         d->chroma_planes = rc_get(&c, &st[0]);
@@ -1311,8 +1409,69 @@ void ffv1o_dec_free(ffv1o_dec *d)
     free(d);
 }
 
-/* decode_plane/decode_line (ffv1dec.c:100-231): reconstruct into P, then
- * store with the pixel format's alignment. */
+/* decode_line (ffv1dec.c:42-117): row y of slice plane P (w wide), samples
+ * masked to `bits` (av_mod_uintp2); the run index persists as in
+ * code_row_golomb. */
+static void decode_row(void *coder, int golomb, plane_state *ps, const int16_t qt[5][256],
+                       int model1, int16_t *P, int w, int y, int bits, int *run_index_io)
+{
+    int run_index = *run_index_io;
+    int run_count = 0, run_mode = 0;
+    for (int x = 0; x < w; x++) {
+        taps t;
+        P[(int64_t)y * w + x] = 0;
+        get_taps(P, w, x, y, &t);
+        int ctx = qt[0][(t.L - t.LT) & 0xFF] + qt[1][(t.LT - t.T) & 0xFF] +
+                  qt[2][(t.T - t.RT) & 0xFF];
+        if (model1)
+            ctx += qt[3][(t.LL - t.L) & 0xFF] + qt[4][(t.TT - t.T) & 0xFF];
+        int sign = ctx < 0, diff;
+        if (sign)
+            ctx = -ctx;
+        if (!golomb) {
+            diff = rc_get_symbol((rc_dec *)coder, ps->rac + (int64_t)ctx * 32, 1);
+        } else {
+            bitr *b = (bitr *)coder;
+            if (ctx == 0 && run_mode == 0)
+                run_mode = 1;
+            if (run_mode) {
+                if (run_count == 0 && run_mode == 1) {
+                    if (br_get(b, 1)) {
+                        run_count = 1 << log2_run[run_index];
+                        if (x + run_count <= w)
+                            run_index++;
+                    } else {
+                        run_count = log2_run[run_index]
+                                        ? br_get(b, log2_run[run_index]) : 0;
+                        if (run_index)
+                            run_index--;
+                        run_mode = 2;
+                    }
+                }
+                run_count--;
+                if (run_count < 0) {
+                    run_mode = 0;
+                    run_count = 0;
+                    diff = vlc_get(b, &ps->vlc[ctx], bits);
+                    if (diff >= 0)
+                        diff++;
+                } else {
+                    diff = 0;
+                }
+            } else {
+                diff = vlc_get(b, &ps->vlc[ctx], bits);
+            }
+        }
+        if (sign)
+            diff = -diff;
+        int pred = median3(t.L, t.L + t.T - t.LT, t.T);
+        P[(int64_t)y * w + x] = (int16_t)((unsigned)(pred + diff) & ((1u << bits) - 1));
+    }
+    *run_index_io = run_index;
+}
+
+/* decode_plane (ffv1dec.c:200-224): reconstruct into P, then store with
+ * the pixel format's alignment. */
 static void decode_plane_any(ffv1o_dec *d, void *coder, int golomb,
                              plane_state *ps, const int16_t qt[5][256],
                              int model1, int w, int h, uint8_t *dst,
@@ -1321,59 +1480,8 @@ static void decode_plane_any(ffv1o_dec *d, void *coder, int golomb,
     int bits = d->bits <= 8 ? 8 : d->bits;
     int16_t *P = d->scratch;
     int run_index = 0;
-    for (int y = 0; y < h; y++) {
-        int run_count = 0, run_mode = 0;
-        for (int x = 0; x < w; x++) {
-            taps t;
-            P[(int64_t)y * w + x] = 0;
-            get_taps(P, w, x, y, &t);
-            int ctx = qt[0][(t.L - t.LT) & 0xFF] + qt[1][(t.LT - t.T) & 0xFF] +
-                      qt[2][(t.T - t.RT) & 0xFF];
-            if (model1)
-                ctx += qt[3][(t.LL - t.L) & 0xFF] + qt[4][(t.TT - t.T) & 0xFF];
-            int sign = ctx < 0, diff;
-            if (sign)
-                ctx = -ctx;
-            if (!golomb) {
-                diff = rc_get_symbol((rc_dec *)coder, ps->rac + (int64_t)ctx * 32, 1);
-            } else {
-                bitr *b = (bitr *)coder;
-                if (ctx == 0 && run_mode == 0)
-                    run_mode = 1;
-                if (run_mode) {
-                    if (run_count == 0 && run_mode == 1) {
-                        if (br_get(b, 1)) {
-                            run_count = 1 << log2_run[run_index];
-                            if (x + run_count <= w)
-                                run_index++;
-                        } else {
-                            run_count = log2_run[run_index]
-                                            ? br_get(b, log2_run[run_index]) : 0;
-                            if (run_index)
-                                run_index--;
-                            run_mode = 2;
-                        }
-                    }
-                    run_count--;
-                    if (run_count < 0) {
-                        run_mode = 0;
-                        run_count = 0;
-                        diff = vlc_get(b, &ps->vlc[ctx], bits);
-                        if (diff >= 0)
-                            diff++;
-                    } else {
-                        diff = 0;
-                    }
-                } else {
-                    diff = vlc_get(b, &ps->vlc[ctx], bits);
-                }
-            }
-            if (sign)
-                diff = -diff;
-            int pred = median3(t.L, t.L + t.T - t.LT, t.T);
-            P[(int64_t)y * w + x] = (int16_t)((unsigned)(pred + diff) & ((1u << bits) - 1));
-        }
-    }
+    for (int y = 0; y < h; y++)
+        decode_row(coder, golomb, ps, qt, model1, P, w, y, bits, &run_index);
     for (int y = 0; y < h; y++) {
         uint8_t *row = dst + (int64_t)(y0 + y) * stride;
         for (int x = 0; x < w; x++) {
@@ -1388,6 +1496,47 @@ static void decode_plane_any(ffv1o_dec *d, void *coder, int golomb,
             }
         }
     }
+}
+
+/* decode_rgb_frame (ffv1dec.c:226-280): G', B', R' lines interleaved, then
+ * the inverse RCT; bgr0 gets B, G, R and a zero fourth byte. */
+static void decode_rgb_slice(ffv1o_dec *d, void *coder, int golomb, dslice *s,
+                             const int16_t qt[5][256], int model1,
+                             uint8_t *const planes[3], const int strides[3])
+{
+    int lbd = d->bits <= 8;
+    int bits = lbd ? 9 : d->bits + 1;
+    int offset = 1 << (lbd ? 8 : d->bits);
+    int64_t n = (int64_t)s->w * s->h;
+    int16_t *P[3] = {d->scratch, d->scratch + n, d->scratch + 2 * n};
+    int run_index = 0;
+    for (int y = 0; y < s->h; y++)
+        for (int p = 0; p < 3; p++)
+            decode_row(coder, golomb, &s->ps[(p + 1) / 2], qt, model1, P[p], s->w, y, bits,
+                       &run_index);
+    for (int y = 0; y < s->h; y++)
+        for (int x = 0; x < s->w; x++) {
+            int64_t i = (int64_t)y * s->w + x;
+            int g = P[0][i], b = P[1][i] - offset, r = P[2][i] - offset;
+            g -= (b + r) >> 2;
+            b += g;
+            r += g;
+            int X = s->x0 + x, Y = s->y0 + y;
+            if (lbd) {
+                uint8_t *px = planes[0] + (int64_t)Y * strides[0] + 4 * (int64_t)X;
+                px[0] = (uint8_t)b;
+                px[1] = (uint8_t)g;
+                px[2] = (uint8_t)r;
+                px[3] = 0;
+            } else {
+                int v[3] = {b, g, r};
+                for (int k = 0; k < 3; k++) {
+                    uint8_t *q = planes[k] + (int64_t)Y * strides[k] + 2 * (int64_t)X;
+                    q[0] = (uint8_t)v[k];
+                    q[1] = (uint8_t)(v[k] >> 8);
+                }
+            }
+        }
 }
 
 int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
@@ -1410,7 +1559,7 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
             } else {
                 d->frame_tab = d->dflt;
             }
-            (void)rc_get_symbol(&c0, st, 0);
+            d->colorspace = rc_get_symbol(&c0, st, 0);
             d->bits = d->version > 0 ? rc_get_symbol(&c0, st, 0) : 8;
             d->chroma_planes = rc_get(&c0, &st[0]);
             d->hs = rc_get_symbol(&c0, st, 0);
@@ -1517,6 +1666,10 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
             b.pos = 0;
             b.nbits = blen * 8;
             coder = &b;
+        }
+        if (d->colorspace) {
+            decode_rgb_slice(d, coder, golomb, s, qt, model1, planes, strides);
+            continue;
         }
         int np = d->chroma_planes ? 3 : 1;
         for (int pl = 0; pl < np; pl++) {

@@ -50,6 +50,8 @@ typedef struct ffv1o_config {
     int num_v_slices;
     int gop_size;             /* 0 => every frame is a keyframe               */
     int sar_num, sar_den;     /* coded in the v3 slice header                 */
+    int colorspace;           /* 0 YCbCr, 1 RGB (encode_rgb_frame: bgr0 packed
+                                 in plane 0, or gbrp planes G, B, R)           */
 } ffv1o_config;
 
 /* encode_init's option -> parameter derivation (ffv1enc.c:669-1029).

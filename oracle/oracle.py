@@ -22,7 +22,7 @@ class Config(ctypes.Structure):
         "width", "height", "chroma_planes", "chroma_h_shift", "chroma_v_shift",
         "transparency", "bits_per_raw_sample", "packed_at_lsb", "sample_bytes",
         "version", "ac", "ec", "context_model", "num_h_slices", "num_v_slices",
-        "gop_size", "sar_num", "sar_den")]
+        "gop_size", "sar_num", "sar_den", "colorspace")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -88,6 +88,8 @@ def configure(width, height, pix_fmt, slices=0, level=-1, coder=-1, context=0,
 
 def plane_shapes(cfg: Config):
     w, h = cfg.width, cfg.height
+    if cfg.colorspace and cfg.sample_bytes == 4:  # bgr0: one packed plane
+        return [(h, 4 * w)]
     cw = -((-w) >> cfg.chroma_h_shift)
     ch = -((-h) >> cfg.chroma_v_shift)
     shapes = [(h, w)]
@@ -183,7 +185,7 @@ class Decoder:
             self._h = None
 
     def decode(self, packet: bytes):
-        dt = np.uint8 if self.cfg.sample_bytes == 1 else np.uint16
+        dt = np.uint8 if self.cfg.sample_bytes in (1, 4) else np.uint16
         planes = [np.zeros(s, dt) for s in plane_shapes(self.cfg)]
         arr, strides = _plane_ptrs(planes)
         pk = np.frombuffer(packet, np.uint8).copy()

@@ -69,8 +69,8 @@ class Stream:
         else:
             cfg = self.oracle_config()
             rng = np.random.default_rng(self.seed)
-            dt = np.uint8 if cfg.sample_bytes == 1 else np.uint16
-            hi = 1 << (cfg.bits_per_raw_sample if cfg.packed_at_lsb or cfg.sample_bytes == 1 else 16)
+            dt = np.uint8 if cfg.sample_bytes in (1, 4) else np.uint16
+            hi = 1 << (cfg.bits_per_raw_sample if cfg.packed_at_lsb or cfg.sample_bytes != 2 else 16)
             for _ in range(self.nframes):
                 fr = []
                 for shp in oracle.plane_shapes(cfg):

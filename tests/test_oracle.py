@@ -121,3 +121,31 @@ def test_pframes_smaller_than_keyframes_and_state_carry_matters():
     for i in range(1, 4):
         assert not pk[i][1] and pi[i][1]
         assert len(pk[i][0]) < len(pi[i][0])
+
+
+RGB_STREAMS = [
+    Stream("bgr0_v3", 176, 144, "bgr0", 4, slices=4, level=3, gop_size=3, source="random"),
+    Stream("bgr0_golomb_v1", 96, 64, "bgr0", 3, level=1, coder=0, gop_size=2, source="random"),
+    Stream("gbrp10_v3", 128, 96, "gbrp10", 3, slices=4, level=3, gop_size=2, source="random"),
+    Stream("gbrp14_ctx1", 64, 48, "gbrp14", 3, slices=4, context=1, gop_size=3, source="random"),
+]
+
+
+@pytest.mark.parametrize("stream", RGB_STREAMS, ids=[s.name for s in RGB_STREAMS])
+def test_oracle_rgb_roundtrip(stream):
+    """RGB through the reversible colour transform (ffv1enc.c:413-473,
+    ffv1dec.c:226-280): lossless, the bgr0 padding byte comes back 0."""
+    frames = list(stream.frames())
+    cfg, ex, pkts = oracle_encode(stream, frames)
+    assert cfg.colorspace == 1
+    if stream.pix_fmt.startswith("gbrp"):
+        assert cfg.ac >= 1 and cfg.version >= 1  # coder forced (ffv1enc.c:810-814)
+    dec = oracle.Decoder(cfg, ex)
+    for (p, key), f in zip(pkts, frames):
+        planes, k = dec.decode(p)
+        assert k == key
+        for a, b in zip(planes, f):
+            if stream.pix_fmt == "bgr0":
+                b = b.copy()
+                b[:, 3::4] = 0
+            np.testing.assert_array_equal(a, b)
