@@ -333,14 +333,17 @@ int ffv1hip_abi_version(void) { return FFV1HIP_ABI_VERSION; }
 int ffv1hip_configure(ffv1hip_params* out, const ffv1hip_options* o) {
   if (!out || !o || !o->pix_fmt || o->width <= 0 || o->height <= 0)
     return set_err(-22, "invalid arguments");
-  struct Fmt { const char* name; int planes, hs, vs, depth; };
+  // rgb: 1 AV_PIX_FMT_0RGB32 (bgr0 bytes), 2 GBRP9..14 (ffv1enc.c:787-814)
+  struct Fmt { const char* name; int planes, hs, vs, depth, rgb; };
   static const Fmt fmts[] = {
-      {"yuv420p", 3, 1, 1, 8},    {"yuv422p", 3, 1, 0, 8},    {"yuv444p", 3, 0, 0, 8},
-      {"yuv440p", 3, 0, 1, 8},    {"yuv411p", 3, 2, 0, 8},    {"yuv410p", 3, 2, 2, 8},
-      {"gray", 1, 0, 0, 8},       {"yuv420p9", 3, 1, 1, 9},   {"yuv422p9", 3, 1, 0, 9},
-      {"yuv444p9", 3, 0, 0, 9},   {"yuv420p10", 3, 1, 1, 10}, {"yuv422p10", 3, 1, 0, 10},
-      {"yuv444p10", 3, 0, 0, 10}, {"yuv420p16", 3, 1, 1, 16}, {"yuv422p16", 3, 1, 0, 16},
-      {"yuv444p16", 3, 0, 0, 16}, {"gray16", 1, 0, 0, 16},
+      {"yuv420p", 3, 1, 1, 8, 0},    {"yuv422p", 3, 1, 0, 8, 0},    {"yuv444p", 3, 0, 0, 8, 0},
+      {"yuv440p", 3, 0, 1, 8, 0},    {"yuv411p", 3, 2, 0, 8, 0},    {"yuv410p", 3, 2, 2, 8, 0},
+      {"gray", 1, 0, 0, 8, 0},       {"yuv420p9", 3, 1, 1, 9, 0},   {"yuv422p9", 3, 1, 0, 9, 0},
+      {"yuv444p9", 3, 0, 0, 9, 0},   {"yuv420p10", 3, 1, 1, 10, 0}, {"yuv422p10", 3, 1, 0, 10, 0},
+      {"yuv444p10", 3, 0, 0, 10, 0}, {"yuv420p16", 3, 1, 1, 16, 0}, {"yuv422p16", 3, 1, 0, 16, 0},
+      {"yuv444p16", 3, 0, 0, 16, 0}, {"gray16", 1, 0, 0, 16, 0},    {"bgr0", 3, 0, 0, 8, 1},
+      {"0rgb32", 3, 0, 0, 8, 1},     {"gbrp9", 3, 0, 0, 9, 2},      {"gbrp10", 3, 0, 0, 10, 2},
+      {"gbrp12", 3, 0, 0, 12, 2},    {"gbrp14", 3, 0, 0, 14, 2},
   };
   const Fmt* f = nullptr;
   for (const Fmt& c : fmts)
@@ -371,7 +374,15 @@ int ffv1hip_configure(ffv1hip_params* out, const ffv1hip_options* o) {
   if (o->coder == -2) ac = 1;
   // sample format (ffv1enc.c:720-820)
   int bits = 0, packed = 0;
-  if (f->depth > 8) {
+  if (f->rgb == 1) {
+    bits = o->bits_per_raw_sample ? o->bits_per_raw_sample : 8;
+    if (bits != 8) return set_err(-38, "bgr0 with %d bits", bits);
+  } else if (f->rgb == 2) {  // GBRPn: bits from the format, raw u16 samples
+    bits = o->bits_per_raw_sample ? o->bits_per_raw_sample : f->depth;
+    packed = 1;
+    if (ac == 0) ac = 2;
+    version = std::max(version, 1);
+  } else if (f->depth > 8) {
     if (f->depth == 9 && !o->bits_per_raw_sample) bits = 9;
     if (f->depth <= 10) {
       packed = 1;
@@ -390,7 +401,8 @@ int ffv1hip_configure(ffv1hip_params* out, const ffv1hip_options* o) {
   p.chroma_v_shift = f->planes == 3 ? f->vs : 0;
   p.bits_per_raw_sample = bits;
   p.packed_at_lsb = packed;
-  p.sample_bytes = f->depth > 8 ? 2 : 1;
+  p.sample_bytes = f->rgb == 1 ? 4 : f->depth > 8 ? 2 : 1;
+  p.colorspace = f->rgb != 0;
   p.version = version;
   p.ac = ac;
   p.context_model = o->context;
@@ -427,7 +439,7 @@ static int build_extradata(ffv1hip_ctx* c) {
   r.symbol(st, p.ac, false);
   if (p.ac == 2)
     for (int i = 1; i < 256; i++) r.symbol(st, c->frame.to1[i] - c->dflt.to1[i], true);
-  r.symbol(st, 0, false);  // YUV colorspace
+  r.symbol(st, p.colorspace, false);
   r.symbol(st, p.bits_per_raw_sample, false);
   r.put(st, p.chroma_planes);
   r.symbol(st, p.chroma_h_shift, false);
@@ -479,7 +491,7 @@ static void build_ops(ffv1hip_ctx* c) {
           L.sym(kSetHdr, 0, p.ac, false);
           if (p.ac == 2)
             for (int i = 1; i < 256; i++) L.sym(kSetHdr, 0, c->frame.to1[i] - c->dflt.to1[i], true);
-          L.sym(kSetHdr, 0, 0, false);
+          L.sym(kSetHdr, 0, p.colorspace, false);
           if (p.version > 0) L.sym(kSetHdr, 0, p.bits_per_raw_sample, false);
           L.bit(kSetHdr, 0, p.chroma_planes);
           L.sym(kSetHdr, 0, p.chroma_h_shift, false);
@@ -636,9 +648,14 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
   };
   if (!params || max_batch_frames <= 0) return fail(set_err(-22, "invalid arguments"));
   const ffv1hip_params& p = *params;
+  const bool fmt_ok = p.colorspace == 0   ? (p.sample_bytes == 1) == (p.bits_per_raw_sample == 8) && p.sample_bytes <= 2
+                     : p.colorspace == 1 ? p.chroma_planes && !p.chroma_h_shift && !p.chroma_v_shift &&
+                                               (p.sample_bytes == 4 ? p.bits_per_raw_sample == 8
+                                                                    : p.sample_bytes == 2 && p.packed_at_lsb &&
+                                                                          p.bits_per_raw_sample <= 14)
+                                         : false;
   if (p.version == 2 || p.version > 3 || p.num_h_slices * p.num_v_slices > 256 ||
-      p.bits_per_raw_sample < 8 || p.bits_per_raw_sample > 16 || p.width <= 0 || p.height <= 0 ||
-      (p.sample_bytes == 1) != (p.bits_per_raw_sample == 8))
+      p.bits_per_raw_sample < 8 || p.bits_per_raw_sample > 16 || p.width <= 0 || p.height <= 0 || !fmt_ok)
     return fail(set_err(-38, "unsupported parameter set"));
   if (p.num_h_slices > p.width || p.num_v_slices > p.height)
     return fail(set_err(-22, "more slices than rows/columns"));
@@ -657,7 +674,7 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
   const int cw = p.chroma_planes ? -((-p.width) >> p.chroma_h_shift) : 0;
   const int ch = p.chroma_planes ? -((-p.height) >> p.chroma_v_shift) : 0;
   c->plane_bytes[0] = int64_t(p.width) * p.height * p.sample_bytes;
-  c->plane_bytes[1] = c->plane_bytes[2] = int64_t(cw) * ch * p.sample_bytes;
+  c->plane_bytes[1] = c->plane_bytes[2] = p.sample_bytes == 4 ? 0 : int64_t(cw) * ch * p.sample_bytes;
   c->frame_bytes = (c->plane_bytes[0] + 2 * c->plane_bytes[1] + 255) & ~int64_t(255);
   // Per-slice geometry and symbol-stream layout (ffv1.c:117-145,
   // ffv1enc.c:1185-1196); each slice's stream is padded to 4 symbols.
@@ -713,7 +730,8 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
   {
     const char* mode = std::getenv("FFV1HIP_CODER");
     const int64_t lds = walk_lds_bytes(int64_t(2) * c->contexts * 32);
-    c->frames_mode = p.ac && lds <= kWalkLdsMax && !(mode && std::strcmp(mode, "chain") == 0);
+    // RGB interleaves the three planes' rows (encode_rgb_frame): chained
+    c->frames_mode = p.ac && !p.colorspace && lds <= kWalkLdsMax && !(mode && std::strcmp(mode, "chain") == 0);
     c->wmax = 2 * (p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample) + 1;
     // the decision-stream coder writes a slice's digits (2 bytes each) where
     // ffv1_sink then writes its bytes
@@ -753,6 +771,14 @@ void ffv1hip_reset(ffv1hip_ctx* c) {
     c->picture_number = 0;
     c->have_states = false;
   }
+}
+
+// The sample width the residuals are folded / Golomb-coded at: RGB codes
+// the transformed G', B' + off, R' + off with one more bit, 9 at 8 bit
+// (ffv1enc.c:464-467).
+static int coded_bits(const ffv1hip_params& p) {
+  if (p.colorspace) return p.bits_per_raw_sample <= 8 ? 9 : p.bits_per_raw_sample + 1;
+  return p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample;
 }
 
 static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_bytes,
@@ -826,7 +852,9 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   sa.sample_bytes = p.sample_bytes;
   sa.packed_at_lsb = p.packed_at_lsb;
   sa.msb_shift = 16 - p.bits_per_raw_sample;
-  sa.coded_bits = p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample;
+  sa.coded_bits = coded_bits(p);
+  sa.rgb = p.colorspace;
+  sa.rct_offset = 1 << p.bits_per_raw_sample;
   sa.contexts = c->contexts;
   sa.model1 = p.context_model;
   sa.qt = c->d_qt;
@@ -863,7 +891,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   ca.slice_stride = c->slice_stride;
   ca.slice_bytes = c->d_slice_bytes;
   ca.version = p.version;
-  ca.coded_bits = p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample;
+  ca.coded_bits = coded_bits(p);
+  ca.rgb = p.colorspace;
 
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev[0], st));
   // brackets one launch with events when profiling (kind: 0 symbols, 1 code, 2 states)
@@ -1143,26 +1172,38 @@ int ffv1hip_device_packets(ffv1hip_ctx* c, void** d_packets, int64_t* packet_str
   return 0;
 }
 
+// Where the planes of one frame sit in a batch slot of d_frames (tightly
+// packed rows): np planes, plane k at off[k] with rows[k] rows of pst[k]
+// bytes.  bgr0 is one packed plane.
+static void slot_layout(const ffv1hip_ctx* c, int64_t off[3], int pst[3], int rows[3], int* np) {
+  const ffv1hip_params& p = c->P;
+  const int cw = -((-p.width) >> p.chroma_h_shift), ch = -((-p.height) >> p.chroma_v_shift);
+  *np = p.sample_bytes == 4 ? 1 : p.chroma_planes ? 3 : 1;
+  off[0] = 0;
+  off[1] = c->plane_bytes[0];
+  off[2] = c->plane_bytes[0] + c->plane_bytes[1];
+  pst[0] = p.width * p.sample_bytes;
+  pst[1] = pst[2] = cw * p.sample_bytes;
+  rows[0] = p.height;
+  rows[1] = rows[2] = ch;
+}
+
 int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides, int n_frames,
                    uint8_t* out, int64_t out_cap, int64_t* sizes, int* key_flags) {
   if (!c || !planes || !strides) return set_err(-22, "null argument");
-  const ffv1hip_params& p = c->P;
   HIP_TRY(hipSetDevice(c->device));
-  const int np = p.chroma_planes ? 3 : 1;
-  const int cw = -((-p.width) >> p.chroma_h_shift), ch = -((-p.height) >> p.chroma_v_shift);
-  int64_t off[3] = {0, c->plane_bytes[0], c->plane_bytes[0] + c->plane_bytes[1]};
-  int pst[3] = {p.width * p.sample_bytes, cw * p.sample_bytes, cw * p.sample_bytes};
+  int64_t off[3];
+  int pst[3], rows[3], np;
+  slot_layout(c, off, pst, rows, &np);
   int64_t used = 0;
   std::vector<int64_t> local_sizes(size_t(c->max_batch));
   for (int base = 0; base < n_frames; base += c->max_batch) {
     const int n = std::min(c->max_batch, n_frames - base);
     for (int i = 0; i < n; i++)
-      for (int k = 0; k < np; k++) {
-        const int rows = k ? ch : p.height;
+      for (int k = 0; k < np; k++)
         HIP_TRY(hipMemcpy2DAsync(c->d_frames + int64_t(i) * c->frame_bytes + off[k], pst[k],
-                                 planes[3 * (base + i) + k], strides[3 * (base + i) + k], pst[k], rows,
+                                 planes[3 * (base + i) + k], strides[3 * (base + i) + k], pst[k], rows[k],
                                  hipMemcpyHostToDevice, c->stream));
-      }
     int rc = run_batch(c, c->d_frames, c->frame_bytes, off, pst, n, c->stream);
     if (rc < 0) return rc;
     rc = ffv1hip_fetch(c, out ? out + used : nullptr, out_cap - used, local_sizes.data(),
@@ -1179,10 +1220,9 @@ int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides
 // The queued frames as one batch: encode, fetch the packets into `ready`.
 static int encode_queue(ffv1hip_ctx* c) {
   const int n = int(c->q_pts.size());
-  const ffv1hip_params& p = c->P;
-  const int cw = -((-p.width) >> p.chroma_h_shift);
-  int64_t off[3] = {0, c->plane_bytes[0], c->plane_bytes[0] + c->plane_bytes[1]};
-  int pst[3] = {p.width * p.sample_bytes, cw * p.sample_bytes, cw * p.sample_bytes};
+  int64_t off[3];
+  int pst[3], rows[3], np;
+  slot_layout(c, off, pst, rows, &np);
   int rc = run_batch(c, c->d_frames, c->frame_bytes, off, pst, n, c->stream);
   if (rc < 0) return rc;
   std::vector<int64_t> sz(n);
@@ -1215,16 +1255,14 @@ int ffv1hip_encode2(ffv1hip_ctx* c, const void* const planes[3], const int strid
     if (!strides) return set_err(-22, "null strides");
     // the frame is copied into the next batch slot (the caller keeps
     // ownership: it may reuse the buffer once the call returns)
-    const ffv1hip_params& p = c->P;
-    const int np = p.chroma_planes ? 3 : 1;
-    const int cw = -((-p.width) >> p.chroma_h_shift), ch = -((-p.height) >> p.chroma_v_shift);
-    const int64_t off[3] = {0, c->plane_bytes[0], c->plane_bytes[0] + c->plane_bytes[1]};
-    const int pst[3] = {p.width * p.sample_bytes, cw * p.sample_bytes, cw * p.sample_bytes};
+    int64_t off[3];
+    int pst[3], rows[3], np;
+    slot_layout(c, off, pst, rows, &np);
     const int64_t slot = int64_t(c->q_pts.size());
     for (int k = 0; k < np; k++) {
       if (!planes[k]) return set_err(-22, "null plane %d", k);
       HIP_TRY(hipMemcpy2D(c->d_frames + slot * c->frame_bytes + off[k], pst[k], planes[k], strides[k], pst[k],
-                          k ? ch : p.height, hipMemcpyHostToDevice));
+                          rows[k], hipMemcpyHostToDevice));
     }
     c->q_pts.push_back(pts);
     // a full queue is encoded once the packets of the previous batch are out
@@ -1382,8 +1420,8 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
   const ffv1hip_params& p = *params;
   if (p.version != 3 || p.ac == 0 || p.context_model != 0 || p.num_h_slices * p.num_v_slices > 256 ||
       p.bits_per_raw_sample < 8 || p.bits_per_raw_sample > 16 || p.width <= 0 || p.height <= 0 ||
-      p.num_h_slices <= 0 || p.num_v_slices <= 0)
-    return fail(set_err(-38, "GPU decoder: version 3, range coder, context model 0 only"));
+      p.num_h_slices <= 0 || p.num_v_slices <= 0 || p.colorspace != 0)
+    return fail(set_err(-38, "GPU decoder: YCbCr, version 3, range coder, context model 0 only"));
   // The stream's extradata must be the one these parameters produce
   // (read_extradata, ffv1dec.c:509-631, would derive the same parameters).
   ffv1hip_ctx tmp;

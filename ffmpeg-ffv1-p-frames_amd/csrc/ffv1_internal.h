@@ -64,6 +64,7 @@ struct SymbolArgs {
   const SliceGeom* geom;
   int nslices, nplanes;
   int sample_bytes, packed_at_lsb, msb_shift, coded_bits;
+  int rgb, rct_offset;        // RGB: the samples are G', B' + off, R' + off, rows interleaved
   int contexts, model1;
   const int16_t* qt;          // [5][256]
   uint32_t* sym;              // [slot][frame_samples]: (row << 16) | (uint16)diff
@@ -136,6 +137,7 @@ struct CodeArgs {
   int* status;                // [0] slices over the byte budget, [1] most bytes a slice needed
   int version;                // bitstream version (Golomb: v3 adds a 129/0 decision)
   int coded_bits;             // "bits" of encode_line (8 for <=8-bit)
+  int rgb;                    // RGB: a slice's three planes are row-interleaved (chained coders)
   int nframes;                // decision-stream mode: frames of the batch
   int nopsets;                // decision-stream mode: op sets the header programs use
   DecisionStream ds;

@@ -135,7 +135,30 @@ __device__ __forceinline__ int wave_incl_scan(int x, int /*lane*/) {
 // the previous lane's value (lane 0: 0), a DPP wave_shr:1
 __device__ __forceinline__ int wave_prev(int x) { return __builtin_amdgcn_update_dpp(0, x, 0x138, 0xf, 0xf, true); }
 
-template <int SB>  // stored sample bytes, 1 or 2
+// RGB (encode_rgb_frame, ffv1enc.c:413-459): pixel (x, y) of the frame as
+// coded plane p of the reversible colour transform, G' = g + (b' + r') >> 2,
+// B' = b - g + off, R' = r - g + off.  bgr0: one u32 per pixel (B, G, R, X
+// bytes); gbrp: three u16 planes read in AVFrame data[] order as b, g, r.
+template <int SB>
+__device__ __forceinline__ int rct_sample(const SymbolArgs& a, const uint8_t* fr, int p, int x, int y) {
+  int b, g, r;
+  if constexpr (SB == 4) {
+    const uint32_t v = reinterpret_cast<const uint32_t*>(fr + a.plane_off[0] + (int64_t)y * a.plane_stride[0])[x];
+    b = v & 0xFF;
+    g = (v >> 8) & 0xFF;
+    r = (v >> 16) & 0xFF;
+  } else {
+    b = reinterpret_cast<const uint16_t*>(fr + a.plane_off[0] + (int64_t)y * a.plane_stride[0])[x];
+    g = reinterpret_cast<const uint16_t*>(fr + a.plane_off[1] + (int64_t)y * a.plane_stride[1])[x];
+    r = reinterpret_cast<const uint16_t*>(fr + a.plane_off[2] + (int64_t)y * a.plane_stride[2])[x];
+  }
+  b -= g;
+  r -= g;
+  g += (b + r) >> 2;
+  return p == 0 ? g : (p == 1 ? b : r) + a.rct_offset;
+}
+
+template <int SB>  // stored sample bytes, 1 or 2; 4: bgr0
 __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   __shared__ int16_t qt[5 * 256];
   __shared__ int red[kSymThreads / kWave];
@@ -151,17 +174,24 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   const int pw = g.pw[p], ph = g.ph[p], px = g.px[p], py = g.py[p];
   const uint8_t* base = a.frames + (int64_t)f * a.frame_bytes + a.plane_off[p];
   const int stride = a.plane_stride[p];
-  uint32_t* out = a.sym + (int64_t)slot * a.frame_samples + g.sym_off + g.plane_sym_off[p];
+  // RGB: the slice's G', B', R' rows interleave (ffv1enc.c:428-471)
+  uint32_t* out = a.sym + (int64_t)slot * a.frame_samples + g.sym_off + (a.rgb ? 0 : g.plane_sym_off[p]);
   const int row0 = p ? a.contexts : 0;  // plane context 1 rows follow plane 0's
 
   // sample of the slice plane as int16 (ffv1enc.c:390-407), at in-plane
   // coordinates: every load is unconditional, so the loads of a step are
   // issued back to back and waited for once
   const int sh = a.packed_at_lsb ? 0 : a.msb_shift;
+  const uint8_t* const fr = a.frames + (int64_t)f * a.frame_bytes;
   auto load = [&](int x, int y) -> int {
-    const uint8_t* r = base + (int64_t)(py + y) * stride;
-    if constexpr (SB == 1) return r[px + x];
-    else return (int16_t)(reinterpret_cast<const uint16_t*>(r)[px + x] >> sh);
+    if constexpr (SB == 4) {
+      return rct_sample<4>(a, fr, p, px + x, py + y);
+    } else {
+      if (SB == 2 && a.rgb) return rct_sample<2>(a, fr, p, px + x, py + y);
+      const uint8_t* r = base + (int64_t)(py + y) * stride;
+      if constexpr (SB == 1) return r[px + x];
+      else return (int16_t)(reinterpret_cast<const uint16_t*>(r)[px + x] >> sh);
+    }
   };
 
   int ndec = 0;
@@ -255,7 +285,7 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
         if (lane < kChunkWords - kWave) dst[kWave + lane] = cs[kWave + lane];
       }
     } else if (valid) {
-      out[idx] = ((uint32_t)(row0 + ctx) << 16) | (uint16_t)diff;
+      out[a.rgb ? ((int64_t)y * 3 + p) * pw + x : idx] = ((uint32_t)(row0 + ctx) << 16) | (uint16_t)diff;
     }
   }
   if (count && b0 < b1) {
@@ -1720,43 +1750,50 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
   const uint32_t* sp = a.sym + (int64_t)seg_i * a.frame_samples + g.sym_off;
   const int bits = a.coded_bits;
   int64_t idx = 0;
-  for (int p = 0; p < 3; p++) {
-    const int pw = g.pw[p], ph = g.ph[p];
-    int run_index = 0;  // per plane (ffv1enc.c:379)
-    for (int y = 0; y < ph; y++) {
-      int run_count = 0, run_mode = 0;
-      for (int x = 0; x < pw; x++, idx++) {
-        const uint32_t sv = sp[idx];
-        const int row = (int)(sv >> 16);
-        const int ctx = p ? row - a.state_bytes / 64 : row;  // context inside its plane
-        int diff = (int16_t)(sv & 0xFFFF);
-        if (ctx == 0) run_mode = 1;
-        if (run_mode) {
-          if (diff) {
-            while (run_count >= (1 << kLog2Run[run_index])) {
-              run_count -= 1 << kLog2Run[run_index];
-              run_index++;
-              b.put(1, 1);
-            }
-            b.put(1 + kLog2Run[run_index], run_count);
-            if (run_index) run_index--;
-            run_count = 0;
-            run_mode = 0;
-            if (diff > 0) diff--;
-          } else {
-            run_count++;
-          }
-        }
-        if (!run_mode) vlc_put(b, table[row], diff, bits);
-      }
+  int run_index = 0;
+  // one row of encode_line's Golomb branch (ffv1enc.c:318-368)
+  auto code_row = [&](int pw, bool chroma) {
+    int run_count = 0, run_mode = 0;
+    for (int x = 0; x < pw; x++, idx++) {
+      const uint32_t sv = sp[idx];
+      const int row = (int)(sv >> 16);
+      const int ctx = chroma ? row - a.state_bytes / 64 : row;  // context inside its plane
+      int diff = (int16_t)(sv & 0xFFFF);
+      if (ctx == 0) run_mode = 1;
       if (run_mode) {
-        while (run_count >= (1 << kLog2Run[run_index])) {
-          run_count -= 1 << kLog2Run[run_index];
-          run_index++;
-          b.put(1, 1);
+        if (diff) {
+          while (run_count >= (1 << kLog2Run[run_index])) {
+            run_count -= 1 << kLog2Run[run_index];
+            run_index++;
+            b.put(1, 1);
+          }
+          b.put(1 + kLog2Run[run_index], run_count);
+          if (run_index) run_index--;
+          run_count = 0;
+          run_mode = 0;
+          if (diff > 0) diff--;
+        } else {
+          run_count++;
         }
-        if (run_count) b.put(1, 1);
       }
+      if (!run_mode) vlc_put(b, table[row], diff, bits);
+    }
+    if (run_mode) {
+      while (run_count >= (1 << kLog2Run[run_index])) {
+        run_count -= 1 << kLog2Run[run_index];
+        run_index++;
+        b.put(1, 1);
+      }
+      if (run_count) b.put(1, 1);
+    }
+  };
+  if (a.rgb) {  // rows of G', B', R' in turn, one run index per slice (ffv1enc.c:423)
+    for (int y = 0; y < g.ph[0]; y++)
+      for (int p = 0; p < 3; p++) code_row(g.pw[0], p != 0);
+  } else {
+    for (int p = 0; p < 3; p++) {
+      run_index = 0;  // per plane (ffv1enc.c:379)
+      for (int y = 0; y < g.ph[p]; y++) code_row(g.pw[p], p != 0);
     }
   }
   b.flush();
@@ -1884,6 +1921,8 @@ int launch_symbols(const SymbolArgs& a, void* stream) {
   dim3 grid(a.nslices, a.nslots, a.nplanes * kSymSplit), block(kSymThreads);
   if (a.sample_bytes == 1)
     hipLaunchKernelGGL(ffv1_symbols<1>, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
+  else if (a.sample_bytes == 4)
+    hipLaunchKernelGGL(ffv1_symbols<4>, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
   else
     hipLaunchKernelGGL(ffv1_symbols<2>, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;

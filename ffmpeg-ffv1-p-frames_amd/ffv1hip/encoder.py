@@ -34,7 +34,8 @@ class Params(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in (
         "width", "height", "chroma_planes", "chroma_h_shift", "chroma_v_shift",
         "bits_per_raw_sample", "packed_at_lsb", "sample_bytes", "version", "ac", "ec",
-        "context_model", "num_h_slices", "num_v_slices", "gop_size", "sar_num", "sar_den")]
+        "context_model", "num_h_slices", "num_v_slices", "gop_size", "sar_num", "sar_den",
+        "colorspace")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -44,6 +45,8 @@ class Params(ctypes.Structure):
         return self.num_h_slices * self.num_v_slices
 
     def plane_shapes(self):
+        if self.sample_bytes == 4:  # bgr0: one packed B, G, R, X plane
+            return [(self.height, 4 * self.width)]
         cw = -((-self.width) >> self.chroma_h_shift)
         ch = -((-self.height) >> self.chroma_v_shift)
         shapes = [(self.height, self.width)]
@@ -208,7 +211,7 @@ class HipEncoder:
         """Encode host frames (each a list of 2-D uint8/uint16 planes) in order."""
         L = load_library()
         n = len(frames)
-        np_planes = 3 if self.params.chroma_planes else 1
+        np_planes = len(self.params.plane_shapes())
         ptrs = (ctypes.c_void_p * (3 * n))()
         strides = (ctypes.c_int * (3 * n))()
         keep = []
@@ -409,7 +412,7 @@ class FFV1Encoder:
         strides = (ctypes.c_int * 3)()
         keep = []
         if frame is not None:
-            np_planes = 3 if self.params.chroma_planes else 1
+            np_planes = len(self.params.plane_shapes())
             for k in range(3):
                 a = np.ascontiguousarray(frame[min(k, np_planes - 1)])
                 keep.append(a)
@@ -471,7 +474,7 @@ class HipDecoder:
             return []
         buf = np.frombuffer(b"".join(packets), np.uint8).copy()
         sizes = (ctypes.c_int64 * n)(*[len(pk) for pk in packets])
-        dt = np.uint8 if self.params.sample_bytes == 1 else np.uint16
+        dt = np.uint8 if self.params.sample_bytes in (1, 4) else np.uint16
         shapes = self.params.plane_shapes()
         frames = [[np.zeros(shp, dt) for shp in shapes] for _ in range(n)]
         ptrs = (ctypes.c_void_p * (3 * n))()

@@ -23,14 +23,15 @@
 extern "C" {
 #endif
 
-#define FFV1HIP_ABI_VERSION 1
+#define FFV1HIP_ABI_VERSION 2
 #define FFV1HIP_AVERROR_INVALIDDATA (-1094995529)
 
 /* AVCodecContext fields + codec private options that encode_init reads
  * (ffv1enc.c:669-1029, options ffv1enc.c:1383-1399, defaults :1408-1413). */
 typedef struct ffv1hip_options {
     int width, height;
-    const char *pix_fmt;      /* "yuv420p", "yuv420p10", "yuv444p16", ...   */
+    const char *pix_fmt;      /* "yuv420p", "yuv420p10", "yuv444p16", ...,
+                                 "bgr0" / "gbrp9".."gbrp14" (RGB)          */
     int slices;               /* avctx->slices (0 = auto)                   */
     int level;                /* avctx->level (-1 = unset)                  */
     int coder;                /* -1 default, 0 rice, 1/2 range_tab, -2 range_def */
@@ -49,8 +50,9 @@ typedef struct ffv1hip_params {
     int chroma_planes;        /* 1 YUV, 0 gray                              */
     int chroma_h_shift, chroma_v_shift;
     int bits_per_raw_sample;
-    int packed_at_lsb;        /* u16 samples LSB-aligned (yuv*p9/p10)       */
-    int sample_bytes;         /* 1 or 2 bytes per stored sample             */
+    int packed_at_lsb;        /* u16 samples LSB-aligned (yuv*p9/p10, gbrp) */
+    int sample_bytes;         /* 1 or 2 bytes per stored sample; 4: bgr0,
+                                 one packed B,G,R,X plane                   */
     int version;              /* 0, 1 or 3                                  */
     int ac;                   /* 0 Golomb-Rice, 1 range default, 2 range custom */
     int ec;                   /* slice CRC-32 trailers                      */
@@ -58,6 +60,9 @@ typedef struct ffv1hip_params {
     int num_h_slices, num_v_slices;
     int gop_size;
     int sar_num, sar_den;
+    int colorspace;           /* 0 YCbCr; 1 RGB through the reversible colour
+                                 transform (ffv1enc.c:413-473): bgr0 or
+                                 gbrp planes in AVFrame data[] order        */
 } ffv1hip_params;
 
 typedef struct ffv1hip_ctx ffv1hip_ctx;

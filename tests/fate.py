@@ -21,7 +21,6 @@ from helpers import GOLDEN_DIR, load_golden
 from ffv1hip import synth
 
 PINS = load_golden("fate_vsynth.json")["pins"]
-YUV_PINS = [p for p in PINS if p["pix_fmt"] != "bgr0"]
 
 
 def raw_clip(pin):

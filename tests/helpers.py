@@ -124,3 +124,17 @@ PARITY_STREAMS = [
            source="random"),
     Stream("golomb_vsynth3", 34, 34, "yuv420p", 13, slices=4, coder=0, gop_size=12),
 ]
+
+# RGB through the reversible colour transform (chained coders on the GPU):
+# bgr0 with both coders and context models, gbrp at 9..14 bits (range coder
+# forced), odd geometry and a 3x3 grid.
+RGB_STREAMS = [
+    Stream("bgr0_v3", 176, 144, "bgr0", 4, slices=4, level=3, gop_size=3, source="random"),
+    Stream("bgr0_golomb_v1", 96, 64, "bgr0", 3, level=1, coder=0, gop_size=2, source="random"),
+    Stream("bgr0_range_ctx1", 120, 90, "bgr0", 4, slices=9, coder=1, context=1, gop_size=2,
+           source="random"),
+    Stream("gbrp9_odd", 75, 49, "gbrp9", 3, slices=4, gop_size=2, source="random"),
+    Stream("gbrp10_v3", 128, 96, "gbrp10", 3, slices=4, level=3, gop_size=2, source="random"),
+    Stream("gbrp12_v1", 64, 48, "gbrp12", 3, level=1, gop_size=3, source="random"),
+    Stream("gbrp14_ctx1", 64, 48, "gbrp14", 3, slices=4, context=1, gop_size=3, source="random"),
+]

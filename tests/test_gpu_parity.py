@@ -11,7 +11,7 @@ import hashlib
 import numpy as np
 import pytest
 
-from helpers import PARITY_STREAMS, Stream, load_golden, md5, oracle_encode
+from helpers import PARITY_STREAMS, RGB_STREAMS, Stream, load_golden, md5, oracle_encode
 from oracle import oracle
 
 pytestmark = pytest.mark.gpu
@@ -50,6 +50,17 @@ def test_hip_matches_oracle(stream):
             n = min(len(g), len(r))
             first = next((k for k in range(n) if g[k] != r[k]), n)
             pytest.fail(f"frame {i}: {len(g)} vs {len(r)} bytes, first diff at {first}")
+
+
+@pytest.mark.parametrize("stream", RGB_STREAMS, ids=[s.name for s in RGB_STREAMS])
+def test_hip_rgb_matches_oracle(stream):
+    """bgr0 / gbrp: the colour transform and the row-interleaved planes of
+    encode_rgb_frame (ffv1enc.c:413-473), bit-exact with the oracle."""
+    frames = list(stream.frames())
+    _, ex_ref, ref = oracle_encode(stream, frames)
+    ex, got = hip_encode(stream, frames, batch=2)
+    assert ex == ex_ref
+    assert got == ref
 
 
 @pytest.mark.parametrize("stream", [s for s in PARITY_STREAMS if s.coder != 0][:6],

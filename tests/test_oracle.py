@@ -10,7 +10,7 @@ import hashlib
 import numpy as np
 import pytest
 
-from helpers import PARITY_STREAMS, Stream, load_golden, md5, oracle_encode
+from helpers import PARITY_STREAMS, RGB_STREAMS, Stream, load_golden, md5, oracle_encode
 from oracle import oracle
 
 PINS = {p["name"]: p for p in load_golden("known_answers.json")["streams"]}
@@ -121,14 +121,6 @@ def test_pframes_smaller_than_keyframes_and_state_carry_matters():
     for i in range(1, 4):
         assert not pk[i][1] and pi[i][1]
         assert len(pk[i][0]) < len(pi[i][0])
-
-
-RGB_STREAMS = [
-    Stream("bgr0_v3", 176, 144, "bgr0", 4, slices=4, level=3, gop_size=3, source="random"),
-    Stream("bgr0_golomb_v1", 96, 64, "bgr0", 3, level=1, coder=0, gop_size=2, source="random"),
-    Stream("gbrp10_v3", 128, 96, "gbrp10", 3, slices=4, level=3, gop_size=2, source="random"),
-    Stream("gbrp14_ctx1", 64, 48, "gbrp14", 3, slices=4, context=1, gop_size=3, source="random"),
-]
 
 
 @pytest.mark.parametrize("stream", RGB_STREAMS, ids=[s.name for s in RGB_STREAMS])
