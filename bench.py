@@ -160,7 +160,13 @@ def load_traffic(frames_per_step, kernel):
     """HBM bytes per launch of `kernel` from the committed PMC profile of the
     same configuration and batch (profiles/pmc_traffic*.json), else None."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json"))):
+    import re
+
+    def newest_first(path):  # pmc_traffic_rNN*.json: the latest round's profile wins
+        m = re.search(r"_r(\d+)", os.path.basename(path))
+        return (-int(m.group(1)) if m else 0, path)
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json")), key=newest_first):
         try:
             d = json.load(open(path))
         except Exception:

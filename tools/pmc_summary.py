@@ -2,7 +2,7 @@
 """Summarise a tools/profile_round.sh run into profiles/.
 
 Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats
-summary, copied) and profiles/pmc_traffic.json: per-kernel HBM bytes per
+summary, copied) and profiles/pmc_traffic_rNN.json: per-kernel HBM bytes per
 launch from the FETCH_SIZE / WRITE_SIZE passes.  FETCH_SIZE and WRITE_SIZE
 are reported by rocprofv3 in KiB; per MI355X_MICROARCH.md (HBM section)
 gfx950 FETCH_SIZE counts half the bytes of wide coalesced reads, so it is
@@ -30,7 +30,7 @@ def per_kernel(path, counter):
     return {k: statistics.mean(v) for k, v in vals.items()}
 
 
-def main(tag, frames_per_launch, config, out_name="pmc_traffic.json"):
+def main(tag, frames_per_launch, config, out_name="pmc_traffic_rNN.json"):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
@@ -61,4 +61,4 @@ def main(tag, frames_per_launch, config, out_name="pmc_traffic.json"):
 if __name__ == "__main__":
     main(sys.argv[1] if len(sys.argv) > 1 else "r01", int(sys.argv[2]) if len(sys.argv) > 2 else 252,
          sys.argv[3] if len(sys.argv) > 3 else "3840x2160 yuv420p10",
-         sys.argv[4] if len(sys.argv) > 4 else "pmc_traffic.json")
+         sys.argv[4] if len(sys.argv) > 4 else "pmc_traffic_rNN.json")
