@@ -1,11 +1,12 @@
-"""Bit-exact AVI writer for the FATE vsynth pins (TEST INFRASTRUCTURE ONLY).
+"""AVI container for FFV1 streams: the bit-exact muxer the reference's
+FATE tests write, and a reader for what it writes.
 
 The reference's FATE tests (tests/fate/vcodec.mak:113-127, enc_dec in
 tests/fate-run.sh:171-193) encode a raw clip to ``<test>.avi`` with
 ``-flags +bitexact -fflags +bitexact`` and record the MD5 and size of that
-file (tests/ref/vsynth/vsynth*-ffv1*).  To compare our packets against those
-pins, this module writes the same single-video-stream AVI the reference
-muxer writes for a seekable output.  It restates:
+file (tests/ref/vsynth/vsynth*-ffv1*).  ``write_avi`` writes the same
+single-video-stream AVI the reference muxer writes for a seekable output,
+so a stream from this encoder lands in the same file bytes.  It restates:
 
 * libavformat/avienc.c:237-525  avi_write_header (avih, strl/strh/strf,
   the OpenDML master-index JUNK placeholder :210-235, the odml JUNK list
@@ -23,12 +24,16 @@ time base 1/25 (rawvideo demuxer default rate), ``bit_rate`` 200000
 ``bits_per_coded_sample`` 0 (so the BMP depth is 24), codec tag 'FFV1'
 (libavformat/riff.c:316), SAR 0/1 (no vprp), no INFO list under bitexact
 (libavformat/mux.c:411-415).
+
+``read_avi`` is the matching demuxer subset (avidec.c: strf extradata,
+``00dc`` chunks in movi order, key flags from idx1).
 """
 from __future__ import annotations
 
 import io
+import math
 import struct
-from typing import Iterable, Tuple
+from typing import Iterable, List, Tuple
 
 AVIF_HASINDEX = 0x10
 AVIF_ISINTERLEAVED = 0x100
@@ -109,7 +114,6 @@ def write_avi(width: int, height: int, extradata: bytes,
     r.wl16(0)          # priority
     r.wl16(0)          # language
     r.wl32(0)          # initial frame
-    import math
     g = math.gcd(tb[0], tb[1])
     r.wl32(tb[0] // g)  # scale
     r.wl32(tb[1] // g)  # rate
@@ -190,3 +194,40 @@ def write_avi(width: int, height: int, extradata: bytes,
     r.end_tag(riff_start)
     r.patch32(frames_hdr_strm + 4, max_size)
     return r.b.getvalue()
+
+
+def read_avi(data: bytes):
+    """The first video stream of an AVI: ``(width, height, fourcc, extradata,
+    [(packet, key), ...])``.  Keyframe flags come from idx1 when present."""
+    if data[:4] != b"RIFF" or data[8:12] != b"AVI ":
+        raise ValueError("not an AVI file")
+    width = height = 0
+    fourcc, extradata = b"", b""
+    packets: List[bytes] = []
+    flags: List[int] = []
+
+    def walk(pos, end):
+        nonlocal width, height, fourcc, extradata
+        while pos + 8 <= end:
+            tag = data[pos:pos + 4]
+            size = struct.unpack_from("<I", data, pos + 4)[0]
+            body = pos + 8
+            if tag == b"LIST":
+                walk(body + 4, min(end, body + size))
+            elif tag == b"strf" and not fourcc:
+                hdr = struct.unpack_from("<IiiHH4s", data, body)
+                width, height, fourcc = hdr[1], abs(hdr[2]), hdr[5]
+                extradata = data[body + 40:body + hdr[0]]
+            elif tag[2:] in (b"dc", b"db") and tag[:2] == b"00":
+                packets.append(data[body:body + size])
+            elif tag == b"idx1":
+                for k in range(size // 16):
+                    ck, fl = struct.unpack_from("<4sI", data, body + 16 * k)
+                    if ck[:2] == b"00" and ck[2:] in (b"dc", b"db"):
+                        flags.append(fl)
+            pos = body + size + (size & 1)
+
+    walk(12, len(data))
+    keys = [bool(f & AVIIF_KEYFRAME) for f in flags] if len(flags) == len(packets) else \
+        [True] * len(packets)
+    return width, height, fourcc, extradata, list(zip(packets, keys))

@@ -380,7 +380,8 @@ class FFV1Encoder:
     capabilities = ("SLICE_THREADS", "DELAY")
     pix_fmts = ("yuv420p", "yuv422p", "yuv444p", "yuv440p", "yuv411p", "yuv410p", "gray",
                 "yuv420p9", "yuv422p9", "yuv444p9", "yuv420p10", "yuv422p10", "yuv444p10",
-                "yuv420p16", "yuv422p16", "yuv444p16", "gray16")
+                "yuv420p16", "yuv422p16", "yuv444p16", "gray16", "bgr0", "0rgb32", "gbrp9",
+                "gbrp10", "gbrp12", "gbrp14")
 
     def __init__(self, batch: int = 12, device: int = 0):
         if batch < 1:

@@ -16,9 +16,9 @@ import os
 
 import numpy as np
 
-from avi_mux import write_avi
 from helpers import GOLDEN_DIR, load_golden
 from ffv1hip import synth
+from ffv1hip.avi import write_avi
 
 PINS = load_golden("fate_vsynth.json")["pins"]
 
