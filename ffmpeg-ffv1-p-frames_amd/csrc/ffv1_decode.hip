@@ -1,20 +1,35 @@
-// ffv1_decode.hip -- FFV1 range-coded slice decoder on gfx950 (the
-// on-device lossless self-check of SURVEY §8f, row 1).
+// ffv1_decode.hip -- FFV1 slice decoder on gfx950: the
+// streams this library encodes, range coder or Golomb-Rice, context model 0
+// or 1, YCbCr or RGB, versions 0, 1 and 3, with the reference's damaged-slice
+// concealment.
 //
-// Reference: ffv1dec.c decode_slice (:248-280 + :361-474), decode_line
-// (:42-117, the range-coder branch), get_symbol_inline (:44-66);
-// rangecoder.h get_rac / refill (:104-147).  Decoding is a serial chain per
-// (GOP segment, slice): each decision's context state and each sample's
-// neighbourhood depend on the decisions before it.  One workgroup of one
-// wave per chain keeps the chain's adaptive states (2 x 666 x 32 bytes),
-// the transition table, the quant tables and two sample rows in LDS; lane 0
-// runs the chain, the other lanes do the bulk state resets and copies.
+// Reference: ffv1dec.c decode_frame (:896-1030), decode_slice (:361-474),
+// decode_slice_header (:282-359), read_header for v0/v1 (:639-700),
+// decode_line (:42-117 range and Golomb branches), decode_plane (:200-224),
+// decode_rgb_frame (:226-280), get_symbol_inline (:44-66), get_vlc_symbol
+// (:68-95); rangecoder.h get_rac / refill (:104-147); golomb.h get_ur_golomb
+// / get_sr_golomb.  Decoding is a serial chain per (GOP segment, slice):
+// each decision's context state and each sample's neighbourhood depend on
+// the decisions before it.  One workgroup of one wave per chain keeps the
+// chain's adaptive states (in LDS when they fit, else in a per-chain global
+// table), the transition tables, the quant tables and two rows per plane in
+// LDS; lane 0 runs the chain, the wave stores each decoded row (coalesced)
+// and does the bulk state resets and copies.  A second kernel
+// (ffv1_conceal) replaces damaged slices by the previous picture's
+// rectangle, frame by frame, as decode_frame does after its slices.
 #include "ffv1_internal.h"
 
 namespace ffv1hip {
 namespace {
 
 constexpr int kDecThreads = 64;
+constexpr int kInvalidData = -1094995529;  // AVERROR_INVALIDDATA, which get_symbol_inline returns as a value
+constexpr uint64_t kVlcInit = (uint64_t)4 << 16 | (uint64_t)1 << 40;  // drift 0, error_sum 4, bias 0, count 1
+constexpr uint8_t kDamageHeader = 2, kDamageEnd = 4;  // bit 0: the host's CRC check
+
+__constant__ uint8_t kLog2Run[41] = {  // ff_log2_run (bitstream.c:40-46)
+    0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 5, 5, 6,
+    6, 7, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24};
 
 struct RacDec {
   uint32_t low, range;
@@ -68,151 +83,429 @@ __device__ inline int rac_get(RacDec& c, uint8_t* st, const uint16_t* tt, const 
   return bit;
 }
 
-// get_symbol_inline (ffv1dec.c:44-66)
+// get_symbol_inline (ffv1dec.c:44-66); an exponent past 31 returns
+// AVERROR_INVALIDDATA, which decode_line then uses as the residual
 __device__ inline int rac_symbol(RacDec& c, uint8_t* st, int is_signed, const uint16_t* tt,
                                  const uint64_t* w) {
   if (rac_get(c, st, tt, w)) return 0;
   int e = 0;
   while (rac_get(c, st + 1 + (e < 9 ? e : 9), tt, w)) {
-    if (++e > 31) return 0;
+    if (++e > 31) return kInvalidData;
   }
-  int a = 1;
-  for (int i = e - 1; i >= 0; i--) a = 2 * a + rac_get(c, st + 22 + (i < 9 ? i : 9), tt, w);
-  if (is_signed && rac_get(c, st + 11 + (e < 10 ? e : 10), tt, w)) return -a;
-  return a;
+  uint32_t a = 1;
+  for (int i = e - 1; i >= 0; i--) a = 2 * a + uint32_t(rac_get(c, st + 22 + (i < 9 ? i : 9), tt, w));
+  if (is_signed && rac_get(c, st + 11 + (e < 10 ? e : 10), tt, w)) return int(0u - a);
+  return int(a);
+}
+
+// GetBitContext over a slice's Golomb bits: MSB first, zeros past the end
+// (the safe bitstream reader).
+struct BitRd {
+  const uint8_t* pk;
+  int64_t pos, end;  // next byte to load, end of the slice
+  uint64_t cache;    // valid bits MSB-aligned
+  int nc;
+};
+
+__device__ inline void br_fill(BitRd& b) {
+  while (b.nc <= 56) {
+    const uint64_t v = b.pos < b.end ? b.pk[b.pos] : 0u;
+    b.pos++;
+    b.cache |= v << (56 - b.nc);
+    b.nc += 8;
+  }
+}
+
+__device__ inline uint32_t br_bits(BitRd& b, int n) {
+  if (n == 0) return 0;
+  br_fill(b);
+  const uint32_t v = uint32_t(b.cache >> (64 - n));
+  b.cache <<= n;
+  b.nc -= n;
+  return v;
+}
+
+__device__ inline int fold_bits(int d, int bits) {
+  const int sh = 32 - bits;
+  return (d << sh) >> sh;
+}
+
+// get_vlc_symbol (ffv1dec.c:68-95): get_sr_golomb(k, limit 12, esc bits)
+// and update_vlc_state (ffv1.h:192-224) on the packed VlcState record
+// drift (int16) | error_sum (u16) << 16 | bias (int8) << 32 | count << 40.
+__device__ inline int vlc_get(BitRd& b, uint64_t& rec, int bits) {
+  int drift = int16_t(rec & 0xFFFF);
+  int error_sum = int((rec >> 16) & 0xFFFF);
+  int bias = int8_t((rec >> 32) & 0xFF);
+  int count = int((rec >> 40) & 0xFF);
+  int k = 0;
+  for (int i = count; i < error_sum; i += i) k++;
+  br_fill(b);
+  const int q = b.cache ? __clzll(b.cache) : 64;
+  uint32_t u;
+  if (q < 12) {
+    b.cache <<= q + 1;
+    b.nc -= q + 1;
+    u = (uint32_t(q) << k) | br_bits(b, k);
+  } else {
+    b.cache <<= 12;
+    b.nc -= 12;
+    u = br_bits(b, bits) + 11;
+  }
+  int v = (u & 1) ? -int((u + 1) >> 1) : int(u >> 1);
+  v ^= (2 * drift + count) >> 31;
+  const int ret = fold_bits(v + bias, bits);
+  error_sum = (error_sum + (v < 0 ? -v : v)) & 0xFFFF;
+  drift += v;
+  if (count == 128) {
+    count >>= 1;
+    drift >>= 1;
+    error_sum >>= 1;
+  }
+  count++;
+  if (drift <= -count) {
+    if (bias > -128) bias--;
+    drift += count;
+    if (drift <= -count) drift = -count + 1;
+  } else if (drift > 0) {
+    if (bias < 127) bias++;
+    drift -= count;
+    if (drift > 0) drift = 0;
+  }
+  rec = (uint64_t)(uint16_t)drift | (uint64_t)(uint16_t)error_sum << 16 | (uint64_t)(uint8_t)bias << 32 |
+        (uint64_t)(uint8_t)count << 40;
+  return ret;
 }
 
 __device__ inline int median3(int a, int b, int c) {
   return max(min(a, b), min(max(a, b), c));
 }
 
+// decode_line (ffv1dec.c:42-117) for one row into `cur`, which holds row y-2
+// until each sample is written; `up` is row y-1.  The neighbourhood is the
+// reference's zeroed ring: L(0) = T(0), LT(0) = row y-2 at 0, RT past the
+// edge = T, LL(0) = 0, LL(1) = T(0), TT = row y-2.
+template <bool GOLOMB>
+__device__ inline void decode_row(RacDec& c, BitRd& b, uint8_t* st8, uint64_t* st64, const uint16_t* tt,
+                                  const uint64_t* pkw, const int16_t* qt, bool model1, int16_t* cur,
+                                  const int16_t* up, int w, int bits, int& run_index) {
+  const int mask = int((1u << bits) - 1u);
+  int T = up[0];
+  const int T0 = T;
+  int L = T;
+  int LT = cur[0];
+  int run_count = 0, run_mode = 0;
+  for (int x = 0; x < w; x++) {
+    const int RT = x + 1 < w ? up[x + 1] : T;
+    int ctx = qt[(L - LT) & 0xFF] + qt[256 + ((LT - T) & 0xFF)] + qt[512 + ((T - RT) & 0xFF)];
+    if (model1) {
+      const int LL = x >= 2 ? cur[x - 2] : (x == 1 ? T0 : 0);
+      const int TT = cur[x];
+      ctx += qt[768 + ((LL - L) & 0xFF)] + qt[1024 + ((TT - T) & 0xFF)];
+    }
+    const int actx = ctx < 0 ? -ctx : ctx;
+    int diff;
+    if constexpr (!GOLOMB) {
+      // one call site: the symbol decoder is the kernel's hot code
+      diff = rac_symbol(c, st8 + actx * 32, 1, tt, pkw);
+    } else {
+      if (actx == 0 && run_mode == 0) run_mode = 1;
+      if (run_mode) {
+        if (run_count == 0 && run_mode == 1) {
+          if (br_bits(b, 1)) {
+            run_count = 1 << kLog2Run[run_index];
+            if (x + run_count <= w) run_index++;
+          } else {
+            run_count = kLog2Run[run_index] ? int(br_bits(b, kLog2Run[run_index])) : 0;
+            if (run_index) run_index--;
+            run_mode = 2;
+          }
+        }
+        run_count--;
+        if (run_count < 0) {
+          run_mode = 0;
+          run_count = 0;
+          diff = vlc_get(b, st64[actx], bits);
+          if (diff >= 0) diff++;
+        } else {
+          diff = 0;
+        }
+      } else {
+        diff = vlc_get(b, st64[actx], bits);
+      }
+    }
+    if (ctx < 0) diff = -diff;
+    const int pred = median3(L, L + T - LT, T);
+    const int16_t v = int16_t((pred + diff) & mask);
+    cur[x] = v;
+    LT = T;
+    T = RT;
+    L = v;
+  }
+}
+
+// read_quant_table (ffv1dec.c:475-497): consumes one table's run lengths
+__device__ inline bool skip_quant_table(RacDec& c, uint8_t* st, const uint16_t* tt, const uint64_t* w) {
+  for (int i = 0; i < 32; i++) st[i] = 128;
+  int i = 0;
+  while (i < 128) {
+    const unsigned len = unsigned(rac_symbol(c, st, 0, tt, w)) + 1u;
+    if (len > unsigned(128 - i) || !len) return false;
+    i += int(len);
+  }
+  return true;
+}
+
+template <bool GOLOMB, bool GSTATES>
 __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) {
   extern __shared__ __align__(16) uint8_t lds[];
   const int s = blockIdx.x, seg = blockIdx.y, lane = threadIdx.x;
   const Segment sg = a.segs[seg];
   const SliceGeom* g = a.geom + s;  // read through the pointer: a by-value copy indexed by plane spills
-  uint8_t* states = lds;                                         // [2][contexts][32]
-  uint16_t* tt = reinterpret_cast<uint16_t*>(lds + a.state_bytes);  // [256] to0 | to1 << 8
-  uint8_t* hdr = lds + a.state_bytes + 512;                      // [32] slice-header states
-  int16_t* qt = reinterpret_cast<int16_t*>(hdr + 32);            // [3][256]
-  int16_t* ring = qt + 3 * 256;                                  // [2][row_cap]
+  const int64_t sb = GSTATES ? 0 : (a.state_bytes + 15) & ~int64_t(15);
+  uint8_t* const states = GSTATES ? a.tables + (int64_t(seg) * a.nslices + s) * a.state_bytes : lds;
+  uint16_t* const tt = reinterpret_cast<uint16_t*>(lds + sb);  // [256] frame table to0 | to1 << 8
+  uint16_t* const dtt = tt + 256;                              // [256] default table
+  uint8_t* const hdr = reinterpret_cast<uint8_t*>(dtt + 256);  // [32] header states, [32] scratch
+  int16_t* const qt = reinterpret_cast<int16_t*>(hdr + 64);    // [5][256]
+  int16_t* const ring = qt + 5 * 256;                          // [rgb ? 3 : 1][2][row_cap]
   __shared__ int bad;
   const uint64_t* pkw = reinterpret_cast<const uint64_t*>(a.pkts);
-  for (int i = lane; i < 256; i += kDecThreads) tt[i] = uint16_t(a.ftab[i] | (a.ftab[256 + i] << 8));
-  for (int i = lane; i < 3 * 256; i += kDecThreads) qt[i] = a.qt[i];
-  if (lane == 0) bad = 0;
-  const int mask = (1 << a.coded_bits) - 1;
-  const int planes = a.nplanes;
+  for (int i = lane; i < 256; i += kDecThreads) {
+    tt[i] = uint16_t(a.ftab[i] | (a.ftab[256 + i] << 8));
+    dtt[i] = uint16_t(a.dtab[i] | (a.dtab[256 + i] << 8));
+  }
+  for (int i = lane; i < 5 * 256; i += kDecThreads) qt[i] = a.qt[i];
+  const int bits = a.coded_bits;
+  const bool model1 = a.context_model != 0;
+  const int64_t words = a.state_bytes / 4;
+  uint32_t* const st4 = reinterpret_cast<uint32_t*>(states);
+  // the chain continues the states the previous call left (the decoder
+  // starts them reset)
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.persist_in + int64_t(s) * a.state_bytes);
+    for (int64_t i = lane; i < words; i += kDecThreads) st4[i] = src[i];
+  }
   RacDec c{};
+  BitRd br{};
   for (int j = 0; j < sg.nframes; j++) {
     const int f = sg.first_frame + j;
     const int key = a.keyflags[f];
-    uint32_t* st4 = reinterpret_cast<uint32_t*>(states);
-    const int64_t words = a.state_bytes / 4;
-    if (key) {  // ff_ffv1_clear_slice_state on keyframes (ffv1dec.c:261-263)
-      for (int64_t i = lane; i < words; i += kDecThreads) st4[i] = 0x80808080u;
-    } else if (j == 0) {  // continue the previous call's chain
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(a.persist_in + int64_t(s) * a.state_bytes);
-      for (int64_t i = lane; i < words; i += kDecThreads) st4[i] = src[i];
-    }
+    const int64_t fs = int64_t(f) * a.nslices + s;
     __syncthreads();
     if (lane == 0) {
-      const int64_t fs = int64_t(f) * a.nslices + s;
       rac_init(c, a.pkts, a.slice_start[fs], a.slice_end[fs]);
-      int ok = 1;
-      if (s == 0) {  // the key bit, state 128 (ffv1dec.c:931-933)
+      int ok = 1, hok = 1;
+      if (s == 0) {  // the key bit, state 128 (ffv1dec.c:927-933)
         hdr[0] = 128;
-        ok &= rac_get(c, hdr, tt, pkw) == key;
+        ok &= rac_get(c, hdr, dtt, pkw) == key;
+        if (key && a.version < 2) {  // read_header, in band (ffv1dec.c:646-700)
+          for (int i = 0; i < 32; i++) hdr[i] = 128;
+          ok &= rac_symbol(c, hdr, 0, dtt, pkw) == a.version;
+          ok &= rac_symbol(c, hdr, 0, dtt, pkw) == a.ac;
+          if (a.ac == 2)
+            for (int i = 1; i < 256; i++) (void)rac_symbol(c, hdr, 1, dtt, pkw);  // the table this decoder was built with
+          ok &= rac_symbol(c, hdr, 0, dtt, pkw) == a.rgb;
+          if (a.version > 0) ok &= rac_symbol(c, hdr, 0, dtt, pkw) == a.bits_per_raw_sample;
+          ok &= rac_get(c, hdr, dtt, pkw) == a.chroma_planes;
+          ok &= rac_symbol(c, hdr, 0, dtt, pkw) == a.chroma_h_shift;
+          ok &= rac_symbol(c, hdr, 0, dtt, pkw) == a.chroma_v_shift;
+          ok &= rac_get(c, hdr, dtt, pkw) == 0;  // transparency
+          for (int t = 0; t < 5 && ok; t++) ok &= skip_quant_table(c, hdr + 32, dtt, pkw);
+        }
       }
-      // decode_slice_header (ffv1dec.c:169-215), checked against the grid
-      for (int i = 0; i < 32; i++) hdr[i] = 128;
-      const int sx = rac_symbol(c, hdr, 0, tt, pkw);
-      const int sy = rac_symbol(c, hdr, 0, tt, pkw);
-      const int sw = rac_symbol(c, hdr, 0, tt, pkw);
-      const int sh = rac_symbol(c, hdr, 0, tt, pkw);
-      const int x0 = int(int64_t(sx) * a.width / a.num_h), y0 = int(int64_t(sy) * a.height / a.num_v);
-      const int x1 = int(int64_t(sx + sw + 1) * a.width / a.num_h);
-      const int y1 = int(int64_t(sy + sh + 1) * a.height / a.num_v);
-      ok &= x0 == g->px[0] && y0 == g->py[0] && x1 - x0 == g->pw[0] && y1 - y0 == g->ph[0];
-      for (int i = 0; i < 2; i++) ok &= rac_symbol(c, hdr, 0, tt, pkw) == a.context_model;
-      (void)rac_symbol(c, hdr, 0, tt, pkw);  // picture structure
-      (void)rac_symbol(c, hdr, 0, tt, pkw);  // sample aspect ratio
-      (void)rac_symbol(c, hdr, 0, tt, pkw);
-      if (!ok) {
-        bad = 1;
-        atomicAdd(&a.status[0], 1);
+      if (a.version > 2) {
+        // decode_slice_header (ffv1dec.c:282-359); a slice naming another
+        // rectangle or quant set than the grid's counts as damaged
+        for (int i = 0; i < 32; i++) hdr[i] = 128;
+        const int sx = rac_symbol(c, hdr, 0, tt, pkw);
+        const int sy = rac_symbol(c, hdr, 0, tt, pkw);
+        const int sw = rac_symbol(c, hdr, 0, tt, pkw);
+        const int sh = rac_symbol(c, hdr, 0, tt, pkw);
+        const int x0 = int(int64_t(sx) * a.width / a.num_h), y0 = int(int64_t(sy) * a.height / a.num_v);
+        const int x1 = int(int64_t(sx + sw + 1) * a.width / a.num_h);
+        const int y1 = int(int64_t(sy + sh + 1) * a.height / a.num_v);
+        hok &= sx >= 0 && sy >= 0 && sw >= 0 && sh >= 0;
+        hok &= x0 == g->px[0] && y0 == g->py[0] && x1 - x0 == g->pw[0] && y1 - y0 == g->ph[0];
+        for (int i = 0; i < 2 && hok; i++) hok &= rac_symbol(c, hdr, 0, tt, pkw) == a.context_model;
+        if (hok) {
+          (void)rac_symbol(c, hdr, 0, tt, pkw);  // picture structure
+          (void)rac_symbol(c, hdr, 0, tt, pkw);  // sample aspect ratio
+          (void)rac_symbol(c, hdr, 0, tt, pkw);
+        }
       }
+      if (!ok) atomicAdd(&a.status[0], 1);
+      bad = !ok ? 2 : !hok ? 1 : 0;
+      if (!hok) a.damage[fs] |= kDamageHeader;
     }
     __syncthreads();
-    if (bad) return;
-    for (int p = 0; p < planes; p++) {
-      for (int i = lane; i < 2 * a.row_cap; i += kDecThreads) ring[i] = 0;
+    if (bad == 2) return;
+    if (bad) continue;  // not decoded: no state update (ffv1dec.c:410-414)
+    if (key) {          // ff_ffv1_clear_slice_state, after the header (ffv1dec.c:418-419)
+      const uint32_t v0 = GOLOMB ? uint32_t(kVlcInit) : 0x80808080u;
+      const uint32_t v1 = GOLOMB ? uint32_t(kVlcInit >> 32) : 0x80808080u;
+      for (int64_t i = lane; i < words; i += kDecThreads) st4[i] = (i & 1) ? v1 : v0;
+    }
+    if (lane == 0 && GOLOMB) {  // ffv1dec.c:426-433
+      if (a.version > 2) {        // micro_version 4: a 0 on state 129, then the Golomb bits
+        hdr[32] = 129;
+        (void)rac_get(c, hdr + 32, tt, pkw);
+      }
+      const int64_t start = a.slice_start[fs];
+      const int64_t acb = (a.version > 2 || (g->px[0] == 0 && g->py[0] == 0)) ? c.ptr - start - 1 : 0;
+      br.pk = a.pkts;
+      br.pos = start + acb;
+      br.end = a.slice_end[fs];
+      br.cache = 0;
+      br.nc = 0;
+    }
+    int run_index = 0;
+    uint8_t* const obase = a.out + int64_t(f) * a.frame_bytes;
+    if (!a.rgb) {
+      for (int p = 0; p < a.nplanes; p++) {
+        for (int i = lane; i < 2 * a.row_cap; i += kDecThreads) ring[i] = 0;
+        __syncthreads();
+        // decode_plane (ffv1dec.c:200-224): lane 0 decodes a row into LDS;
+        // the wave then stores it (coalesced), so the serial loop issues no
+        // global stores
+        uint8_t* pst = states + (p ? a.state_bytes / 2 : 0);
+        const int w = g->pw[p], h = g->ph[p];
+        const int64_t poff = p == 0 ? a.plane_off[0] : (p == 1 ? a.plane_off[1] : a.plane_off[2]);
+        const int pw = p == 0 ? a.plane_w[0] : (p == 1 ? a.plane_w[1] : a.plane_w[2]);
+        run_index = 0;  // per plane (ffv1dec.c:204)
+        for (int y = 0; y < h; y++) {
+          int16_t* cur = ring + (y & 1) * a.row_cap;  // holds row y-2 until written
+          const int16_t* up = ring + ((y + 1) & 1) * a.row_cap;
+          if (lane == 0)
+            decode_row<GOLOMB>(c, br, pst, reinterpret_cast<uint64_t*>(pst), tt, pkw, qt, model1, cur, up, w, bits,
+                               run_index);
+          __syncthreads();
+          const int64_t orow = int64_t(g->py[p] + y) * pw + g->px[p];
+          if (a.sample_bytes == 1) {
+            for (int x = lane; x < w; x += kDecThreads) obase[poff + orow + x] = uint8_t(cur[x]);
+          } else {
+            uint16_t* o16 = reinterpret_cast<uint16_t*>(obase + poff) + orow;
+            for (int x = lane; x < w; x += kDecThreads) {
+              const uint32_t u = uint16_t(cur[x]);
+              o16[x] = uint16_t(a.packed_at_lsb ? u : (u << a.msb_shift));
+            }
+          }
+          __syncthreads();
+        }
+      }
+    } else {
+      // decode_rgb_frame (ffv1dec.c:226-280): the rows of G', B', R' in
+      // turn, one run index for the slice, then the inverse transform
+      for (int i = lane; i < 6 * a.row_cap; i += kDecThreads) ring[i] = 0;
       __syncthreads();
-      // decode_plane / decode_line (ffv1dec.c:42-117, :248-280): the same
-      // zeroed-ring neighbourhood as the encoder's encode_plane.  Lane 0
-      // decodes a row into LDS; the wave then stores it (coalesced), so the
-      // serial loop issues no global stores.
-      uint8_t* pst = states + (p ? a.state_bytes / 2 : 0);
-      const int w = g->pw[p], h = g->ph[p];
-      const int64_t poff = p == 0 ? a.plane_off[0] : (p == 1 ? a.plane_off[1] : a.plane_off[2]);
-      const int pw = p == 0 ? a.plane_w[0] : (p == 1 ? a.plane_w[1] : a.plane_w[2]);
-      uint8_t* obase = a.out + int64_t(f) * a.frame_bytes + poff;
-      const int16_t* q0 = qt;
-      const int16_t* q1 = qt + 256;
-      const int16_t* q2 = qt + 512;
+      const int w = g->pw[0], h = g->ph[0];
       for (int y = 0; y < h; y++) {
-        int16_t* cur = ring + (y & 1) * a.row_cap;  // holds row y-2 until written
-        const int16_t* up = ring + ((y + 1) & 1) * a.row_cap;
-        if (lane == 0) {
-          int T = up[0];
-          int L = T;
-          int LT = cur[0];  // two rows up, column 0
-          for (int x = 0; x < w; x++) {
-            const int RT = x + 1 < w ? up[x + 1] : T;
-            const int ctx = q0[(L - LT) & 0xFF] + q1[(LT - T) & 0xFF] + q2[(T - RT) & 0xFF];
-            const int pred = median3(L, L + T - LT, T);
-            // one call site: the symbol decoder is the kernel's hot code
-            const int sym = rac_symbol(c, pst + (ctx < 0 ? -ctx : ctx) * 32, 1, tt, pkw);
-            const int diff = ctx < 0 ? -sym : sym;
-            const int16_t v = int16_t((pred + diff) & mask);
-            cur[x] = v;
-            LT = T;
-            T = RT;
-            L = v;
+        if (lane == 0)
+          for (int p = 0; p < 3; p++) {
+            uint8_t* pst = states + (p ? a.state_bytes / 2 : 0);
+            int16_t* cur = ring + (2 * p + (y & 1)) * a.row_cap;
+            const int16_t* up = ring + (2 * p + ((y + 1) & 1)) * a.row_cap;
+            decode_row<GOLOMB>(c, br, pst, reinterpret_cast<uint64_t*>(pst), tt, pkw, qt, model1, cur, up, w, bits,
+                               run_index);
+          }
+        __syncthreads();
+        const int16_t* G = ring + (y & 1) * a.row_cap;
+        const int16_t* B = ring + (2 + (y & 1)) * a.row_cap;
+        const int16_t* R = ring + (4 + (y & 1)) * a.row_cap;
+        const int64_t Y = g->py[0] + y;
+        for (int x = lane; x < w; x += kDecThreads) {
+          int gg = G[x], bb = B[x] - a.rct_offset, rr = R[x] - a.rct_offset;
+          gg -= (bb + rr) >> 2;
+          bb += gg;
+          rr += gg;
+          const int64_t X = g->px[0] + x;
+          if (a.sample_bytes == 4) {  // *(uint32_t *) = b + (g << 8) + (r << 16) + (a << 24), a = 0
+            reinterpret_cast<uint32_t*>(obase + a.plane_off[0] + Y * a.plane_w[0] * 4)[X] =
+                uint32_t(bb) + (uint32_t(gg) << 8) + (uint32_t(rr) << 16);
+          } else {
+            reinterpret_cast<uint16_t*>(obase + a.plane_off[0] + Y * a.plane_w[0] * 2)[X] = uint16_t(bb);
+            reinterpret_cast<uint16_t*>(obase + a.plane_off[1] + Y * a.plane_w[1] * 2)[X] = uint16_t(gg);
+            reinterpret_cast<uint16_t*>(obase + a.plane_off[2] + Y * a.plane_w[2] * 2)[X] = uint16_t(rr);
           }
         }
         __syncthreads();
-        const int64_t orow = int64_t(g->py[p] + y) * pw + g->px[p];
-        if (a.sample_bytes == 1) {
-          for (int x = lane; x < w; x += kDecThreads) obase[orow + x] = uint8_t(cur[x]);
-        } else {
-          uint16_t* o16 = reinterpret_cast<uint16_t*>(obase) + orow;
-          for (int x = lane; x < w; x += kDecThreads) {
-            const uint32_t u = uint16_t(cur[x]);
-            o16[x] = uint16_t(a.packed_at_lsb ? u : (u << a.msb_shift));
-          }
-        }
       }
-      __syncthreads();
+    }
+    if (lane == 0 && !GOLOMB && a.version > 2) {  // ffv1dec.c:461-467: where the slice's bytes end
+      hdr[32] = 129;
+      (void)rac_get(c, hdr + 32, tt, pkw);
+      if (c.end - c.ptr - 2 - 5 * a.ec) a.damage[fs] |= kDamageEnd;
     }
   }
+  __syncthreads();
   if (sg.save_states) {
-    const uint32_t* st4 = reinterpret_cast<const uint32_t*>(states);
     uint32_t* dst = reinterpret_cast<uint32_t*>(a.persist_out + int64_t(s) * a.state_bytes);
-    for (int64_t i = lane; i < a.state_bytes / 4; i += kDecThreads) dst[i] = st4[i];
+    for (int64_t i = lane; i < words; i += kDecThreads) dst[i] = st4[i];
   }
+}
+
+// decode_frame's concealment (ffv1dec.c:998-1021), one block per slice over
+// the batch's frames in order: slice_damaged is set by a CRC, header or end
+// mismatch and cleared only by a keyframe's read_header (:820-825); a
+// damaged slice with a rectangle takes the previous picture's.  The x offset
+// is (slice_x >> shift) << (depth > 8), as the reference computes it, which
+// for packed bgr0 is slice_x bytes.
+__global__ void __launch_bounds__(256) ffv1_conceal(DecodeArgs a) {
+  const int s = blockIdx.x;
+  const SliceGeom* g = a.geom + s;
+  uint8_t sticky = a.sticky[s];
+  const int np = a.rgb && a.sample_bytes == 4 ? 1 : a.nplanes;
+  for (int f = 0; f < a.nframes; f++) {
+    if (a.keyflags[f]) sticky = 0;
+    const uint8_t dmg = a.damage[int64_t(f) * a.nslices + s];
+    sticky |= dmg != 0;
+    const uint8_t* src = f ? a.out + int64_t(f - 1) * a.frame_bytes : a.last;
+    if (!sticky || (dmg & kDamageHeader) || !src) continue;
+    uint8_t* dst = a.out + int64_t(f) * a.frame_bytes;
+    for (int k = 0; k < np; k++) {
+      const int hs = k ? a.chroma_h_shift : 0, vs = k ? a.chroma_v_shift : 0;
+      const int bpp = a.sample_bytes;
+      const int64_t row = int64_t(k == 0 ? a.plane_w[0] : a.plane_w[k]) * bpp;
+      const int64_t xoff = int64_t(g->px[0] >> hs) << (bpp == 2 ? 1 : 0);
+      const int64_t bytes = int64_t(-((-g->pw[0]) >> hs)) * bpp;
+      const int rows = -((-g->ph[0]) >> vs);
+      const int64_t y0 = g->py[0] >> vs;
+      const int64_t poff = k == 0 ? a.plane_off[0] : (k == 1 ? a.plane_off[1] : a.plane_off[2]);
+      for (int64_t i = threadIdx.x; i < int64_t(rows) * bytes; i += blockDim.x) {
+        const int64_t y = i / bytes, x = i - y * bytes;
+        const int64_t o = poff + (y0 + y) * row + xoff + x;
+        dst[o] = src[o];
+      }
+    }
+    __syncthreads();  // the next frame's copy reads this one
+  }
+  if (threadIdx.x == 0) a.sticky[s] = sticky;
 }
 
 }  // namespace
 
-int64_t decode_lds_bytes(int64_t state_bytes, int row_cap) {
-  return state_bytes + 512 + 32 + 3 * 256 * 2 + int64_t(2) * row_cap * 2;
+int64_t decode_lds_bytes(const DecodeArgs& a, bool global_states) {
+  const int64_t sb = global_states ? 0 : (a.state_bytes + 15) & ~int64_t(15);
+  return sb + 1024 + 64 + 5 * 256 * 2 + int64_t(a.rgb ? 6 : 2) * a.row_cap * 2;
 }
 
 int launch_decode(const DecodeArgs& a, int nsegs, void* stream) {
   dim3 grid(a.nslices, nsegs), block(kDecThreads);
-  hipLaunchKernelGGL(ffv1_decode_slices, grid, block, decode_lds_bytes(a.state_bytes, a.row_cap),
-                     reinterpret_cast<hipStream_t>(stream), a);
+  const bool glob = a.tables != nullptr;
+  const int64_t lds = decode_lds_bytes(a, glob);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (a.ac == 0) {
+    if (glob) hipLaunchKernelGGL((ffv1_decode_slices<true, true>), grid, block, lds, st, a);
+    else hipLaunchKernelGGL((ffv1_decode_slices<true, false>), grid, block, lds, st, a);
+  } else {
+    if (glob) hipLaunchKernelGGL((ffv1_decode_slices<false, true>), grid, block, lds, st, a);
+    else hipLaunchKernelGGL((ffv1_decode_slices<false, false>), grid, block, lds, st, a);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_conceal(const DecodeArgs& a, void* stream) {
+  hipLaunchKernelGGL(ffv1_conceal, dim3(a.nslices), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -1386,16 +1386,23 @@ struct ffv1hip_dec {
   int64_t frame_bytes = 0;
   int64_t plane_off[3]{};
   int plane_w[3]{};
+  int out_planes = 0;      // planes handed back per frame (bgr0: one packed plane)
+  int out_rows[3]{};
   int row_cap = 0;
+  bool global_states = false;
   bool have_states = false;
+  bool have_last = false;  // d_last holds the previous picture (concealment)
   std::vector<SliceGeom> geom;
   uint8_t* d_persist[2] = {nullptr, nullptr};  // read [pcur], written [pcur ^ 1]
   int pcur = 0;
   SliceGeom* d_geom = nullptr;
   int16_t* d_qt = nullptr;
-  uint8_t* d_ftab = nullptr;
+  uint8_t* d_tabs = nullptr;  // frame table to0 | to1, default table to0 | to1
   int* d_status = nullptr;
+  uint8_t* d_sticky = nullptr;  // [slice] slice_damaged across calls
+  uint8_t* d_last = nullptr;
   hipStream_t stream = nullptr;
+  int last_damaged = 0;
 };
 
 static void dec_free(ffv1hip_dec* d) {
@@ -1403,9 +1410,27 @@ static void dec_free(ffv1hip_dec* d) {
   (void)hipFree(d->d_persist[1]);
   (void)hipFree(d->d_geom);
   (void)hipFree(d->d_qt);
-  (void)hipFree(d->d_ftab);
+  (void)hipFree(d->d_tabs);
   (void)hipFree(d->d_status);
+  (void)hipFree(d->d_sticky);
+  (void)hipFree(d->d_last);
   if (d->stream) (void)hipStreamDestroy(d->stream);
+}
+
+// The context states a slice starts from (ff_ffv1_clear_slice_state): all
+// 128 for the range coder, VlcState{drift 0, error_sum 4, bias 0, count 1}
+// per context for Golomb-Rice.
+static int dec_reset_states(ffv1hip_dec* d) {
+  for (uint8_t* pb : d->d_persist) {
+    if (d->P.ac) {
+      HIP_TRY(hipMemset(pb, 128, size_t(d->state_bytes) * d->nslices));
+    } else {
+      std::vector<uint64_t> v(size_t(d->state_bytes / 8) * d->nslices, uint64_t(4) << 16 | uint64_t(1) << 40);
+      HIP_TRY(hipMemcpy(pb, v.data(), v.size() * 8, hipMemcpyHostToDevice));
+    }
+  }
+  HIP_TRY(hipMemset(d->d_sticky, 0, size_t(d->nslices)));
+  return 0;
 }
 
 extern "C" {
@@ -1418,12 +1443,14 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
   };
   if (!params) return fail(set_err(-22, "invalid arguments"));
   const ffv1hip_params& p = *params;
-  if (p.version != 3 || p.ac == 0 || p.context_model != 0 || p.num_h_slices * p.num_v_slices > 256 ||
-      p.bits_per_raw_sample < 8 || p.bits_per_raw_sample > 16 || p.width <= 0 || p.height <= 0 ||
-      p.num_h_slices <= 0 || p.num_v_slices <= 0 || p.colorspace != 0)
-    return fail(set_err(-38, "GPU decoder: YCbCr, version 3, range coder, context model 0 only"));
+  if (p.version == 2 || p.version > 3 || p.num_h_slices * p.num_v_slices > 256 || p.bits_per_raw_sample < 8 ||
+      p.bits_per_raw_sample > 16 || p.width <= 0 || p.height <= 0 || p.num_h_slices <= 0 || p.num_v_slices <= 0 ||
+      (p.version < 2 && p.num_h_slices * p.num_v_slices != 1) || p.context_model < 0 || p.context_model > 1 ||
+      p.colorspace < 0 || p.colorspace > 1 || p.ac < 0 || p.ac > 2)
+    return fail(set_err(-38, "GPU decoder: unsupported parameter set"));
   // The stream's extradata must be the one these parameters produce
-  // (read_extradata, ffv1dec.c:509-631, would derive the same parameters).
+  // (read_extradata, ffv1dec.c:509-631, would derive the same parameters);
+  // versions 0 and 1 have none, their header is in band.
   ffv1hip_ctx tmp;
   tmp.P = p;
   tmp.contexts = contexts_of(p.context_model);
@@ -1431,23 +1458,28 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
   tmp.frame = p.ac == 2 ? custom_tables(tmp.dflt) : tmp.dflt;
   quant_set(tmp.qt, p.context_model, p.bits_per_raw_sample);
   build_extradata(&tmp);
-  if (!extradata || extradata_size != int(tmp.extradata.size()) ||
-      std::memcmp(extradata, tmp.extradata.data(), tmp.extradata.size()) != 0)
+  if (extradata_size != int(tmp.extradata.size()) ||
+      (extradata_size && (!extradata || std::memcmp(extradata, tmp.extradata.data(), tmp.extradata.size()) != 0)))
     return fail(set_err(FFV1HIP_AVERROR_INVALIDDATA, "extradata does not match the parameters"));
   ffv1hip_dec* d = new ffv1hip_dec();
   d->P = p;
   d->device = device;
   d->nslices = p.num_h_slices * p.num_v_slices;
   d->contexts = tmp.contexts;
-  d->state_bytes = int64_t(2) * d->contexts * 32;
+  d->state_bytes = int64_t(2) * d->contexts * (p.ac ? 32 : 8);
   const int cw = p.chroma_planes ? -((-p.width) >> p.chroma_h_shift) : 0;
   const int ch = p.chroma_planes ? -((-p.height) >> p.chroma_v_shift) : 0;
-  const int64_t pb0 = int64_t(p.width) * p.height * p.sample_bytes, pb1 = int64_t(cw) * ch * p.sample_bytes;
+  const bool bgr0 = p.sample_bytes == 4;
+  const int64_t pb0 = int64_t(p.width) * p.height * p.sample_bytes;
+  const int64_t pb1 = bgr0 ? 0 : int64_t(cw) * ch * p.sample_bytes;
   d->plane_off[0] = 0;
   d->plane_off[1] = pb0;
   d->plane_off[2] = pb0 + pb1;
   d->plane_w[0] = p.width;
   d->plane_w[1] = d->plane_w[2] = cw;
+  d->out_planes = bgr0 ? 1 : p.chroma_planes ? 3 : 1;
+  d->out_rows[0] = p.height;
+  d->out_rows[1] = d->out_rows[2] = ch;
   d->frame_bytes = (pb0 + 2 * pb1 + 255) & ~int64_t(255);
   d->geom.resize(d->nslices);
   for (int s = 0; s < d->nslices; s++) {  // ffv1.c:117-145, ffv1dec.c:361-474
@@ -1469,7 +1501,14 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
     d->row_cap = std::max(d->row_cap, g.pw[0]);
   }
   d->row_cap = (d->row_cap + 7) & ~7;
-  if (decode_lds_bytes(d->state_bytes, d->row_cap) > 64 * 1024) {
+  // states in LDS when they fit beside the rows, else one global table per chain
+  DecodeArgs la{};
+  la.state_bytes = d->state_bytes;
+  la.rgb = p.colorspace;
+  la.row_cap = d->row_cap;
+  constexpr int64_t kDecLds = 64 * 1024;
+  d->global_states = decode_lds_bytes(la, false) > kDecLds;
+  if (decode_lds_bytes(la, true) > kDecLds) {
     delete d;
     return fail(set_err(-38, "GPU decoder: slice too wide for the LDS row buffer"));
   }
@@ -1479,14 +1518,20 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
     HIP_TRY(hipMalloc(&d->d_persist[0], d->state_bytes * d->nslices));
     HIP_TRY(hipMalloc(&d->d_persist[1], d->state_bytes * d->nslices));
     HIP_TRY(hipMalloc(&d->d_geom, sizeof(SliceGeom) * d->nslices));
-    HIP_TRY(hipMalloc(&d->d_qt, sizeof(int16_t) * 3 * 256));
-    HIP_TRY(hipMalloc(&d->d_ftab, 512));
+    HIP_TRY(hipMalloc(&d->d_qt, sizeof(int16_t) * 5 * 256));
+    HIP_TRY(hipMalloc(&d->d_tabs, 1024));
     HIP_TRY(hipMalloc(&d->d_status, sizeof(int) * 4));
+    HIP_TRY(hipMalloc(&d->d_sticky, size_t(d->nslices)));
+    HIP_TRY(hipMalloc(&d->d_last, size_t(d->frame_bytes)));
     HIP_TRY(hipMemcpy(d->d_geom, d->geom.data(), sizeof(SliceGeom) * d->nslices, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d->d_qt, tmp.qt, sizeof(int16_t) * 3 * 256, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d->d_ftab, tmp.frame.to0, 256, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d->d_ftab + 256, tmp.frame.to1, 256, hipMemcpyHostToDevice));
-    return 0;
+    HIP_TRY(hipMemcpy(d->d_qt, tmp.qt, sizeof(int16_t) * 5 * 256, hipMemcpyHostToDevice));
+    uint8_t tabs[1024];
+    std::memcpy(tabs, tmp.frame.to0, 256);
+    std::memcpy(tabs + 256, tmp.frame.to1, 256);
+    std::memcpy(tabs + 512, tmp.dflt.to0, 256);
+    std::memcpy(tabs + 768, tmp.dflt.to1, 256);
+    HIP_TRY(hipMemcpy(d->d_tabs, tabs, 1024, hipMemcpyHostToDevice));
+    return dec_reset_states(d);
   };
   int rc = init();
   if (rc < 0) {
@@ -1509,6 +1554,7 @@ int ffv1hip_decode(ffv1hip_dec* d, const uint8_t* packets, const int64_t* sizes,
                    void* const* planes, const int* strides, int* key_flags) {
   if (!d || !packets || !sizes || n_frames < 0 || (n_frames && (!planes || !strides)))
     return set_err(-22, "null argument");
+  d->last_damaged = 0;
   if (n_frames == 0) return 0;
   const ffv1hip_params& p = d->P;
   const int ns = d->nslices;
@@ -1522,32 +1568,40 @@ int ffv1hip_decode(ffv1hip_dec* d, const uint8_t* packets, const int64_t* sizes,
     if (size < 2) return set_err(FFV1HIP_AVERROR_INVALIDDATA, "frame %d: packet too small", f);
     // key bit: the first decision with state 128 from range 0xFF00 (ffv1dec.c:931)
     keys[f] = ((pk[0] << 8) | pk[1]) >= 0x7F80;
-    // the slice chain, from the packet end (ffv1dec.c:948-989)
+    // the slice chain, from the packet end (ffv1dec.c:948-989); below v3
+    // the only slice runs to the end
     const uint8_t* q = pk + size;
     for (int i = ns - 1; i >= 0; i--) {
-      if (q - pk < trailer) return set_err(FFV1HIP_AVERROR_INVALIDDATA, "frame %d: slice %d trailer", f, i);
-      const int64_t v = ((int64_t(q[-trailer]) << 16) | (q[-trailer + 1] << 8) | q[-trailer + 2]) + trailer;
+      int64_t v;
+      if (i || p.version > 2) {
+        if (q - pk < trailer) return set_err(FFV1HIP_AVERROR_INVALIDDATA, "frame %d: slice %d trailer", f, i);
+        v = ((int64_t(q[-trailer]) << 16) | (q[-trailer + 1] << 8) | q[-trailer + 2]) + trailer;
+      } else {
+        v = q - pk;
+      }
       if (v > q - pk) return set_err(FFV1HIP_AVERROR_INVALIDDATA, "frame %d: slice %d size", f, i);
       ends[size_t(f) * ns + i] = (q - packets);
       q -= v;
       starts[size_t(f) * ns + i] = (q - packets);
     }
     if (q != pk) return set_err(FFV1HIP_AVERROR_INVALIDDATA, "frame %d: %d slices do not span the packet", f, ns);
+    if (ends[size_t(f) * ns] - starts[size_t(f) * ns] < 2)
+      return set_err(FFV1HIP_AVERROR_INVALIDDATA, "frame %d: first slice too small", f);
     total += size;
   }
-  if (p.ec) {  // slice CRCs (ffv1dec.c:964): residue 0, checked on host threads
-    const size_t nse = size_t(n_frames) * ns;
-    std::atomic<int64_t> bad{-1};
+  // slice CRCs (ffv1dec.c:963-977): a mismatch marks the slice damaged, it
+  // is still decoded, then concealed; checked on host threads
+  const size_t nse = size_t(n_frames) * ns;
+  std::vector<uint8_t> damage(nse, 0);
+  if (p.ec) {
     const int nt = int(std::max<size_t>(1, std::min<size_t>({nse, 16, std::thread::hardware_concurrency()})));
     std::vector<std::thread> pool;
     for (int t = 0; t < nt; t++)
       pool.emplace_back([&, t] {
         for (size_t k = size_t(t); k < nse; k += size_t(nt))
-          if (crc32_msb_fast(packets + starts[k], size_t(ends[k] - starts[k])) != 0) bad = int64_t(k);
+          damage[k] = crc32_msb_fast(packets + starts[k], size_t(ends[k] - starts[k])) != 0;
       });
     for (auto& th : pool) th.join();
-    if (bad >= 0)
-      return set_err(FFV1HIP_AVERROR_INVALIDDATA, "frame %d: slice %d CRC mismatch", int(bad / ns), int(bad % ns));
   }
   if (!keys[0] && !d->have_states)
     return set_err(FFV1HIP_AVERROR_INVALIDDATA, "stream does not start with a keyframe");
@@ -1563,13 +1617,16 @@ int ffv1hip_decode(ffv1hip_dec* d, const uint8_t* packets, const int64_t* sizes,
   uint8_t* d_keys = nullptr;
   Segment* d_segs = nullptr;
   uint8_t* d_out = nullptr;
+  uint8_t* d_dmg = nullptr;
+  uint8_t* d_tables = nullptr;
   auto run = [&]() -> int {
-    const size_t nse = size_t(n_frames) * ns;
     HIP_TRY(hipMalloc(&d_pk, size_t(total) + 64));
     HIP_TRY(hipMalloc(&d_se, 2 * nse * sizeof(int64_t)));
     HIP_TRY(hipMalloc(&d_keys, size_t(n_frames)));
     HIP_TRY(hipMalloc(&d_segs, segs.size() * sizeof(Segment)));
     HIP_TRY(hipMalloc(&d_out, size_t(d->frame_bytes) * n_frames));
+    HIP_TRY(hipMalloc(&d_dmg, nse));
+    if (d->global_states) HIP_TRY(hipMalloc(&d_tables, size_t(d->state_bytes) * ns * segs.size()));
     HIP_TRY(hipMemsetAsync(d_pk + total, 0, 64, d->stream));
     // samples no slice codes (odd chroma offsets, ffv1enc.c:1186-1188) read as 0
     HIP_TRY(hipMemsetAsync(d_out, 0, size_t(d->frame_bytes) * n_frames, d->stream));
@@ -1578,6 +1635,7 @@ int ffv1hip_decode(ffv1hip_dec* d, const uint8_t* packets, const int64_t* sizes,
     HIP_TRY(hipMemcpyAsync(d_se + nse, ends.data(), nse * sizeof(int64_t), hipMemcpyHostToDevice, d->stream));
     HIP_TRY(hipMemcpyAsync(d_keys, keys.data(), size_t(n_frames), hipMemcpyHostToDevice, d->stream));
     HIP_TRY(hipMemcpyAsync(d_segs, segs.data(), segs.size() * sizeof(Segment), hipMemcpyHostToDevice, d->stream));
+    HIP_TRY(hipMemcpyAsync(d_dmg, damage.data(), nse, hipMemcpyHostToDevice, d->stream));
     HIP_TRY(hipMemsetAsync(d->d_status, 0, sizeof(int) * 4, d->stream));
     DecodeArgs a{};
     a.pkts = d_pk;
@@ -1589,10 +1647,12 @@ int ffv1hip_decode(ffv1hip_dec* d, const uint8_t* packets, const int64_t* sizes,
     a.nslices = ns;
     a.nplanes = p.chroma_planes ? 3 : 1;
     a.qt = d->d_qt;
-    a.ftab = d->d_ftab;
+    a.ftab = d->d_tabs;
+    a.dtab = d->d_tabs + 512;
     a.state_bytes = d->state_bytes;
     a.persist_in = d->d_persist[d->pcur];
     a.persist_out = d->d_persist[d->pcur ^ 1];
+    a.tables = d_tables;
     a.out = d_out;
     a.frame_bytes = d->frame_bytes;
     for (int k = 0; k < 3; k++) {
@@ -1602,30 +1662,48 @@ int ffv1hip_decode(ffv1hip_dec* d, const uint8_t* packets, const int64_t* sizes,
     a.sample_bytes = p.sample_bytes;
     a.packed_at_lsb = p.packed_at_lsb;
     a.msb_shift = 16 - p.bits_per_raw_sample;
-    a.coded_bits = p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample;
+    a.coded_bits = coded_bits(p);
     a.width = p.width;
     a.height = p.height;
     a.num_h = p.num_h_slices;
     a.num_v = p.num_v_slices;
     a.context_model = p.context_model;
+    a.version = p.version;
+    a.ac = p.ac;
+    a.ec = p.ec;
+    a.rgb = p.colorspace;
+    a.rct_offset = 1 << p.bits_per_raw_sample;
+    a.contexts = d->contexts;
+    a.chroma_planes = p.chroma_planes;
+    a.chroma_h_shift = p.chroma_h_shift;
+    a.chroma_v_shift = p.chroma_v_shift;
+    a.bits_per_raw_sample = p.bits_per_raw_sample;
     a.row_cap = d->row_cap;
     a.status = d->d_status;
+    a.damage = d_dmg;
+    a.last = d->have_last ? d->d_last : nullptr;
+    a.sticky = d->d_sticky;
+    a.nframes = n_frames;
     if (launch_decode(a, int(segs.size()), d->stream) < 0)
       return set_err(-5, "ffv1_decode_slices launch failed: %s", hipGetErrorString(hipGetLastError()));
     int status = 0;
     HIP_TRY(hipMemcpyAsync(&status, d->d_status, sizeof(int), hipMemcpyDeviceToHost, d->stream));
     HIP_TRY(hipStreamSynchronize(d->stream));
-    if (status) return set_err(FFV1HIP_AVERROR_INVALIDDATA, "%d slice(s) with a bad key bit or slice header", status);
-    const int np = p.chroma_planes ? 3 : 1;
+    if (status) return set_err(FFV1HIP_AVERROR_INVALIDDATA, "%d frame(s) with a bad key bit or in-band header", status);
+    if (launch_conceal(a, d->stream) < 0)
+      return set_err(-5, "ffv1_conceal launch failed: %s", hipGetErrorString(hipGetLastError()));
+    HIP_TRY(hipMemcpyAsync(d->d_last, d_out + int64_t(n_frames - 1) * d->frame_bytes, size_t(d->frame_bytes),
+                           hipMemcpyDeviceToDevice, d->stream));
+    HIP_TRY(hipMemcpyAsync(damage.data(), d_dmg, nse, hipMemcpyDeviceToHost, d->stream));
     for (int f = 0; f < n_frames; f++)
-      for (int k = 0; k < np; k++) {
-        const int rows = k ? -((-p.height) >> p.chroma_v_shift) : p.height;
-        const int wb = d->plane_w[k] * p.sample_bytes;
+      for (int k = 0; k < d->out_planes; k++) {
+        const int64_t wb = int64_t(d->plane_w[k]) * p.sample_bytes;
         HIP_TRY(hipMemcpy2DAsync(planes[3 * f + k], strides[3 * f + k],
-                                 d_out + int64_t(f) * d->frame_bytes + d->plane_off[k], wb, wb, rows,
-                                 hipMemcpyDeviceToHost, d->stream));
+                                 d_out + int64_t(f) * d->frame_bytes + d->plane_off[k], size_t(wb), size_t(wb),
+                                 d->out_rows[k], hipMemcpyDeviceToHost, d->stream));
       }
     HIP_TRY(hipStreamSynchronize(d->stream));
+    for (uint8_t v : damage) d->last_damaged += v != 0;
     return 0;
   };
   int rc = run();
@@ -1634,16 +1712,25 @@ int ffv1hip_decode(ffv1hip_dec* d, const uint8_t* packets, const int64_t* sizes,
   (void)hipFree(d_keys);
   (void)hipFree(d_segs);
   (void)hipFree(d_out);
+  (void)hipFree(d_dmg);
+  if (d_tables) (void)hipFree(d_tables);
   if (rc < 0) return rc;
   d->pcur ^= 1;
   d->have_states = true;
+  d->have_last = true;
   if (key_flags)
     for (int f = 0; f < n_frames; f++) key_flags[f] = keys[f];
   return 0;
 }
 
+int ffv1hip_dec_damaged_slices(const ffv1hip_dec* d) { return d ? d->last_damaged : -22; }
+
 void ffv1hip_dec_reset(ffv1hip_dec* d) {
-  if (d) d->have_states = false;
+  if (!d) return;
+  d->have_states = false;
+  d->have_last = false;
+  (void)hipSetDevice(d->device);
+  (void)dec_reset_states(d);
 }
 
 }  // extern "C"

@@ -202,22 +202,32 @@ struct DecodeArgs {
   const Segment* segs;
   const SliceGeom* geom;
   int nslices, nplanes;
-  const int16_t* qt;           // [3][256]
+  const int16_t* qt;           // [5][256]
   const uint8_t* ftab;         // frame transition table: to0[256] | to1[256]
-  int64_t state_bytes;         // 2 * contexts * 32
+  const uint8_t* dtab;         // default table (key bit, v0/v1 header): to0 | to1
+  int64_t state_bytes;         // range coder: 2 * contexts * 32; Golomb: 2 * contexts * 8
   const uint8_t* persist_in;   // [slice][state_bytes]: the chain carried across calls
   uint8_t* persist_out;        // (two buffers: a launch never reads what it writes)
+  uint8_t* tables;             // global states [seg][slice][state_bytes] when they exceed the LDS
   uint8_t* out;                // [frame] regions of frame_bytes, planes tightly packed
   int64_t frame_bytes;
   int64_t plane_off[3];
   int plane_w[3];
   int sample_bytes, packed_at_lsb, msb_shift, coded_bits;
   int width, height, num_h, num_v, context_model;
+  int version, ac, ec, rgb, rct_offset, contexts;
+  int chroma_planes, chroma_h_shift, chroma_v_shift, bits_per_raw_sample;
   int row_cap;                 // widest slice plane (samples)
-  int* status;                 // [0] slices whose key bit or header disagrees
+  int* status;                 // [0] slices whose key bit or v0/v1 header disagrees
+  uint8_t* damage;             // [frame][slice]: 2 slice header failed (not decoded), 4 end mismatch
+  // concealment pass (ffv1_conceal)
+  const uint8_t* last;         // the picture before frame 0 (previous call), or null
+  uint8_t* sticky;             // [slice] slice_damaged carried across calls
+  int nframes;
 };
 int launch_decode(const DecodeArgs& a, int nsegs, void* stream);
-int64_t decode_lds_bytes(int64_t state_bytes, int row_cap);
+int launch_conceal(const DecodeArgs& a, void* stream);
+int64_t decode_lds_bytes(const DecodeArgs& a, bool global_states);
 
 int launch_symbols(const SymbolArgs& a, void* stream);
 int launch_code(const CodeArgs& a, void* stream);

@@ -63,7 +63,7 @@ EXPORTED_SYMBOLS = (
     "ffv1hip_abi_version", "ffv1hip_set_profiling", "ffv1hip_last_kernel_ms",
     "ffv1hip_last_kernel_stats", "ffv1hip_synchronize",
     "ffv1hip_dec_create", "ffv1hip_dec_destroy", "ffv1hip_decode", "ffv1hip_dec_reset",
-    "ffv1hip_set_picture_number", "ffv1hip_encode2",
+    "ffv1hip_set_picture_number", "ffv1hip_encode2", "ffv1hip_dec_damaged_slices",
 )
 
 
@@ -140,6 +140,8 @@ def load_library():
     L.ffv1hip_decode.restype = ctypes.c_int
     L.ffv1hip_dec_reset.argtypes = [vp]
     L.ffv1hip_dec_reset.restype = None
+    L.ffv1hip_dec_damaged_slices.argtypes = [vp]
+    L.ffv1hip_dec_damaged_slices.restype = ctypes.c_int
     L.ffv1hip_abi_version.argtypes = []
     L.ffv1hip_abi_version.restype = ctypes.c_int
     _lib = L
@@ -465,6 +467,12 @@ class HipDecoder:
 
     def reset(self):
         load_library().ffv1hip_dec_reset(self._h)
+
+    @property
+    def damaged_slices(self) -> int:
+        """(frame, slice) pairs of the last decode call that were damaged
+        (CRC, slice header or end mismatch) and concealed."""
+        return load_library().ffv1hip_dec_damaged_slices(self._h)
 
     def decode(self, packets: Sequence[bytes]) -> List[Tuple[List[np.ndarray], bool]]:
         """Decode packets in order; returns (planes, key) per frame, planes as

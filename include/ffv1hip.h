@@ -180,12 +180,14 @@ typedef struct ffv1hip_kernel_stats {
 int ffv1hip_last_kernel_stats(ffv1hip_ctx *ctx, ffv1hip_kernel_stats *out);
 
 /* Decoder: the AVCodec callbacks of ff_ffv1_decoder (ffv1dec.c decode_init
- * :1007, decode_frame :896-1005, decode_end) for the streams this library
- * encodes: version 3, range coder, context model 0 (the on-device lossless
- * self-check).  ffv1hip_dec_create takes the stream's parameters and its
- * extradata, which must be the one those parameters produce (what
- * read_extradata, ffv1dec.c:509-631, would parse); otherwise
- * FFV1HIP_AVERROR_INVALIDDATA.  Unsupported parameters give -ENOSYS. */
+ * :1007, decode_frame :896-1030, decode_end) for the streams this library
+ * encodes: versions 0, 1 and 3, range coder (default or custom table) or
+ * Golomb-Rice, context model 0 or 1, YCbCr or RGB.  ffv1hip_dec_create takes
+ * the stream's parameters and its extradata, which must be the one those
+ * parameters produce (what read_extradata, ffv1dec.c:509-631, would parse;
+ * none below version 2, whose in-band keyframe header must agree with the
+ * parameters); otherwise FFV1HIP_AVERROR_INVALIDDATA.  Unsupported
+ * parameters give -ENOSYS. */
 typedef struct ffv1hip_dec ffv1hip_dec;
 ffv1hip_dec *ffv1hip_dec_create(const ffv1hip_params *params,
                                 const uint8_t *extradata, int extradata_size,
@@ -194,14 +196,22 @@ void ffv1hip_dec_destroy(ffv1hip_dec *dec);
 /* decode_frame over a batch: packets back to back in HOST memory (sizes[i]
  * bytes each); plane p of frame i goes to planes[3*i + p] with row stride
  * strides[3*i + p] (the encoder's input layout).  The key bit and the slice
- * chain (3-byte sizes, CRC-32 when ec) are checked on the host as in
+ * chain (3-byte sizes, CRC-32 when ec) are read on the host as in
  * ffv1dec.c:931-989; every (GOP segment, slice) chain decodes on the GPU.
  * Context states carry across calls like the encoder's.  key_flags may be
  * NULL. */
 int ffv1hip_decode(ffv1hip_dec *dec, const uint8_t *packets,
                    const int64_t *sizes, int n_frames, void *const *planes,
                    const int *strides, int *key_flags);
-/* Forget the carried states: the next frame must be a keyframe. */
+/* Damaged slices are decoded on and concealed as the reference does
+ * (ffv1dec.c:963-977, 410-414, 461-467, 998-1021): a slice failing its CRC,
+ * its slice header or its end position takes the previous picture's
+ * rectangle in that frame and in every later frame up to the next
+ * keyframe.  This is how many (frame, slice) pairs of the last
+ * ffv1hip_decode call were damaged. */
+int ffv1hip_dec_damaged_slices(const ffv1hip_dec *dec);
+/* Forget the carried states and the previous picture: the next frame must
+ * be a keyframe. */
 void ffv1hip_dec_reset(ffv1hip_dec *dec);
 /* Last error message (thread-local) and the ABI version. */
 const char *ffv1hip_last_error(void);

@@ -290,14 +290,14 @@ static int rc_get_symbol(rc_dec *c, uint8_t st[32], int is_signed)
     int e = 0;
     while (rc_get(c, &st[1 + (e < 9 ? e : 9)])) {
         if (++e > 31)
-            return 0;
+            return FFV1O_AVERROR_INVALIDDATA; /* ffv1dec.c:53-54: the caller uses it as a value */
     }
-    int a = 1;
+    unsigned a = 1; /* wraps like the reference's int at e = 31 */
     for (int i = e - 1; i >= 0; i--)
-        a = 2 * a + rc_get(c, &st[22 + (i < 9 ? i : 9)]);
+        a = 2 * a + (unsigned)rc_get(c, &st[22 + (i < 9 ? i : 9)]);
     if (is_signed && rc_get(c, &st[11 + (e < 10 ? e : 10)]))
-        return -a;
-    return a;
+        return (int)(0u - a);
+    return (int)a;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1274,6 +1274,7 @@ int64_t ffv1o_slice_symbols(const ffv1o_config *cfg,
 typedef struct dslice {
     int x0, y0, w, h;
     plane_state ps[2];
+    int damaged; /* slice_damaged: set by a CRC / header / end mismatch, cleared by read_header */
 } dslice;
 
 struct ffv1o_dec {
@@ -1290,7 +1291,26 @@ struct ffv1o_dec {
     dslice *sl;
     int key_ok;
     int16_t *scratch;
+    /* last_picture for the concealment copy (ffv1dec.c:998-1021) */
+    uint8_t *last[3];
+    int last_row[3], last_rows[3];
+    int have_last;
 };
+
+/* Rows and row bytes of the output planes (the encoder's input layout). */
+static int out_planes(const ffv1o_dec *d, int row[3], int rows[3])
+{
+    const ffv1o_config *c = &d->cfg;
+    int sb = c->sample_bytes;
+    row[0] = c->width * sb;
+    rows[0] = c->height;
+    int np = c->chroma_planes && sb != 4 ? 3 : 1;
+    for (int k = 1; k < 3; k++) {
+        row[k] = k < np ? ceil_rshift(c->width, c->chroma_h_shift) * sb : 0;
+        rows[k] = k < np ? ceil_rshift(c->height, c->chroma_v_shift) : 0;
+    }
+    return np;
+}
 
 /* read_quant_table(s), ffv1dec.c:475-515 */
 static int get_quant_tables(rc_dec *c, int16_t qt[5][256])
@@ -1404,6 +1424,8 @@ void ffv1o_dec_free(ffv1o_dec *d)
             free(d->sl[i].ps[p].rac);
             free(d->sl[i].ps[p].vlc);
         }
+    for (int k = 0; k < 3; k++)
+        free(d->last[k]);
     free(d->sl);
     free(d->scratch);
     free(d);
@@ -1522,12 +1544,13 @@ static void decode_rgb_slice(ffv1o_dec *d, void *coder, int golomb, dslice *s,
             b += g;
             r += g;
             int X = s->x0 + x, Y = s->y0 + y;
-            if (lbd) {
+            if (lbd) { /* one 32-bit store of b + (g << 8) + (r << 16): carries cross bytes */
                 uint8_t *px = planes[0] + (int64_t)Y * strides[0] + 4 * (int64_t)X;
-                px[0] = (uint8_t)b;
-                px[1] = (uint8_t)g;
-                px[2] = (uint8_t)r;
-                px[3] = 0;
+                uint32_t v = (uint32_t)b + ((uint32_t)g << 8) + ((uint32_t)r << 16);
+                px[0] = (uint8_t)v;
+                px[1] = (uint8_t)(v >> 8);
+                px[2] = (uint8_t)(v >> 16);
+                px[3] = (uint8_t)(v >> 24);
             } else {
                 int v[3] = {b, g, r};
                 for (int k = 0; k < 3; k++) {
@@ -1579,6 +1602,7 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
     /* slice chain from the end of the packet, ffv1dec.c:948-989 */
     int trailer = 3 + (d->ec ? 5 : 0);
     int64_t starts[256], lens[256];
+    int crc_bad[256];
     int n = d->nslices;
     const uint8_t *p = pkt + size;
     if (d->version > 2) { /* count slices (read_header :805-818) */
@@ -1603,11 +1627,13 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
         if (p - pkt < v)
             return -1;
         p -= v;
-        if (d->ec && ffv1o_crc32(0, p, v) != 0)
-            return -2;
+        crc_bad[i] = d->ec && ffv1o_crc32(0, p, v) != 0; /* ffv1dec.c:963-977 */
         starts[i] = p - pkt;
         lens[i] = v;
     }
+    if (key) /* read_header clears slice_damaged (ffv1dec.c:820-825) */
+        for (int i = 0; i < n; i++)
+            d->sl[i].damaged = 0;
 
     for (int i = 0; i < n; i++) {
         dslice *s = &d->sl[i];
@@ -1622,21 +1648,32 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
         const int16_t(*qt)[256] = (const int16_t(*)[256])d->qt;
         int model1 = 0;
         int contexts = d->contexts;
+        d->sl[i].damaged |= crc_bad[i];
         if (d->version > 2) { /* decode_slice_header, ffv1dec.c:282-359 */
             uint8_t st[32];
             memset(st, 128, 32);
-            int sx = rc_get_symbol(&c, st, 0), sy = rc_get_symbol(&c, st, 0);
-            int sw = rc_get_symbol(&c, st, 0), sh = rc_get_symbol(&c, st, 0);
-            int x0 = sx * d->cfg.width / d->num_h;
-            int y0 = sy * d->cfg.height / d->num_v;
-            int x1 = (sx + sw + 1) * d->cfg.width / d->num_h;
-            int y1 = (sy + sh + 1) * d->cfg.height / d->num_v;
-            s->x0 = x0; s->y0 = y0; s->w = x1 - x0; s->h = y1 - y0;
+            int64_t W = d->cfg.width, H = d->cfg.height;
+            int64_t sx = rc_get_symbol(&c, st, 0) * W, sy = rc_get_symbol(&c, st, 0) * H;
+            int64_t sw = (rc_get_symbol(&c, st, 0) + 1) * W + sx;
+            int64_t sh = (rc_get_symbol(&c, st, 0) + 1) * H + sy;
+            sx /= d->num_h;
+            sy /= d->num_v;
+            sw = sw / d->num_h - sx;
+            sh = sh / d->num_v - sy;
+            int ok = (uint32_t)sw <= W && (uint32_t)sh <= H && (uint32_t)sx + (uint64_t)(uint32_t)sw <= (uint64_t)W &&
+                     (uint32_t)sy + (uint64_t)(uint32_t)sh <= (uint64_t)H;
             int qi = 0;
-            for (int j = 0; j < 2; j++)
-                qi = rc_get_symbol(&c, st, 0);
-            if (qi > 1)
-                return -1;
+            for (int j = 0; ok && j < 2; j++) {
+                unsigned idx = (unsigned)rc_get_symbol(&c, st, 0);
+                ok = idx < 2;
+                qi = (int)idx; /* plane 0 and plane 1 read their own index; ours agree */
+            }
+            if (!ok) { /* ffv1dec.c:410-414: no decode, an empty rectangle */
+                s->x0 = s->y0 = s->w = s->h = 0;
+                s->damaged = 1;
+                continue;
+            }
+            s->x0 = (int)sx; s->y0 = (int)sy; s->w = (int)sw; s->h = (int)sh;
             (void)rc_get_symbol(&c, st, 0); /* picture structure */
             (void)rc_get_symbol(&c, st, 0);
             (void)rc_get_symbol(&c, st, 0);
@@ -1669,8 +1706,7 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
         }
         if (d->colorspace) {
             decode_rgb_slice(d, coder, golomb, s, qt, model1, planes, strides);
-            continue;
-        }
+        } else {
         int np = d->chroma_planes ? 3 : 1;
         for (int pl = 0; pl < np; pl++) {
             int x0 = s->x0, y0 = s->y0, w = s->w, h = s->h;
@@ -1683,7 +1719,47 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
             decode_plane_any(d, coder, golomb, &s->ps[pl ? 1 : 0], qt, model1,
                              w, h, planes[pl], strides[pl], x0, y0);
         }
+        }
+        if (!golomb && d->version > 2) { /* ffv1dec.c:461-467 */
+            uint8_t st = 129;
+            (void)rc_get(&c, &st);
+            if (c.end - c.ptr - 2 - 5 * d->ec)
+                s->damaged = 1;
+        }
     }
+
+    /* concealment (ffv1dec.c:998-1021): a damaged slice's rectangle comes
+     * from the previous picture; the x offset is in samples << (depth > 8),
+     * which for packed bgr0 is x bytes (not 4x) */
+    int row[3], rows[3];
+    int np = out_planes(d, row, rows);
+    for (int i = n - 1; i >= 0 && d->have_last; i--) {
+        dslice *s = &d->sl[i];
+        if (!s->damaged || !s->w || !s->h)
+            continue;
+        for (int k = 0; k < np; k++) {
+            int hs = k ? d->cfg.chroma_h_shift : 0, vs = k ? d->cfg.chroma_v_shift : 0;
+            int pix = d->cfg.sample_bytes == 2;
+            int bpp = d->cfg.sample_bytes;
+            int64_t xoff = (int64_t)(s->x0 >> hs) << pix;
+            int64_t bytes = (int64_t)ceil_rshift(s->w, hs) * bpp;
+            for (int y = 0; y < ceil_rshift(s->h, vs); y++) {
+                int64_t yy = (s->y0 >> vs) + y;
+                memcpy(planes[k] + yy * strides[k] + xoff,
+                       d->last[k] + yy * d->last_row[k] + xoff, (size_t)bytes);
+            }
+        }
+    }
+    for (int k = 0; k < np; k++) {
+        if (!d->last[k]) {
+            d->last[k] = malloc((size_t)row[k] * rows[k] + 16);
+            d->last_row[k] = row[k];
+            d->last_rows[k] = rows[k];
+        }
+        for (int y = 0; y < rows[k]; y++)
+            memcpy(d->last[k] + (int64_t)y * row[k], planes[k] + (int64_t)y * strides[k], (size_t)row[k]);
+    }
+    d->have_last = 1;
     if (key_out)
         *key_out = key;
     return 0;

@@ -28,6 +28,8 @@
 
 #include <stdint.h>
 
+#define FFV1O_AVERROR_INVALIDDATA (-1094995529)
+
 #ifdef __cplusplus
 extern "C" {
 #endif

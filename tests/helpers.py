@@ -138,3 +138,26 @@ RGB_STREAMS = [
     Stream("gbrp12_v1", 64, 48, "gbrp12", 3, level=1, gop_size=3, source="random"),
     Stream("gbrp14_ctx1", 64, 48, "gbrp14", 3, slices=4, context=1, gop_size=3, source="random"),
 ]
+
+
+def corrupt_slice(packet: bytes, ec: bool, nslices: int, slice_index: int) -> bytes:
+    """Flip one byte in the middle of a slice's coded bytes (not its header
+    or trailer): the slice then fails its CRC (ffv1dec.c:963-977)."""
+    trailer = 3 + (5 if ec else 0)
+    end, spans = len(packet), []
+    for _ in range(nslices):
+        size = int.from_bytes(packet[end - trailer:end - trailer + 3], "big")
+        spans.append((end - trailer - size, end - trailer))
+        end -= size + trailer
+    a, b = spans[nslices - 1 - slice_index]
+    k = (a + b) // 2 + 16
+    assert a + 16 < k < b
+    return packet[:k] + bytes([packet[k] ^ 0x5A]) + packet[k + 1:]
+
+
+def slice_rect(cfg, i):
+    nh, nv = cfg.num_h_slices, cfg.num_v_slices
+    sx, sy = i % nh, i // nh
+    x0, x1 = cfg.width * sx // nh, cfg.width * (sx + 1) // nh
+    y0, y1 = cfg.height * sy // nv, cfg.height * (sy + 1) // nv
+    return x0, y0, x1, y1

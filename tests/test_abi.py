@@ -113,9 +113,10 @@ def test_decoder_contract_checks_before_the_gpu():
     from oracle import oracle
     p = configure(352, 288, "yuv420p10", coder=1, slices=4)
     ex = oracle.Encoder(oracle.configure(352, 288, "yuv420p10", coder=1, slices=4)).extradata()
-    for field, value in (("context_model", 1), ("ac", 0), ("version", 1)):
+    for field, value in (("version", 2), ("version", 1), ("context_model", 2), ("colorspace", 2),
+                         ("ac", 3)):
         q = configure(352, 288, "yuv420p10", coder=1, slices=4)
-        setattr(q, field, value)
+        setattr(q, field, value)  # version 1 has a single slice
         with pytest.raises(FFV1Error) as e:
             HipDecoder(q, ex, 0)
         assert e.value.code == -38, field

@@ -10,7 +10,8 @@ import hashlib
 import numpy as np
 import pytest
 
-from helpers import PARITY_STREAMS, RGB_STREAMS, Stream, load_golden, md5, oracle_encode
+from helpers import (PARITY_STREAMS, RGB_STREAMS, Stream, corrupt_slice, load_golden, md5, oracle_encode,
+                     slice_rect)
 from oracle import oracle
 
 PINS = {p["name"]: p for p in load_golden("known_answers.json")["streams"]}
@@ -141,3 +142,29 @@ def test_oracle_rgb_roundtrip(stream):
                 b = b.copy()
                 b[:, 3::4] = 0
             np.testing.assert_array_equal(a, b)
+
+
+def test_oracle_conceals_damaged_slices():
+    """A P-frame slice failing its CRC is replaced by the previous picture's
+    rectangle and stays so until the next keyframe (slice_damaged is only
+    cleared by read_header; ffv1dec.c:820-825, 998-1021)."""
+    s = Stream("conceal", 176, 144, "yuv420p", 8, slices=4, gop_size=4)
+    frames = list(s.frames())
+    cfg, ex, pkts = oracle_encode(s, frames)
+    bad = [p for p, _ in pkts]
+    bad[1] = corrupt_slice(bad[1], True, 4, 2)
+    dec = oracle.Decoder(cfg, ex)
+    out = [dec.decode(p)[0] for p in bad]
+    x0, y0, x1, y1 = slice_rect(cfg, 2)
+    for f in range(8):
+        for k in range(3):
+            sh = 1 if k else 0
+            got, want = out[f][k], frames[f][k]
+            r = (slice(y0 >> sh, -(-y1 >> sh)), slice(x0 >> sh, -(-x1 >> sh)))
+            if f in (1, 2, 3):  # damaged from frame 1 to the end of the GOP
+                np.testing.assert_array_equal(got[r], frames[0][k][r])
+                m = np.ones(got.shape, bool)
+                m[r] = False
+                np.testing.assert_array_equal(got[m], want[m])
+            else:
+                np.testing.assert_array_equal(got, want)
