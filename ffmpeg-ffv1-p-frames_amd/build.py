@@ -53,7 +53,7 @@ def build_hip(force=False, extra=()):
     os.makedirs(LIB, exist_ok=True)
     out = os.path.join(LIB, "libffv1hip.so")
     srcs = [os.path.join(CSRC, "ffv1_kernels.hip"), os.path.join(CSRC, "ffv1_decode.hip"),
-            os.path.join(CSRC, "ffv1_host.cpp")]
+            os.path.join(CSRC, "ffv1_host.cpp"), os.path.join(CSRC, "ffv1_twopass.cpp")]
     deps = srcs + [os.path.join(CSRC, "ffv1_internal.h"), os.path.join(INCLUDE, "ffv1hip.h")]
     if force or _stale(out, deps):
         _run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",

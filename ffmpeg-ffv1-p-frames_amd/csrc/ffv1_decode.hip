@@ -342,9 +342,14 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
     if (bad == 2) return;
     if (bad) continue;  // not decoded: no state update (ffv1dec.c:410-414)
     if (key) {          // ff_ffv1_clear_slice_state, after the header (ffv1dec.c:418-419)
-      const uint32_t v0 = GOLOMB ? uint32_t(kVlcInit) : 0x80808080u;
-      const uint32_t v1 = GOLOMB ? uint32_t(kVlcInit >> 32) : 0x80808080u;
-      for (int64_t i = lane; i < words; i += kDecThreads) st4[i] = (i & 1) ? v1 : v0;
+      if (!GOLOMB && a.init) {  // initial states from the extradata (ffv1.c:185-189)
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.init);
+        for (int64_t i = lane; i < words; i += kDecThreads) st4[i] = src[i % (words / 2)];
+      } else {
+        const uint32_t v0 = GOLOMB ? uint32_t(kVlcInit) : 0x80808080u;
+        const uint32_t v1 = GOLOMB ? uint32_t(kVlcInit >> 32) : 0x80808080u;
+        for (int64_t i = lane; i < words; i += kDecThreads) st4[i] = (i & 1) ? v1 : v0;
+      }
     }
     if (lane == 0 && GOLOMB) {  // ffv1dec.c:426-433
       if (a.version > 2) {        // micro_version 4: a 0 on state 129, then the Golomb bits

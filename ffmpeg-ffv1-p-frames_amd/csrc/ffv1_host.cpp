@@ -287,6 +287,15 @@ struct ffv1hip_ctx {
   int* d_slot_frames = nullptr;  // [j][slot]
   int* d_status = nullptr;       // [set][4]: [0] slices over budget, [1] most bytes one needed
   hipStream_t stream = nullptr;
+  // 2-pass (ffv1enc.c:898-986): pass 1 counts into d_rcstat ([256][2] state
+  // counts, then [contexts][32][2] slot counts); pass 2 starts keyframes
+  // from init_states[context_model] (d_init)
+  int pass = 0;
+  unsigned long long* d_rcstat = nullptr;
+  unsigned long long* d_rcstat_bak = nullptr;  // before the last batch (its re-encode)
+  int64_t gob_count = 0;                       // keyframes coded (ffv1enc.c:1302)
+  std::vector<uint8_t> init_states[2];
+  uint8_t* d_init = nullptr;
   // ordering between calls: the next batch's launch stream waits for `dep`
   // (the previous batch's last use of the buffers it rewrites first), and
   // ffv1hip_synchronize waits for `done` (the previous batch's last kernel)
@@ -305,6 +314,7 @@ struct ffv1hip_ctx {
     int64_t pn0 = 0;
     bool have0 = false;
     int pcur0 = 0, buf0 = 0, status_set = 0;
+    int64_t gob0 = 0;
   } last;
   int last_n = 0;
   std::vector<int> last_keys;
@@ -358,7 +368,7 @@ int ffv1hip_configure(ffv1hip_params* out, const ffv1hip_options* o) {
   p.sar_den = 1;
   // version (ffv1enc.c:678-706)
   int version = 0;
-  if (o->slices > 1) version = 2;
+  if (o->pass || o->slices > 1) version = 2;  // AV_CODEC_FLAG_PASS1 | PASS2 (ffv1enc.c:680-682)
   if (o->slices == 0 && o->level < 0 && int64_t(o->width) * o->height > 720 * 576) version = 2;
   if (o->level <= 0 && version == 2) version = 3;
   if (o->level >= 0 && o->level <= 4) {
@@ -460,8 +470,18 @@ static int build_extradata(ffv1hip_ctx* c) {
       r.symbol(qs, i - last - 1, false);
     }
   }
-  r.put(st, 0);  // default initial states for both quant sets
-  r.put(st, 0);
+  uint8_t st2[32][32];
+  std::memset(st2, 128, sizeof(st2));
+  for (int set = 0; set < 2; set++) {  // initial states (ffv1enc.c:591-607)
+    const std::vector<uint8_t>& is = c->init_states[set];
+    const bool any = std::any_of(is.begin(), is.end(), [](uint8_t v) { return v != 128; });
+    r.put(st, any);
+    if (!any) continue;
+    for (size_t i = 0; i < is.size(); i++) {
+      const int pred = i >= 32 ? is[i - 32] : 128;
+      r.symbol(st2[i & 31], int8_t(is[i] - pred), true);
+    }
+  }
   if (p.version > 2) {
     r.symbol(st, p.ec, false);
     r.symbol(st, p.gop_size < 2, false);
@@ -538,6 +558,8 @@ static void free_device(ffv1hip_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t& e : c->kev)
     if (e) (void)hipEventDestroy(e);
+  for (void* q : {(void*)c->d_rcstat, (void*)c->d_rcstat_bak, (void*)c->d_init})
+    if (q) (void)hipFree(q);
   if (c->dep_ev) (void)hipEventDestroy(c->dep_ev);
   if (c->done_ev) (void)hipEventDestroy(c->done_ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -773,6 +795,65 @@ void ffv1hip_reset(ffv1hip_ctx* c) {
   }
 }
 
+int ffv1hip_set_pass(ffv1hip_ctx* c, int pass, const char* stats_in) {
+  if (!c || pass < 0 || pass > 2 || (pass == 2 && !stats_in)) return set_err(-22, "invalid arguments");
+  if (c->picture_number || c->have_states || c->pass)
+    return set_err(-22, "the pass is chosen once, before the first frame");
+  if (pass == 0) return 0;
+  const ffv1hip_params& p = c->P;
+  if (p.version < 2) return set_err(-22, "2-pass needs version >= 2 (ffv1hip_options.pass)");
+  HIP_TRY(hipSetDevice(c->device));
+  if (pass == 1) {
+    // the range coder's counts come from the decision stream (the
+    // frame-parallel mode); Golomb-Rice codes no range decisions and
+    // writes zero counts, as the reference does
+    if (p.ac && !c->frames_mode)
+      return set_err(-38, "pass-1 statistics need the frame-parallel range coder (YCbCr, context model 0)");
+    const size_t bytes = sizeof(unsigned long long) * (512 + size_t(64) * c->contexts);
+    HIP_TRY(hipMalloc(&c->d_rcstat, bytes));
+    HIP_TRY(hipMalloc(&c->d_rcstat_bak, bytes));
+    HIP_TRY(hipMemset(c->d_rcstat, 0, bytes));
+    c->pass = 1;
+    return 0;
+  }
+  uint8_t stt[256];
+  std::memcpy(stt, c->frame.to1, 256);
+  std::string err;
+  const int rc = pass2_states(stats_in, p.ac == 2, stt, c->dflt.to1, c->init_states, &err);
+  if (rc < 0) return set_err(rc, "%s", err.c_str());
+  if (p.ac == 2) {  // the sorted table (ffv1enc.c:955-956), installed as in ffv1.c:95-101
+    for (int i = 1; i < 256; i++) {
+      c->frame.to1[i] = stt[i];
+      c->frame.to0[256 - i] = uint8_t(256 - stt[i]);
+    }
+    HIP_TRY(hipMemcpy(c->d_tabs + 512, c->frame.to0, 256, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_tabs + 768, c->frame.to1, 256, hipMemcpyHostToDevice));
+  }
+  const std::vector<uint8_t>& is = c->init_states[p.context_model];
+  HIP_TRY(hipMalloc(&c->d_init, is.size()));
+  HIP_TRY(hipMemcpy(c->d_init, is.data(), is.size(), hipMemcpyHostToDevice));
+  build_extradata(c);
+  c->pass = 2;
+  return 0;
+}
+
+int64_t ffv1hip_stats_out(ffv1hip_ctx* c, char* buf, int64_t cap) {
+  if (!c) return set_err(-22, "null ctx");
+  if (c->pass != 1) return set_err(-22, "not a pass-1 context");
+  HIP_TRY(hipSetDevice(c->device));
+  const int rc = ffv1hip_synchronize(c);
+  if (rc < 0) return rc;
+  std::vector<uint64_t> h(512 + size_t(64) * c->contexts, 0);
+  if (c->P.ac)
+    HIP_TRY(hipMemcpy(h.data(), c->d_rcstat, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  const std::string t = pass1_text(h.data(), h.data() + 512, c->contexts, c->P.context_model, int(c->gob_count));
+  if (buf) {
+    if (cap < int64_t(t.size()) + 1) return set_err(-22, "stats buffer too small");
+    std::memcpy(buf, t.c_str(), t.size() + 1);
+  }
+  return int64_t(t.size());
+}
+
 // The sample width the residuals are folded / Golomb-coded at: RGB codes
 // the transformed G', B' + off, R' + off with one more bit, 9 at 8 bit
 // (ffv1enc.c:464-467).
@@ -814,6 +895,11 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   c->last.have0 = c->have_states;
   c->last.pcur0 = c->pcur;
   c->last.buf0 = c->buf;
+  c->last.gob0 = c->gob_count;
+  for (uint8_t k : keys) c->gob_count += k;
+  if (c->pass == 1)
+    HIP_TRY(hipMemcpyAsync(c->d_rcstat_bak, c->d_rcstat, sizeof(unsigned long long) * (512 + size_t(64) * c->contexts),
+                           hipMemcpyDeviceToDevice, st));
   // the previous batch (possibly on another stream) is done with what this
   // one rewrites first: segments, slot lists, keyflags, the persist buffer
   if (c->dep_valid) HIP_TRY(hipStreamWaitEvent(st, c->dep_ev, 0));
@@ -893,6 +979,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   ca.version = p.version;
   ca.coded_bits = coded_bits(p);
   ca.rgb = p.colorspace;
+  ca.init = c->d_init;
 
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev[0], st));
   // brackets one launch with events when profiling (kind: 0 symbols, 1 code, 2 states)
@@ -976,6 +1063,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     wa.scratch = c->d_scratch;
     static const bool force_multi = std::getenv("FFV1HIP_FORCE_MULTI") && std::atoi(std::getenv("FFV1HIP_FORCE_MULTI"));
     wa.force_multi = force_multi;
+    wa.init = c->d_init;
     // FFV1HIP_WALKDBG=1 (measurement hook): per-block cycle split to stderr
     static const bool walkdbg = std::getenv("FFV1HIP_WALKDBG") && std::atoi(std::getenv("FFV1HIP_WALKDBG"));
     uint64_t* d_dbg = nullptr;
@@ -987,6 +1075,18 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     }
     if (timed(2, st, [&] { return launch_walk(wa, nsegs, st); }) < 0)
       return set_err(-5, "walk launch failed: %s", hipGetErrorString(hipGetLastError()));
+    StatsArgs sta{};
+    if (c->pass == 1) {  // slot counts from the records, before the next batch's symbols rewrite them
+      sta.rec = d_rec;
+      sta.frame_samples = c->frame_samples;
+      sta.geom = c->d_geom;
+      sta.nslices = c->nslices;
+      sta.nframes = n;
+      sta.ds = ds;
+      sta.rc_stat = c->d_rcstat;
+      sta.rc_stat2 = c->d_rcstat + 512;
+      if (launch_stats(sta, false, st) < 0) return set_err(-5, "stats launch failed");
+    }
     if (walkdbg) {
       std::vector<uint64_t> h(size_t(4) * nblk);
       HIP_TRY(hipMemcpyAsync(h.data(), d_dbg, h.size() * 8, hipMemcpyDeviceToHost, st));
@@ -1008,6 +1108,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     HIP_TRY(hipEventRecord(c->walked[fb], st));
     HIP_TRY(hipStreamWaitEvent(cst, c->walked[fb], 0));
     HIP_TRY(hipStreamWaitEvent(cst, c->bitsed[fb], 0));
+    if (c->pass == 1 && launch_stats(sta, true, cst) < 0) return set_err(-5, "stats launch failed");
     ca.nframes = n;
     ca.nopsets = c->nopsets;
     ca.opsets = c->d_opsets;
@@ -1131,6 +1232,10 @@ int ffv1hip_fetch(ffv1hip_ctx* c, uint8_t* out, int64_t out_cap, int64_t* sizes,
     c->have_states = L.have0;
     c->pcur = L.pcur0;
     c->buf = L.buf0;
+    c->gob_count = L.gob0;
+    if (c->pass == 1)
+      HIP_TRY(hipMemcpy(c->d_rcstat, c->d_rcstat_bak, sizeof(unsigned long long) * (512 + size_t(64) * c->contexts),
+                        hipMemcpyDeviceToDevice));
     c->dep_valid = false;  // synchronised above
     int rc = grow_slice_budget(c, status[1]);
     if (rc < 0) return rc;
@@ -1401,6 +1506,7 @@ struct ffv1hip_dec {
   int* d_status = nullptr;
   uint8_t* d_sticky = nullptr;  // [slice] slice_damaged across calls
   uint8_t* d_last = nullptr;
+  uint8_t* d_init = nullptr;  // initial states from the extradata (2-pass streams)
   hipStream_t stream = nullptr;
   int last_damaged = 0;
 };
@@ -1414,7 +1520,107 @@ static void dec_free(ffv1hip_dec* d) {
   (void)hipFree(d->d_status);
   (void)hipFree(d->d_sticky);
   (void)hipFree(d->d_last);
+  if (d->d_init) (void)hipFree(d->d_init);
   if (d->stream) (void)hipStreamDestroy(d->stream);
+}
+
+// Range decoder over host bytes (rangecoder.h:104-147), for the extradata.
+struct HostRacDec {
+  const uint8_t* b;
+  size_t n, pos = 2;
+  int low, range = 0xFF00;
+  const Tables* t;
+  HostRacDec(const uint8_t* buf, size_t size, const Tables* tab) : b(buf), n(size), low((buf[0] << 8) | buf[1]), t(tab) {}
+  int get(uint8_t* st) {
+    const int r1 = (range * *st) >> 8;
+    int bit;
+    range -= r1;
+    if (low < range) {
+      bit = 0;
+      *st = t->to0[*st];
+    } else {
+      low -= range;
+      range = r1;
+      bit = 1;
+      *st = t->to1[*st];
+    }
+    if (range < 0x100) {
+      range <<= 8;
+      low <<= 8;
+      if (pos < n) low += b[pos];
+      pos++;
+    }
+    return bit;
+  }
+  int symbol(uint8_t* st, bool sgn) {
+    if (get(st)) return 0;
+    int e = 0;
+    while (get(st + 1 + std::min(e, 9)))
+      if (++e > 31) return 0;
+    unsigned a = 1;
+    for (int i = e - 1; i >= 0; i--) a = 2 * a + unsigned(get(st + 22 + std::min(i, 9)));
+    return sgn && get(st + 11 + std::min(e, 10)) ? -int(a) : int(a);
+  }
+};
+
+// read_extra_header (ffv1dec.c:509-631) as far as the custom transition
+// table and the initial states, into c->frame / c->init_states; the
+// caller compares the whole extradata afterwards.
+static void read_extra_states(const uint8_t* ex, int size, ffv1hip_ctx* c) {
+  if (size < 2) return;
+  HostRacDec r(ex, size_t(size), &c->dflt);
+  uint8_t st[32];
+  std::memset(st, 128, 32);
+  const int version = r.symbol(st, false);
+  if (version > 2) (void)r.symbol(st, false);  // micro_version
+  const int ac = r.symbol(st, false);
+  if (ac == 2) {
+    uint8_t stt[256] = {0};
+    for (int i = 1; i < 256; i++) stt[i] = uint8_t(r.symbol(st, true) + c->dflt.to1[i]);
+    c->frame = c->dflt;
+    for (int i = 1; i < 256; i++) {
+      c->frame.to1[i] = stt[i];
+      c->frame.to0[256 - i] = uint8_t(256 - stt[i]);
+    }
+  }
+  (void)r.symbol(st, false);  // colorspace
+  (void)r.symbol(st, false);  // bits_per_raw_sample
+  (void)r.get(st);            // chroma_planes
+  (void)r.symbol(st, false);  // chroma_h_shift
+  (void)r.symbol(st, false);  // chroma_v_shift
+  (void)r.get(st);            // transparency
+  (void)r.symbol(st, false);  // num_h_slices - 1
+  (void)r.symbol(st, false);  // num_v_slices - 1
+  const int nq = r.symbol(st, false);
+  if (nq < 1 || nq > 2) return;
+  for (int i = 0; i < nq; i++)  // the quant tables (ffv1dec.c:475-507), skipped
+    for (int t = 0; t < 5; t++) {
+      uint8_t qs[32];
+      std::memset(qs, 128, 32);
+      for (int k = 0; k < 128;) {
+        const unsigned len = unsigned(r.symbol(qs, false)) + 1u;
+        if (len > unsigned(128 - k) || !len) return;
+        k += int(len);
+      }
+    }
+  // The initial states come in the encoder's context numbering and count
+  // (666 / 7563, ffv1enc.c:868-869), which is what the encoder wrote.  The
+  // reference decoder counts contexts from the tables it read instead
+  // (ffv1dec.c:497-507), which above 8 bits (9-level tables: 365 / 4105
+  // contexts) is fewer than the encoder wrote, so it misreads a 2-pass
+  // extradata there; this decoder reads what was written.
+  const int counts[2] = {contexts_of(0), contexts_of(1)};
+  uint8_t st2[32][32];
+  std::memset(st2, 128, sizeof(st2));
+  for (int i = 0; i < nq; i++) {  // ffv1dec.c:592-601
+    if (!r.get(st)) continue;
+    std::vector<uint8_t>& is = c->init_states[i];
+    is.assign(size_t(counts[i]) * 32, 128);
+    for (size_t j = 0; j < is.size(); j++) {
+      const int pred = j >= 32 ? is[j - 32] : 128;
+      is[j] = uint8_t((pred + r.symbol(st2[j & 31], true)) & 0xFF);
+    }
+  }
 }
 
 // The context states a slice starts from (ff_ffv1_clear_slice_state): all
@@ -1457,6 +1663,10 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
   tmp.dflt = default_tables();
   tmp.frame = p.ac == 2 ? custom_tables(tmp.dflt) : tmp.dflt;
   quant_set(tmp.qt, p.context_model, p.bits_per_raw_sample);
+  // a 2-pass stream carries its own (sorted) custom table and initial
+  // states: take them from the extradata, the rest must be what p produces
+  if (p.version >= 2 && extradata && extradata_size > 4 && p.ac)
+    read_extra_states(extradata, extradata_size - 4, &tmp);
   build_extradata(&tmp);
   if (extradata_size != int(tmp.extradata.size()) ||
       (extradata_size && (!extradata || std::memcmp(extradata, tmp.extradata.data(), tmp.extradata.size()) != 0)))
@@ -1531,6 +1741,11 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
     std::memcpy(tabs + 512, tmp.dflt.to0, 256);
     std::memcpy(tabs + 768, tmp.dflt.to1, 256);
     HIP_TRY(hipMemcpy(d->d_tabs, tabs, 1024, hipMemcpyHostToDevice));
+    const std::vector<uint8_t>& is = tmp.init_states[p.context_model];
+    if (std::any_of(is.begin(), is.end(), [](uint8_t v) { return v != 128; })) {
+      HIP_TRY(hipMalloc(&d->d_init, is.size()));
+      HIP_TRY(hipMemcpy(d->d_init, is.data(), is.size(), hipMemcpyHostToDevice));
+    }
     return dec_reset_states(d);
   };
   int rc = init();
@@ -1684,6 +1899,7 @@ int ffv1hip_decode(ffv1hip_dec* d, const uint8_t* packets, const int64_t* sizes,
     a.last = d->have_last ? d->d_last : nullptr;
     a.sticky = d->d_sticky;
     a.nframes = n_frames;
+    a.init = d->d_init;
     if (launch_decode(a, int(segs.size()), d->stream) < 0)
       return set_err(-5, "ffv1_decode_slices launch failed: %s", hipGetErrorString(hipGetLastError()));
     int status = 0;

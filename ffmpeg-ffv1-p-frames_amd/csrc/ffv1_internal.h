@@ -5,6 +5,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+#include <vector>
+
 namespace ffv1hip {
 
 // One "header op" coded before the planes of a slice: the key bit
@@ -143,7 +146,21 @@ struct CodeArgs {
   DecisionStream ds;
   uint64_t* dbg;              // optional [wave][4] cycle counters (FFV1HIP_CODEDBG)
   uint8_t* opsets;            // decision-stream mode: [stream][nopsets * 32] header op states
+  const uint8_t* init;        // chained range coder: 2-pass initial states [contexts][32], or null
 };
+
+// Pass-1 statistics (ffv1enc.c:190-199): rc_stat[state][bit] from the
+// decision stream, rc_stat2[context][slot][bit] from the walk records.
+struct StatsArgs {
+  const uint4* rec;           // [batch frame][frame_samples]
+  int64_t frame_samples;
+  const SliceGeom* geom;
+  int nslices, nframes;
+  DecisionStream ds;
+  unsigned long long* rc_stat;   // [256][2]
+  unsigned long long* rc_stat2;  // [contexts][32][2]
+};
+int launch_stats(const StatsArgs& a, bool states, void* stream);
 
 // Kernel 2a: the context-state walk.  The adaptive states a slice's range
 // coder sees depend only on the decisions of the earlier symbols of its GOP,
@@ -167,6 +184,7 @@ struct WalkArgs {
   uint8_t* scratch;           // >= 2 KiB: where idle chains write their stage
   uint64_t* dbg;              // optional [block][4] cycle counters (FFV1HIP_WALKDBG)
   int force_multi;            // measurement hook: every chunk on the checked (multi) step
+  const uint8_t* init;        // 2-pass initial states [contexts][32] at keyframes, or null (all 128)
 };
 
 // Kernel 2b: the decision bits, from the chunks' packed words to their place
@@ -224,8 +242,15 @@ struct DecodeArgs {
   const uint8_t* last;         // the picture before frame 0 (previous call), or null
   uint8_t* sticky;             // [slice] slice_damaged carried across calls
   int nframes;
+  const uint8_t* init;         // range coder: initial states [contexts][32] from the extradata, or null
 };
 int launch_decode(const DecodeArgs& a, int nsegs, void* stream);
+
+// 2-pass host arithmetic (ffv1_twopass.cpp): pass-2 states from stats_in
+// (stt: in, the custom table; out, sorted when custom) and the pass-1 text.
+int pass2_states(const char* stats, bool custom, uint8_t stt[256], const uint8_t default_one[256],
+                 std::vector<uint8_t> init[2], std::string* err);
+std::string pass1_text(const uint64_t* rc_stat, const uint64_t* rc_stat2, int contexts, int model, int gob_count);
 int launch_conceal(const DecodeArgs& a, void* stream);
 int64_t decode_lds_bytes(const DecodeArgs& a, bool global_states);
 

@@ -734,6 +734,10 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
     if (a.j == 0 && seg.load_states) {
       const uint4* src = reinterpret_cast<const uint4*>(a.persist_in + (int64_t)slice * a.state_bytes);
       for (int64_t i = 0; i < a.state_bytes / 16; i++) reinterpret_cast<uint4*>(table)[i] = src[i];
+    } else if (key && a.init) {  // ff_ffv1_clear_slice_state with 2-pass initial states
+      const uint4* src = reinterpret_cast<const uint4*>(a.init);
+      const int64_t half = a.state_bytes / 32;  // uint4s of one plane context's table
+      for (int64_t i = 0; i < a.state_bytes / 16; i++) reinterpret_cast<uint4*>(table)[i] = src[i % half];
     } else if (key) {
       const uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
       for (int64_t i = 0; i < a.state_bytes / 16; i++) reinterpret_cast<uint4*>(table)[i] = v;
@@ -1296,6 +1300,9 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
     if (seg.load_states && live) {
       const uint4* src = reinterpret_cast<const uint4*>(a.persist_in + (int64_t)sl * a.state_bytes + goff);
       for (int64_t i = k; i < n16; i += 32) t4[i] = src[i];
+    } else if (a.init) {  // the segment starts at a keyframe: 2-pass initial states
+      const uint4* src = reinterpret_cast<const uint4*>(a.init);
+      for (int64_t i = k; i < n16; i += 32) t4[i] = src[i];
     } else {  // the segment starts at a keyframe (ff_ffv1_clear_slice_state)
       const uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
       for (int64_t i = k; i < n16; i += 32) t4[i] = v;
@@ -1810,6 +1817,74 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Pass-1 statistics (ffv1enc.c:190-199, summed over slices at :1241-1258).
+// rc_stat[state][bit]: one block per (frame, slice) stream histograms the
+// recorded state byte and bit of every decision in LDS.  rc_stat2[context]
+// [slot][bit]: the decisions of a symbol and their slots follow from its
+// residual alone (put_symbol_inline's binarisation), so one thread per
+// sample counts them from the walk record; the busiest contexts (smooth
+// content lands in the low ones) count in LDS first.
+constexpr int kStatsThreads = 256;
+constexpr int kStatsLdsCtx = 32;
+
+__global__ __launch_bounds__(kStatsThreads) void ffv1_stats_states(StatsArgs a) {
+  __shared__ uint32_t h[512];
+  for (int i = threadIdx.x; i < 512; i += kStatsThreads) h[i] = 0;
+  __syncthreads();
+  const int64_t st = (int64_t)blockIdx.y * a.nslices + blockIdx.x;
+  const int* dc = a.ds.dcount + st * 3;
+  const int64_t base = a.ds.dbase[st];
+  for (int part = 0; part < 2; part++) {
+    const int64_t n = part ? (int64_t)dc[1] + dc[2] : dc[0];
+    const int64_t pb = base + (part ? chroma_start(dc[0]) : 0);
+    for (int64_t d = threadIdx.x; d < n; d += kStatsThreads) {
+      const int64_t i = pb + d;
+      const int bit = (a.ds.bits[i >> 5] >> (i & 31)) & 1;
+      atomicAdd(&h[2 * a.ds.pre[i] + bit], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += kStatsThreads)
+    if (h[i]) atomicAdd(&a.rc_stat[i], (unsigned long long)h[i]);
+}
+
+__global__ __launch_bounds__(kStatsThreads) void ffv1_stats_slots(StatsArgs a) {
+  __shared__ uint32_t h[kStatsLdsCtx * 64];
+  for (int i = threadIdx.x; i < kStatsLdsCtx * 64; i += kStatsThreads) h[i] = 0;
+  __syncthreads();
+  const int slice = blockIdx.x, f = blockIdx.y, p = blockIdx.z;
+  const SliceGeom& g = a.geom[slice];
+  const int64_t n = (int64_t)g.pw[p] * g.ph[p];
+  const uint4* r = a.rec + (int64_t)f * a.frame_samples + g.sym_off + g.plane_sym_off[p];
+  for (int64_t i = threadIdx.x; i < n; i += kStatsThreads) {
+    const uint4 v = r[i];
+    const int ctx = (int)(v.x & 0xFFFFu) >> 5;
+    const int diff = (int16_t)(v.x >> 16);
+    const bool lds = ctx < kStatsLdsCtx;
+    uint32_t* hl = h + ctx * 64;
+    unsigned long long* hg = a.rc_stat2 + (int64_t)ctx * 64;
+    auto count = [&](int slot, int bit) {
+      if (lds) atomicAdd(&hl[2 * slot + bit], 1u);
+      else atomicAdd(&hg[2 * slot + bit], 1ull);
+    };
+    if (!diff) {
+      count(0, 1);
+      continue;
+    }
+    const unsigned mag = diff < 0 ? 0u - (unsigned)diff : (unsigned)diff;
+    const int e = 31 - __builtin_clz(mag);
+    count(0, 0);
+    for (int k = 0; k < e; k++) count(1 + min(k, 9), 1);
+    count(1 + min(e, 9), 0);
+    for (int k = e - 1; k >= 0; k--) count(22 + min(k, 9), (mag >> k) & 1);
+    count(11 + min(e, 10), diff < 0);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kStatsLdsCtx * 64; i += kStatsThreads)
+    if (h[i]) atomicAdd(&a.rc_stat2[i], (unsigned long long)h[i]);
+}
+
+// ---------------------------------------------------------------------------
 // Packet assembly + slice CRC.
 constexpr uint32_t kCrcPoly = 0x04C11DB7u;
 
@@ -1965,6 +2040,15 @@ int launch_bits(const BitsArgs& a, void* stream) {
 int launch_layout(const int* dcount, int nstreams, int64_t* dbase, int64_t* total, void* stream) {
   hipLaunchKernelGGL(ffv1_layout, dim3(1), dim3(kLayoutThreads), 0, reinterpret_cast<hipStream_t>(stream), dcount,
                      nstreams, dbase, total);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_stats(const StatsArgs& a, bool states, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (states)
+    hipLaunchKernelGGL(ffv1_stats_states, dim3(a.nslices, a.nframes), dim3(kStatsThreads), 0, st, a);
+  else
+    hipLaunchKernelGGL(ffv1_stats_slots, dim3(a.nslices, a.nframes, 3), dim3(kStatsThreads), 0, st, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -27,7 +27,7 @@ class Options(ctypes.Structure):
                 ("slices", ctypes.c_int), ("level", ctypes.c_int), ("coder", ctypes.c_int),
                 ("context", ctypes.c_int), ("gop_size", ctypes.c_int),
                 ("bits_per_raw_sample", ctypes.c_int), ("slicecrc", ctypes.c_int),
-                ("allow_large_grid", ctypes.c_int)]
+                ("allow_large_grid", ctypes.c_int), ("pass_", ctypes.c_int)]
 
 
 class Params(ctypes.Structure):
@@ -64,6 +64,7 @@ EXPORTED_SYMBOLS = (
     "ffv1hip_last_kernel_stats", "ffv1hip_synchronize",
     "ffv1hip_dec_create", "ffv1hip_dec_destroy", "ffv1hip_decode", "ffv1hip_dec_reset",
     "ffv1hip_set_picture_number", "ffv1hip_encode2", "ffv1hip_dec_damaged_slices",
+    "ffv1hip_set_pass", "ffv1hip_stats_out",
 )
 
 
@@ -106,6 +107,10 @@ def load_library():
     L.ffv1hip_encode2.argtypes = [vp, P(vp), P(ctypes.c_int), i64, u8p, i64, P(i64), P(i64),
                                   P(ctypes.c_int), P(ctypes.c_int)]
     L.ffv1hip_encode2.restype = ctypes.c_int
+    L.ffv1hip_set_pass.argtypes = [vp, ctypes.c_int, ctypes.c_char_p]
+    L.ffv1hip_set_pass.restype = ctypes.c_int
+    L.ffv1hip_stats_out.argtypes = [vp, ctypes.c_char_p, i64]
+    L.ffv1hip_stats_out.restype = i64
     L.ffv1hip_encode_device.argtypes = [vp, vp, i64, P(i64), P(ctypes.c_int), ctypes.c_int, vp]
     L.ffv1hip_encode_device.restype = ctypes.c_int
     L.ffv1hip_fetch.argtypes = [vp, u8p, i64, P(i64), P(ctypes.c_int)]
@@ -158,16 +163,31 @@ class FFV1Error(RuntimeError):
 def configure(width: int, height: int, pix_fmt: str, slices: int = 0, level: int = -1,
               coder: int = -1, context: int = 0, gop_size: int = 12,
               bits_per_raw_sample: int = 0, slicecrc: int = -1,
-              allow_large_grid: bool = False) -> Params:
-    """encode_init's option -> bitstream-parameter derivation (ffv1enc.c:669-1029)."""
+              allow_large_grid: bool = False, pass_: int = 0) -> Params:
+    """encode_init's option -> bitstream-parameter derivation (ffv1enc.c:669-1029);
+    pass_ 1 / 2 are AV_CODEC_FLAG_PASS1 / PASS2."""
     L = load_library()
     o = Options(width, height, pix_fmt.encode(), slices, level, coder, context, gop_size,
-                bits_per_raw_sample, slicecrc, int(allow_large_grid))
+                bits_per_raw_sample, slicecrc, int(allow_large_grid), pass_)
     p = Params()
     rc = L.ffv1hip_configure(ctypes.byref(p), ctypes.byref(o))
     if rc < 0:
         raise FFV1Error(rc, "ffv1hip_configure")
     return p
+
+
+def check_planes(params: Params, planes: Sequence[np.ndarray]):
+    """The library copies rows x row-bytes of every plane from host memory:
+    a plane smaller than the parameters say would be read past its end."""
+    shapes = params.plane_shapes()
+    if len(planes) < len(shapes):
+        raise ValueError(f"{len(planes)} planes, {params.width}x{params.height} needs {len(shapes)}")
+    itemsize = 1 if params.sample_bytes in (1, 4) else 2
+    for k, (rows, cols) in enumerate(shapes):
+        a = np.asarray(planes[k])
+        if a.ndim != 2 or a.shape[0] < rows or a.shape[1] * a.itemsize < cols * itemsize:
+            raise ValueError(f"plane {k}: shape {a.shape} ({a.dtype}), need {rows} rows of {cols} "
+                             f"{'bytes' if itemsize == 1 else 'u16 samples'}")
 
 
 def _u8p(a):
@@ -193,6 +213,25 @@ class HipEncoder:
 
     __del__ = close
 
+    def set_pass(self, pass_: int, stats_in: Optional[str] = None):
+        """2-pass mode, before the first frame (ffv1hip_set_pass)."""
+        rc = load_library().ffv1hip_set_pass(self._h, pass_,
+                                             stats_in.encode() if stats_in is not None else None)
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_set_pass")
+
+    def stats_out(self) -> str:
+        """Pass 1: the statistics text (avctx->stats_out at the end of the stream)."""
+        L = load_library()
+        n = L.ffv1hip_stats_out(self._h, None, 0)
+        if n < 0:
+            raise FFV1Error(n, "ffv1hip_stats_out")
+        buf = ctypes.create_string_buffer(n + 1)
+        n = L.ffv1hip_stats_out(self._h, buf, n + 1)
+        if n < 0:
+            raise FFV1Error(n, "ffv1hip_stats_out")
+        return buf.value.decode()
+
     def extradata(self) -> bytes:
         L = load_library()
         n = L.ffv1hip_extradata(self._h, None, 0)
@@ -214,6 +253,8 @@ class HipEncoder:
         L = load_library()
         n = len(frames)
         np_planes = len(self.params.plane_shapes())
+        for fr in frames:
+            check_planes(self.params, fr)
         ptrs = (ctypes.c_void_p * (3 * n))()
         strides = (ctypes.c_int * (3 * n))()
         keep = []
@@ -358,7 +399,14 @@ class AVCodecContext:
     slicecrc: int = -1
     extradata: bytes = b""
     allow_large_grid: bool = False
+    flags: int = 0                   # AV_CODEC_FLAG_PASS1 / PASS2
+    stats_in: Optional[str] = None   # pass 2: what pass 1 left in stats_out
+    stats_out: str = ""              # pass 1: written at the flush (ffv1enc.c:1236-1277)
     priv: dict = field(default_factory=dict)
+
+
+AV_CODEC_FLAG_PASS1 = 1 << 9   # avcodec.h
+AV_CODEC_FLAG_PASS2 = 1 << 10
 
 
 class FFV1Encoder:
@@ -393,16 +441,21 @@ class FFV1Encoder:
         self.avctx: Optional[AVCodecContext] = None
         self.params: Optional[Params] = None
         self._enc: Optional[HipEncoder] = None
+        self._pass = 0
         self._frames_in = 0
         self._out = None
 
     def init(self, avctx: AVCodecContext) -> int:
         self.avctx = avctx
+        pass_ = 1 if avctx.flags & AV_CODEC_FLAG_PASS1 else 2 if avctx.flags & AV_CODEC_FLAG_PASS2 else 0
         self.params = configure(avctx.width, avctx.height, avctx.pix_fmt, avctx.slices,
                                 avctx.level, avctx.coder, avctx.context, avctx.gop_size,
                                 avctx.bits_per_raw_sample, avctx.slicecrc,
-                                avctx.allow_large_grid)
+                                avctx.allow_large_grid, pass_)
         self._enc = HipEncoder(self.params, self.device, self.batch)
+        self._pass = pass_
+        if pass_ == 1 or (pass_ == 2 and avctx.stats_in is not None):
+            self._enc.set_pass(pass_, avctx.stats_in)
         avctx.extradata = self._enc.extradata()
         self._out = np.empty(self._enc.max_packet_size(), np.uint8)
         return 0
@@ -415,6 +468,7 @@ class FFV1Encoder:
         strides = (ctypes.c_int * 3)()
         keep = []
         if frame is not None:
+            check_planes(self.params, frame)
             np_planes = len(self.params.plane_shapes())
             for k in range(3):
                 a = np.ascontiguousarray(frame[min(k, np_planes - 1)])
@@ -433,6 +487,8 @@ class FFV1Encoder:
         if rc < 0:
             raise FFV1Error(rc, "ffv1hip_encode2")
         if not got.value:
+            if frame is None and self._pass == 1:  # the flush: stats_out (ffv1enc.c:1236-1277)
+                self.avctx.stats_out = self._enc.stats_out()
             return None
         return AVPacket(self._out[:size.value].tobytes(), pts_out.value, pts_out.value, bool(key.value))
 

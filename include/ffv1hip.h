@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define FFV1HIP_ABI_VERSION 2
+#define FFV1HIP_ABI_VERSION 3
 #define FFV1HIP_AVERROR_INVALIDDATA (-1094995529)
 
 /* AVCodecContext fields + codec private options that encode_init reads
@@ -42,6 +42,8 @@ typedef struct ffv1hip_options {
     int allow_large_grid;     /* 1: accept up to 256 slices (16x16), which the
                                  reference decoder reads but its encoder
                                  refuses (ffv1enc.c:988-1000); used for 8K  */
+    int pass;                 /* 1 / 2: AV_CODEC_FLAG_PASS1 / PASS2 (version
+                                 >= 2, ffv1enc.c:680-682); see ffv1hip_set_pass */
 } ffv1hip_options;
 
 /* Effective bitstream parameters (what encode_init derives). */
@@ -74,6 +76,21 @@ int ffv1hip_configure(ffv1hip_params *out, const ffv1hip_options *opt);
  * to max_batch_frames frames per call on HIP device `device`. */
 ffv1hip_ctx *ffv1hip_create(const ffv1hip_params *params, int device,
                             int max_batch_frames, int *err);
+
+/* 2-pass encoding (ffv1enc.c:898-986, 1236-1277), chosen after
+ * ffv1hip_create and before the first frame, for parameters configured with
+ * options.pass.  pass 1: the encoder counts every plane decision by state
+ * value and by (context, slot); ffv1hip_stats_out then returns the text
+ * encode_frame writes into avctx->stats_out at the end of the stream
+ * (needs the frame-parallel range coder, or Golomb-Rice whose counts are
+ * zero).  pass 2: stats_in is that text; the custom transition table is
+ * re-sorted and every context's initial state derived from it, keyframes
+ * start from those states and the extradata carries them.  Returns 0 or a
+ * negative error (AVERROR_INVALIDDATA for malformed statistics). */
+int ffv1hip_set_pass(ffv1hip_ctx *ctx, int pass, const char *stats_in);
+/* Pass 1: the statistics so far as text (NUL-terminated in buf); returns
+ * its length, or the length needed when buf is NULL. */
+int64_t ffv1hip_stats_out(ffv1hip_ctx *ctx, char *buf, int64_t cap);
 
 /* AVCodec.close (ffv1enc.c:1375 encode_close). */
 void ffv1hip_destroy(ffv1hip_ctx *ctx);

@@ -11,6 +11,8 @@
  */
 #include "ffv1_oracle.h"
 
+#include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -553,6 +555,15 @@ int ffv1o_configure(ffv1o_config *cfg, int width, int height,
                     int context, int gop_size, int bits_per_raw_sample,
                     int slicecrc)
 {
+    return ffv1o_configure2(cfg, width, height, pix_fmt, slices, level, coder, context, gop_size,
+                            bits_per_raw_sample, slicecrc, 0);
+}
+
+int ffv1o_configure2(ffv1o_config *cfg, int width, int height,
+                     const char *pix_fmt, int slices, int level, int coder,
+                     int context, int gop_size, int bits_per_raw_sample,
+                     int slicecrc, int pass)
+{
     const pixfmt_info *pf = NULL;
     for (size_t i = 0; i < sizeof(PIXFMTS) / sizeof(PIXFMTS[0]); i++)
         if (!strcmp(PIXFMTS[i].name, pix_fmt))
@@ -569,7 +580,7 @@ int ffv1o_configure(ffv1o_config *cfg, int width, int height,
 
     /* version selection, ffv1enc.c:678-697 */
     int version = 0;
-    if (slices > 1)
+    if (pass || slices > 1) /* AV_CODEC_FLAG_PASS1 | PASS2 (:680-682) */
         version = 2;
     if (slices == 0 && level < 0 && width * height > 720 * 576)
         version = 2;
@@ -695,6 +706,12 @@ struct ffv1o_enc {
     slice_ctx *sl;
     int64_t picture_number;
     int16_t *scratch;   /* one slice plane of samples */
+    /* 2-pass (ffv1enc.c:898-986, 1236-1277) */
+    int pass1;
+    uint64_t rc_stat[256][2];    /* per state value, decisions 0 / 1 */
+    uint64_t (*rc_stat2)[32][2]; /* per context and slot, of the quant set in use */
+    int gob_count;
+    uint8_t *init_states[2];     /* [context][32] per quant set, NULL = all 128 */
 };
 
 static void slice_rects(const ffv1o_config *cfg, int i, int *x0, int *y0,
@@ -755,6 +772,239 @@ ffv1o_enc *ffv1o_enc_new(const ffv1o_config *cfg)
     return e;
 }
 
+/* find_best_state (ffv1enc.c:139-183): for a probability i/256 of a one and
+ * k decisions seen, the starting state whose adaptation through one_state
+ * codes the first k decisions in the fewest bits. */
+static void find_best_state(uint8_t best[256][256], const uint8_t one_state[256])
+{
+    double l2[256];
+    for (int i = 1; i < 256; i++)
+        l2[i] = log2(i / 256.0);
+    for (int i = 0; i < 256; i++) {
+        double best_len[256];
+        double p = i / 256.0;
+        for (int j = 0; j < 256; j++)
+            best_len[j] = 1 << 30;
+        for (int j = i - 10 > 1 ? i - 10 : 1; j < (i + 11 < 256 ? i + 11 : 256); j++) {
+            double occ[256] = {0};
+            double len = 0;
+            occ[j] = 1.0;
+            if (!one_state[j])
+                continue;
+            for (int k = 0; k < 256; k++) {
+                double nocc[256] = {0};
+                for (int m = 1; m < 256; m++)
+                    if (occ[m])
+                        len -= occ[m] * (p * l2[m] + (1 - p) * l2[256 - m]);
+                if (len < best_len[k]) {
+                    best_len[k] = len;
+                    best[i][k] = (uint8_t)j;
+                }
+                for (int m = 1; m < 256; m++)
+                    if (occ[m]) {
+                        nocc[one_state[m]] += occ[m] * p;
+                        nocc[256 - one_state[256 - m]] += occ[m] * (1 - p);
+                    }
+                memcpy(occ, nocc, sizeof(occ));
+            }
+        }
+    }
+}
+
+/* FFSWAP(int, ...) on the 64-bit counters (ffv1enc.c:642-647): the value
+ * moved through the int comes back truncated and sign-extended. */
+static void swap_int(uint64_t *a, uint64_t *b)
+{
+    int t = (int)(uint32_t)*a;
+    *a = *b;
+    *b = (uint64_t)(int64_t)t;
+}
+
+/* sort_stt (ffv1enc.c:621-667): swap neighbouring states of the custom
+ * transition table while that lowers the pass-1 cost. */
+static void sort_stt(uint64_t rc_stat[256][2], uint8_t stt[256])
+{
+#define COST(o, n) ((double)rc_stat[o][0] * -log2((256 - (n)) / 256.0) + (double)rc_stat[o][1] * -log2((n) / 256.0))
+#define COST2(o, n) (COST(o, n) + COST(256 - (o), 256 - (n)))
+    int changed;
+    do {
+        changed = 0;
+        for (int i = 12; i < 244; i++) {
+            for (int i2 = i + 1; i2 < 245 && i2 < i + 4; i2++) {
+                double size0 = COST2(i, i) + COST2(i2, i2);
+                double sizeX = COST2(i, i2) + COST2(i2, i);
+                if (size0 - sizeX > size0 * (1e-14) && i != 128 && i2 != 128) {
+                    uint8_t t = stt[i];
+                    stt[i] = stt[i2];
+                    stt[i2] = t;
+                    swap_int(&rc_stat[i][0], &rc_stat[i2][0]);
+                    swap_int(&rc_stat[i][1], &rc_stat[i2][1]);
+                    if (i != 256 - i2) {
+                        t = stt[256 - i];
+                        stt[256 - i] = stt[256 - i2];
+                        stt[256 - i2] = t;
+                        swap_int(&rc_stat[256 - i][0], &rc_stat[256 - i2][0]);
+                        swap_int(&rc_stat[256 - i][1], &rc_stat[256 - i2][1]);
+                    }
+                    for (int j = 1; j < 256; j++) {
+                        if (stt[j] == i)
+                            stt[j] = (uint8_t)i2;
+                        else if (stt[j] == i2)
+                            stt[j] = (uint8_t)i;
+                        if (i != 256 - i2) {
+                            if (stt[256 - j] == 256 - i)
+                                stt[256 - j] = (uint8_t)(256 - i2);
+                            else if (stt[256 - j] == 256 - i2)
+                                stt[256 - j] = (uint8_t)(256 - i);
+                        }
+                    }
+                    changed = 1;
+                }
+            }
+        }
+    } while (changed);
+#undef COST
+#undef COST2
+}
+
+static int clip_int(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
+
+/* Pass 2 (ffv1enc.c:906-986): parse stats_in (the last complete block
+ * wins), sort the custom table, and derive every context's initial states
+ * from the pass-1 decision counts. */
+static int enc_pass2(ffv1o_enc *e, const char *stats)
+{
+    uint64_t rc_stat[256][2];
+    uint64_t(*st2[2])[32][2];
+    int counts[2] = {context_count_of(0), context_count_of(1)};
+    int gob_count = 0, rc = 0;
+    st2[0] = calloc((size_t)counts[0], sizeof(*st2[0]));
+    st2[1] = calloc((size_t)counts[1], sizeof(*st2[1]));
+    uint8_t(*best)[256] = malloc(256 * 256);
+    const char *p = stats;
+    char *next;
+    for (;;) {
+        for (int j = 0; j < 256; j++)
+            for (int i = 0; i < 2; i++) {
+                rc_stat[j][i] = (uint64_t)strtol(p, &next, 0);
+                if (next == p) {
+                    rc = AVERR_INVALIDDATA;
+                    goto done;
+                }
+                p = next;
+            }
+        for (int i = 0; i < 2; i++)
+            for (int j = 0; j < counts[i]; j++)
+                for (int k = 0; k < 32; k++)
+                    for (int m = 0; m < 2; m++) {
+                        st2[i][j][k][m] = (uint64_t)strtol(p, &next, 0);
+                        if (next == p) {
+                            rc = AVERR_INVALIDDATA;
+                            goto done;
+                        }
+                        p = next;
+                    }
+        gob_count = (int)strtol(p, &next, 0);
+        if (next == p || gob_count <= 0) {
+            rc = AVERR_INVALIDDATA;
+            goto done;
+        }
+        p = next;
+        while (*p == '\n' || *p == ' ')
+            p++;
+        if (p[0] == 0)
+            break;
+    }
+    if (e->cfg.ac == 2) {
+        sort_stt(rc_stat, e->stt);
+        rc_custom_tables(&e->frame_tab, &e->dflt, e->stt);
+    }
+    find_best_state(best, e->cfg.ac == 2 ? e->stt : e->dflt.to1);
+    for (int i = 0; i < 2; i++) {
+        uint8_t(*is)[32] = malloc((size_t)counts[i] * 32);
+        for (int k = 0; k < 32; k++) {
+            double a = 0, b = 0;
+            int jp = 0;
+            for (int j = 0; j < counts[i]; j++) {
+                double pr = 128;
+                if ((st2[i][j][k][0] + st2[i][j][k][1] > 200 && j) || a + b > 200) {
+                    if (a + b)
+                        pr = 256.0 * b / (a + b);
+                    is[jp][k] = best[clip_int((int)round(pr), 1, 255)][clip_int((int)((a + b) / gob_count), 0, 255)];
+                    for (jp++; jp < j; jp++)
+                        is[jp][k] = is[jp - 1][k];
+                    a = b = 0;
+                }
+                a += (double)st2[i][j][k][0];
+                b += (double)st2[i][j][k][1];
+                if (a + b)
+                    pr = 256.0 * b / (a + b);
+                is[j][k] = best[clip_int((int)round(pr), 1, 255)][clip_int((int)((a + b) / gob_count), 0, 255)];
+            }
+        }
+        e->init_states[i] = (uint8_t *)is;
+    }
+done:
+    free(best);
+    free(st2[0]);
+    free(st2[1]);
+    return rc;
+}
+
+ffv1o_enc *ffv1o_enc_new2(const ffv1o_config *cfg, int pass, const char *stats_in)
+{
+    if (pass && cfg->version < 2)
+        return NULL; /* av_assert0(s->version >= 2) */
+    ffv1o_enc *e = ffv1o_enc_new(cfg);
+    if (!e)
+        return NULL;
+    if (pass == 1) {
+        e->pass1 = 1;
+        e->rc_stat2 = calloc((size_t)e->contexts, sizeof(*e->rc_stat2));
+    } else if (pass == 2 && stats_in) {
+        if (enc_pass2(e, stats_in) < 0) {
+            ffv1o_enc_free(e);
+            return NULL;
+        }
+    }
+    return e;
+}
+
+/* The pass-1 statistics as encode_frame writes them into stats_out at the
+ * end of the stream (ffv1enc.c:1236-1277): 256 state pairs, a newline, the
+ * (context, slot) pairs of both quant sets (the unused one all zero), the
+ * keyframe count.  Returns the text length (without the NUL). */
+int64_t ffv1o_enc_stats_out(const ffv1o_enc *e, char *buf, int64_t cap)
+{
+    if (!e->pass1)
+        return AVERR_EINVAL;
+    int64_t n = 0;
+#define EMIT(...)                                                              \
+    do {                                                                       \
+        char tmp[64];                                                          \
+        int l = snprintf(tmp, sizeof(tmp), __VA_ARGS__);                       \
+        if (buf && n + l < cap)                                                \
+            memcpy(buf + n, tmp, (size_t)l + 1);                               \
+        n += l;                                                                \
+    } while (0)
+    for (int j = 0; j < 256; j++)
+        EMIT("%llu %llu ", (unsigned long long)e->rc_stat[j][0], (unsigned long long)e->rc_stat[j][1]);
+    EMIT("\n");
+    for (int i = 0; i < 2; i++)
+        for (int j = 0; j < context_count_of(i); j++)
+            for (int m = 0; m < 32; m++) {
+                uint64_t a = 0, b = 0;
+                if (i == e->cfg.context_model) {
+                    a = e->rc_stat2[j][m][0];
+                    b = e->rc_stat2[j][m][1];
+                }
+                EMIT("%llu %llu ", (unsigned long long)a, (unsigned long long)b);
+            }
+    EMIT("%d\n", e->gob_count);
+#undef EMIT
+    return n;
+}
+
 void ffv1o_enc_free(ffv1o_enc *e)
 {
     if (!e)
@@ -768,6 +1018,9 @@ void ffv1o_enc_free(ffv1o_enc *e)
     }
     free(e->sl);
     free(e->scratch);
+    free(e->rc_stat2);
+    free(e->init_states[0]);
+    free(e->init_states[1]);
     free(e);
 }
 
@@ -821,8 +1074,23 @@ int ffv1o_enc_extradata(ffv1o_enc *e, uint8_t *buf, int cap)
         build_quant_set(qt, set, cfg->bits_per_raw_sample);
         put_quant_tables(&c, qt);
     }
-    for (int set = 0; set < 2; set++)
-        rc_put(&c, &st[0], 0); /* initial states are all 128 */
+    uint8_t st2[32][32];
+    memset(st2, 128, sizeof(st2));
+    for (int set = 0; set < 2; set++) { /* ffv1enc.c:591-607 */
+        const uint8_t *is = e->init_states[set];
+        int n = context_count_of(set) * 32, j = 0;
+        while (is && j < n && is[j] == 128)
+            j++;
+        if (!is || j == n) {
+            rc_put(&c, &st[0], 0);
+            continue;
+        }
+        rc_put(&c, &st[0], 1);
+        for (int i = 0; i < n; i++) {
+            int pred = i >= 32 ? is[i - 32] : 128;
+            rc_put_symbol(&c, st2[i & 31], (int8_t)(is[i] - pred), 1);
+        }
+    }
     if (cfg->version > 2) {
         rc_put_symbol(&c, st, cfg->ec, 0);
         rc_put_symbol(&c, st, cfg->gop_size < 2, 0);
@@ -940,6 +1208,38 @@ static void sample_symbol(const int16_t qt[5][256], int model1, int bits,
     *diff_out = fold_residual(diff, bits);
 }
 
+/* put_symbol_inline's statistics (ffv1enc.c:190-199): every decision of a
+ * plane symbol counts into rc_stat[state before][bit] and rc_stat2[slot][bit],
+ * counted here before the symbol is coded (the states then adapt the same
+ * way in rc_put_symbol). */
+static void count_symbol(ffv1o_enc *e, const uint8_t st[32], uint64_t stat2[32][2], int v)
+{
+    uint8_t s[32];
+    memcpy(s, st, 32);
+    const rc_tables *t = &e->frame_tab;
+#define COUNT(slot, bit)                                  \
+    do {                                                  \
+        int b_ = (bit);                                   \
+        e->rc_stat[s[slot]][b_]++;                        \
+        stat2[slot][b_]++;                                \
+        s[slot] = b_ ? t->to1[s[slot]] : t->to0[s[slot]]; \
+    } while (0)
+    if (v == 0) {
+        COUNT(0, 1);
+        return;
+    }
+    unsigned a = v < 0 ? -(unsigned)v : (unsigned)v;
+    int ex = ilog2u(a);
+    COUNT(0, 0);
+    for (int i = 0; i < ex; i++)
+        COUNT(1 + (i < 9 ? i : 9), 1);
+    COUNT(1 + (ex < 9 ? ex : 9), 0);
+    for (int i = ex - 1; i >= 0; i--)
+        COUNT(22 + (i < 9 ? i : 9), (a >> i) & 1);
+    COUNT(11 + (ex < 10 ? ex : 10), v < 0);
+#undef COUNT
+}
+
 /* encode_line for the range coder: row y of slice plane P (w wide) */
 static void code_row_rac(ffv1o_enc *e, rc_enc *c, plane_state *ps,
                          const int16_t *P, int w, int y)
@@ -950,6 +1250,8 @@ static void code_row_rac(ffv1o_enc *e, rc_enc *c, plane_state *ps,
         int ctx, diff;
         get_taps(P, w, x, y, &t);
         sample_symbol(e->qt, model1, e->coded_bits, &t, &ctx, &diff);
+        if (e->pass1)
+            count_symbol(e, ps->rac + (int64_t)ctx * 32, e->rc_stat2[ctx], diff);
         rc_put_symbol(c, ps->rac + (int64_t)ctx * 32, diff, 1);
     }
 }
@@ -1074,8 +1376,12 @@ static void code_rgb_slice(ffv1o_enc *e, slice_ctx *s, const uint8_t *const plan
 
 static void reset_slice_states(ffv1o_enc *e, slice_ctx *s)
 {
+    const uint8_t *is = e->init_states[e->cfg.context_model];
     for (int p = 0; p < 2; p++) {
-        memset(s->ps[p].rac, 128, (size_t)e->contexts * 32);
+        if (is) /* ff_ffv1_clear_slice_state (ffv1.c:185-189) */
+            memcpy(s->ps[p].rac, is, (size_t)e->contexts * 32);
+        else
+            memset(s->ps[p].rac, 128, (size_t)e->contexts * 32);
         for (int j = 0; j < e->contexts; j++)
             vlc_reset(&s->ps[p].vlc[j]);
     }
@@ -1120,6 +1426,8 @@ int64_t ffv1o_enc_frame(ffv1o_enc *e, const uint8_t *const planes[3],
 {
     const ffv1o_config *cfg = &e->cfg;
     int key = cfg->gop_size == 0 || e->picture_number % cfg->gop_size == 0;
+    if (key)
+        e->gob_count++; /* ffv1enc.c:1302 */
 
     for (int i = 0; i < e->nslices; i++) {
         slice_ctx *s = &e->sl[i];
@@ -1295,6 +1603,7 @@ struct ffv1o_dec {
     uint8_t *last[3];
     int last_row[3], last_rows[3];
     int have_last;
+    uint8_t *init_states[2]; /* per quant set from the extradata, NULL = all 128 */
 };
 
 /* Rows and row bytes of the output planes (the encoder's input layout). */
@@ -1396,9 +1705,19 @@ ffv1o_dec *ffv1o_dec_new(const ffv1o_config *cfg, const uint8_t *ex, int exn)
             if (d->ctx_count[i] < 0)
                 goto fail;
         }
-        for (int i = 0; i < nq; i++)
-            if (rc_get(&c, &st[0])) /* non-default initial states unsupported */
-                goto fail;
+        uint8_t st2[32][32];
+        memset(st2, 128, sizeof(st2));
+        for (int i = 0; i < nq; i++) { /* read_extra_header, ffv1dec.c:592-601 */
+            if (!rc_get(&c, &st[0]))
+                continue;
+            int n = d->ctx_count[i] * 32;
+            uint8_t *is = malloc((size_t)n);
+            for (int j = 0; j < n; j++) {
+                int pred = j >= 32 ? is[j - 32] : 128;
+                is[j] = (uint8_t)((pred + rc_get_symbol(&c, st2[j & 31], 1)) & 0xFF);
+            }
+            d->init_states[i] = is;
+        }
         if (d->version > 2) {
             d->ec = rc_get_symbol(&c, st, 0);
             if (d->micro_version > 2)
@@ -1426,6 +1745,8 @@ void ffv1o_dec_free(ffv1o_dec *d)
         }
     for (int k = 0; k < 3; k++)
         free(d->last[k]);
+    free(d->init_states[0]);
+    free(d->init_states[1]);
     free(d->sl);
     free(d->scratch);
     free(d);
@@ -1683,7 +2004,10 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
         }
         if (key)
             for (int pp = 0; pp < 2; pp++) {
-                memset(s->ps[pp].rac, 128, (size_t)contexts * 32);
+                if (d->version > 2 && d->init_states[model1])
+                    memcpy(s->ps[pp].rac, d->init_states[model1], (size_t)contexts * 32);
+                else
+                    memset(s->ps[pp].rac, 128, (size_t)contexts * 32);
                 for (int j = 0; j < contexts; j++)
                     vlc_reset(&s->ps[pp].vlc[j]);
             }

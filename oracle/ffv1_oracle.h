@@ -69,9 +69,21 @@ int ffv1o_configure(ffv1o_config *cfg, int width, int height,
                     int context, int gop_size, int bits_per_raw_sample,
                     int slicecrc);
 
+/* As ffv1o_configure, with AVCodecContext.flags' AV_CODEC_FLAG_PASS1 (pass
+ * 1) or PASS2 (pass 2), which select version >= 2 (ffv1enc.c:680-682). */
+int ffv1o_configure2(ffv1o_config *cfg, int width, int height,
+                     const char *pix_fmt, int slices, int level, int coder,
+                     int context, int gop_size, int bits_per_raw_sample,
+                     int slicecrc, int pass);
+
 typedef struct ffv1o_enc ffv1o_enc;
 
 ffv1o_enc *ffv1o_enc_new(const ffv1o_config *cfg);
+/* pass 1: collect the statistics of ffv1o_enc_stats_out; pass 2: the
+ * initial states (and sorted custom table) derived from stats_in, the text
+ * a pass-1 run wrote (ffv1enc.c:898-986). */
+ffv1o_enc *ffv1o_enc_new2(const ffv1o_config *cfg, int pass, const char *stats_in);
+int64_t    ffv1o_enc_stats_out(const ffv1o_enc *e, char *buf, int64_t cap);
 void       ffv1o_enc_free(ffv1o_enc *e);
 /* Writes the v>=2 extradata (incl. CRC) and returns its size (0 for v<2). */
 int        ffv1o_enc_extradata(ffv1o_enc *e, uint8_t *buf, int cap);

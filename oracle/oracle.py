@@ -65,6 +65,13 @@ def lib():
         L.ffv1o_dec_free.argtypes = [ctypes.c_void_p]
         L.ffv1o_dec_frame.argtypes = [ctypes.c_void_p, u8p, ctypes.c_int64, P(u8p), P(ctypes.c_int), P(ctypes.c_int)]
         L.ffv1o_dec_frame.restype = ctypes.c_int
+        L.ffv1o_configure2.argtypes = [P(Config), ctypes.c_int, ctypes.c_int, ctypes.c_char_p] + \
+            [ctypes.c_int] * 8
+        L.ffv1o_configure2.restype = ctypes.c_int
+        L.ffv1o_enc_new2.argtypes = [P(Config), ctypes.c_int, ctypes.c_char_p]
+        L.ffv1o_enc_new2.restype = ctypes.c_void_p
+        L.ffv1o_enc_stats_out.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64]
+        L.ffv1o_enc_stats_out.restype = ctypes.c_int64
         L.ffv1o_crc32.argtypes = [ctypes.c_uint32, u8p, ctypes.c_int64]
         L.ffv1o_crc32.restype = ctypes.c_uint32
         _lib = L
@@ -76,11 +83,13 @@ def _u8p(a: np.ndarray):
 
 
 def configure(width, height, pix_fmt, slices=0, level=-1, coder=-1, context=0,
-              gop_size=12, bits_per_raw_sample=0, slicecrc=-1) -> Config:
-    """encode_init's parameter derivation (ffv1enc.c:669-1029)."""
+              gop_size=12, bits_per_raw_sample=0, slicecrc=-1, pass_=0) -> Config:
+    """encode_init's parameter derivation (ffv1enc.c:669-1029); pass_ 1 / 2
+    are AV_CODEC_FLAG_PASS1 / PASS2."""
     cfg = Config()
-    rc = lib().ffv1o_configure(ctypes.byref(cfg), width, height, pix_fmt.encode(), slices,
-                               level, coder, context, gop_size, bits_per_raw_sample, slicecrc)
+    rc = lib().ffv1o_configure2(ctypes.byref(cfg), width, height, pix_fmt.encode(), slices,
+                                level, coder, context, gop_size, bits_per_raw_sample, slicecrc,
+                                pass_)
     if rc < 0:
         raise ValueError(f"ffv1o_configure rejected {pix_fmt} {width}x{height} slices={slices}: {rc}")
     return cfg
@@ -114,11 +123,21 @@ def _plane_ptrs(planes):
 class Encoder:
     """The oracle encoder: one instance = one stream (keeps P-frame state)."""
 
-    def __init__(self, cfg: Config):
+    def __init__(self, cfg: Config, pass_: int = 0, stats_in: str = None):
         self.cfg = cfg
-        self._h = lib().ffv1o_enc_new(ctypes.byref(cfg))
+        self._h = lib().ffv1o_enc_new2(ctypes.byref(cfg), pass_,
+                                       stats_in.encode() if stats_in is not None else None)
         if not self._h:
             raise ValueError("ffv1o_enc_new failed")
+
+    def stats_out(self) -> str:
+        """Pass 1: the statistics text (avctx->stats_out at the flush)."""
+        n = lib().ffv1o_enc_stats_out(self._h, None, 0)
+        if n < 0:
+            raise RuntimeError(n)
+        buf = ctypes.create_string_buffer(int(n) + 1)
+        lib().ffv1o_enc_stats_out(self._h, buf, n + 1)
+        return buf.value.decode()
 
     def __del__(self):
         if getattr(self, "_h", None):
@@ -126,13 +145,17 @@ class Encoder:
             self._h = None
 
     def extradata(self) -> bytes:
-        buf = np.zeros(1 << 16, np.uint8)
+        buf = np.zeros(10000 + 4 + (7563 + 666) * 32 * 4, np.uint8)  # ffv1enc.c:556-557, generously
         n = lib().ffv1o_enc_extradata(self._h, _u8p(buf), buf.size)
         if n < 0:
             raise RuntimeError(n)
         return buf[:n].tobytes()
 
     def encode(self, planes):
+        for k, (rows, cols) in enumerate(plane_shapes(self.cfg)):
+            a = planes[k]
+            if a.shape[0] < rows or a.shape[1] < cols:
+                raise ValueError(f"plane {k}: shape {a.shape}, the configuration needs {(rows, cols)}")
         arr, strides = _plane_ptrs(planes)
         cap = 1 << 20
         for p in planes:

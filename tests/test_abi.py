@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), f"{n} declared in include/ffv1hip.h but not exported"
     assert set(names) == set(EXPORTED_SYMBOLS)
-    assert lib.ffv1hip_abi_version() == 2
+    assert lib.ffv1hip_abi_version() == 3
 
 
 FIELDS = ["width", "height", "chroma_planes", "chroma_h_shift", "chroma_v_shift",
@@ -136,3 +136,32 @@ def test_decoder_no_silent_cpu_fallback_without_gpu():
     with pytest.raises(FFV1Error) as e:
         HipDecoder(p, ex, 0)
     assert e.value.code == -5
+
+
+def test_configure_pass_flags_select_version_3():
+    """AV_CODEC_FLAG_PASS1/2 force version >= 2 (ffv1enc.c:680-682), v3 at the default level."""
+    from ffv1hip import configure
+    for pass_ in (1, 2):
+        got = configure(352, 288, "yuv420p", pass_=pass_).as_dict()
+        ref = oracle.configure(352, 288, "yuv420p", pass_=pass_).as_dict()
+        assert got["version"] == ref["version"] == 3
+        assert {f: got[f] for f in FIELDS} == {f: ref[f] for f in FIELDS}
+
+
+def test_host_planes_are_checked_before_the_copy():
+    """A plane smaller than the parameters say is refused before the library
+    would read past its end (4:2:2 needs full-height chroma)."""
+    import numpy as np
+    from ffv1hip import configure
+    from ffv1hip.encoder import check_planes
+    p = configure(160, 120, "yuv422p10", slices=4)
+    good = [np.zeros((120, 160), np.uint16), np.zeros((120, 80), np.uint16), np.zeros((120, 80), np.uint16)]
+    check_planes(p, good)
+    with pytest.raises(ValueError):
+        check_planes(p, [good[0], good[1][:60], good[2][:60]])
+    with pytest.raises(ValueError):
+        check_planes(p, [g.astype(np.uint8) for g in good])
+    q = configure(64, 32, "bgr0")
+    check_planes(q, [np.zeros((32, 256), np.uint8)])
+    with pytest.raises(ValueError):
+        check_planes(q, [np.zeros((32, 64), np.uint8)])

@@ -168,3 +168,39 @@ def test_oracle_conceals_damaged_slices():
                 np.testing.assert_array_equal(got[m], want[m])
             else:
                 np.testing.assert_array_equal(got, want)
+
+
+def two_pass(stream: Stream, frames, coder):
+    """Pass 1 then pass 2 through the oracle (ffv1enc.c:898-986)."""
+    kw = dict(slices=stream.slices, coder=coder, context=stream.context, gop_size=stream.gop_size)
+    cfg = oracle.configure(stream.width, stream.height, stream.pix_fmt, pass_=1, **kw)
+    e1 = oracle.Encoder(cfg, 1)
+    p1 = [e1.encode(f) for f in frames]
+    stats = e1.stats_out()
+    cfg2 = oracle.configure(stream.width, stream.height, stream.pix_fmt, pass_=2, **kw)
+    e2 = oracle.Encoder(cfg2, 2, stats)
+    return cfg2, stats, p1, e2.extradata(), [e2.encode(f) for f in frames]
+
+
+@pytest.mark.parametrize("coder", [1, -2], ids=["custom_table", "default_table"])
+def test_oracle_two_pass(coder):
+    """Pass 1 writes the decision counts; pass 2's initial states and
+    (custom) re-sorted table code the same clip smaller, the decoder reads
+    them back from the extradata and the clip is lossless."""
+    s = Stream("2pass", 176, 144, "yuv420p", 6, slices=4, gop_size=3)
+    frames = list(s.frames())
+    cfg, stats, p1, ex, p2 = two_pass(s, frames, coder)
+    assert cfg.version == 3
+    head, rest = stats.split("\n", 1)
+    assert len(head.split()) == 512 and rest.split()[-1] == "2"  # two keyframes
+    assert len(rest.split()) == (666 + 7563) * 64 + 1
+    assert sum(len(p) for p, _ in p2) < sum(len(p) for p, _ in p1)
+    dec = oracle.Decoder(cfg, ex)
+    for (p, _), f in zip(p2, frames):
+        for a, b in zip(dec.decode(p)[0], f):
+            np.testing.assert_array_equal(a, b)
+    # stats_in may hold several runs; the last one counts (ffv1enc.c:914-953)
+    e = oracle.Encoder(cfg, 2, "0 " * 512 + "\n" + "0 " * ((666 + 7563) * 64) + "7\n" + stats)
+    assert e.extradata() == ex
+    with pytest.raises(ValueError):
+        oracle.Encoder(cfg, 2, stats.rsplit(" ", 3)[0])
