@@ -1040,8 +1040,16 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     ba.ds = ds;
     // the bits run beside the walk, on their own stream; the coder waits for both
     // FFV1HIP_BITS_INLINE=1 (measurement hook): the bits kernel before the walk, on its stream
-    static const bool bits_inline = std::getenv("FFV1HIP_BITS_INLINE") && std::atoi(std::getenv("FFV1HIP_BITS_INLINE"));
-    hipStream_t const bst = serial || bits_inline ? st : c->bits_stream;
+    // FFV1HIP_BITS (measurement hook): side (its own stream, beside the
+    // walk), code (on the coder stream, after the previous batch's packets:
+    // by then the walk's waves are all on the CUs), inline (before the walk)
+    static const int bits_mode = [] {
+      const char* e = std::getenv("FFV1HIP_BITS");
+      if (std::getenv("FFV1HIP_BITS_INLINE") && std::atoi(std::getenv("FFV1HIP_BITS_INLINE"))) return 1;
+      if (!e) return 0;
+      return std::strcmp(e, "inline") == 0 ? 1 : std::strcmp(e, "code") == 0 ? 2 : 0;
+    }();
+    hipStream_t const bst = serial || bits_mode == 1 ? st : bits_mode == 2 ? cst : c->bits_stream;
     HIP_TRY(hipEventRecord(c->laid[fb], st));
     HIP_TRY(hipStreamWaitEvent(bst, c->laid[fb], 0));
     if (timed(5, bst, [&] { return launch_bits(ba, bst); }) < 0)

@@ -158,7 +158,10 @@ __device__ __forceinline__ int rct_sample(const SymbolArgs& a, const uint8_t* fr
   return p == 0 ? g : (p == 1 ? b : r) + a.rct_offset;
 }
 
-template <int SB>  // stored sample bytes, 1 or 2; 4: bgr0
+// SB: stored sample bytes, 1 or 2; 4: bgr0.  RGB: the colour transform
+// (a template argument: a run-time test inside the sample loads would keep
+// them from issuing back to back)
+template <int SB, bool RGB>
 __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   __shared__ int16_t qt[5 * 256];
   __shared__ int red[kSymThreads / kWave];
@@ -175,7 +178,7 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   const uint8_t* base = a.frames + (int64_t)f * a.frame_bytes + a.plane_off[p];
   const int stride = a.plane_stride[p];
   // RGB: the slice's G', B', R' rows interleave (ffv1enc.c:428-471)
-  uint32_t* out = a.sym + (int64_t)slot * a.frame_samples + g.sym_off + (a.rgb ? 0 : g.plane_sym_off[p]);
+  uint32_t* out = a.sym + (int64_t)slot * a.frame_samples + g.sym_off + (RGB ? 0 : g.plane_sym_off[p]);
   const int row0 = p ? a.contexts : 0;  // plane context 1 rows follow plane 0's
 
   // sample of the slice plane as int16 (ffv1enc.c:390-407), at in-plane
@@ -187,7 +190,7 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
     if constexpr (SB == 4) {
       return rct_sample<4>(a, fr, p, px + x, py + y);
     } else {
-      if (SB == 2 && a.rgb) return rct_sample<2>(a, fr, p, px + x, py + y);
+      if constexpr (SB == 2 && RGB) return rct_sample<2>(a, fr, p, px + x, py + y);
       const uint8_t* r = base + (int64_t)(py + y) * stride;
       if constexpr (SB == 1) return r[px + x];
       else return (int16_t)(reinterpret_cast<const uint16_t*>(r)[px + x] >> sh);
@@ -285,7 +288,7 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
         if (lane < kChunkWords - kWave) dst[kWave + lane] = cs[kWave + lane];
       }
     } else if (valid) {
-      out[a.rgb ? ((int64_t)y * 3 + p) * pw + x : idx] = ((uint32_t)(row0 + ctx) << 16) | (uint16_t)diff;
+      out[RGB ? ((int64_t)y * 3 + p) * pw + x : idx] = ((uint32_t)(row0 + ctx) << 16) | (uint16_t)diff;
     }
   }
   if (count && b0 < b1) {
@@ -1994,12 +1997,17 @@ __global__ __launch_bounds__(kAsmThreads) void ffv1_assemble_packets(AssembleArg
 
 int launch_symbols(const SymbolArgs& a, void* stream) {
   dim3 grid(a.nslices, a.nslots, a.nplanes * kSymSplit), block(kSymThreads);
-  if (a.sample_bytes == 1)
-    hipLaunchKernelGGL(ffv1_symbols<1>, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
-  else if (a.sample_bytes == 4)
-    hipLaunchKernelGGL(ffv1_symbols<4>, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (a.sample_bytes == 1 && !a.rgb)
+    hipLaunchKernelGGL((ffv1_symbols<1, false>), grid, block, 0, st, a);
+  else if (a.sample_bytes == 4 && a.rgb)
+    hipLaunchKernelGGL((ffv1_symbols<4, true>), grid, block, 0, st, a);
+  else if (a.sample_bytes == 2 && a.rgb)
+    hipLaunchKernelGGL((ffv1_symbols<2, true>), grid, block, 0, st, a);
+  else if (a.sample_bytes == 2)
+    hipLaunchKernelGGL((ffv1_symbols<2, false>), grid, block, 0, st, a);
   else
-    hipLaunchKernelGGL(ffv1_symbols<2>, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
+    return -1;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
