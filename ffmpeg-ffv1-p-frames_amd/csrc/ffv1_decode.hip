@@ -98,6 +98,186 @@ __device__ inline int rac_symbol(RacDec& c, uint8_t* st, int is_signed, const ui
   return int(a);
 }
 
+// The range-coded rows run on the scalar unit: every lane of the wave runs
+// the same chain on the same values, each LDS or packet load is made uniform
+// with readfirstlane, so the compiler keeps the coder state, the context
+// row and the sample taps in SGPRs and codes a decision in SALU instructions
+// with scalar branches (a lane-0-only chain pays a VALU issue slot and an
+// exec-mask branch for every step).  Stores come from lane 0.
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int uni(int v) { return int(__builtin_amdgcn_readfirstlane(uint32_t(v))); }
+__device__ __forceinline__ int64_t uni(int64_t v) {
+  return int64_t((uint64_t(uni(uint32_t(uint64_t(v) >> 32))) << 32) | uni(uint32_t(v)));
+}
+__device__ __forceinline__ uint64_t uni(uint64_t v) { return (uint64_t(uni(uint32_t(v >> 32))) << 32) | uni(uint32_t(v)); }
+
+__device__ __forceinline__ void uni_coder(RacDec& c) {
+  c.low = uni(c.low);
+  c.range = uni(c.range);
+  c.ptr = uni(c.ptr);
+  c.end = uni(c.end);
+  c.wi = uni(c.wi);
+  c.w0 = uni(c.w0);
+  c.w1 = uni(c.w1);
+}
+
+__device__ __forceinline__ void refill_u(RacDec& c, const uint64_t* w) {
+  c.range <<= 8;
+  c.low <<= 8;
+  if (c.ptr < c.end) {
+    const int64_t wi = c.ptr >> 3;
+    if (wi != c.wi) {
+      c.w0 = c.w1;
+      c.w1 = uni(w[wi + 1]);
+      c.wi = wi;
+    }
+    c.low += uint32_t(c.w0 >> ((c.ptr & 7) * 8)) & 0xFF;
+  }
+  c.ptr++;
+}
+
+// Read-only tables through the scalar cache (constant address space,
+// uniform index): transition pairs and quant tables (DecodeArgs::stab)
+typedef const int32_t __attribute__((address_space(4))) sconst_i32;
+
+// get_rac (rangecoder.h:117-147) on state byte SH of row word `src`; the
+// successor state goes into `dst` (the row's new image), so the next
+// decision, on another slot, does not wait for this one's table lookup
+__device__ __forceinline__ int get_u(RacDec& c, uint32_t src, uint32_t& dst, int SH, const sconst_i32* sk,
+                                     const uint64_t* w) {
+  const uint32_t s = (src >> SH) & 0xFFu;
+  const uint32_t pair = uint32_t(sk[s]);
+  const uint32_t r1 = (c.range * s) >> 8;
+  const uint32_t rr = c.range - r1;
+  const int bit = c.low >= rr;
+  if (bit) {
+    c.low -= rr;
+    c.range = r1;
+  } else {
+    c.range = rr;
+  }
+  const uint32_t ns = bit ? pair >> 8 : pair & 0xFFu;
+  dst = (dst & ~(0xFFu << SH)) | (ns << SH);
+  if (c.range < 0x100) refill_u(c, w);
+  return bit;
+}
+
+template <int K>
+__device__ __forceinline__ int get_ku(RacDec& c, const uint32_t (&r)[8], uint32_t (&n)[8], const sconst_i32* sk,
+                                      const uint64_t* w) {
+  return get_u(c, r[K >> 2], n[K >> 2], (K & 3) * 8, sk, w);
+}
+
+// the exponent's unary run on slots K..9 (e = K-1 on entry)
+template <int K>
+__device__ __forceinline__ void unary_u(RacDec& c, const uint32_t (&r)[8], uint32_t (&n)[8], int& e,
+                                        const sconst_i32* sk, const uint64_t* w) {
+  if constexpr (K <= 9) {
+    if (get_ku<K>(c, r, n, sk, w)) {
+      e = K;
+      unary_u<K + 1>(c, r, n, e, sk, w);
+    }
+  }
+}
+
+// mantissa bits i = K .. 0 on slots 22 + i (those below e)
+template <int K>
+__device__ __forceinline__ void mant_u(RacDec& c, const uint32_t (&r)[8], uint32_t (&n)[8], int e, uint32_t& a,
+                                       const sconst_i32* sk, const uint64_t* w) {
+  if constexpr (K >= 0) {
+    if (K < e) a = 2 * a + uint32_t(get_ku<22 + K>(c, r, n, sk, w));
+    mant_u<K - 1>(c, r, n, e, a, sk, w);
+  }
+}
+
+// get_symbol_inline (ffv1dec.c:44-66), signed, on the row at `row` (32-byte
+// aligned; LDS or a global table): the row's 32 states read once into
+// registers; every slot but 10 and 31 codes at most one decision, so a
+// decision reads its state from the row as read and writes its successor
+// into the new image n, written back at the end
+__device__ inline int symbol_u(RacDec& c, uint8_t* row, const sconst_i32* sk, const uint64_t* w) {
+  uint32_t* const r1w = reinterpret_cast<uint32_t*>(row);
+  uint32_t r[8], n[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) n[i] = r[i] = uni(r1w[i]);
+  if (get_ku<0>(c, r, n, sk, w)) {
+    if (threadIdx.x == 0) r1w[0] = n[0];  // only slot 0 moved
+    return 0;
+  }
+  int e = 0, ret;
+  unary_u<1>(c, r, n, e, sk, w);
+  bool bad = false;
+  if (e == 9) {  // slot 10 for the rest of the run: its state from n after its first decision
+    uint32_t src = r[2];
+    while (get_u(c, src, n[2], 16, sk, w)) {
+      src = n[2];
+      if (++e > 31) {
+        bad = true;
+        break;
+      }
+    }
+  }
+  if (bad) {
+    ret = kInvalidData;
+  } else {
+    uint32_t a = 1, src = r[7];
+    for (int i = e - 1; i >= 9; i--) {  // slot 31
+      a = 2 * a + uint32_t(get_u(c, src, n[7], 24, sk, w));
+      src = n[7];
+    }
+    mant_u<8>(c, r, n, e, a, sk, w);
+    const int j = 11 + (e < 10 ? e : 10);  // the sign slot, row words 2..5
+    const int sh = (j & 3) * 8;
+    int sg;
+    switch (j >> 2) {
+      case 2: sg = get_u(c, r[2], n[2], sh, sk, w); break;
+      case 3: sg = get_u(c, r[3], n[3], sh, sk, w); break;
+      case 4: sg = get_u(c, r[4], n[4], sh, sk, w); break;
+      default: sg = get_u(c, r[5], n[5], sh, sk, w); break;
+    }
+    ret = sg ? int(0u - a) : int(a);
+  }
+  if (threadIdx.x == 0) {
+    uint4* const r4 = reinterpret_cast<uint4*>(row);
+    r4[0] = make_uint4(n[0], n[1], n[2], n[3]);
+    r4[1] = make_uint4(n[4], n[5], n[6], n[7]);
+  }
+  return ret;
+}
+
+__device__ inline int median3u(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
+
+// decode_line (ffv1dec.c:42-117), range coder, by the whole wave on uniform
+// values: one row into `cur` (which holds row y-2 until each sample is
+// written; `up` is row y-1), the reference's zeroed-ring neighbourhood
+__device__ inline void decode_row_u(RacDec& c, uint8_t* st8, const sconst_i32* sk, const uint64_t* pkw,
+                                    bool model1, int16_t* cur, const int16_t* up, int w, int bits) {
+  const sconst_i32* const q = sk + 256;  // quant tables [5][256]
+  const int mask = int((1u << bits) - 1u);
+  int T = uni(int(up[0]));
+  const int T0 = T;
+  int L = T;
+  int LT = uni(int(cur[0]));
+  for (int x = 0; x < w; x++) {
+    const int RT = x + 1 < w ? uni(int(up[x + 1])) : T;
+    int ctx = q[(L - LT) & 0xFF] + q[256 + ((LT - T) & 0xFF)] + q[512 + ((T - RT) & 0xFF)];
+    if (model1) {
+      const int LL = x >= 2 ? uni(int(cur[x - 2])) : (x == 1 ? T0 : 0);
+      const int TT = uni(int(cur[x]));
+      ctx += q[768 + ((LL - L) & 0xFF)] + q[1024 + ((TT - T) & 0xFF)];
+    }
+    const int actx = ctx < 0 ? -ctx : ctx;
+    int diff = symbol_u(c, st8 + actx * 32, sk, pkw);
+    if (ctx < 0) diff = -diff;
+    const int pred = median3u(L, L + T - LT, T);
+    const int v = int(int16_t((pred + diff) & mask));
+    if (threadIdx.x == 0) cur[x] = int16_t(v);
+    LT = T;
+    T = RT;
+    L = v;
+  }
+}
+
 // GetBitContext over a slice's Golomb bits: MSB first, zeros past the end
 // (the safe bitstream reader).
 struct BitRd {
@@ -262,8 +442,15 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
   const int s = blockIdx.x, seg = blockIdx.y, lane = threadIdx.x;
   const Segment sg = a.segs[seg];
   const SliceGeom* g = a.geom + s;  // read through the pointer: a by-value copy indexed by plane spills
-  const int64_t sb = GSTATES ? 0 : (a.state_bytes + 15) & ~int64_t(15);
+  // swap mode (range coder, YCbCr): the LDS holds one plane group's states,
+  // the chain's other group waits in its global table (a.tables) and the two
+  // trade places where the plane group changes (twice a frame), so that twice
+  // the chains fit on a CU
+  const bool swap = !GSTATES && a.swap;
+  const int64_t sb = GSTATES ? 0 : ((swap ? a.state_bytes / 2 : a.state_bytes) + 15) & ~int64_t(15);
   uint8_t* const states = GSTATES ? a.tables + (int64_t(seg) * a.nslices + s) * a.state_bytes : lds;
+  uint32_t* const bk4 = swap ? reinterpret_cast<uint32_t*>(a.tables + (int64_t(seg) * a.nslices + s) * a.state_bytes)
+                             : nullptr;
   uint16_t* const tt = reinterpret_cast<uint16_t*>(lds + sb);  // [256] frame table to0 | to1 << 8
   uint16_t* const dtt = tt + 256;                              // [256] default table
   uint8_t* const hdr = reinterpret_cast<uint8_t*>(dtt + 256);  // [32] header states, [32] scratch
@@ -279,12 +466,21 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
   const int bits = a.coded_bits;
   const bool model1 = a.context_model != 0;
   const int64_t words = a.state_bytes / 4;
+  const int64_t hw = words / 2;  // one plane group
   uint32_t* const st4 = reinterpret_cast<uint32_t*>(states);
+  int cur = 0;  // swap mode: the plane group in the LDS
   // the chain continues the states the previous call left (the decoder
   // starts them reset)
   {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(a.persist_in + int64_t(s) * a.state_bytes);
-    for (int64_t i = lane; i < words; i += kDecThreads) st4[i] = src[i];
+    if (swap) {
+      for (int64_t i = lane; i < hw; i += kDecThreads) {
+        st4[i] = src[i];
+        bk4[hw + i] = src[hw + i];
+      }
+    } else {
+      for (int64_t i = lane; i < words; i += kDecThreads) st4[i] = src[i];
+    }
   }
   RacDec c{};
   BitRd br{};
@@ -342,7 +538,14 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
     if (bad == 2) return;
     if (bad) continue;  // not decoded: no state update (ffv1dec.c:410-414)
     if (key) {          // ff_ffv1_clear_slice_state, after the header (ffv1dec.c:418-419)
-      if (!GOLOMB && a.init) {  // initial states from the extradata (ffv1.c:185-189)
+      if (swap) {  // the LDS group and the other group in the global table
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.init);
+        for (int64_t i = lane; i < hw; i += kDecThreads) {
+          const uint32_t v = a.init ? src[i] : 0x80808080u;
+          st4[i] = v;
+          bk4[(cur ^ 1) * hw + i] = v;
+        }
+      } else if (!GOLOMB && a.init) {  // initial states from the extradata (ffv1.c:185-189)
         const uint32_t* src = reinterpret_cast<const uint32_t*>(a.init);
         for (int64_t i = lane; i < words; i += kDecThreads) st4[i] = src[i % (words / 2)];
       } else {
@@ -364,16 +567,27 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
       br.cache = 0;
       br.nc = 0;
     }
+    if constexpr (!GOLOMB) uni_coder(c);  // lane 0's coder after the header, to every lane
     int run_index = 0;
     uint8_t* const obase = a.out + int64_t(f) * a.frame_bytes;
     if (!a.rgb) {
       for (int p = 0; p < a.nplanes; p++) {
         for (int i = lane; i < 2 * a.row_cap; i += kDecThreads) ring[i] = 0;
+        const int grp = p ? 1 : 0;
+        if (swap && grp != cur) {  // the other plane group's states into the LDS
+          __syncthreads();
+          for (int64_t i = lane; i < hw; i += kDecThreads) {
+            const uint32_t v = bk4[grp * hw + i];
+            bk4[cur * hw + i] = st4[i];
+            st4[i] = v;
+          }
+          cur = grp;
+        }
         __syncthreads();
         // decode_plane (ffv1dec.c:200-224): lane 0 decodes a row into LDS;
         // the wave then stores it (coalesced), so the serial loop issues no
         // global stores
-        uint8_t* pst = states + (p ? a.state_bytes / 2 : 0);
+        uint8_t* pst = states + (p && !swap ? a.state_bytes / 2 : 0);
         const int w = g->pw[p], h = g->ph[p];
         const int64_t poff = p == 0 ? a.plane_off[0] : (p == 1 ? a.plane_off[1] : a.plane_off[2]);
         const int pw = p == 0 ? a.plane_w[0] : (p == 1 ? a.plane_w[1] : a.plane_w[2]);
@@ -381,7 +595,9 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
         for (int y = 0; y < h; y++) {
           int16_t* cur = ring + (y & 1) * a.row_cap;  // holds row y-2 until written
           const int16_t* up = ring + ((y + 1) & 1) * a.row_cap;
-          if (lane == 0)
+          if constexpr (!GOLOMB)
+            decode_row_u(c, pst, (const sconst_i32*)(a.stab), pkw, model1, cur, up, w, bits);
+          else if (lane == 0)
             decode_row<GOLOMB>(c, br, pst, reinterpret_cast<uint64_t*>(pst), tt, pkw, qt, model1, cur, up, w, bits,
                                run_index);
           __syncthreads();
@@ -405,14 +621,16 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
       __syncthreads();
       const int w = g->pw[0], h = g->ph[0];
       for (int y = 0; y < h; y++) {
-        if (lane == 0)
-          for (int p = 0; p < 3; p++) {
-            uint8_t* pst = states + (p ? a.state_bytes / 2 : 0);
-            int16_t* cur = ring + (2 * p + (y & 1)) * a.row_cap;
-            const int16_t* up = ring + (2 * p + ((y + 1) & 1)) * a.row_cap;
+        for (int p = 0; p < 3; p++) {
+          uint8_t* pst = states + (p ? a.state_bytes / 2 : 0);
+          int16_t* cur = ring + (2 * p + (y & 1)) * a.row_cap;
+          const int16_t* up = ring + (2 * p + ((y + 1) & 1)) * a.row_cap;
+          if constexpr (!GOLOMB)
+            decode_row_u(c, pst, (const sconst_i32*)(a.stab), pkw, model1, cur, up, w, bits);
+          else if (lane == 0)
             decode_row<GOLOMB>(c, br, pst, reinterpret_cast<uint64_t*>(pst), tt, pkw, qt, model1, cur, up, w, bits,
                                run_index);
-          }
+        }
         __syncthreads();
         const int16_t* G = ring + (y & 1) * a.row_cap;
         const int16_t* B = ring + (2 + (y & 1)) * a.row_cap;
@@ -445,7 +663,14 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
   __syncthreads();
   if (sg.save_states) {
     uint32_t* dst = reinterpret_cast<uint32_t*>(a.persist_out + int64_t(s) * a.state_bytes);
-    for (int64_t i = lane; i < words; i += kDecThreads) dst[i] = st4[i];
+    if (swap) {
+      for (int64_t i = lane; i < hw; i += kDecThreads) {
+        dst[cur * hw + i] = st4[i];
+        dst[(cur ^ 1) * hw + i] = bk4[(cur ^ 1) * hw + i];
+      }
+    } else {
+      for (int64_t i = lane; i < words; i += kDecThreads) dst[i] = st4[i];
+    }
   }
 }
 
@@ -490,13 +715,13 @@ __global__ void __launch_bounds__(256) ffv1_conceal(DecodeArgs a) {
 }  // namespace
 
 int64_t decode_lds_bytes(const DecodeArgs& a, bool global_states) {
-  const int64_t sb = global_states ? 0 : (a.state_bytes + 15) & ~int64_t(15);
+  const int64_t sb = global_states ? 0 : ((a.swap ? a.state_bytes / 2 : a.state_bytes) + 15) & ~int64_t(15);
   return sb + 1024 + 64 + 5 * 256 * 2 + int64_t(a.rgb ? 6 : 2) * a.row_cap * 2;
 }
 
 int launch_decode(const DecodeArgs& a, int nsegs, void* stream) {
   dim3 grid(a.nslices, nsegs), block(kDecThreads);
-  const bool glob = a.tables != nullptr;
+  const bool glob = a.tables != nullptr && !a.swap;
   const int64_t lds = decode_lds_bytes(a, glob);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (a.ac == 0) {

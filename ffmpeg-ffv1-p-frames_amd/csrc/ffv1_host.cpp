@@ -1503,6 +1503,7 @@ struct ffv1hip_dec {
   int out_rows[3]{};
   int row_cap = 0;
   bool global_states = false;
+  bool swap = false;  // range coder, YCbCr: one plane group's states in the LDS at a time
   bool have_states = false;
   bool have_last = false;  // d_last holds the previous picture (concealment)
   std::vector<SliceGeom> geom;
@@ -1511,6 +1512,7 @@ struct ffv1hip_dec {
   SliceGeom* d_geom = nullptr;
   int16_t* d_qt = nullptr;
   uint8_t* d_tabs = nullptr;  // frame table to0 | to1, default table to0 | to1
+  int32_t* d_stab = nullptr;  // the same frame table as pairs and the quant tables, int32 (DecodeArgs::stab)
   int* d_status = nullptr;
   uint8_t* d_sticky = nullptr;  // [slice] slice_damaged across calls
   uint8_t* d_last = nullptr;
@@ -1525,6 +1527,7 @@ static void dec_free(ffv1hip_dec* d) {
   (void)hipFree(d->d_geom);
   (void)hipFree(d->d_qt);
   (void)hipFree(d->d_tabs);
+  (void)hipFree(d->d_stab);
   (void)hipFree(d->d_status);
   (void)hipFree(d->d_sticky);
   (void)hipFree(d->d_last);
@@ -1726,6 +1729,9 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
   la.row_cap = d->row_cap;
   constexpr int64_t kDecLds = 64 * 1024;
   d->global_states = decode_lds_bytes(la, false) > kDecLds;
+  // FFV1HIP_DEC_SWAP=0 (measurement hook): both plane groups in the LDS
+  const char* sw = std::getenv("FFV1HIP_DEC_SWAP");
+  d->swap = !d->global_states && p.ac && !p.colorspace && p.chroma_planes && !(sw && std::atoi(sw) == 0);
   if (decode_lds_bytes(la, true) > kDecLds) {
     delete d;
     return fail(set_err(-38, "GPU decoder: slice too wide for the LDS row buffer"));
@@ -1749,6 +1755,11 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
     std::memcpy(tabs + 512, tmp.dflt.to0, 256);
     std::memcpy(tabs + 768, tmp.dflt.to1, 256);
     HIP_TRY(hipMemcpy(d->d_tabs, tabs, 1024, hipMemcpyHostToDevice));
+    std::vector<int32_t> stab(256 + 5 * 256);
+    for (int i = 0; i < 256; i++) stab[i] = int32_t(tmp.frame.to0[i]) | (int32_t(tmp.frame.to1[i]) << 8);
+    for (int i = 0; i < 5 * 256; i++) stab[256 + i] = tmp.qt[i / 256][i % 256];
+    HIP_TRY(hipMalloc(&d->d_stab, stab.size() * sizeof(int32_t)));
+    HIP_TRY(hipMemcpy(d->d_stab, stab.data(), stab.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     const std::vector<uint8_t>& is = tmp.init_states[p.context_model];
     if (std::any_of(is.begin(), is.end(), [](uint8_t v) { return v != 128; })) {
       HIP_TRY(hipMalloc(&d->d_init, is.size()));
@@ -1849,7 +1860,7 @@ int ffv1hip_decode(ffv1hip_dec* d, const uint8_t* packets, const int64_t* sizes,
     HIP_TRY(hipMalloc(&d_segs, segs.size() * sizeof(Segment)));
     HIP_TRY(hipMalloc(&d_out, size_t(d->frame_bytes) * n_frames));
     HIP_TRY(hipMalloc(&d_dmg, nse));
-    if (d->global_states) HIP_TRY(hipMalloc(&d_tables, size_t(d->state_bytes) * ns * segs.size()));
+    if (d->global_states || d->swap) HIP_TRY(hipMalloc(&d_tables, size_t(d->state_bytes) * ns * segs.size()));
     HIP_TRY(hipMemsetAsync(d_pk + total, 0, 64, d->stream));
     // samples no slice codes (odd chroma offsets, ffv1enc.c:1186-1188) read as 0
     HIP_TRY(hipMemsetAsync(d_out, 0, size_t(d->frame_bytes) * n_frames, d->stream));
@@ -1872,6 +1883,7 @@ int ffv1hip_decode(ffv1hip_dec* d, const uint8_t* packets, const int64_t* sizes,
     a.qt = d->d_qt;
     a.ftab = d->d_tabs;
     a.dtab = d->d_tabs + 512;
+    a.stab = d->d_stab;
     a.state_bytes = d->state_bytes;
     a.persist_in = d->d_persist[d->pcur];
     a.persist_out = d->d_persist[d->pcur ^ 1];
@@ -1908,6 +1920,7 @@ int ffv1hip_decode(ffv1hip_dec* d, const uint8_t* packets, const int64_t* sizes,
     a.sticky = d->d_sticky;
     a.nframes = n_frames;
     a.init = d->d_init;
+    a.swap = d->swap;
     if (launch_decode(a, int(segs.size()), d->stream) < 0)
       return set_err(-5, "ffv1_decode_slices launch failed: %s", hipGetErrorString(hipGetLastError()));
     int status = 0;

@@ -243,6 +243,8 @@ struct DecodeArgs {
   uint8_t* sticky;             // [slice] slice_damaged carried across calls
   int nframes;
   const uint8_t* init;         // range coder: initial states [contexts][32] from the extradata, or null
+  int swap;                    // one plane group's states in the LDS, the other in `tables` (range, YCbCr)
+  const int32_t* stab;         // [256] frame table pairs to0 | to1 << 8, then [5][256] quant tables (scalar loads)
 };
 int launch_decode(const DecodeArgs& a, int nsegs, void* stream);
 
