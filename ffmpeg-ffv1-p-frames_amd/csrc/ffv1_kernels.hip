@@ -134,6 +134,8 @@ __device__ __forceinline__ int wave_incl_scan(int x, int /*lane*/) {
 
 // the previous lane's value (lane 0: 0), a DPP wave_shr:1
 __device__ __forceinline__ int wave_prev(int x) { return __builtin_amdgcn_update_dpp(0, x, 0x138, 0xf, 0xf, true); }
+// the next lane's value (lane 63: 0), a DPP wave_shl:1
+__device__ __forceinline__ int wave_next(int x) { return __builtin_amdgcn_update_dpp(0, x, 0x130, 0xf, 0xf, true); }
 
 // RGB (encode_rgb_frame, ffv1enc.c:413-459): pixel (x, y) of the frame as
 // coded plane p of the reversible colour transform, G' = g + (b' + r') >> 2,
@@ -221,21 +223,30 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
     // neighbourhood as the zeroed two/three-row ring exposes it:
     // rows above the slice read 0; L(x=0) = T; LT(x=0) = sample two rows up
     // in column 0; RT past the right edge = T; LL(x=0) = 0, LL(x=1) = T(0).
+    // A wave's 64 lanes hold 64 consecutive samples of the plane, so the
+    // L / LT / RT taps are the neighbouring lanes' X / T (DPP wave shifts):
+    // only X and T are loaded per lane, plus two fix-up loads that touch new
+    // memory on the wave's edge lanes and on the lanes at x = 0 only (every
+    // other lane re-reads its own X / T address)
     const int ym1 = y ? y - 1 : 0, ym2 = y >= 2 ? y - 2 : 0;
-    const int xm1 = x ? x - 1 : 0, xp1 = x + 1 < pw ? x + 1 : x;
+    const bool first = lane == 0, last = lane == kWave - 1;
     const int X = load(x, y);
-    const int rT = load(x, ym1), rT0 = load(0, ym1), rL = load(xm1, y);
-    const int rLT = load(xm1, ym1), rLT0 = load(0, ym2), rRT = load(xp1, ym1);
-    int rLL = 0, rTT = 0;
+    const int rT = load(x, ym1);
+    const bool fe = first && x, le = last && x + 1 < pw;
+    const int f1 = load(fe ? x - 1 : x, x ? y : ym2);          // L on lane 0, LT at x = 0, else X again
+    const int f2 = load(fe ? x - 1 : (le ? x + 1 : x), ym1);  // LT on lane 0, RT on lane 63, else T again
+    const int pX = wave_prev(X), pT = wave_prev(rT), nT = wave_next(rT);
+    int rLL = 0, rTT = 0, rT0 = 0;
     if (a.model1) {
       rLL = load(x >= 2 ? x - 2 : 0, y);
       rTT = load(x, ym2);
+      rT0 = load(0, ym1);
     }
     const int T = y ? rT : 0;
-    const int T0 = y ? rT0 : 0;
-    const int L = x ? rL : T0;
-    const int LT = x ? (y ? rLT : 0) : (y >= 2 ? rLT0 : 0);
-    const int RT = x + 1 < pw ? (y ? rRT : 0) : T;
+    const int T0 = a.model1 ? (y ? rT0 : 0) : T;  // T at x = 0; model 1 also needs it at x = 1
+    const int L = x ? (first ? f1 : pX) : T;
+    const int LT = x ? (y ? (first ? f2 : pT) : 0) : (y >= 2 ? f1 : 0);
+    const int RT = x + 1 < pw ? (y ? (last ? f2 : nT) : 0) : T;
     int ctx = qt[(L - LT) & 0xFF] + qt[256 + ((LT - T) & 0xFF)] + qt[512 + ((T - RT) & 0xFF)];
     if (a.model1) {
       const int LL = x >= 2 ? rLL : (x == 1 ? T0 : 0);
