@@ -1166,7 +1166,7 @@ struct StepIn {
   int pos;        // stage byte of the decision (the lane's dummy byte for none)
   int addr;       // the slot's state byte in the tables
   bool same;      // same row as the previous symbol
-  bool same2;     // same row as the symbol two back (and not the previous one's)
+  bool same2;     // same row as the previous symbol or the one two back (same decides first)
 };
 
 __device__ __forceinline__ StepIn derive(const uint4& r, const WalkLane& W, int kc) {
@@ -1177,7 +1177,7 @@ __device__ __forceinline__ StepIn derive(const uint4& r, const WalkLane& W, int 
   d.pos = d.code == 2u ? W.dummy : pos;
   d.addr = (int)(r.x & 0xFFFFu) + W.kk;
   d.same = (int)r.w < 0;  // kRecSame
-  d.same2 = (r.w & kRecSame2) != 0u;
+  d.same2 = r.w >= kRecSame2;  // bit 31 or 30: one compare, no mask (same wins in walk_step)
   return d;
 }
 
