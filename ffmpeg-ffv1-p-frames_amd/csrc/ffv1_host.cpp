@@ -265,11 +265,14 @@ struct ffv1hip_ctx {
   uint8_t* d_tables = nullptr;   // [slot][slice][2][contexts][32]
   uint32_t* d_sym = nullptr;     // [slot][frame_samples]; frames mode: walk records (uint4), 2 x [batch frame][frame_samples]
   // frames mode, two buffer sets: the walk of batch k+1 runs while batch k codes
-  uint8_t* d_keys2 = nullptr;    // 2 x [batch frame] keyflags
+  uint8_t* d_keys2 = nullptr;    // 3 x [batch frame] keyflags
   uint32_t* d_cbits = nullptr;   // 2 x [batch frame][frame_chunks][kChunkWords] packed decision bits
-  int* d_dcount = nullptr;       // 2 x [batch frame][slice][3] decisions per plane
-  int64_t* d_dbase = nullptr;    // 2 x [batch frame][slice] first decision of each stream
-  int64_t* d_dtotal = nullptr;   // [2] decisions of the batch (incl. alignment)
+  // the per-batch stream metadata has three sets (index tri): the symbols of
+  // batch k rewrite set k % 3 while the coder of batch k-1 may still read its
+  // set and the walk of batch k-1 run
+  int* d_dcount = nullptr;       // 3 x [batch frame][slice][3] decisions per plane
+  int64_t* d_dbase = nullptr;    // 3 x [batch frame][slice] first decision of each stream
+  int64_t* d_dtotal = nullptr;   // [3] decisions of the batch (incl. alignment)
   int64_t* h_dtotal = nullptr;   // pinned readback of d_dtotal
   uint8_t* d_pre[2] = {nullptr, nullptr};    // [decision] state before the decision
   uint8_t* d_scratch = nullptr;               // where idle walk chains write their stage
@@ -283,6 +286,21 @@ struct ffv1hip_ctx {
   hipEvent_t laid[2] = {nullptr, nullptr};    // set k's stream layout and zeroed bits are ready
   hipEvent_t bitsed[2] = {nullptr, nullptr};  // set k's decision bits are in place
   hipEvent_t coded[2] = {nullptr, nullptr};  // the coder of the batch that last used set k is done
+  int tri = 0;                                // metadata set of the next batch
+  hipEvent_t coded3[3] = {nullptr, nullptr, nullptr};  // the coder of the batch that last used metadata set k
+  // Split schedule (a second set of walk records and chunk bits, when HBM
+  // allows): the walk is launched in two parts, first the waves the CUs hold
+  // at once (the long plane group's chains and some of the short), then the
+  // rest; the symbols, layout and bits of batch k+1 run on the bits stream
+  // once the first part of batch k's walk is done, beside its second part,
+  // instead of in front of the next walk on its stream
+  bool two_rec = false;
+  uint4* d_rec2 = nullptr;       // [batch frame][frame_samples] walk records of set 1
+  uint32_t* d_cbits2 = nullptr;  // chunk bits of set 1
+  int* d_ident = nullptr;        // [batch frame] i: the frames mode's frame of each slot
+  hipEvent_t entry[2] = {nullptr, nullptr};  // set k's batch: the launch stream's work so far
+  hipEvent_t walk_a = nullptr;               // the first part of the last batch's walk is done
+  bool walk_a_valid = false;
   SliceGeom* d_geom = nullptr;
   int* d_slot_frames = nullptr;  // [j][slot]
   int* d_status = nullptr;       // [set][4]: [0] slices over budget, [1] most bytes one needed
@@ -313,7 +331,7 @@ struct ffv1hip_ctx {
     hipStream_t st = nullptr;
     int64_t pn0 = 0;
     bool have0 = false;
-    int pcur0 = 0, buf0 = 0, status_set = 0;
+    int pcur0 = 0, buf0 = 0, tri0 = 0, status_set = 0;
     int64_t gob0 = 0;
   } last;
   int last_n = 0;
@@ -550,7 +568,8 @@ static void free_device(ffv1hip_ctx* c) {
   void* ptrs[] = {c->d_frames, c->d_qt, c->d_tabs, c->d_ops, c->d_nops, c->d_segs, c->d_keys,
                   c->d_slice_out, c->d_slice_bytes, c->d_packets, c->d_packet_size, c->d_persist[0],
                   c->d_persist[1], c->d_tables, c->d_sym, c->d_keys2, c->d_cbits, c->d_dcount, c->d_dbase, c->d_dtotal, c->d_pre[0],
-                  c->d_pre[1], c->d_bits[0], c->d_bits[1], c->d_scratch, c->d_opsets, c->d_geom, c->d_slot_frames, c->d_status};
+                  c->d_pre[1], c->d_bits[0], c->d_bits[1], c->d_scratch, c->d_opsets, c->d_geom, c->d_slot_frames, c->d_status,
+                  c->d_rec2, c->d_cbits2, c->d_ident};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_dtotal) (void)hipHostFree(c->h_dtotal);
@@ -573,6 +592,11 @@ static void free_device(ffv1hip_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t& e : c->coded)
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t& e : c->coded3)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t& e : c->entry)
+    if (e) (void)hipEventDestroy(e);
+  if (c->walk_a) (void)hipEventDestroy(c->walk_a);
 }
 
 // Decision-stream buffers of set k for `need` decisions.  The set's previous
@@ -628,12 +652,21 @@ static int alloc_device(ffv1hip_ctx* c) {
     // the walk records and chunk bits: one set (the next batch's symbols run
     // after this batch's walk on the same stream, and wait for its bits)
     HIP_TRY(hipMalloc(&c->d_sym, sizeof(uint4) * size_t(c->frame_samples) * nb));
-    HIP_TRY(hipMalloc(&c->d_keys2, 2 * size_t(nb)));
+    HIP_TRY(hipMalloc(&c->d_keys2, 3 * size_t(nb)));
     HIP_TRY(hipMalloc(&c->d_cbits, sizeof(uint32_t) * kChunkWords * size_t(c->frame_chunks) * nb));
-    HIP_TRY(hipMalloc(&c->d_dcount, 2 * sizeof(int) * 3 * size_t(nb) * c->nslices));
-    HIP_TRY(hipMalloc(&c->d_dbase, 2 * sizeof(int64_t) * size_t(nb) * c->nslices));
-    HIP_TRY(hipMalloc(&c->d_dtotal, 2 * sizeof(int64_t)));
-    HIP_TRY(hipHostMalloc(&c->h_dtotal, 2 * sizeof(int64_t), hipHostMallocDefault));
+    HIP_TRY(hipMalloc(&c->d_dcount, 3 * sizeof(int) * 3 * size_t(nb) * c->nslices));
+    HIP_TRY(hipMalloc(&c->d_dbase, 3 * sizeof(int64_t) * size_t(nb) * c->nslices));
+    HIP_TRY(hipMalloc(&c->d_dtotal, 3 * sizeof(int64_t)));
+    HIP_TRY(hipHostMalloc(&c->h_dtotal, 3 * sizeof(int64_t), hipHostMallocDefault));
+    for (hipEvent_t& e : c->coded3) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (hipEvent_t& e : c->entry) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->walk_a, hipEventDisableTiming));
+    {
+      std::vector<int> ident(nb);
+      for (int i = 0; i < nb; i++) ident[i] = i;
+      HIP_TRY(hipMalloc(&c->d_ident, sizeof(int) * size_t(nb)));
+      HIP_TRY(hipMemcpy(c->d_ident, ident.data(), sizeof(int) * size_t(nb), hipMemcpyHostToDevice));
+    }
     HIP_TRY(hipStreamCreateWithFlags(&c->code_stream, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&c->bits_stream, hipStreamNonBlocking));
     for (hipEvent_t& e : c->laid) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -650,6 +683,23 @@ static int alloc_device(ffv1hip_ctx* c) {
     const int64_t cap = worst <= (int64_t(1) << 31) ? worst : std::min(worst, guess);
     for (int k = 0; k < 2; k++)
       if (grow_decisions(c, k, cap) < 0) return -5;
+    // the second records set, only with room to spare (a later batch may
+    // still grow the decision buffers); FFV1HIP_RECSETS=1 keeps one set
+    const char* rs = std::getenv("FFV1HIP_RECSETS");
+    const size_t rec_bytes = sizeof(uint4) * size_t(c->frame_samples) * nb;
+    const size_t cb_bytes = sizeof(uint32_t) * kChunkWords * size_t(c->frame_chunks) * nb;
+    size_t free_b = 0, total_b = 0;
+    HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+    const size_t margin = (size_t(c->dcap[0]) + size_t(c->dcap[1])) / 4 + (size_t(4) << 30);
+    if (!(rs && std::atoi(rs) == 1) && free_b > rec_bytes + cb_bytes + margin) {
+      if (hipMalloc(&c->d_rec2, rec_bytes) == hipSuccess && hipMalloc(&c->d_cbits2, cb_bytes) == hipSuccess) {
+        c->two_rec = true;
+      } else {
+        (void)hipGetLastError();
+        if (c->d_rec2) (void)hipFree(c->d_rec2);
+        c->d_rec2 = nullptr;
+      }
+    }
   } else {
     const size_t chains = (size_t(c->max_slots) * c->nslices + 63) & ~size_t(63);
     HIP_TRY(hipMalloc(&c->d_tables, state_bytes * chains));
@@ -895,34 +945,58 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   c->last.have0 = c->have_states;
   c->last.pcur0 = c->pcur;
   c->last.buf0 = c->buf;
+  c->last.tri0 = c->tri;
   c->last.gob0 = c->gob_count;
   for (uint8_t k : keys) c->gob_count += k;
   if (c->pass == 1)
     HIP_TRY(hipMemcpyAsync(c->d_rcstat_bak, c->d_rcstat, sizeof(unsigned long long) * (512 + size_t(64) * c->contexts),
                            hipMemcpyDeviceToDevice, st));
-  // the previous batch (possibly on another stream) is done with what this
-  // one rewrites first: segments, slot lists, keyflags, the persist buffer
-  if (c->dep_valid) HIP_TRY(hipStreamWaitEvent(st, c->dep_ev, 0));
   // frames mode: the coder stream may still be on the previous batch, so the
   // buffers it reads alternate between two sets; set fb was last read by the
   // coder of batch k-2, which must be done before this batch rewrites it
+  // (the stream metadata: three sets, t3)
   const int fb = c->buf;
-  uint8_t* const d_keys = c->frames_mode ? c->d_keys2 + size_t(fb) * c->max_batch : c->d_keys;
+  const int t3 = c->frames_mode ? c->tri : 0;
+  uint8_t* const d_keys = c->frames_mode ? c->d_keys2 + size_t(t3) * c->max_batch : c->d_keys;
   // FFV1HIP_SERIAL=1 (measurement hook): no walk/code overlap
   static const bool serial = std::getenv("FFV1HIP_SERIAL") && std::atoi(std::getenv("FFV1HIP_SERIAL"));
   hipStream_t const cst = c->frames_mode && !serial ? c->code_stream : st;
+  // the split schedule: symbols, layout and bits on the bits stream
+  hipStream_t const sst = c->frames_mode && c->two_rec && !serial ? c->bits_stream : st;
+  if (sst != st) {
+    // the caller's work on st so far (the frames), then what the symbols
+    // rewrite: records set fb (read by the walk of batch k-2) and metadata
+    // set t3 (read by the coder of batch k-3); and they start once the first
+    // part of the previous batch's walk is done and its second part's waves
+    // are on the CUs (a short wait kernel, FFV1HIP_SYM_DELAY_US)
+    HIP_TRY(hipEventRecord(c->entry[fb], st));
+    HIP_TRY(hipStreamWaitEvent(sst, c->entry[fb], 0));
+    HIP_TRY(hipStreamWaitEvent(sst, c->walked[fb], 0));
+    HIP_TRY(hipStreamWaitEvent(sst, c->coded3[t3], 0));
+    if (c->walk_a_valid) {
+      HIP_TRY(hipStreamWaitEvent(sst, c->walk_a, 0));
+      static const int delay_us =
+          std::getenv("FFV1HIP_SYM_DELAY_US") ? std::atoi(std::getenv("FFV1HIP_SYM_DELAY_US")) : 1000;
+      if (delay_us > 0 && launch_delay(delay_us, sst) < 0) return set_err(-5, "delay launch failed");
+    }
+  }
+  // the previous batch (possibly on another stream) is done with what this
+  // one rewrites first: segments, slot lists, keyflags, the persist buffer
+  if (c->dep_valid) HIP_TRY(hipStreamWaitEvent(st, c->dep_ev, 0));
   if (c->frames_mode) HIP_TRY(hipStreamWaitEvent(st, c->coded[fb], 0));
-  HIP_TRY(hipMemcpyAsync(d_keys, keys.data(), n, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(d_keys, keys.data(), n, hipMemcpyHostToDevice, sst));
   HIP_TRY(hipMemcpyAsync(c->d_segs, segs.data(), segs.size() * sizeof(Segment), hipMemcpyHostToDevice, st));
 
   int maxlen = 0;
   for (const Segment& g : segs) maxlen = std::max(maxlen, g.nframes);
-  std::vector<int> slot_frames(size_t(maxlen) * nsegs, -1);
-  for (int j = 0; j < maxlen; j++)
-    for (int k = 0; k < nsegs; k++)
-      if (j < segs[k].nframes) slot_frames[size_t(j) * nsegs + k] = segs[k].first_frame + j;
-  HIP_TRY(hipMemcpyAsync(c->d_slot_frames, slot_frames.data(), sizeof(int) * slot_frames.size(),
-                         hipMemcpyHostToDevice, st));
+  if (!c->frames_mode) {
+    std::vector<int> slot_frames(size_t(maxlen) * nsegs, -1);
+    for (int j = 0; j < maxlen; j++)
+      for (int k = 0; k < nsegs; k++)
+        if (j < segs[k].nframes) slot_frames[size_t(j) * nsegs + k] = segs[k].first_frame + j;
+    HIP_TRY(hipMemcpyAsync(c->d_slot_frames, slot_frames.data(), sizeof(int) * slot_frames.size(),
+                           hipMemcpyHostToDevice, st));
+  }
 
   SymbolArgs sa{};
   sa.frames = d_frames;
@@ -945,9 +1019,12 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   sa.model1 = p.context_model;
   sa.qt = c->d_qt;
   uint32_t* const d_sym = c->frames_mode ? nullptr : c->d_sym;
-  uint4* const d_rec = c->frames_mode ? reinterpret_cast<uint4*>(c->d_sym) : nullptr;
-  int* const d_dcount = c->frames_mode ? c->d_dcount + size_t(fb) * 3 * c->max_batch * c->nslices : nullptr;
-  int64_t* const d_dbase = c->frames_mode ? c->d_dbase + size_t(fb) * c->max_batch * c->nslices : nullptr;
+  // walk records / chunk bits: set fb when there are two sets
+  const bool rec1 = c->frames_mode && c->two_rec && fb == 1;
+  uint4* const d_rec = c->frames_mode ? (rec1 ? c->d_rec2 : reinterpret_cast<uint4*>(c->d_sym)) : nullptr;
+  uint32_t* const d_cbits = rec1 ? c->d_cbits2 : c->d_cbits;
+  int* const d_dcount = c->frames_mode ? c->d_dcount + size_t(t3) * 3 * c->max_batch * c->nslices : nullptr;
+  int64_t* const d_dbase = c->frames_mode ? c->d_dbase + size_t(t3) * c->max_batch * c->nslices : nullptr;
   sa.sym = d_sym;
   sa.frame_samples = c->frame_samples;
 
@@ -1004,32 +1081,32 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   if (c->frames_mode) {
     // symbols of every frame, the decision layout, the states walk, then all
     // (frame, slice) streams at once
-    std::vector<int> ident(n);
-    for (int i = 0; i < n; i++) ident[i] = i;
-    HIP_TRY(hipMemcpyAsync(c->d_slot_frames, ident.data(), sizeof(int) * n, hipMemcpyHostToDevice, st));
-    sa.frame_of_slot = c->d_slot_frames;
+    sa.frame_of_slot = c->d_ident;
     sa.nslots = n;
     sa.dcount = d_dcount;  // accumulated by the symbols blocks of each plane
-    HIP_TRY(hipMemsetAsync(d_dcount, 0, sizeof(int) * 3 * size_t(n) * c->nslices, st));
+    HIP_TRY(hipMemsetAsync(d_dcount, 0, sizeof(int) * 3 * size_t(n) * c->nslices, sst));
     sa.rec = d_rec;
-    sa.cbits = c->d_cbits;
-    // the previous batch's bits kernel (its own stream) has read the chunk bits
-    HIP_TRY(hipStreamWaitEvent(st, c->bitsed[fb ^ 1], 0));
+    sa.cbits = d_cbits;
+    // one set: the previous batch's bits kernel (its own stream) has read the chunk bits
+    if (sst == st) HIP_TRY(hipStreamWaitEvent(st, c->bitsed[fb ^ 1], 0));
     sa.frame_chunks = c->frame_chunks;
-    if (timed(0, st, [&] { return launch_symbols(sa, st); }) < 0)
+    if (timed(0, sst, [&] { return launch_symbols(sa, sst); }) < 0)
       return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
-    if (timed(4, st, [&] { return launch_layout(d_dcount, n * c->nslices, d_dbase, c->d_dtotal + fb, st); }) < 0)
+    if (timed(4, sst, [&] { return launch_layout(d_dcount, n * c->nslices, d_dbase, c->d_dtotal + t3, sst); }) < 0)
       return set_err(-5, "layout launch failed: %s", hipGetErrorString(hipGetLastError()));
     // decisions of this batch: the worst case fits without asking the device
     int64_t need = int64_t(n) * c->frame_samples * c->wmax + int64_t(n) * c->nslices * kStreamSlack;
     if (need > c->dcap[fb]) {
-      HIP_TRY(hipMemcpyAsync(c->h_dtotal + fb, c->d_dtotal + fb, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipStreamSynchronize(st));  // also: set fb's previous coder is done (waited above)
-      need = c->h_dtotal[fb];
+      HIP_TRY(hipMemcpyAsync(c->h_dtotal + t3, c->d_dtotal + t3, sizeof(int64_t), hipMemcpyDeviceToHost, sst));
+      HIP_TRY(hipStreamSynchronize(sst));
+      HIP_TRY(hipEventSynchronize(c->coded[fb]));  // set fb's previous coder is done
+      need = c->h_dtotal[t3];
       if (need > c->dcap[fb] && grow_decisions(c, fb, need + need / 8) < 0)
         return set_err(-12, "decision buffers for %lld decisions: %s", (long long)need, g_err);
     }
-    HIP_TRY(hipMemsetAsync(c->d_bits[fb], 0, size_t((need + 31) / 32) * 4, st));
+    HIP_TRY(hipEventRecord(c->laid[fb], sst));  // the records and the stream layout: the walk may start
+    if (sst != st) HIP_TRY(hipStreamWaitEvent(sst, c->coded[fb], 0));  // d_bits[fb]: the coder of batch k-2
+    HIP_TRY(hipMemsetAsync(c->d_bits[fb], 0, size_t((need + 31) / 32) * 4, sst));
     DecisionStream ds{d_dcount, d_dbase, c->d_pre[fb], c->d_bits[fb]};
     BitsArgs ba{};
     ba.cbits = sa.cbits;
@@ -1049,15 +1126,16 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       if (!e) return 0;
       return std::strcmp(e, "inline") == 0 ? 1 : std::strcmp(e, "code") == 0 ? 2 : 0;
     }();
-    hipStream_t const bst = serial || bits_mode == 1 ? st : bits_mode == 2 ? cst : c->bits_stream;
-    HIP_TRY(hipEventRecord(c->laid[fb], st));
-    HIP_TRY(hipStreamWaitEvent(bst, c->laid[fb], 0));
+    hipStream_t const bst = sst != st ? sst : serial || bits_mode == 1 ? st : bits_mode == 2 ? cst : c->bits_stream;
+    if (sst == st) HIP_TRY(hipEventRecord(c->laid[fb], st));  // after the bits memset
+    if (bst != sst) HIP_TRY(hipStreamWaitEvent(bst, c->laid[fb], 0));
+    if (sst != st) HIP_TRY(hipStreamWaitEvent(st, c->laid[fb], 0));
     if (timed(5, bst, [&] { return launch_bits(ba, bst); }) < 0)
       return set_err(-5, "bits launch failed: %s", hipGetErrorString(hipGetLastError()));
     HIP_TRY(hipEventRecord(c->bitsed[fb], bst));
     WalkArgs wa{};
     wa.rec = d_rec;
-    wa.cbits = sa.cbits;
+    wa.cbits = d_cbits;
     wa.frame_chunks = c->frame_chunks;
     wa.frame_samples = c->frame_samples;
     wa.geom = c->d_geom;
@@ -1081,8 +1159,23 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       HIP_TRY(hipMemsetAsync(d_dbg, 0, sizeof(uint64_t) * 4 * nblk, st));
       wa.dbg = d_dbg;
     }
-    if (timed(2, st, [&] { return launch_walk(wa, nsegs, st); }) < 0)
+    // split schedule: the first part is what the CUs hold at once
+    // (FFV1HIP_WALK_SPLIT=0: one launch); one timed region either way
+    static const bool split_env = !(std::getenv("FFV1HIP_WALK_SPLIT") && std::atoi(std::getenv("FFV1HIP_WALK_SPLIT")) == 0);
+    const int nitems = walk_items(nsegs, c->nslices);
+    const int first = sst != st && split_env ? walk_resident(wa) : 0;
+    // ... and only when the second part leaves room on the CUs for the
+    // symbols beside it (c3: 576 of 768 slots; c5's 768 of 768 ran slower)
+    const bool two_parts = first > 0 && first < nitems && int64_t(nitems - first) * 5 <= int64_t(first) * 4;
+    if (timed(2, st, [&] {
+          if (!two_parts) return launch_walk(wa, nsegs, st);
+          if (launch_walk(wa, nsegs, st, 0, first) < 0) return -1;
+          if (hipEventRecord(c->walk_a, st) != hipSuccess) return -1;
+          return launch_walk(wa, nsegs, st, first, -1);
+        }) < 0)
       return set_err(-5, "walk launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (!two_parts) HIP_TRY(hipEventRecord(c->walk_a, st));
+    c->walk_a_valid = sst != st;
     StatsArgs sta{};
     if (c->pass == 1) {  // slot counts from the records, before the next batch's symbols rewrite them
       sta.rec = d_rec;
@@ -1180,7 +1273,9 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev[2], cst));
   if (c->frames_mode) {
     HIP_TRY(hipEventRecord(c->coded[fb], cst));
+    HIP_TRY(hipEventRecord(c->coded3[t3], cst));
     c->buf ^= 1;
+    c->tri = (c->tri + 1) % 3;
   }
   HIP_TRY(hipEventRecord(c->dep_ev, st));  // frames mode: after the states walk
   HIP_TRY(hipEventRecord(c->done_ev, cst));
@@ -1240,6 +1335,8 @@ int ffv1hip_fetch(ffv1hip_ctx* c, uint8_t* out, int64_t out_cap, int64_t* sizes,
     c->have_states = L.have0;
     c->pcur = L.pcur0;
     c->buf = L.buf0;
+    c->tri = L.tri0;
+    c->walk_a_valid = false;
     c->gob_count = L.gob0;
     if (c->pass == 1)
       HIP_TRY(hipMemcpy(c->d_rcstat, c->d_rcstat_bak, sizeof(unsigned long long) * (512 + size_t(64) * c->contexts),

@@ -185,6 +185,7 @@ struct WalkArgs {
   uint64_t* dbg;              // optional [block][4] cycle counters (FFV1HIP_WALKDBG)
   int force_multi;            // measurement hook: every chunk on the checked (multi) step
   const uint8_t* init;        // 2-pass initial states [contexts][32] at keyframes, or null (all 128)
+  int nitems, item0;          // set by launch_walk: all items of the batch, the launch's first
 };
 
 // Kernel 2b: the decision bits, from the chunks' packed words to their place
@@ -259,7 +260,11 @@ int64_t decode_lds_bytes(const DecodeArgs& a, bool global_states);
 int launch_symbols(const SymbolArgs& a, void* stream);
 int launch_code(const CodeArgs& a, void* stream);
 int launch_layout(const int* dcount, int nstreams, int64_t* dbase, int64_t* total, void* stream);
-int launch_walk(const WalkArgs& a, int nsegs, void* stream);
+// items [first, first + count) of the batch's walk (count < 0: to the end)
+int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first = 0, int count = -1);
+int walk_items(int nsegs, int nslices);
+int walk_resident(const WalkArgs& a);
+int launch_delay(int us, void* stream);
 int launch_dcode(const CodeArgs& a, void* stream);
 int launch_sink(const CodeArgs& a, void* stream);
 int launch_bits(const BitsArgs& a, void* stream);

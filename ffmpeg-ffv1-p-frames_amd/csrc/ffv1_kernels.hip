@@ -1290,12 +1290,15 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   // the longer plane group's chains first (luma at 4:2:0, twice as long as
   // chroma; chroma at 4:4:4, where Cb and Cr make one chain twice luma's);
   // the shorter ones then fill the CUs as those waves finish
-  const int nblk = gridDim.x / 2;
+  // item = (plane group, segment, slice pair): the launch may cover a part
+  // of the items (launch_walk's first / count)
+  const int item = (int)blockIdx.x + a.item0;
+  const int nblk = a.nitems / 2;
   const SliceGeom& g0 = a.geom[0];
   const bool chroma_first = 2 * (int64_t)g0.pw[1] * g0.ph[1] > (int64_t)g0.pw[0] * g0.ph[0];
-  const int grp = ((int)blockIdx.x >= nblk) != chroma_first;
+  const int grp = (item >= nblk) != chroma_first;
   const int npairs = (a.nslices + 1) / 2;
-  const int bi = (int)blockIdx.x - ((int)blockIdx.x >= nblk ? nblk : 0);
+  const int bi = item - (item >= nblk ? nblk : 0);
   const int seg_i = bi / npairs, pair = bi % npairs;
   const Segment seg = a.segs[seg_i];
   const int sl = 2 * pair + h;              // this half's slice
@@ -1510,9 +1513,9 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
     for (int64_t i = k; i < n16; i += 32) dst[i] = t4[i];
   }
   if (a.dbg && lane == 0) {
-    a.dbg[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memtime() - t_all;
-    a.dbg[blockIdx.x * 4 + 1] = t_loop;
-    a.dbg[blockIdx.x * 4 + 2] = n_steps;
+    a.dbg[item * 4 + 0] = __builtin_amdgcn_s_memtime() - t_all;
+    a.dbg[item * 4 + 1] = t_loop;
+    a.dbg[item * 4 + 2] = n_steps;
   }
 }
 
@@ -2038,15 +2041,46 @@ int launch_dcode(const CodeArgs& a, void* stream) {
 
 int64_t walk_lds_bytes(int64_t state_bytes) { return walk_lds_bytes_dev(state_bytes); }
 
-int launch_walk(const WalkArgs& a, int nsegs, void* stream) {
+int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first, int count) {
   if (walk_lds_bytes_dev(a.state_bytes) > kWalkLdsMax) return -1;
   size_t dyn = (size_t)(2 * (a.state_bytes / 2 + 32));  // the tables; the fixed part is static
   // FFV1HIP_WALK_LDS_PAD (measurement hook): extra LDS per walk wave, to
   // run the walk at a lower occupancy
   static const long pad = std::getenv("FFV1HIP_WALK_LDS_PAD") ? std::atol(std::getenv("FFV1HIP_WALK_LDS_PAD")) : 0;
   dyn += (size_t)pad;
-  dim3 grid((unsigned)(nsegs * ((a.nslices + 1) / 2) * 2)), block(kWalkThreads);
-  hipLaunchKernelGGL(ffv1_walk, grid, block, dyn, reinterpret_cast<hipStream_t>(stream), a);
+  WalkArgs b = a;
+  b.nitems = nsegs * ((a.nslices + 1) / 2) * 2;
+  if (count < 0) count = b.nitems - first;
+  if (first < 0 || count <= 0 || first + count > b.nitems) return count == 0 ? 0 : -1;
+  b.item0 = first;
+  hipLaunchKernelGGL(ffv1_walk, dim3((unsigned)count), dim3(kWalkThreads), dyn, reinterpret_cast<hipStream_t>(stream), b);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int walk_items(int nsegs, int nslices) { return nsegs * ((nslices + 1) / 2) * 2; }
+
+// Walk waves one CU holds at once (LDS-bound), for launch splitting.
+int walk_resident(const WalkArgs& a) {
+  const size_t dyn = (size_t)(2 * (a.state_bytes / 2 + 32));
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ffv1_walk, kWalkThreads, dyn) != hipSuccess ||
+      hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return per_cu * cus;
+}
+
+// A one-wave wait of `us` microseconds (s_memrealtime: 100 MHz), in front of
+// a kernel that should start only after the kernels that became ready with
+// it have their waves on the CUs.
+__global__ __launch_bounds__(64) void ffv1_delay(int64_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
+int launch_delay(int us, void* stream) {
+  hipLaunchKernelGGL(ffv1_delay, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), (int64_t)us * 100);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
