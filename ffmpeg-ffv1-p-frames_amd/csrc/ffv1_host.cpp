@@ -1149,6 +1149,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     wa.scratch = c->d_scratch;
     static const bool force_multi = std::getenv("FFV1HIP_FORCE_MULTI") && std::atoi(std::getenv("FFV1HIP_FORCE_MULTI"));
     wa.force_multi = force_multi;
+    static const int walk_prio = std::getenv("FFV1HIP_WALK_PRIO") ? std::atoi(std::getenv("FFV1HIP_WALK_PRIO")) : 2;
+    wa.prio = walk_prio;
     wa.init = c->d_init;
     // FFV1HIP_WALKDBG=1 (measurement hook): per-block cycle split to stderr
     static const bool walkdbg = std::getenv("FFV1HIP_WALKDBG") && std::atoi(std::getenv("FFV1HIP_WALKDBG"));
@@ -1211,6 +1213,9 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     HIP_TRY(hipStreamWaitEvent(cst, c->bitsed[fb], 0));
     if (c->pass == 1 && launch_stats(sta, true, cst) < 0) return set_err(-5, "stats launch failed");
     ca.nframes = n;
+    static const int code_prio =
+        std::getenv("FFV1HIP_CODE_WAVE_PRIO") ? std::atoi(std::getenv("FFV1HIP_CODE_WAVE_PRIO")) : 0;
+    ca.prio = code_prio;
     ca.nopsets = c->nopsets;
     ca.opsets = c->d_opsets;
     ca.ds = ds;

@@ -145,6 +145,7 @@ struct CodeArgs {
   int nopsets;                // decision-stream mode: op sets the header programs use
   DecisionStream ds;
   uint64_t* dbg;              // optional [wave][4] cycle counters (FFV1HIP_CODEDBG)
+  int prio;                   // ffv1_dcode's wave priority (s_setprio)
   uint8_t* opsets;            // decision-stream mode: [stream][nopsets * 32] header op states
   const uint8_t* init;        // chained range coder: 2-pass initial states [contexts][32], or null
 };
@@ -186,6 +187,7 @@ struct WalkArgs {
   int force_multi;            // measurement hook: every chunk on the checked (multi) step
   const uint8_t* init;        // 2-pass initial states [contexts][32] at keyframes, or null (all 128)
   int nitems, item0;          // set by launch_walk: all items of the batch, the launch's first
+  int prio;                   // wave priority (s_setprio)
 };
 
 // Kernel 2b: the decision bits, from the chunks' packed words to their place

@@ -922,6 +922,12 @@ __host__ __device__ constexpr size_t dcode_lds_bytes(int /*nopsets*/) {
 
 __global__ __launch_bounds__(kCodeThreads) void ffv1_dcode(CodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  switch (a.prio) {  // wave priority against the walk beside it (FFV1HIP_CODE_WAVE_PRIO, default 0)
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    case 3: __builtin_amdgcn_s_setprio(3); break;
+    default: break;
+  }
   const int osb = a.nopsets * 32;
   const uint8_t* const tabs = a.tabs;
   uint32_t* const ring = reinterpret_cast<uint32_t*>(lds);
@@ -1361,7 +1367,12 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
 
   // the walk is the longer of the two pipelines it overlaps with (the coder
   // of the previous batch): it wins the VALU arbitration on a shared SIMD
-  __builtin_amdgcn_s_setprio(2);
+  switch (a.prio) {  // wave priority (FFV1HIP_WALK_PRIO, default 2)
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 3: __builtin_amdgcn_s_setprio(3); break;
+    default: __builtin_amdgcn_s_setprio(2); break;
+  }
 #ifdef FFV1_WALK_FAT
   // the whole register file of a SIMD: no other wave shares this one's SIMD
   asm volatile("" ::: "v255", "a255");
