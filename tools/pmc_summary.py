@@ -44,15 +44,24 @@ def main(tag, frames_per_launch, config, out_name="pmc_traffic_rNN.json"):
         f2 = 2.0 * fetch.get(k, 0.0)
         w = write.get(k, 0.0)
         kernels[k] = {"fetch_bytes_x2": int(f2), "write_bytes": int(w), "hbm_bytes": int(f2 + w)}
-    stats = {}
+    stats, calls = {}, {}
     for r in csv.DictReader(open(os.path.join(dst, f"{tag}_kernel_stats.csv"))):
         stats[short(r["Name"])] = float(r["AverageNs"]) / 1e6
+        calls[short(r["Name"])] = int(r["Calls"])
+    # launches per step: the split schedule launches the walk in two parts
+    per_step = calls.get("ffv1_dcode", 0)
+    for k, v in kernels.items():
+        n = max(1, round(calls.get(k, per_step) / per_step)) if per_step else 1
+        v["launches_per_step"] = n
+        v["hbm_bytes_per_step"] = v["hbm_bytes"] * n
     out = {
         "tag": tag, "config": config, "frames_per_launch": frames_per_launch,
         "note": "per-launch means over the profiled bench run; FETCH_SIZE doubled (gfx950), WRITE_SIZE as is",
         "kernels": kernels,
         "rocprof_avg_ms": stats,
         "encode_hbm_bytes_per_launch": kernels.get("ffv1_dcode", {}).get("hbm_bytes"),
+        "encode_hbm_bytes_per_step": sum(v["hbm_bytes_per_step"] for k, v in kernels.items()
+                                         if k != "ffv1_decode_slices"),
     }
     json.dump(out, open(os.path.join(dst, out_name), "w"), indent=1)
     print(json.dumps(out, indent=1))
