@@ -1165,10 +1165,14 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     // (FFV1HIP_WALK_SPLIT=0: one launch); one timed region either way
     static const bool split_env = !(std::getenv("FFV1HIP_WALK_SPLIT") && std::atoi(std::getenv("FFV1HIP_WALK_SPLIT")) == 0);
     const int nitems = walk_items(nsegs, c->nslices);
-    const int first = sst != st && split_env ? walk_resident(wa) : 0;
+    // FFV1HIP_WALK_PART_A (test hook, read per batch): the first part's waves
+    const char* pa = std::getenv("FFV1HIP_WALK_PART_A");
+    const int first = sst != st && split_env ? (pa ? std::atoi(pa) : walk_resident(wa)) : 0;
     // ... and only when the second part leaves room on the CUs for the
     // symbols beside it (c3: 576 of 768 slots; c5's 768 of 768 ran slower)
-    const bool two_parts = first > 0 && first < nitems && int64_t(nitems - first) * 5 <= int64_t(first) * 4;
+    // (FFV1HIP_SPLIT_MAX: that share in percent, default 80)
+    const int split_max = std::getenv("FFV1HIP_SPLIT_MAX") ? std::atoi(std::getenv("FFV1HIP_SPLIT_MAX")) : 80;
+    const bool two_parts = first > 0 && first < nitems && int64_t(nitems - first) * 100 <= int64_t(first) * split_max;
     if (timed(2, st, [&] {
           if (!two_parts) return launch_walk(wa, nsegs, st);
           if (launch_walk(wa, nsegs, st, 0, first) < 0) return -1;

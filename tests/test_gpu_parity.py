@@ -75,6 +75,21 @@ def test_chained_coder_matches_oracle(stream, monkeypatch):
     assert got == ref
 
 
+@pytest.mark.parametrize("stream", [s for s in PARITY_STREAMS if s.coder != 0 and s.gop_size != 1][:4],
+                         ids=[s.name for s in PARITY_STREAMS if s.coder != 0 and s.gop_size != 1][:4])
+def test_split_walk_matches_oracle(stream, monkeypatch):
+    """The split schedule with a walk in two launches (first part 3 waves,
+    forced by the test hooks) and the next batch's symbols beside its second
+    part: the same bytes as the oracle across batches."""
+    monkeypatch.setenv("FFV1HIP_WALK_PART_A", "3")
+    monkeypatch.setenv("FFV1HIP_SPLIT_MAX", "100000")
+    frames = list(stream.frames())
+    _, ex_ref, ref = oracle_encode(stream, frames)
+    ex, got = hip_encode(stream, frames, batch=4)
+    assert ex == ex_ref
+    assert got == ref
+
+
 def test_whole_batch_equals_split_batches():
     s = PARITY_STREAMS[1]
     frames = list(s.frames())
