@@ -301,6 +301,13 @@ struct ffv1hip_ctx {
   hipEvent_t entry[2] = {nullptr, nullptr};  // set k's batch: the launch stream's work so far
   hipEvent_t walk_a = nullptr;               // the first part of the last batch's walk is done
   bool walk_a_valid = false;
+  // With one records set the same overlap is partial: the next batch's
+  // symbols beside part B skip the plane group and frames part B reads
+  // (frames from part_b_f0 of group part_b_grp, all groups when part_b_all);
+  // those run on the walk's stream after part B
+  int part_b_f0 = 0, part_b_grp = 0;
+  bool part_b_all = true;
+  hipEvent_t zeroed = nullptr, sym1 = nullptr;  // the stream counts are zeroed / part 1 of the symbols is done
   SliceGeom* d_geom = nullptr;
   int* d_slot_frames = nullptr;  // [j][slot]
   int* d_status = nullptr;       // [set][4]: [0] slices over budget, [1] most bytes one needed
@@ -597,6 +604,8 @@ static void free_device(ffv1hip_ctx* c) {
   for (hipEvent_t& e : c->entry)
     if (e) (void)hipEventDestroy(e);
   if (c->walk_a) (void)hipEventDestroy(c->walk_a);
+  if (c->zeroed) (void)hipEventDestroy(c->zeroed);
+  if (c->sym1) (void)hipEventDestroy(c->sym1);
 }
 
 // Decision-stream buffers of set k for `need` decisions.  The set's previous
@@ -661,6 +670,8 @@ static int alloc_device(ffv1hip_ctx* c) {
     for (hipEvent_t& e : c->coded3) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->entry) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->walk_a, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->zeroed, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->sym1, hipEventDisableTiming));
     {
       std::vector<int> ident(nb);
       for (int i = 0; i < nb; i++) ident[i] = i;
@@ -961,8 +972,17 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   // FFV1HIP_SERIAL=1 (measurement hook): no walk/code overlap
   static const bool serial = std::getenv("FFV1HIP_SERIAL") && std::atoi(std::getenv("FFV1HIP_SERIAL"));
   hipStream_t const cst = c->frames_mode && !serial ? c->code_stream : st;
-  // the split schedule: symbols, layout and bits on the bits stream
-  hipStream_t const sst = c->frames_mode && c->two_rec && !serial ? c->bits_stream : st;
+  // the split schedule: symbols, layout and bits on the bits stream; with one
+  // records set (part), the symbols the previous batch's walk part B does
+  // not read on the bits stream, the rest and the layout on st after the walk
+  // (not in pass 1, whose slot counts read all of a batch's records after
+  // its walk).  Off unless FFV1HIP_PARTIAL=1 (read per batch): measured
+  // slower (c4 5.7 -> 4.9, c3 with one set 11.6 -> 10.9 Gpix/s), the walk's
+  // second part slows beside the symbols
+  const bool part_env = std::getenv("FFV1HIP_PARTIAL") && std::atoi(std::getenv("FFV1HIP_PARTIAL")) == 1;
+  const bool part = c->frames_mode && !c->two_rec && !serial && c->pass != 1 && part_env;
+  hipStream_t const sst = c->frames_mode && (c->two_rec || part) && !serial ? c->bits_stream : st;
+  hipStream_t const lst = part ? st : sst;  // the layout's stream
   if (sst != st) {
     // the caller's work on st so far (the frames), then what the symbols
     // rewrite: records set fb (read by the walk of batch k-2) and metadata
@@ -1090,21 +1110,49 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     // one set: the previous batch's bits kernel (its own stream) has read the chunk bits
     if (sst == st) HIP_TRY(hipStreamWaitEvent(st, c->bitsed[fb ^ 1], 0));
     sa.frame_chunks = c->frame_chunks;
-    if (timed(0, sst, [&] { return launch_symbols(sa, sst); }) < 0)
-      return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
-    if (timed(4, sst, [&] { return launch_layout(d_dcount, n * c->nslices, d_dbase, c->d_dtotal + t3, sst); }) < 0)
+    if (!part) {
+      if (timed(0, sst, [&] { return launch_symbols(sa, sst); }) < 0)
+        return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
+    } else {
+      // part 1 on the bits stream: the plane group part B does not read, and
+      // part B's group in the frames before part_b_f0; part 2 on st
+      const int np = p.chroma_planes ? 3 : 1;
+      const int f0 = c->part_b_all ? 0 : std::min(n, c->part_b_f0);
+      const int g2 = c->part_b_grp;
+      const int g2lo = g2 ? 1 : 0, g2hi = g2 ? np : 1;  // planes of the group part B reads
+      const int g1lo = g2 ? 0 : 1, g1hi = g2 ? 1 : np;
+      auto launch_part = [&](hipStream_t q, int plo, int phi, int flo, int fhi) -> int {
+        if (phi <= plo || fhi <= flo) return 0;
+        SymbolArgs b = sa;
+        b.p_lo = plo;
+        b.p_hi = phi;
+        b.frame_of_slot = c->d_ident + flo;
+        b.nslots = fhi - flo;
+        return timed(0, q, [&] { return launch_symbols(b, q); });
+      };
+      HIP_TRY(hipEventRecord(c->zeroed, sst));
+      if ((c->part_b_all ? 0 : launch_part(sst, g1lo, g1hi, 0, n)) < 0 || launch_part(sst, g2lo, g2hi, 0, f0) < 0)
+        return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
+      HIP_TRY(hipEventRecord(c->sym1, sst));
+      HIP_TRY(hipStreamWaitEvent(st, c->zeroed, 0));
+      if ((c->part_b_all ? launch_part(st, 0, np, 0, n) : launch_part(st, g2lo, g2hi, f0, n)) < 0)
+        return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
+      HIP_TRY(hipStreamWaitEvent(st, c->sym1, 0));
+    }
+    if (timed(4, lst, [&] { return launch_layout(d_dcount, n * c->nslices, d_dbase, c->d_dtotal + t3, lst); }) < 0)
       return set_err(-5, "layout launch failed: %s", hipGetErrorString(hipGetLastError()));
     // decisions of this batch: the worst case fits without asking the device
     int64_t need = int64_t(n) * c->frame_samples * c->wmax + int64_t(n) * c->nslices * kStreamSlack;
     if (need > c->dcap[fb]) {
-      HIP_TRY(hipMemcpyAsync(c->h_dtotal + t3, c->d_dtotal + t3, sizeof(int64_t), hipMemcpyDeviceToHost, sst));
-      HIP_TRY(hipStreamSynchronize(sst));
+      HIP_TRY(hipMemcpyAsync(c->h_dtotal + t3, c->d_dtotal + t3, sizeof(int64_t), hipMemcpyDeviceToHost, lst));
+      HIP_TRY(hipStreamSynchronize(lst));
       HIP_TRY(hipEventSynchronize(c->coded[fb]));  // set fb's previous coder is done
       need = c->h_dtotal[t3];
       if (need > c->dcap[fb] && grow_decisions(c, fb, need + need / 8) < 0)
         return set_err(-12, "decision buffers for %lld decisions: %s", (long long)need, g_err);
     }
-    HIP_TRY(hipEventRecord(c->laid[fb], sst));  // the records and the stream layout: the walk may start
+    HIP_TRY(hipEventRecord(c->laid[fb], lst));  // the records and the stream layout: the walk may start
+    if (lst != sst) HIP_TRY(hipStreamWaitEvent(sst, c->laid[fb], 0));
     if (sst != st) HIP_TRY(hipStreamWaitEvent(sst, c->coded[fb], 0));  // d_bits[fb]: the coder of batch k-2
     HIP_TRY(hipMemsetAsync(c->d_bits[fb], 0, size_t((need + 31) / 32) * 4, sst));
     DecisionStream ds{d_dcount, d_dbase, c->d_pre[fb], c->d_bits[fb]};
@@ -1182,6 +1230,17 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       return set_err(-5, "walk launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (!two_parts) HIP_TRY(hipEventRecord(c->walk_a, st));
     c->walk_a_valid = sst != st;
+    // what part B reads, for the next batch's partial split: items from nblk
+    // on are the second-dispatched plane group, segment by segment
+    {
+      const int nblk = nitems / 2, npairs = (c->nslices + 1) / 2;
+      const bool chroma_first = 2 * int64_t(c->geom[0].pw[1]) * c->geom[0].ph[1] >
+                                int64_t(c->geom[0].pw[0]) * c->geom[0].ph[0];
+      c->part_b_all = two_parts && first < nblk;
+      c->part_b_grp = chroma_first ? 0 : 1;
+      c->part_b_f0 = !two_parts ? n : segs[std::min(nsegs - 1, (first - nblk) / npairs)].first_frame;
+      if (two_parts && first >= nblk && !(p.chroma_planes) && c->part_b_grp == 1) c->part_b_f0 = n;
+    }
     StatsArgs sta{};
     if (c->pass == 1) {  // slot counts from the records, before the next batch's symbols rewrite them
       sta.rec = d_rec;
@@ -1346,6 +1405,7 @@ int ffv1hip_fetch(ffv1hip_ctx* c, uint8_t* out, int64_t out_cap, int64_t* sizes,
     c->buf = L.buf0;
     c->tri = L.tri0;
     c->walk_a_valid = false;
+    c->part_b_all = true;
     c->gob_count = L.gob0;
     if (c->pass == 1)
       HIP_TRY(hipMemcpy(c->d_rcstat, c->d_rcstat_bak, sizeof(unsigned long long) * (512 + size_t(64) * c->contexts),

@@ -76,6 +76,7 @@ struct SymbolArgs {
   uint4* rec;                 // optional, instead of sym: [slot][frame_samples] walk records
   uint32_t* cbits;            // with rec: [slot][frame_chunks][kChunkWords]
   int64_t frame_chunks;
+  int p_lo, p_hi;             // planes of this launch (p_hi 0: all); with rec, outputs by batch frame
 };
 
 // Walk record of one sample (frame-parallel mode), written by ffv1_symbols.

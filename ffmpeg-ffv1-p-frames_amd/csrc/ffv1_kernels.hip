@@ -171,10 +171,13 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   for (int i = threadIdx.x; i < 5 * 256; i += kSymThreads) qt[i] = a.qt[i];
   __syncthreads();
   // a plane of a slice is split into kSymSplit runs of whole 256-sample steps
-  const int slice = blockIdx.x, slot = blockIdx.y, p = blockIdx.z / kSymSplit, part = blockIdx.z % kSymSplit;
+  const int slice = blockIdx.x, slot = blockIdx.y, p = a.p_lo + blockIdx.z / kSymSplit, part = blockIdx.z % kSymSplit;
   const int f = a.frame_of_slot[slot];
   if (f < 0 || p >= a.nplanes) return;
-  int* const count = a.dcount ? a.dcount + ((int64_t)slot * a.nslices + slice) * 3 + p : nullptr;  // zeroed
+  // frames mode (walk records): the outputs are indexed by batch frame (a
+  // launch may cover a subset of the frames)
+  const int fs = a.rec ? f : slot;
+  int* const count = a.dcount ? a.dcount + ((int64_t)fs * a.nslices + slice) * 3 + p : nullptr;  // zeroed
   const SliceGeom& g = a.geom[slice];
   const int pw = g.pw[p], ph = g.ph[p], px = g.px[p], py = g.py[p];
   const uint8_t* base = a.frames + (int64_t)f * a.frame_bytes + a.plane_off[p];
@@ -204,10 +207,10 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   const int64_t span = (n + kSymSplit * kSymThreads - 1) / (kSymSplit * kSymThreads) * kSymThreads;
   const int64_t b0 = part * span, b1 = min(n, b0 + span);
   const int lane = threadIdx.x & (kWave - 1);
-  uint4* const rec = a.rec ? a.rec + (int64_t)slot * a.frame_samples + g.sym_off + g.plane_sym_off[p] : nullptr;
+  uint4* const rec = a.rec ? a.rec + (int64_t)fs * a.frame_samples + g.sym_off + g.plane_sym_off[p] : nullptr;
   // the plane's chunk headers (read once: a reload inside the loop would
   // wait for the record stores)
-  uint32_t* const cbase = rec ? a.cbits + ((int64_t)slot * a.frame_chunks + g.chunk_off[p]) * kChunkWords : nullptr;
+  uint32_t* const cbase = rec ? a.cbits + ((int64_t)fs * a.frame_chunks + g.chunk_off[p]) * kChunkWords : nullptr;
   // the lane's sample, stepped along the plane without a division per step
   int cy = (int)((b0 + threadIdx.x) / pw), cx = (int)((b0 + threadIdx.x) - (int64_t)cy * pw);
   // whole waves per step: a wave's 64 consecutive samples are one walk chunk
@@ -2021,7 +2024,9 @@ __global__ __launch_bounds__(kAsmThreads) void ffv1_assemble_packets(AssembleArg
 }  // namespace
 
 int launch_symbols(const SymbolArgs& a, void* stream) {
-  dim3 grid(a.nslices, a.nslots, a.nplanes * kSymSplit), block(kSymThreads);
+  const int np = a.p_hi > a.p_lo ? a.p_hi - a.p_lo : a.nplanes - a.p_lo;
+  if (np <= 0 || a.nslots <= 0) return 0;
+  dim3 grid(a.nslices, a.nslots, np * kSymSplit), block(kSymThreads);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (a.sample_bytes == 1 && !a.rgb)
     hipLaunchKernelGGL((ffv1_symbols<1, false>), grid, block, 0, st, a);

@@ -75,12 +75,16 @@ def test_chained_coder_matches_oracle(stream, monkeypatch):
     assert got == ref
 
 
+@pytest.mark.parametrize("recsets", [2, 1])
 @pytest.mark.parametrize("stream", [s for s in PARITY_STREAMS if s.coder != 0 and s.gop_size != 1][:4],
                          ids=[s.name for s in PARITY_STREAMS if s.coder != 0 and s.gop_size != 1][:4])
-def test_split_walk_matches_oracle(stream, monkeypatch):
+def test_split_walk_matches_oracle(stream, recsets, monkeypatch):
     """The split schedule with a walk in two launches (first part 3 waves,
     forced by the test hooks) and the next batch's symbols beside its second
-    part: the same bytes as the oracle across batches."""
+    part (two records sets: all of them; one set: those part B does not read,
+    the rest after it): the same bytes as the oracle across batches."""
+    monkeypatch.setenv("FFV1HIP_RECSETS", str(recsets))
+    monkeypatch.setenv("FFV1HIP_PARTIAL", "1")
     monkeypatch.setenv("FFV1HIP_WALK_PART_A", "3")
     monkeypatch.setenv("FFV1HIP_SPLIT_MAX", "100000")
     frames = list(stream.frames())

@@ -1,14 +1,13 @@
 #!/bin/bash
-# Equal wave priorities; larger c3 batches with the split forced (under gpurun).
+# Partial split (one records set): GPU suite, then c4 / c3 benches (under gpurun).
 set -o pipefail
-O=gpurun_out/prio5
+O=gpurun_out/part
 mkdir -p $O
-B="python bench.py --no-cpu-baseline --no-decode-check --steps 10"
-run() { local tag=$1; shift; timeout -k 10 240 env "$@" $B $EXTRA > $O/$tag.json 2> $O/$tag.err || exit 1; }
-EXTRA="" run base FFV1HIP_WALK_PRIO=2
-EXTRA="" run w1c1 FFV1HIP_WALK_PRIO=1 FFV1HIP_CODE_WAVE_PRIO=1
-EXTRA="" run w2c2 FFV1HIP_CODE_WAVE_PRIO=2
-EXTRA="" run w3c2 FFV1HIP_WALK_PRIO=3 FFV1HIP_CODE_WAVE_PRIO=2
-EXTRA="--gops 22" run g22 FFV1HIP_SPLIT_MAX=95
-EXTRA="--gops 23" run g23 FFV1HIP_SPLIT_MAX=95
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/tests.log 2>&1 || exit 1
+B="python bench.py --no-cpu-baseline"
+run() { local tag=$1; shift; timeout -k 10 300 env "$@" $B $EXTRA > $O/$tag.json 2> $O/$tag.err || exit 1; }
+EXTRA="--config c4" run c4 FFV1HIP_PARTIAL=1
+EXTRA="--config c4" run c4_off FFV1HIP_PARTIAL=0
+EXTRA="--no-decode-check" run c3_one FFV1HIP_RECSETS=1
+EXTRA="--no-decode-check" run c3 FFV1HIP_RECSETS=2
 echo done
