@@ -1174,9 +1174,15 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       if (!e) return 0;
       return std::strcmp(e, "inline") == 0 ? 1 : std::strcmp(e, "code") == 0 ? 2 : 0;
     }();
-    hipStream_t const bst = sst != st ? sst : serial || bits_mode == 1 ? st : bits_mode == 2 ? cst : c->bits_stream;
+    hipStream_t const bst = sst != st ? (bits_mode == 2 && !part ? cst : sst)
+                                      : serial || bits_mode == 1 ? st : bits_mode == 2 ? cst : c->bits_stream;
     if (sst == st) HIP_TRY(hipEventRecord(c->laid[fb], st));  // after the bits memset
-    if (bst != sst) HIP_TRY(hipStreamWaitEvent(bst, c->laid[fb], 0));
+    if (sst != st && bst != sst) {  // split schedule, bits on the coder stream: after the memset
+      HIP_TRY(hipEventRecord(c->zeroed, sst));
+      HIP_TRY(hipStreamWaitEvent(bst, c->zeroed, 0));
+    } else if (bst != sst) {
+      HIP_TRY(hipStreamWaitEvent(bst, c->laid[fb], 0));
+    }
     if (sst != st) HIP_TRY(hipStreamWaitEvent(st, c->laid[fb], 0));
     if (timed(5, bst, [&] { return launch_bits(ba, bst); }) < 0)
       return set_err(-5, "bits launch failed: %s", hipGetErrorString(hipGetLastError()));

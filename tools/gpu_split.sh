@@ -1,10 +1,13 @@
 #!/bin/bash
-# c5 GOPs per step with the split schedule (under gpurun).
+# Bits kernel placement under the split schedule (under gpurun).
 set -o pipefail
-O=gpurun_out/c5g
+O=gpurun_out/bitsplace
 mkdir -p $O
-B="python bench.py --no-cpu-baseline --no-decode-check --config c5"
-for g in 5 6 7; do
-  timeout -k 10 300 $B --gops $g > $O/g$g.json 2> $O/g$g.err || exit 1
-done
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 240 --timeout-method thread -k "split or config3" > $O/tests.log 2>&1 || exit 1
+B="python bench.py --no-cpu-baseline --no-decode-check"
+run() { local tag=$1; shift; timeout -k 10 240 env "$@" $B $EXTRA > $O/$tag.json 2> $O/$tag.err || exit 1; }
+EXTRA="" run side FFV1HIP_BITS=side
+EXTRA="" run code FFV1HIP_BITS=code
+EXTRA="--config c5" run c5code FFV1HIP_BITS=code
+EXTRA="--config c2" run c2code FFV1HIP_BITS=code
 echo done
