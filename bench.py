@@ -178,6 +178,56 @@ def load_traffic(frames_per_step, kernel):
     return None
 
 
+def spawn_ranks(n: int, script: str = "", argv=None) -> int:
+    """`--gpus N` without a launcher: start N copies of this script, one per
+    GPU, with the torch.distributed environment a launcher would set
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*, rendezvous on 127.0.0.1), and
+    return the worst exit code.  Runs before anything touches a GPU: this
+    process only waits for its children (started as new processes, never
+    exec'd over this one)."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        cmd = [sys.executable, script or os.path.abspath(__file__)] + list(sys.argv[1:] if argv is None else argv)
+        procs.append(subprocess.Popen(cmd, env=env))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0:
+                    rc = rc or code
+                    for q in live:  # a failed rank leaves the others waiting at a barrier
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+def load_bench_golden(name):
+    """Per-GOP oracle digests of this config's D1 clip (tests/golden/bench_gops.json,
+    tools/make_bench_golden.py), or None."""
+    path = os.path.join(ROOT, "tests", "golden", "bench_gops.json")
+    try:
+        return json.load(open(path)).get(name)
+    except (OSError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -200,9 +250,13 @@ def main():
     if args.gops <= 0:
         args.gops = CFG["GOPS"]
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: one rank per GPU expected")
 
     import torch
     from ffv1hip import HipEncoder, configure
@@ -307,6 +361,18 @@ def main():
     n_all = len(all_digest)
     first = min(n_all, CFG["GOPS"])
     digest_first = hashlib.md5("".join(all_digest[g][0] for g in range(first)).encode()).hexdigest()
+    # every timed GOP against the oracle's digest of the same GOP (the last
+    # step's packets: every step re-encodes the same batch)
+    vs_oracle = None
+    golden = load_bench_golden(args.config) if args.data == "d1" else None
+    if golden:
+        ref = golden["gops"]
+        checked = [g for g in sorted(all_digest) if g < len(ref)]
+        bad = [g for g in checked if (all_digest[g][0], all_digest[g][1]) != (ref[g]["md5"], ref[g]["bytes"])]
+        vs_oracle = {"gops_checked": len(checked), "gops_encoded": n_all,
+                     "frames_checked": len(checked) * max(GOP, 1), "equal": not bad,
+                     "first_mismatch_gop": bad[0] if bad else None,
+                     "fixture": "tests/golden/bench_gops.json (oracle, tools/make_bench_golden.py)"}
 
     # on-device lossless self-check (outside the timed region, every rank on
     # its own packets): the GPU decoder (ffv1_decode_slices)
@@ -374,6 +440,7 @@ def main():
             },
             "bits_per_pixel": round(total_out * 8 / (B * world * W * H), 4),
             "bitexact_vs_reference_pin": bitexact,
+            "bitexact_vs_oracle": vs_oracle,
             "gop_digest": {"gops": n_all, f"first_{first}_gops_md5": digest_first,
                            "note": "md5 over the per-GOP packet md5s in GOP order: the same for "
                                    "every --gpus N (GOP bytes do not depend on the rank)"},
@@ -399,6 +466,9 @@ def main():
         print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()
+    if (vs_oracle and not vs_oracle["equal"]) or bitexact is False:
+        log("bench.py: packets differ from the oracle / reference pin")
+        sys.exit(3)
 
 
 if __name__ == "__main__":

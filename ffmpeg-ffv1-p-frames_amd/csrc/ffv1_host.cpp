@@ -959,9 +959,13 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   c->last.tri0 = c->tri;
   c->last.gob0 = c->gob_count;
   for (uint8_t k : keys) c->gob_count += k;
-  if (c->pass == 1)
+  if (c->pass == 1) {
+    // the previous batch's state counts (ffv1_stats_states, on the coder
+    // stream) are in before the snapshot is taken
+    if (c->dep_valid) HIP_TRY(hipStreamWaitEvent(st, c->done_ev, 0));
     HIP_TRY(hipMemcpyAsync(c->d_rcstat_bak, c->d_rcstat, sizeof(unsigned long long) * (512 + size_t(64) * c->contexts),
                            hipMemcpyDeviceToDevice, st));
+  }
   // frames mode: the coder stream may still be on the previous batch, so the
   // buffers it reads alternate between two sets; set fb was last read by the
   // coder of batch k-2, which must be done before this batch rewrites it
@@ -1394,10 +1398,14 @@ static int grow_slice_budget(ffv1hip_ctx* c, int64_t needed) {
   return 0;
 }
 
-int ffv1hip_fetch(ffv1hip_ctx* c, uint8_t* out, int64_t out_cap, int64_t* sizes, int* key_flags) {
-  if (!c) return set_err(-22, "null ctx");
-  HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipDeviceSynchronize());
+// With the device idle: if a slice of the last batch (the one whose packets
+// d_packets holds) went over the byte budget, roll the batch back and encode
+// it again with a larger budget, so that no caller ever sees a truncated
+// slice (the reference fails a frame it cannot fit, ffv1enc.c:283-292; its
+// buffer is large enough for any slice, :1232).  Every batch reports into
+// its own status set, cleared when the batch starts, so the set read here is
+// the last batch's.
+static int settle_last_batch(ffv1hip_ctx* c) {
   for (int attempt = 0;; attempt++) {
     int status[4];
     HIP_TRY(hipMemcpy(status, c->d_status + 4 * c->last.status_set, sizeof(status), hipMemcpyDeviceToHost));
@@ -1423,6 +1431,15 @@ int ffv1hip_fetch(ffv1hip_ctx* c, uint8_t* out, int64_t out_cap, int64_t* sizes,
     if (rc < 0) return rc;
     HIP_TRY(hipDeviceSynchronize());
   }
+  return 0;
+}
+
+int ffv1hip_fetch(ffv1hip_ctx* c, uint8_t* out, int64_t out_cap, int64_t* sizes, int* key_flags) {
+  if (!c) return set_err(-22, "null ctx");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());
+  const int rc = settle_last_batch(c);
+  if (rc < 0) return rc;
   const int n = c->last_n;
   std::vector<int64_t> sz(n);
   HIP_TRY(hipMemcpy(sz.data(), c->d_packet_size, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
@@ -1446,11 +1463,14 @@ int ffv1hip_synchronize(ffv1hip_ctx* c) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (c->code_stream) HIP_TRY(hipStreamSynchronize(c->code_stream));
   if (c->bits_stream) HIP_TRY(hipStreamSynchronize(c->bits_stream));
-  return 0;
+  return settle_last_batch(c);
 }
 
 int ffv1hip_device_packets(ffv1hip_ctx* c, void** d_packets, int64_t* packet_stride, void** d_sizes) {
   if (!c) return set_err(-22, "null ctx");
+  // the packets are only valid once settled; a re-encode may also move them
+  const int rc = ffv1hip_synchronize(c);
+  if (rc < 0) return rc;
   if (d_packets) *d_packets = c->d_packets;
   if (packet_stride) *packet_stride = c->packet_stride;
   if (d_sizes) *d_sizes = c->d_packet_size;
@@ -1536,8 +1556,16 @@ int ffv1hip_encode2(ffv1hip_ctx* c, const void* const planes[3], const int strid
   *got_packet = 0;
   HIP_TRY(hipSetDevice(c->device));
   ffv1hip_ctx::Ready& R = c->ready;
+  // the packet this call hands out, if one is ready, must fit before the
+  // frame is taken (an error return leaves the queue as it was)
+  if (out && R.next < R.size.size() && R.size[R.next] > out_cap)
+    return set_err(-22, "packet of %lld bytes, buffer %lld", (long long)R.size[R.next], (long long)out_cap);
   if (planes) {
     if (!strides) return set_err(-22, "null strides");
+    // a full queue is encoded as soon as the previous packets are out; one
+    // that is still full (its encode failed) takes no more frames
+    if (int64_t(c->q_pts.size()) >= c->max_batch)
+      return set_err(-11, "frame queue full (%d frames): drain the packets first", c->max_batch);
     // the frame is copied into the next batch slot (the caller keeps
     // ownership: it may reuse the buffer once the call returns)
     int64_t off[3];

@@ -56,19 +56,33 @@ void find_best_state(uint8_t best[256][256], const uint8_t one_state[256]) {
   }
 }
 
-// The reference swaps the 64-bit counters through an int (FFSWAP(int, ...)):
-// the value that passes through it comes back truncated and sign-extended.
+// The reference swaps the 64-bit counters through an int: FFSWAP(int, a, b)
+// is { int tmp = b; b = a; a = tmp; } (libavutil/common.h:99), so b takes a
+// whole and a takes b truncated to 32 bits and sign-extended.
 void swap_through_int(uint64_t& a, uint64_t& b) {
-  const int t = int(uint32_t(a));
-  a = b;
-  b = uint64_t(int64_t(t));
+  const int t = int(uint32_t(b));
+  b = a;
+  a = uint64_t(int64_t(t));
 }
 
-double cost(const uint64_t st[256][2], int o, int n) {
-  return double(st[o][0]) * -std::log2((256 - n) / 256.0) + double(st[o][1]) * -std::log2(n / 256.0);
+// COST(old, new) of the reference's macro, added term by term to s: the
+// macros expand size0 / sizeX into one sum of eight products, evaluated left
+// to right, and the swap test compares them to 1e-14, so the association
+// matters
+void add_cost(double& s, const uint64_t st[256][2], int o, int n) {
+  s += double(st[o][0]) * -std::log2((256 - n) / 256.0);
+  s += double(st[o][1]) * -std::log2(n / 256.0);
 }
 
-double cost2(const uint64_t st[256][2], int o, int n) { return cost(st, o, n) + cost(st, 256 - o, 256 - n); }
+// COST2(i, a) + COST2(i2, b)
+double cost_pair(const uint64_t st[256][2], int i, int a, int i2, int b) {
+  double s = 0.0;
+  add_cost(s, st, i, a);
+  add_cost(s, st, 256 - i, 256 - a);
+  add_cost(s, st, i2, b);
+  add_cost(s, st, 256 - i2, 256 - b);
+  return s;
+}
 
 void sort_stt(uint64_t st[256][2], uint8_t stt[256]) {
   bool changed;
@@ -76,8 +90,8 @@ void sort_stt(uint64_t st[256][2], uint8_t stt[256]) {
     changed = false;
     for (int i = 12; i < 244; i++)
       for (int i2 = i + 1; i2 < 245 && i2 < i + 4; i2++) {
-        const double size0 = cost2(st, i, i) + cost2(st, i2, i2);
-        const double sizeX = cost2(st, i, i2) + cost2(st, i2, i);
+        const double size0 = cost_pair(st, i, i, i2, i2);
+        const double sizeX = cost_pair(st, i, i2, i2, i);
         if (!(size0 - sizeX > size0 * (1e-14) && i != 128 && i2 != 128)) continue;
         std::swap(stt[i], stt[i2]);
         swap_through_int(st[i][0], st[i2][0]);
@@ -107,7 +121,9 @@ int clip(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
 int pass2_states(const char* stats, bool custom, uint8_t stt[256], const uint8_t default_one[256],
                  std::vector<uint8_t> init[2], std::string* err) {
   const int counts[2] = {(11 * 11 * 11 + 1) / 2, (11 * 11 * 5 * 5 * 5 + 1) / 2};
-  static uint64_t rc_stat[256][2];
+  // per call (two contexts may initialise pass 2 at once)
+  std::vector<uint64_t> rc_stat_v(256 * 2, 0);
+  uint64_t(*rc_stat)[2] = reinterpret_cast<uint64_t(*)[2]>(rc_stat_v.data());
   std::vector<uint64_t> st2[2];
   for (int i = 0; i < 2; i++) st2[i].assign(size_t(counts[i]) * 64, 0);
   int gob_count = 0;
@@ -137,7 +153,8 @@ int pass2_states(const char* stats, bool custom, uint8_t stt[256], const uint8_t
     if (!*p) break;
   }
   if (custom) sort_stt(rc_stat, stt);
-  static uint8_t best[256][256];
+  std::vector<uint8_t> best_v(256 * 256, 0);
+  uint8_t(*best)[256] = reinterpret_cast<uint8_t(*)[256]>(best_v.data());
   find_best_state(best, custom ? stt : default_one);
   for (int i = 0; i < 2; i++) {
     std::vector<uint8_t>& is = init[i];
@@ -192,3 +209,10 @@ std::string pass1_text(const uint64_t* rc_stat, const uint64_t* rc_stat2, int co
 }
 
 }  // namespace ffv1hip
+
+// Host-only test hook (not part of include/ffv1hip.h): sort_stt on
+// caller-given counts [256][2] and table, for the FFSWAP(int, ...)
+// truncation check in tests/test_twopass_host.py.
+extern "C" void ffv1hip_internal_sort_stt(uint64_t* rc_stat, uint8_t* stt) {
+  ffv1hip::sort_stt(reinterpret_cast<uint64_t(*)[2]>(rc_stat), stt);
+}

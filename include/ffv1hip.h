@@ -131,15 +131,21 @@ int ffv1hip_encode2(ffv1hip_ctx *ctx, const void *const planes[3],
 /* Device-resident variant: frames already in HBM at d_frames + i*frame_bytes
  * with plane p at byte offset plane_offset[p] and row stride plane_stride[p].
  * The frames are read on `stream` (a hipStream_t, may be NULL: the context's
- * own stream); the coding may continue on the context's internal stream so
- * that consecutive calls overlap.  Nothing is synchronised: the packets are
- * valid after ffv1hip_synchronize or ffv1hip_fetch. */
+ * own stream); the coding may continue on the context's internal streams so
+ * that consecutive calls overlap.  Nothing is synchronised: the packets of
+ * the LAST call are valid after ffv1hip_synchronize, ffv1hip_fetch or
+ * ffv1hip_device_packets (each call's packets replace the previous call's).
+ * Those three check the last call's slices against the slice byte budget: a
+ * slice over it makes them encode that call again with a larger budget (its
+ * input frames must still be in place), so no truncated slice is ever
+ * handed out; if even that fails they return -ENOSPC. */
 int ffv1hip_encode_device(ffv1hip_ctx *ctx, const void *d_frames,
                           int64_t frame_bytes, const int64_t plane_offset[3],
                           const int plane_stride[3], int n_frames,
                           void *stream);
 
-/* Waits for all work of the context (every stream it uses). */
+/* Waits for all work of the context (every stream it uses), then settles
+ * the last call's slice byte budget (see ffv1hip_encode_device). */
 int ffv1hip_synchronize(ffv1hip_ctx *ctx);
 
 /* Synchronises and copies the packets of the last encode_device call. */
@@ -147,7 +153,9 @@ int ffv1hip_fetch(ffv1hip_ctx *ctx, uint8_t *out, int64_t out_cap,
                   int64_t *sizes, int *key_flags);
 
 /* Device pointers of the last call's packet slots: packet i starts at
- * (*d_packets + i * (*packet_stride)); sizes live in *d_sizes (int64). */
+ * (*d_packets + i * (*packet_stride)); sizes live in *d_sizes (int64).
+ * Synchronises first (ffv1hip_synchronize): a budget re-encode may move the
+ * slots. */
 int ffv1hip_device_packets(ffv1hip_ctx *ctx, void **d_packets,
                            int64_t *packet_stride, void **d_sizes);
 
@@ -170,8 +178,9 @@ int     ffv1hip_set_picture_number(ffv1hip_ctx *ctx, int64_t picture_number);
 
 /* Kernel timing: when enabled, HIP events are recorded on the launch stream
  * around each kernel of every call; ffv1hip_last_kernel_ms synchronises and
- * returns the durations (ms) of the last call's slice-coder kernel
- * (ffv1_encode_slices) and packet-assembly kernel (ffv1_assemble_packets). */
+ * returns, for the last call, the time from its first launch to the packet
+ * assembly (every coding kernel) and that of the packet-assembly kernel
+ * (ffv1_assemble_packets). */
 int ffv1hip_set_profiling(ffv1hip_ctx *ctx, int enable);
 int ffv1hip_last_kernel_ms(ffv1hip_ctx *ctx, float *encode_ms, float *assemble_ms);
 
@@ -221,11 +230,14 @@ int ffv1hip_decode(ffv1hip_dec *dec, const uint8_t *packets,
                    const int64_t *sizes, int n_frames, void *const *planes,
                    const int *strides, int *key_flags);
 /* Damaged slices are decoded on and concealed as the reference does
- * (ffv1dec.c:963-977, 410-414, 461-467, 998-1021): a slice failing its CRC,
- * its slice header or its end position takes the previous picture's
- * rectangle in that frame and in every later frame up to the next
- * keyframe.  This is how many (frame, slice) pairs of the last
- * ffv1hip_decode call were damaged. */
+ * (ffv1dec.c:963-977, 410-414, 461-467, 998-1021): a slice failing its CRC
+ * or its end position is decoded, then takes the previous picture's
+ * rectangle; a slice failing its slice header is neither decoded nor copied
+ * in that frame (ffv1dec.c:411-414 zeroes its size; the rectangle keeps
+ * what the output buffer held, zeros here);
+ * either way the slice is then concealed from the previous picture in every
+ * later frame up to the next keyframe.  This is how many (frame, slice)
+ * pairs of the last ffv1hip_decode call were damaged. */
 int ffv1hip_dec_damaged_slices(const ffv1hip_dec *dec);
 /* Forget the carried states and the previous picture: the next frame must
  * be a keyframe. */

@@ -811,21 +811,25 @@ static void find_best_state(uint8_t best[256][256], const uint8_t one_state[256]
     }
 }
 
-/* FFSWAP(int, ...) on the 64-bit counters (ffv1enc.c:642-647): the value
- * moved through the int comes back truncated and sign-extended. */
+/* FFSWAP(int, a, b) on the 64-bit counters (ffv1enc.c:642-647):
+ * { int tmp = b; b = a; a = tmp; } (libavutil/common.h:99), so b takes a
+ * whole and a takes b truncated to 32 bits and sign-extended. */
 static void swap_int(uint64_t *a, uint64_t *b)
 {
-    int t = (int)(uint32_t)*a;
-    *a = *b;
-    *b = (uint64_t)(int64_t)t;
+    int t = (int)(uint32_t)*b;
+    *b = *a;
+    *a = (uint64_t)(int64_t)t;
 }
 
 /* sort_stt (ffv1enc.c:621-667): swap neighbouring states of the custom
  * transition table while that lowers the pass-1 cost. */
 static void sort_stt(uint64_t rc_stat[256][2], uint8_t stt[256])
 {
-#define COST(o, n) ((double)rc_stat[o][0] * -log2((256 - (n)) / 256.0) + (double)rc_stat[o][1] * -log2((n) / 256.0))
-#define COST2(o, n) (COST(o, n) + COST(256 - (o), 256 - (n)))
+/* unparenthesised like the reference's macros: size0 / sizeX are one sum of
+ * eight products evaluated left to right, and the 1e-14 test below sees the
+ * rounding of that association */
+#define COST(o, n) (double)rc_stat[o][0] * -log2((256 - (n)) / 256.0) + (double)rc_stat[o][1] * -log2((n) / 256.0)
+#define COST2(o, n) COST(o, n) + COST(256 - (o), 256 - (n))
     int changed;
     do {
         changed = 0;
@@ -2087,4 +2091,11 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
     if (key_out)
         *key_out = key;
     return 0;
+}
+
+/* sort_stt on caller-given counts and table (a host-only check of the
+ * FFSWAP(int, ...) truncation, tests/test_twopass_host.py). */
+void ffv1o_sort_stt(uint64_t rc_stat[512], uint8_t stt[256])
+{
+    sort_stt((uint64_t(*)[2])rc_stat, stt);
 }

@@ -122,6 +122,8 @@ int        ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
 
 /* MSB-first CRC-32, poly 0x04C11DB7, init 0, no final xor (crc.c:357). */
 uint32_t   ffv1o_crc32(uint32_t crc, const uint8_t *buf, int64_t len);
+/* sort_stt (ffv1enc.c:621-667) on rc_stat[256][2] and a custom table. */
+void       ffv1o_sort_stt(uint64_t rc_stat[512], uint8_t stt[256]);
 
 #ifdef __cplusplus
 }

@@ -262,3 +262,81 @@ def test_avcodec_mirror_c3_known_answer(batch):
     for p in pkts:
         h.update(p.data)
     assert h.hexdigest() == pin["stream_md5"]
+
+
+def _d2h(ptr, nbytes):
+    """Device bytes at `ptr` through the HIP runtime the library links."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    out = np.empty(max(nbytes, 1), np.uint8)
+    assert hip.hipMemcpy(out.ctypes.data, ctypes.c_void_p(ptr), nbytes, 2) == 0  # DeviceToHost
+    return out[:nbytes]
+
+
+def _device_batch(params, frames):
+    """Frames packed planar into one HBM buffer the way bench.py stages them."""
+    import torch
+    shapes = params.plane_shapes()
+    plane_bytes = [h * w * params.sample_bytes for h, w in shapes]
+    frame_bytes = (sum(plane_bytes) + 255) // 256 * 256
+    host = np.zeros((len(frames), frame_bytes), np.uint8)
+    for i, f in enumerate(frames):
+        flat = np.concatenate([p.reshape(-1).view(np.uint8) for p in f])
+        host[i, :flat.size] = flat
+    offs = [0, plane_bytes[0], plane_bytes[0] + plane_bytes[1]]
+    strides = [shapes[k][1] * params.sample_bytes for k in range(3)]
+    return torch.from_numpy(host).to("cuda:0"), frame_bytes, offs, strides
+
+
+@pytest.mark.parametrize("sync", ["synchronize", "device_packets"])
+def test_device_path_never_truncates(sync, monkeypatch):
+    """encode_device twice back to back with a 512-byte starting slice budget
+    (every slice over it), then the packets of the last call through
+    ffv1hip_synchronize / ffv1hip_device_packets: the oracle's bytes (the
+    budget re-encode runs there), never capped slices (VERDICT r2, weak 4;
+    the reference fails a frame it cannot fit, ffv1enc.c:283-292)."""
+    import torch
+    from ffv1hip import HipEncoder
+    monkeypatch.setenv("FFV1HIP_SLICE_CAP", "512")
+    s = PARITY_STREAMS[1]  # 480x270 10-bit, 4 slices, gop 4
+    frames = list(s.frames())[:8]
+    _, _, ref = oracle_encode(s, frames)
+    params = hip_params(s)
+    enc = HipEncoder(params, 0, 4)
+    a = _device_batch(params, frames[:4])
+    b = _device_batch(params, frames[4:])
+    enc.encode_device(a[0].data_ptr(), a[1], a[2], a[3], 4)
+    enc.encode_device(b[0].data_ptr(), b[1], b[2], b[3], 4)
+    if sync == "synchronize":
+        enc.synchronize()
+    d_p, stride, d_s = enc.device_packets()
+    sizes = _d2h(d_s, 8 * 4).view(np.int64)
+    got = [_d2h(d_p + i * stride, int(sizes[i])).tobytes() for i in range(4)]
+    torch.cuda.synchronize()
+    enc.close()
+    assert got == [p for p, _ in ref[4:]]
+
+
+FULL_SIZE = {
+    # BASELINE configs[3]: 4K yuv444p16 at 12 bit (u16 >> 4), videogen content
+    "c4_4k_444p12": Stream("c4", 3840, 2160, "yuv444p16", 3, slices=64, gop_size=12,
+                           bits_per_raw_sample=12, depth=16, chroma444=True),
+    # BASELINE configs[4]: 8K yuv420p10, the 16x16 grid (no reference bitstream)
+    "c5_8k_p10_grid16": Stream("c5", 7680, 4320, "yuv420p10", 3, slices=256, gop_size=12, depth=10,
+                               allow_large_grid=True, extra={"grid": (16, 16)}),
+}
+
+
+@pytest.mark.parametrize("name", sorted(FULL_SIZE))
+def test_full_size_configs_match_oracle(name):
+    """The bench's c4 and c5 workloads at full size on the D1 clip (a
+    keyframe and two P-frames), every byte against the oracle encoder
+    (8K parity is the CPU restatement, bit-exact)."""
+    s = FULL_SIZE[name]
+    frames = list(s.frames())
+    _, ex_ref, ref = oracle_encode(s, frames)
+    ex, got = hip_encode(s, frames, batch=3)
+    assert ex == ex_ref
+    assert [len(p) for p, _ in got] == [len(p) for p, _ in ref]
+    assert got == ref
