@@ -73,7 +73,8 @@ def hip_configure():
                      allow_large_grid=GRID)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 KERNEL = {"symbols": "ffv1_symbols", "layout": "ffv1_layout", "bits": "ffv1_bits", "states": "ffv1_walk",
-          "code": "ffv1_dcode", "sink": "ffv1_sink", "assemble": "ffv1_assemble_packets"}
+          "code": "ffv1_range", "dseg": "ffv1_dseg", "dfix": "ffv1_dfix", "sink": "ffv1_sink",
+          "assemble": "ffv1_assemble_packets"}
 PIN_MD5_24 = "08e3975d4d0f5f2e5c82cd4037764789"  # tests/golden/known_answers.json (config 3)
 
 
@@ -398,11 +399,11 @@ def main():
                           "packets and D2H of the frames"}
         log(f"[rank {rank}] GPU decode self-check: {B} frames in {td:.2f}s, lossless={lossless}")
 
-    names = ("symbols", "layout", "bits", "states", "code", "sink", "assemble")
+    names = ("symbols", "layout", "bits", "states", "code", "dseg", "dfix", "sink", "assemble")
     per_step = {k: stats[k + "_ms"] / args.steps for k in names}
     launches = {k: stats[k + "_launches"] // args.steps for k in names}
     # Dominant kernel: the longest per step of the two serial chains, the
-    # states walk (ffv1_walk) and the range coder (ffv1_dcode): each is ONE
+    # states walk (ffv1_walk) and the range coder's serial pass (ffv1_range): each is ONE
     # launch per step over every frame of the batch.  Algorithmic bytes per
     # launch: the input planes of the batch (3.0 B per luma
     # pixel at 4:2:0 10 bit) + the packet bytes it produces.
@@ -445,7 +446,7 @@ def main():
                            "note": "md5 over the per-GOP packet md5s in GOP order: the same for "
                                    "every --gpus N (GOP bytes do not depend on the rank)"},
             # kernels of the overlapped pipelines: symbols -> layout -> walk
-            # (batch k+1), bits beside the walk, dcode -> sink -> assemble (batch k)
+            # (batch k+1), bits beside the walk, range -> dseg -> dfix -> sink -> assemble (batch k)
             "kernel_ms_per_step": dict(
                 **{KERNEL[k]: round(per_step[k], 3) for k in names},
                 launches={KERNEL[k]: launches[k] for k in names}),

@@ -243,7 +243,6 @@ struct ffv1hip_ctx {
   int64_t frame_samples = 0;  // symbols of one frame (each slice padded to 4)
   int64_t frame_chunks = 0;   // 64-sample walk chunks of one frame
   int max_ops = 0;
-  int nopsets = 1;         // op sets the header programs use (<= kOpSets)
   std::vector<SliceGeom> geom;
   // device buffers
   uint8_t* d_frames = nullptr;
@@ -277,7 +276,21 @@ struct ffv1hip_ctx {
   uint8_t* d_pre[2] = {nullptr, nullptr};    // [decision] state before the decision
   uint8_t* d_scratch = nullptr;               // where idle walk chains write their stage
   uint32_t* d_bits[2] = {nullptr, nullptr};  // [decision / 32] decision bits
-  uint8_t* d_opsets = nullptr;   // [coder lane][kOpSets * 32] header op states of the coder
+  // the three-pass coder (ffv1_range / ffv1_dseg / ffv1_dfix): the header's
+  // digits per (key, slice), the per-stream segment layout (three sets, with
+  // the stream metadata), checkpoints and segment records (one set: only
+  // the coder stream uses them)
+  HdrState* d_hdr = nullptr;
+  uint32_t* d_hdr_digits = nullptr;
+  std::vector<HdrState> hdr;
+  std::vector<uint32_t> hdr_digits;
+  StreamSegs* d_segs_info = nullptr;  // 3 x [batch frame][slice]
+  int* d_seg_totals = nullptr;        // 3 x [2]
+  int* d_wmap = nullptr;              // 3 x [64-segment group]
+  int64_t max_groups = 0;             // 64-segment groups a batch can have
+  int64_t max_segs = 0;               // segments a batch can have
+  uint2* d_ck = nullptr;
+  uint2* d_segrec = nullptr;
   int64_t dcap[2] = {0, 0};      // decisions d_pre/d_bits hold
   int buf = 0;                   // buffer set of the next batch
   hipStream_t code_stream = nullptr;  // ffv1_dcode + assembly, behind the states walk
@@ -346,7 +359,8 @@ struct ffv1hip_ctx {
   bool profiling = false;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> kev;  // [2 * launches]: start/stop per kernel launch
-  std::vector<int> kev_kind;    // per launch: 0 symbols, 1 code, 2 states, 3 assembly, 4 layout, 5 bits
+  std::vector<int> kev_kind;    // per launch: 0 symbols, 1 code (ffv1_range), 2 states, 3 assembly, 4 layout,
+                                // 5 bits, 6 sink, 7 dseg, 8 dfix
   int nkev = 0;
   int last_nsegs = 0;
   // ffv1hip_encode2 (AV_CODEC_CAP_DELAY): frames queued in d_frames slots
@@ -518,12 +532,16 @@ static int build_extradata(ffv1hip_ctx* c) {
   return 0;
 }
 
+// Decision-stream mode: a slice slot holds the values of low at the
+// stream's shifts as u32 (about one per output byte) with a segment's worth
+// of slack, which ffv1_sink then overwrites with the bytes.
+static int64_t slice_stride_frames(int64_t slice_cap) { return 4 * (slice_cap + kSeg + 64); }
+
 // Header programs: per (key, slice), the decisions coded before the planes.
 static void build_ops(ffv1hip_ctx* c) {
   const ffv1hip_params& p = c->P;
   c->ops.assign(size_t(2) * c->nslices * kMaxOps, Op{0, 0, 0, 0});
   c->nops.assign(size_t(2) * c->nslices, 0);
-  c->nopsets = 1;
   // the sets a v3 stream uses first: its coder then keeps only two per lane
   enum { kSetKey = 0, kSetSlice = 1, kSetHdr = 2, kSetQ0 = 3 };
   for (int key = 0; key < 2; key++)
@@ -565,18 +583,88 @@ static void build_ops(ffv1hip_ctx* c) {
         L.sym(kSetSlice, 1, p.sar_den, false);
       }
       const size_t sel = size_t(key) * c->nslices + s;
-      for (const Op& op : L.ops) c->nopsets = std::max(c->nopsets, int(op.set) + 1);
       c->nops[sel] = int(L.ops.size());
       std::memcpy(&c->ops[sel * kMaxOps], L.ops.data(), L.ops.size() * sizeof(Op));
     }
+}
+
+// The header decisions of each (key, slice) stream (the op programs above)
+// do not depend on the pixels, so the decision-stream coder starts every
+// stream after them: low, range and the values of low at their shifts
+// (renorm_encoder's input, rangecoder.h:52-75), coded here once.
+static void build_hdr(ffv1hip_ctx* c) {
+  c->hdr.assign(size_t(2) * c->nslices, HdrState{0, 0xFF00, 0, 0});
+  c->hdr_digits.clear();
+  for (int key = 0; key < 2; key++)
+    for (int s = 0; s < c->nslices; s++) {
+      const size_t sel = size_t(key) * c->nslices + s;
+      uint8_t os[kOpSets][32];
+      std::memset(os, 128, sizeof(os));
+      int low = 0, range = 0xFF00;
+      const int off = int(c->hdr_digits.size());
+      auto put = [&](uint8_t* st, int bit, const Tables& t) {
+        const int r1 = (range * *st) >> 8;
+        if (bit) {
+          low += range - r1;
+          range = r1;
+          *st = t.to1[*st];
+        } else {
+          range -= r1;
+          *st = t.to0[*st];
+        }
+        while (range < 0x100) {
+          c->hdr_digits.push_back(uint32_t(low));
+          low = (low & 0xFF) << 8;
+          range <<= 8;
+        }
+      };
+      for (int q = 0; q < c->nops[sel]; q++) {
+        const Op& op = c->ops[sel * kMaxOps + q];
+        const Tables& t = op.tab ? c->frame : c->dflt;
+        uint8_t* st = os[op.set];
+        if (op.kind == kOpBit) {
+          put(st, op.value, t);
+          continue;
+        }
+        const int v = op.value;
+        if (!v) {
+          put(st, 1, t);
+          continue;
+        }
+        const unsigned a = v < 0 ? 0u - unsigned(v) : unsigned(v);
+        const int e = 31 - __builtin_clz(a);
+        put(st, 0, t);
+        for (int i = 0; i < e; i++) put(st + 1 + std::min(i, 9), 1, t);
+        put(st + 1 + std::min(e, 9), 0, t);
+        for (int i = e - 1; i >= 0; i--) put(st + 22 + std::min(i, 9), (a >> i) & 1, t);
+        if (op.kind == kOpSymS) put(st + 11 + std::min(e, 10), v < 0, t);
+      }
+      c->hdr[sel] = HdrState{low, range, int(c->hdr_digits.size()) - off, off};
+    }
+}
+
+static int upload_hdr(ffv1hip_ctx* c) {
+  if (!c->frames_mode) return 0;
+  if (c->d_hdr) HIP_TRY(hipFree(c->d_hdr));
+  if (c->d_hdr_digits) HIP_TRY(hipFree(c->d_hdr_digits));
+  c->d_hdr = nullptr;
+  c->d_hdr_digits = nullptr;
+  HIP_TRY(hipMalloc(&c->d_hdr, sizeof(HdrState) * c->hdr.size()));
+  HIP_TRY(hipMemcpy(c->d_hdr, c->hdr.data(), sizeof(HdrState) * c->hdr.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&c->d_hdr_digits, sizeof(uint32_t) * (c->hdr_digits.size() + 1)));
+  if (!c->hdr_digits.empty())
+    HIP_TRY(hipMemcpy(c->d_hdr_digits, c->hdr_digits.data(), sizeof(uint32_t) * c->hdr_digits.size(),
+                      hipMemcpyHostToDevice));
+  return 0;
 }
 
 static void free_device(ffv1hip_ctx* c) {
   void* ptrs[] = {c->d_frames, c->d_qt, c->d_tabs, c->d_ops, c->d_nops, c->d_segs, c->d_keys,
                   c->d_slice_out, c->d_slice_bytes, c->d_packets, c->d_packet_size, c->d_persist[0],
                   c->d_persist[1], c->d_tables, c->d_sym, c->d_keys2, c->d_cbits, c->d_dcount, c->d_dbase, c->d_dtotal, c->d_pre[0],
-                  c->d_pre[1], c->d_bits[0], c->d_bits[1], c->d_scratch, c->d_opsets, c->d_geom, c->d_slot_frames, c->d_status,
-                  c->d_rec2, c->d_cbits2, c->d_ident};
+                  c->d_pre[1], c->d_bits[0], c->d_bits[1], c->d_scratch, c->d_hdr, c->d_hdr_digits, c->d_geom, c->d_slot_frames, c->d_status,
+                  c->d_rec2, c->d_cbits2, c->d_ident, c->d_segs_info, c->d_seg_totals, c->d_wmap, c->d_ck,
+                  c->d_segrec};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_dtotal) (void)hipHostFree(c->h_dtotal);
@@ -687,7 +775,22 @@ static int alloc_device(ffv1hip_ctx* c) {
     // decision capacity: the worst case when it is small, else ~12 per symbol
     // (real content codes ~10); a batch that needs more grows the set
     HIP_TRY(hipMalloc(&c->d_scratch, 4096));
-    HIP_TRY(hipMalloc(&c->d_opsets, (size_t(nb) * c->nslices + 64) * kOpSets * 32));  // + a wave of padding lanes
+    // the coder's segments: at most wmax decisions per sample
+    c->max_segs = 0;
+    c->max_groups = 0;
+    for (const SliceGeom& g : c->geom) {
+      const int64_t l = int64_t(g.pw[0]) * g.ph[0] * c->wmax;
+      const int64_t ch = (int64_t(g.pw[1]) * g.ph[1] + int64_t(g.pw[2]) * g.ph[2]) * c->wmax;
+      const int64_t n = std::max<int64_t>(1, (l + kSeg - 1) / kSeg + (ch + kSeg - 1) / kSeg);
+      c->max_segs += n * nb;
+      c->max_groups += (n + 63) / 64 * nb;
+    }
+    HIP_TRY(hipMalloc(&c->d_segs_info, 3 * sizeof(StreamSegs) * size_t(nb) * c->nslices));
+    HIP_TRY(hipMalloc(&c->d_seg_totals, 3 * 2 * sizeof(int)));
+    HIP_TRY(hipMalloc(&c->d_wmap, 3 * sizeof(int) * size_t(c->max_groups)));
+    HIP_TRY(hipMalloc(&c->d_ck, sizeof(uint2) * size_t(c->max_segs)));
+    HIP_TRY(hipMalloc(&c->d_segrec, sizeof(uint2) * size_t(c->max_segs)));
+    if (upload_hdr(c) < 0) return -5;
     const int64_t align = int64_t(nb) * c->nslices * kStreamSlack;
     const int64_t worst = int64_t(nb) * c->frame_samples * c->wmax + align;
     const int64_t guess = int64_t(nb) * c->frame_samples * 12 + align;
@@ -753,6 +856,7 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
   quant_set(c->qt, p.context_model, p.bits_per_raw_sample);
   build_extradata(c);
   build_ops(c);
+  build_hdr(c);
   // layout of a frame in the batch buffer (planar, tightly packed)
   const int cw = p.chroma_planes ? -((-p.width) >> p.chroma_h_shift) : 0;
   const int ch = p.chroma_planes ? -((-p.height) >> p.chroma_v_shift) : 0;
@@ -818,7 +922,7 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
     c->wmax = 2 * (p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample) + 1;
     // the decision-stream coder writes a slice's digits (2 bytes each) where
     // ffv1_sink then writes its bytes
-    c->slice_stride = c->frames_mode ? 2 * c->slice_cap : c->slice_cap;
+    c->slice_stride = c->frames_mode ? slice_stride_frames(c->slice_cap) : c->slice_cap;
   }
   int rc = alloc_device(c);
   if (rc < 0) {
@@ -894,6 +998,9 @@ int ffv1hip_set_pass(ffv1hip_ctx* c, int pass, const char* stats_in) {
   HIP_TRY(hipMalloc(&c->d_init, is.size()));
   HIP_TRY(hipMemcpy(c->d_init, is.data(), is.size(), hipMemcpyHostToDevice));
   build_extradata(c);
+  build_hdr(c);  // the slice header codes with the frame table
+  const int urc = upload_hdr(c);
+  if (urc < 0) return urc;
   c->pass = 2;
   return 0;
 }
@@ -1049,6 +1156,9 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   uint32_t* const d_cbits = rec1 ? c->d_cbits2 : c->d_cbits;
   int* const d_dcount = c->frames_mode ? c->d_dcount + size_t(t3) * 3 * c->max_batch * c->nslices : nullptr;
   int64_t* const d_dbase = c->frames_mode ? c->d_dbase + size_t(t3) * c->max_batch * c->nslices : nullptr;
+  StreamSegs* const d_segs = c->frames_mode ? c->d_segs_info + size_t(t3) * c->max_batch * c->nslices : nullptr;
+  int* const d_segtot = c->frames_mode ? c->d_seg_totals + 2 * t3 : nullptr;
+  int* const d_wmap = c->frames_mode ? c->d_wmap + size_t(t3) * c->max_groups : nullptr;
   sa.sym = d_sym;
   sa.frame_samples = c->frame_samples;
 
@@ -1143,7 +1253,9 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
         return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
       HIP_TRY(hipStreamWaitEvent(st, c->sym1, 0));
     }
-    if (timed(4, lst, [&] { return launch_layout(d_dcount, n * c->nslices, d_dbase, c->d_dtotal + t3, lst); }) < 0)
+    if (timed(4, lst, [&] {
+          return launch_layout(d_dcount, n * c->nslices, d_dbase, c->d_dtotal + t3, d_segs, d_segtot, d_wmap, lst);
+        }) < 0)
       return set_err(-5, "layout launch failed: %s", hipGetErrorString(hipGetLastError()));
     // decisions of this batch: the worst case fits without asking the device
     int64_t need = int64_t(n) * c->frame_samples * c->wmax + int64_t(n) * c->nslices * kStreamSlack;
@@ -1286,42 +1398,27 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     HIP_TRY(hipStreamWaitEvent(cst, c->bitsed[fb], 0));
     if (c->pass == 1 && launch_stats(sta, true, cst) < 0) return set_err(-5, "stats launch failed");
     ca.nframes = n;
-    static const int code_prio =
-        std::getenv("FFV1HIP_CODE_WAVE_PRIO") ? std::atoi(std::getenv("FFV1HIP_CODE_WAVE_PRIO")) : 0;
-    ca.prio = code_prio;
-    ca.nopsets = c->nopsets;
-    ca.opsets = c->d_opsets;
     ca.ds = ds;
-    // FFV1HIP_CODEDBG=1 (measurement hook): per-wave cycle split to stderr
-    static const bool codedbg = std::getenv("FFV1HIP_CODEDBG") && std::atoi(std::getenv("FFV1HIP_CODEDBG"));
-    const int nwaves = int((int64_t(n) * c->nslices + 63) / 64);
-    uint64_t* d_cdbg = nullptr;
+    ca.hdr = c->d_hdr;
+    ca.hdr_digits = c->d_hdr_digits;
+    ca.segs_info = d_segs;
+    ca.seg_totals = d_segtot;
+    ca.wmap = d_wmap;
+    ca.ck = c->d_ck;
+    ca.segrec = c->d_segrec;
+    ca.digit_cap = c->slice_stride / 4;
+    ca.dseg_blocks = int(std::min<int64_t>(c->max_groups, 16384));
     HIP_TRY(hipMemsetAsync(ca.status, 0, sizeof(int) * 4, cst));
-    if (codedbg) {
-      HIP_TRY(hipMalloc(&d_cdbg, sizeof(uint64_t) * 4 * nwaves));
-      HIP_TRY(hipMemsetAsync(d_cdbg, 0, sizeof(uint64_t) * 4 * nwaves, cst));
-      ca.dbg = d_cdbg;
-    }
-    if (timed(1, cst, [&] { return launch_dcode(ca, cst); }) < 0)
-      return set_err(-5, "code launch failed: %s", hipGetErrorString(hipGetLastError()));
+    // range alone (the serial chain), every segment from its checkpoint,
+    // the segments joined, then the bytes
+    if (timed(1, cst, [&] { return launch_range(ca, cst); }) < 0)
+      return set_err(-5, "range launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (timed(7, cst, [&] { return launch_dseg(ca, cst); }) < 0)
+      return set_err(-5, "dseg launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (timed(8, cst, [&] { return launch_dfix(ca, cst); }) < 0)
+      return set_err(-5, "dfix launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (timed(6, cst, [&] { return launch_sink(ca, cst); }) < 0)
       return set_err(-5, "sink launch failed: %s", hipGetErrorString(hipGetLastError()));
-    if (codedbg) {
-      std::vector<uint64_t> h(size_t(4) * nwaves);
-      HIP_TRY(hipMemcpyAsync(h.data(), d_cdbg, h.size() * 8, hipMemcpyDeviceToHost, cst));
-      HIP_TRY(hipStreamSynchronize(cst));
-      HIP_TRY(hipFree(d_cdbg));
-      double all = 0, fl = 0, dec = 0, mx = 0, its = 0;
-      for (int w = 0; w < nwaves; w++) {
-        all += double(h[4 * w]);
-        fl += double(h[4 * w + 1]);
-        dec += double(h[4 * w + 2]);
-        its += double(h[4 * w + 3]);
-        mx = std::max(mx, double(h[4 * w]));
-      }
-      std::fprintf(stderr, "codedbg: waves %d, memtime per wave %.3g (max %.3g), flush share %.3f, memtime/decision %.1f, decisions per wave %.3g, flush iterations per wave %.3g, memtime per iteration %.1f\n",
-                   nwaves, all / nwaves, mx, fl / all, all / dec, dec / nwaves, its / nwaves, fl / its);
-    }
   } else {
     HIP_TRY(hipMemsetAsync(ca.status, 0, sizeof(int) * 4, st));
     for (int j = 0; j < maxlen; j++) {
@@ -1390,7 +1487,7 @@ static int grow_slice_budget(ffv1hip_ctx* c, int64_t needed) {
   c->d_slice_out = nullptr;
   c->d_packets = nullptr;
   c->slice_cap = cap;
-  c->slice_stride = c->frames_mode ? 2 * cap : cap;
+  c->slice_stride = c->frames_mode ? slice_stride_frames(cap) : cap;
   c->packet_stride = ((cap + 16) * c->nslices + 255) & ~int64_t(255);
   if (hipMalloc(&c->d_slice_out, size_t(c->slice_stride) * c->nslices * c->max_batch) != hipSuccess ||
       hipMalloc(&c->d_packets, size_t(c->packet_stride) * c->max_batch) != hipSuccess)
@@ -1644,6 +1741,8 @@ int ffv1hip_last_kernel_stats(ffv1hip_ctx* c, ffv1hip_kernel_stats* out) {
       case 4: s.layout_ms += ms; s.layout_launches++; break;
       case 5: s.bits_ms += ms; s.bits_launches++; break;
       case 6: s.sink_ms += ms; s.sink_launches++; break;
+      case 7: s.dseg_ms += ms; s.dseg_launches++; break;
+      case 8: s.dfix_ms += ms; s.dfix_launches++; break;
       default: s.assemble_ms += ms; s.assemble_launches++; break;
     }
   }

@@ -113,11 +113,31 @@ struct DecisionStream {
   uint32_t* bits;
 };
 
+// The decision-stream range coder runs in three passes (ffv1_kernels.hip):
+// ffv1_range walks `range` alone per (frame, slice) stream and leaves a
+// checkpoint every kSeg decisions, ffv1_dseg codes every segment from its
+// checkpoint in parallel, ffv1_dfix joins the segments' low values.
+constexpr int kSeg = 4096;  // decisions per segment (a multiple of 32 and of the part alignment 64)
+// Per stream (layout): its segments, luma first (s_luma of them), then the
+// chroma chain's; their first index over the batch; the first of the
+// 64-segment groups ffv1_dseg takes one wave each.
+struct StreamSegs {
+  int seg_base, s_luma, s_all, wave_base;
+};
+// Per (key, slice): the range coder after the header decisions (key bit,
+// v0/v1 header, v3 slice header), which do not depend on the pixels: low,
+// range, how many renormalisation shifts they took, and where the values of
+// low at those shifts (the stream's first digits) are in hdr_digits.
+struct HdrState {
+  int low, range, ndig, off;
+};
+
 // Kernel 2: the SIMT range coder.
 //  chained (launch_code): one lane per (segment, slice) chain, one frame of
 //    every segment per launch, context states carried in `tables`;
-//  decision stream (launch_dcode): one lane per (frame, slice) stream of the
-//    whole batch, pure range arithmetic over the states ffv1_walk recorded.
+//  decision stream (launch_range / launch_dseg / launch_dfix): every
+//    (frame, slice) stream of the whole batch, pure range arithmetic over
+//    the states ffv1_walk recorded.
 struct CodeArgs {
   const uint32_t* sym;        // from kernel 1 (slot = segment)
   int64_t frame_samples;
@@ -136,19 +156,26 @@ struct CodeArgs {
   uint8_t* persist_out;       // [slice][state_bytes]: the carry it leaves (the other buffer)
   uint8_t* slice_out;         // [batch frame][slice][slice_stride]
   int64_t slice_cap;          // byte budget of a slice
-  int64_t slice_stride;       // bytes per slice slot (decision-stream mode: 2 x slice_cap, for the digits)
+  int64_t slice_stride;       // bytes per slice slot (decision-stream mode: 4 x (slice_cap + kSeg + 64),
+                              // the values of low at the shifts, u32, then ffv1_sink's bytes over them)
   int64_t* slice_bytes;       // [batch frame][slice]
   int* status;                // [0] slices over the byte budget, [1] most bytes a slice needed
   int version;                // bitstream version (Golomb: v3 adds a 129/0 decision)
   int coded_bits;             // "bits" of encode_line (8 for <=8-bit)
   int rgb;                    // RGB: a slice's three planes are row-interleaved (chained coders)
   int nframes;                // decision-stream mode: frames of the batch
-  int nopsets;                // decision-stream mode: op sets the header programs use
   DecisionStream ds;
-  uint64_t* dbg;              // optional [wave][4] cycle counters (FFV1HIP_CODEDBG)
-  int prio;                   // ffv1_dcode's wave priority (s_setprio)
-  uint8_t* opsets;            // decision-stream mode: [stream][nopsets * 32] header op states
   const uint8_t* init;        // chained range coder: 2-pass initial states [contexts][32], or null
+  // decision-stream mode (three passes)
+  const HdrState* hdr;        // [key][slice]
+  const uint32_t* hdr_digits; // values of low at the header's shifts
+  const StreamSegs* segs_info;  // [stream]
+  const int* seg_totals;      // device: [0] segments, [1] 64-segment groups of the batch
+  const int* wmap;            // [group] its stream
+  uint2* ck;                  // [segment] {range before it, shifts before it}
+  uint2* segrec;              // [segment] {local low at its end, its shifts}
+  int64_t digit_cap;          // values of low a slice slot holds (slice_stride / 4)
+  int dseg_blocks;            // ffv1_dseg grid
 };
 
 // Pass-1 statistics (ffv1enc.c:190-199): rc_stat[state][bit] from the
@@ -262,13 +289,16 @@ int64_t decode_lds_bytes(const DecodeArgs& a, bool global_states);
 
 int launch_symbols(const SymbolArgs& a, void* stream);
 int launch_code(const CodeArgs& a, void* stream);
-int launch_layout(const int* dcount, int nstreams, int64_t* dbase, int64_t* total, void* stream);
+int launch_layout(const int* dcount, int nstreams, int64_t* dbase, int64_t* total, StreamSegs* segs,
+                  int* seg_totals, int* wmap, void* stream);
 // items [first, first + count) of the batch's walk (count < 0: to the end)
 int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first = 0, int count = -1);
 int walk_items(int nsegs, int nslices);
 int walk_resident(const WalkArgs& a);
 int launch_delay(int us, void* stream);
-int launch_dcode(const CodeArgs& a, void* stream);
+int launch_range(const CodeArgs& a, void* stream);
+int launch_dseg(const CodeArgs& a, void* stream);
+int launch_dfix(const CodeArgs& a, void* stream);
 int launch_sink(const CodeArgs& a, void* stream);
 int launch_bits(const BitsArgs& a, void* stream);
 int64_t walk_lds_bytes(int64_t state_bytes);

@@ -445,32 +445,6 @@ __device__ __forceinline__ void flush(Lane& L, Sink& S) {
   L.rp = L.ring;
 }
 
-// Digit writer (decision-stream coder): the ring's values of `low` go out
-// unreplayed, one u16 each, qv = low >> 8 | (low & 0xFF ? 0x200 : 0);
-// ffv1_sink then turns them into the slice's bytes.
-struct DigitSink {
-  uint16_t* out;
-  int n, cap;  // digits so far, capacity
-  __device__ __forceinline__ void put(uint32_t low, int t, bool act) {
-    const int i = n + t;
-    if (act && i < cap) out[i] = (uint16_t)((low >> 8) | ((low & 0xFFu) ? 0x200u : 0u));
-  }
-  __device__ __forceinline__ int64_t finish() { return n; }
-};
-
-__device__ __forceinline__ void flush(Lane& L, DigitSink& D) {
-  const int n = (int)(L.rp - L.ring);
-  for (int t = 0; __ballot(t < n); t += 4) {
-    const uint32_t d0 = L.ring[t], d1 = L.ring[t + 1], d2 = L.ring[t + 2], d3 = L.ring[t + 3];
-    D.put(d0, t, t < n);
-    D.put(d1, t + 1, t + 1 < n);
-    D.put(d2, t + 2, t + 2 < n);
-    D.put(d3, t + 3, t + 3 < n);
-  }
-  D.n += n;
-  L.rp = L.ring;
-}
-
 template <class SinkT>
 __device__ __forceinline__ void flush_if(Lane& L, SinkT& S, int above) {
   if (__ballot((int)(L.rp - L.ring) > above)) flush(L, S);
@@ -849,33 +823,29 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Kernel 2, decision-stream form: one lane per (frame, slice) stream of the
-// batch.  ffv1_walk recorded every decision's state and ffv1_bits its bit,
-// so what is left is put_rac's arithmetic (rangecoder.h:90-102) and the
-// renormalisation (rangecoder.h:52-75), 32 decisions per step from 32 state
-// bytes + one bit word: no per-symbol structure, so no lane waits on
-// another's exponent.  The ring is small (a flush check every 16 decisions)
-// so that a coder wave fits in the LDS the states walk leaves on a CU.
-constexpr int kDRing = 32;                   // renorm digits per lane before a flush
-constexpr int kDRingStride = kDRing + 3;  // odd: lanes at equal heads hit distinct banks
-constexpr int kDFlushAt = kDRing - 17;       // checked every 16 decisions
-
-// flush_if, timed into *tf when tf is set (FFV1HIP_CODEDBG)
-// flush_if, timed (FFV1HIP_CODEDBG): cycles into tf, wave-max entries into ti
-struct FlushTimer {
-  bool on;
-  uint64_t tf, ti;
-};
-
-template <class SinkT>
-__device__ __forceinline__ void flush_if_t(Lane& L, SinkT& S, int above, FlushTimer& T) {
-  if (__ballot((int)(L.rp - L.ring) > above)) {
-    const uint64_t t0 = T.on ? __builtin_amdgcn_s_memtime() : 0;
-    if (T.on) T.ti += wave_max((int)(L.rp - L.ring));
-    flush(L, S);
-    if (T.on) T.tf += __builtin_amdgcn_s_memtime() - t0;
-  }
-}
+// Kernel 2, decision-stream form: every (frame, slice) stream of the batch,
+// the states ffv1_walk recorded and the bits ffv1_bits placed, in three
+// passes.  put_rac (rangecoder.h:85-102) makes `range` a function of
+// (range, state, bit) alone: r1 = range * state >> 8, then range - r1 (a 0)
+// or r1 (a 1), renormalised by << 8 while below 0x100; `low` never feeds
+// back into it.  So:
+//
+//   ffv1_range  one lane per stream walks `range` only (about half the
+//               work of a full put_rac per decision: this serial chain is
+//               what sets the coder's time) and stores, at the start of
+//               every segment of kSeg decisions, {range, shifts so far}.
+//   ffv1_dseg   every segment codes in parallel from its checkpoint with
+//               low = 0, writing the value of low at each of its shifts
+//               (renorm_encoder's input, a "digit") at its place in the
+//               stream, and its low at the end.
+//   ffv1_dfix   one lane per stream joins the segments in order.  Only
+//               additions and << 8 shifts act on low, so the real low is
+//               the local one plus what entered from the previous segments;
+//               that carry-in (< 2^17) is out of the 16-bit window after two
+//               shifts, so it changes the segment's first two digits only.
+//
+// ffv1_sink then replays renorm_encoder's outstanding-byte logic over the
+// digits as before, and the bytes are those of the serial coder.
 
 // the first rem state bytes of a 16-byte block (rem may be <= 0 or >= 16)
 __device__ __forceinline__ uint32_t tail_word(uint32_t w, int rem) {
@@ -885,89 +855,196 @@ __device__ __forceinline__ uint4 tail_mask(const uint4& v, int rem) {
   return make_uint4(tail_word(v.x, rem), tail_word(v.y, rem - 4), tail_word(v.z, rem - 8), tail_word(v.w, rem - 12));
 }
 
-template <class SinkT>
-__device__ __forceinline__ void decide32(Lane& L, SinkT& S, const uint4& wa, const uint4& wb, uint32_t bw,
-                                         FlushTimer& tf) {
-  static_for<0, 32>([&](auto jc) {
+// state byte J of a block of 32 (two uint4)
+template <int J>
+__device__ __forceinline__ uint32_t state_word(const uint4& wa, const uint4& wb) {
+  if constexpr (J < 4) return wa.x;
+  else if constexpr (J < 8) return wa.y;
+  else if constexpr (J < 12) return wa.z;
+  else if constexpr (J < 16) return wa.w;
+  else if constexpr (J < 20) return wb.x;
+  else if constexpr (J < 24) return wb.y;
+  else if constexpr (J < 28) return wb.z;
+  else return wb.w;
+}
+
+// The decision masks of 8 decisions (all ones for a 1), made opaque to the
+// compiler together: seen as a sign-extended bit, a mask would be turned
+// into a compare + v_cndmask (with its vcc wait states) instead of one
+// bitwise select, and an empty asm per decision costs a wait state each.
+struct Masks8 {
+  int m[8];
+};
+template <int G>
+__device__ __forceinline__ Masks8 masks8(uint32_t bw) {
+  Masks8 k;
+  static_for<0, 8>([&](auto jc) {
     constexpr int J = decltype(jc)::value;
-    constexpr int SH = (J & 3) * 8;
-    uint32_t w;
-    if constexpr (J < 4) w = wa.x;
-    else if constexpr (J < 8) w = wa.y;
-    else if constexpr (J < 12) w = wa.z;
-    else if constexpr (J < 16) w = wa.w;
-    else if constexpr (J < 20) w = wb.x;
-    else if constexpr (J < 24) w = wb.y;
-    else if constexpr (J < 28) w = wb.z;
-    else w = wb.w;
-    const int m = __builtin_amdgcn_sbfe((int)bw, J, 1);         // all ones for a 1 decision
-    // put_rac (rangecoder.h:90-102): r1 = range * state >> 8; a 1 decision
-    // keeps r1 and adds range - r1 to low, a 0 decision keeps range - r1
-    const int r1 = (int)(__umul24((unsigned)L.range, (w >> SH) & 0xFFu) >> 8);
-    const int d = L.range - r1;
-    int nl = L.low + (d & m);
-    int nr;  // m ? r1 : d, one v_bfi (the compiler would make it a compare and two selects)
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(nr) : "v"(m), "v"(r1), "v"(d));
-    L.low = nl;
-    L.range = nr;
-    renorm(L);
-    if constexpr (J == 15) flush_if_t(L, S, kDFlushAt, tf);
+    k.m[J] = __builtin_amdgcn_sbfe((int)bw, 8 * G + J, 1);
+  });
+  asm volatile("" : "+v"(k.m[0]), "+v"(k.m[1]), "+v"(k.m[2]), "+v"(k.m[3]), "+v"(k.m[4]), "+v"(k.m[5]),
+               "+v"(k.m[6]), "+v"(k.m[7]));
+  return k;
+}
+
+// 32 decisions on `range` alone; shifts counts the renormalisations (x 8).  A
+// state-0 decision of bit 0 (the zeroed tail of a stream) leaves range as
+// it is: r1 = 0, range - r1 = range.
+__device__ __forceinline__ void range32(int& range, int& shifts, const uint4& wa, const uint4& wb, uint32_t bw) {
+  static_for<0, 4>([&](auto gc) {
+    constexpr int G = decltype(gc)::value;
+    const Masks8 k = masks8<G>(bw);
+    static_for<0, 8>([&](auto jc) {
+      constexpr int J = 8 * G + decltype(jc)::value;
+      constexpr int SH = (J & 3) * 8;
+      const uint32_t w = state_word<J>(wa, wb);
+      const int m = k.m[J & 7];
+      const int r1 = (int)(__umul24((unsigned)range, (w >> SH) & 0xFFu) >> 8);
+      const int d = range - r1;
+      const int nr = (m & r1) | (~m & d);  // m ? r1 : d, one bitwise select
+      // renormalisation without a compare: nr in [1, 0xFFFF] has 16..31
+      // leading zeros, 24 or more (bit 3 set) exactly when nr < 0x100
+      const int sh = (int)(__builtin_clz((unsigned)nr) & 8u);
+      shifts += sh;  // in units of 8
+      range = nr << sh;
+    });
   });
 }
 
-// The header ops keep their states in global memory and read their
-// transition tables from there (a few dozen decisions per stream): the
-// coder's LDS is its rings only, so that it fits beside three states-walk
-// waves on a CU.
-__host__ __device__ constexpr size_t dcode_lds_bytes(int /*nopsets*/) {
-  return (size_t)kCodeThreads * kDRingStride * 4;
+// The stream a lane codes: slice-major, so that the lanes of a wave code one
+// slice of consecutive frames (streams of similar length).
+struct StreamRef {
+  bool live;
+  int slice, f;
+  int64_t st;  // [frame][slice] index of the per-stream arrays
+};
+__device__ __forceinline__ StreamRef stream_of(const CodeArgs& a, int64_t c) {
+  StreamRef r;
+  r.live = c < (int64_t)a.nframes * a.nslices;
+  r.slice = r.live ? (int)(c / a.nframes) : 0;
+  r.f = r.live ? (int)(c % a.nframes) : 0;
+  r.st = (int64_t)r.f * a.nslices + r.slice;
+  return r;
 }
 
-__global__ __launch_bounds__(kCodeThreads) void ffv1_dcode(CodeArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  switch (a.prio) {  // wave priority against the walk beside it (FFV1HIP_CODE_WAVE_PRIO, default 0)
-    case 1: __builtin_amdgcn_s_setprio(1); break;
-    case 2: __builtin_amdgcn_s_setprio(2); break;
-    case 3: __builtin_amdgcn_s_setprio(3); break;
-    default: break;
-  }
-  const int osb = a.nopsets * 32;
-  const uint8_t* const tabs = a.tabs;
-  uint32_t* const ring = reinterpret_cast<uint32_t*>(lds);
-  const int lane = threadIdx.x;
-  // slice-major: the lanes of a wave code one slice of consecutive frames,
-  // streams of similar length
-  const int64_t c = (int64_t)blockIdx.x * kCodeThreads + lane;
-  const bool live = c < (int64_t)a.nframes * a.nslices;
-  const int slice = live ? (int)(c / a.nframes) : 0;
-  const int f = live ? (int)(c % a.nframes) : 0;
-  const int key = live ? a.keyflags[f] : 0;
-
-  Lane L;
-  lane_init(L, ring + lane * kDRingStride);
-  // the stream's digits, in its slice_out slot (2 bytes per digit; ffv1_sink
-  // rewrites the slot with the bytes in place)
-  DigitSink S{reinterpret_cast<uint16_t*>(a.slice_out + ((int64_t)f * a.nslices + slice) * a.slice_stride), 0,
-              live ? (int)(a.slice_stride / 2) : 0};
-  // every lane its own op states, the padding lanes of the last wave included
-  run_header_ops(a, L, S, a.opsets + c * osb, key, slice, live, tabs, tabs + 512, osb, kDRing - 30);
-  flush_if(L, S, kDFlushAt);
-
-  const int64_t st = (int64_t)f * a.nslices + slice;
-  const int* dc = a.ds.dcount + st * 3;
-  const int64_t base = live ? a.ds.dbase[st] : 0;  // multiple of kStreamAlign
-  uint64_t ndec = 0;
-  FlushTimer tf{a.dbg != nullptr, 0, 0};
-  const uint64_t t_all = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+constexpr int kRangeThreads = kWave;
+__global__ __launch_bounds__(kRangeThreads) void ffv1_range(CodeArgs a) {
+  const StreamRef sr = stream_of(a, (int64_t)blockIdx.x * kRangeThreads + threadIdx.x);
+  const int key = sr.live ? a.keyflags[sr.f] : 0;
+  const HdrState h = a.hdr[key * a.nslices + sr.slice];
+  const int* dc = a.ds.dcount + sr.st * 3;
+  const int64_t base = sr.live ? a.ds.dbase[sr.st] : 0;  // a multiple of kStreamAlign
+  uint2* ck = a.ck + (sr.live ? a.segs_info[sr.st].seg_base : 0);
+  int range = h.range, shifts = h.ndig << 3;  // renormalisation shifts x 8
   // the luma chain's decisions, then the chroma chain's at their own start
   for (int part = 0; part < 2; part++) {
-    const int n = live ? (part ? dc[1] + dc[2] : dc[0]) : 0;
-    const int64_t pb = base + (part && live ? chroma_start(dc[0]) : 0);  // multiple of 64
+    const int n = sr.live ? (part ? dc[1] + dc[2] : dc[0]) : 0;
+    const int64_t pb = base + (part && sr.live ? chroma_start(dc[0]) : 0);  // multiple of 64
     const uint4* P = reinterpret_cast<const uint4*>(a.ds.pre + pb);
     const uint32_t* B = a.ds.bits + (pb >> 5);
     const int nmax = wave_max(n);
     // blocks of 32 decisions (32 state bytes + one bits word), loaded two
     // blocks ahead (parts are padded to 64 decisions: reads stay inside)
+    const uint4 z4 = make_uint4(0, 0, 0, 0);
+    uint4 na = z4, nb = z4, ma = z4, mb = z4;
+    uint32_t nw = 0u, mw = 0u;
+    if (n > 0) {
+      na = P[0];
+      nb = P[1];
+      nw = B[0];
+    }
+    if (n > 32) {
+      ma = P[2];
+      mb = P[3];
+      mw = B[1];
+    }
+    for (int i = 0; i < nmax; i += 32) {
+      if ((i & (kSeg - 1)) == 0 && i < n) *ck++ = make_uint2((uint32_t)range, (uint32_t)shifts >> 3);
+      uint4 wa = na, wb = nb;
+      uint32_t bw = nw;
+      na = ma;
+      nb = mb;
+      nw = mw;
+      if (i + 64 < n) {
+        ma = P[(i >> 4) + 4];
+        mb = P[(i >> 4) + 5];
+        mw = B[(i >> 5) + 2];
+      }
+      const int rem = n - i;
+      if (rem < 32) {
+        wa = tail_mask(wa, rem);
+        wb = tail_mask(wb, rem - 16);
+        bw = rem > 0 ? bw & ((1u << rem) - 1u) : 0u;
+      }
+      range32(range, shifts, wa, wb, bw);
+    }
+  }
+}
+
+// ffv1_dseg: one wave per 64 consecutive segments of a stream, one lane per
+// segment; no LDS, so that its waves fit beside the next batch's states walk
+// (which holds the CUs' LDS).  The values of low at the shifts go straight
+// to the stream's digit area (u32), at the stream-wide shift index the
+// checkpoint gives.
+constexpr int kDsegThreads = kWave;
+
+// Where a segment's digits go: a buffer resource over its stream's digit
+// area (the wave's 64 segments are one stream's) and the byte offset of the
+// lane's next digit.  Every decision issues the store; the lanes without a
+// shift give an offset past the resource, which the hardware drops (no
+// branch around the store), as it drops the stores of a stream running past
+// its slot (the join then reports the overflow).
+struct DigitOut {
+  __amdgpu_buffer_rsrc_t rs;
+  int kb;
+};
+constexpr int kBufDword3 = 0x00020000;  // gfx9-family raw buffer (32-bit data format)
+
+// put_rac + renorm_encoder's shift (rangecoder.h:52-102): the value of low
+// before a shift is stored as the lane's next digit.
+__device__ __forceinline__ void put_dec(int& low, int& range, DigitOut& o, int s, int m) {
+  const int r1 = (int)(__umul24((unsigned)range, (unsigned)s) >> 8);
+  const int d = range - r1;
+  low += d & m;
+  const int nr = (m & r1) | (~m & d);  // m ? r1 : d, one bitwise select
+  // all ones when a byte shifts out: nr < 0x100 (24+ leading zeros, see range32)
+  const int sm = __builtin_amdgcn_sbfe((int)__builtin_clz((unsigned)nr), 3, 1);
+  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)low, o.rs, o.kb | (~sm & (int)0x80000000), 0, 0);
+  o.kb += sm & 4;
+  const int shifted = (int)__builtin_amdgcn_perm(0u, (uint32_t)low, 0x0c0c000cu);  // (low & 0xFF) << 8
+  low = (sm & shifted) | (~sm & low);
+  range = nr << (sm & 8);
+}
+
+__global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
+  const int lane = threadIdx.x;
+  const int ngroups = a.seg_totals[1];
+  for (int w = blockIdx.x; w < ngroups; w += gridDim.x) {
+    const int st = a.wmap[w];  // wave-uniform
+    const StreamSegs ss = a.segs_info[st];
+    const int s = (w - ss.wave_base) * kDsegThreads + lane;  // this lane's segment of the stream
+    const bool act = s < ss.s_all;
+    const int* dc = a.ds.dcount + (int64_t)st * 3;
+    const int part = act && s >= ss.s_luma ? 1 : 0;
+    const int sp = part ? s - ss.s_luma : s;
+    const int npart = part ? dc[1] + dc[2] : dc[0];
+    const int off = sp * kSeg;
+    const int n = act ? min(kSeg, npart - off) : 0;
+    const bool last = act && s == ss.s_all - 1;
+    const int64_t pb = a.ds.dbase[st] + (part ? chroma_start(dc[0]) : 0) + off;  // multiple of 64
+    const uint2 ck = act ? a.ck[ss.seg_base + s] : make_uint2(0x100u, 0u);
+    int range = (int)ck.x, low = 0;
+    // the segment's digits: stream-wide shift index ck.y; a segment that
+    // could run past the slot writes to the dummy area (the fixup sees the
+    // overflow and the batch is encoded again with a larger budget)
+    DigitOut o;
+    o.rs = __builtin_amdgcn_make_buffer_rsrc(a.slice_out + (int64_t)st * a.slice_stride, 0,
+                                            (int)(a.digit_cap * 4), kBufDword3);
+    o.kb = (int)ck.y * 4;
+    const int kb0 = o.kb;
+    const uint4* P = reinterpret_cast<const uint4*>(a.ds.pre + pb);
+    const uint32_t* B = a.ds.bits + (pb >> 5);
+    const int nmax = wave_max(n);
     const uint4 z4 = make_uint4(0, 0, 0, 0);
     uint4 na = z4, nb = z4, ma = z4, mb = z4;
     uint32_t nw = 0u, mw = 0u;
@@ -992,52 +1069,102 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_dcode(CodeArgs a) {
         mb = P[(i >> 4) + 5];
         mw = B[(i >> 5) + 2];
       }
-      // the tail: a state-0 decision of bit 0 leaves low and range as they
-      // are (r1 = 0, range - r1 = range), so the bytes past the end are
-      // zeroed and the same code runs (one copy of it: the I-cache is shared
-      // with the walker on the CU)
       const int rem = n - i;
       if (rem < 32) {
         wa = tail_mask(wa, rem);
         wb = tail_mask(wb, rem - 16);
         bw = rem > 0 ? bw & ((1u << rem) - 1u) : 0u;
       }
-      decide32(L, S, wa, wb, bw, tf);
-      flush_if_t(L, S, kDFlushAt, tf);  // <= 16 digits per half block
+      static_for<0, 4>([&](auto gc) {
+        constexpr int G = decltype(gc)::value;
+        const Masks8 k = masks8<G>(bw);
+        static_for<0, 8>([&](auto jc) {
+          constexpr int J = 8 * G + decltype(jc)::value;
+          const uint32_t sw = state_word<J>(wa, wb);
+          put_dec(low, range, o, (int)((sw >> ((J & 3) * 8)) & 0xFFu), k.m[J & 7]);
+        });
+      });
     }
-    ndec += nmax;
-  }
-  if (a.dbg && lane == 0) {
-    a.dbg[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memtime() - t_all;
-    a.dbg[blockIdx.x * 4 + 1] = tf.tf;
-    a.dbg[blockIdx.x * 4 + 2] = ndec;
-    a.dbg[blockIdx.x * 4 + 3] = tf.ti;
-  }
-  if (live) {
-    const int64_t ndig = terminate(L, S, true, kDRing);
-    if (ndig > a.slice_stride / 2) {
-      atomicAdd(a.status, 1);
-      atomicMax(a.status + 1, (int)ndig);
+    if (last) {  // a 0 on state 129, then ff_rac_terminate (ffv1enc.c:1331-1334, rangecoder.c:104-116)
+      put_dec(low, range, o, 129, 0);
+      low += 0xFF;
+      __builtin_amdgcn_raw_buffer_store_b32((uint32_t)low, o.rs, o.kb, 0, 0);  // range = 0xFF: one shift
+      low = (low & 0xFF) << 8;
+      __builtin_amdgcn_raw_buffer_store_b32((uint32_t)low, o.rs, o.kb + 4, 0, 0);  // range = 0xFF again
+      low = (low & 0xFF) << 8;
+      o.kb += 8;
     }
-    a.slice_bytes[st] = min(ndig, a.slice_stride / 2);  // digits, until ffv1_sink; never past the slot
+    if (act) a.segrec[ss.seg_base + s] = make_uint2((uint32_t)low, (uint32_t)((o.kb - kb0) >> 2));
   }
+}
+
+// ffv1_dfix: one lane per stream.  The header's digits (fixed per key and
+// slice, computed on the host) go first; then, segment by segment, with L
+// the real low entering it and v, u its local lows at its first two shifts:
+// the real lows there are x = L + v and u + ((x & 0xFF) - (v & 0xFF)) << 8
+// (the window after the first shift is (low & 0xFF) << 8), and the low
+// leaving it is its own from the second shift on, L + its local low when it
+// has no shift.
+constexpr int kFixThreads = kWave;
+__global__ __launch_bounds__(kFixThreads) void ffv1_dfix(CodeArgs a) {
+  const int64_t st = (int64_t)blockIdx.x * kFixThreads + threadIdx.x;
+  if (st >= (int64_t)a.nframes * a.nslices) return;
+  const int f = (int)(st / a.nslices), slice = (int)(st % a.nslices);
+  const HdrState h = a.hdr[a.keyflags[f] * a.nslices + slice];
+  const StreamSegs ss = a.segs_info[st];
+  uint32_t* const out = reinterpret_cast<uint32_t*>(a.slice_out + st * a.slice_stride);
+  const int64_t cap = a.digit_cap;
+  for (int k = 0; k < h.ndig; k++) out[k] = a.hdr_digits[h.off + k];
+  int L = h.low;
+  int64_t total = h.ndig;
+  const uint2* ck = a.ck + ss.seg_base;
+  const uint2* sr = a.segrec + ss.seg_base;
+  for (int s = 0; s < ss.s_all; s++) {
+    const int64_t J = ck[s].y;
+    const uint2 r = sr[s];
+    const int e = (int)r.x, n = (int)r.y;
+    total = J + n;
+    if (J + 2 > cap) continue;  // past the slot (dropped): the batch is encoded again
+    if (n == 0) {
+      L += e;
+      continue;
+    }
+    const int v = (int)out[J];
+    const int x = L + v;
+    out[J] = (uint32_t)x;
+    const int delta = ((x & 0xFF) - (v & 0xFF)) << 8;
+    if (n == 1) {
+      L = e + delta;
+    } else {
+      out[J + 1] = out[J + 1] + (uint32_t)delta;
+      L = e;
+    }
+  }
+  // over the byte budget (the bytes are the digits but the last one or so):
+  // the stores past the slot were dropped and the batch is encoded again
+  if (total > a.slice_cap) {
+    atomicAdd(a.status, 1);
+    atomicMax(a.status + 1, (int)min(total, (int64_t)0x7FFFFFFF));
+  }
+  a.slice_bytes[st] = min(total, cap);  // digits, until ffv1_sink
 }
 
 // The byte writer of the decision-stream coder, one wave per (frame, slice)
 // stream.  renorm_encoder (rangecoder.h:52-75) emits, for every digit j but
 // the last non-run one and the 0xFF-run digits after it, the byte
-// (qv_j + c_j) & 0xFF, where c_j is the carry (qv_k >> 8) of the first
-// non-run digit k after j (a run digit: qv = 0xFF with a non-zero low byte,
-// never the first).  So 64 digits at a time are turned into bytes in
-// parallel; only the tail of a block, from its last non-run digit, waits for
-// the next block with a non-run digit.  The bytes go over the digits (byte i
-// never passes digit i, which sits at bytes 2i, 2i+1).
+// (qv_j + c_j) & 0xFF, where qv_j = low_j >> 8 and c_j is the carry
+// (qv_k >> 8) of the first non-run digit k after j (a run digit: low in
+// (0xFF00, 0x10000), qv = 0xFF with a non-zero low byte, never the first).
+// So 64 digits at a time are turned into bytes in parallel; only the tail of
+// a block, from its last non-run digit, waits for the next block with a
+// non-run digit.  The bytes go over the digits (byte i never passes digit
+// i, which sits at bytes 4i .. 4i+3).
 constexpr int kSinkThreads = kWave;
 __global__ __launch_bounds__(kSinkThreads) void ffv1_sink(CodeArgs a) {
   const int64_t st = blockIdx.x;
   const int lane = threadIdx.x;
   uint8_t* const out = a.slice_out + st * a.slice_stride;
-  const uint16_t* const din = reinterpret_cast<const uint16_t*>(out);
+  const uint32_t* const din = reinterpret_cast<const uint32_t*>(out);  // values of low at the shifts
   const int n = (int)a.slice_bytes[st];  // digits
   const int cap = (int)a.slice_cap;
   int pend = -1;       // the last non-run digit so far: its byte and its run's wait for a carry
@@ -1047,8 +1174,8 @@ __global__ __launch_bounds__(kSinkThreads) void ffv1_sink(CodeArgs a) {
     const int j = b * kWave + lane;
     const uint32_t d = nx;
     nx = j + kWave < n ? din[j + kWave] : 0u;  // the next block, in flight
-    const uint32_t qv = d & 0x1FFu;
-    const bool nonrun = j < n && !(j > 0 && qv == 0xFFu && (d & 0x200u));
+    const uint32_t qv = d >> 8;  // low < 2^17
+    const bool nonrun = j < n && !(j > 0 && qv == 0xFFu && (d & 0xFFu));
     const uint64_t m = __ballot(nonrun);
     if (!m) continue;  // a run goes on
     __builtin_amdgcn_wave_barrier();  // every lane has read its digit before any byte lands
@@ -1538,8 +1665,10 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
 // chroma_start, its pad (ffv1_internal.h, DecisionStream).
 constexpr int kLayoutThreads = 1024;
 __global__ __launch_bounds__(kLayoutThreads) void ffv1_layout(const int* dcount, int nstreams, int64_t* dbase,
-                                                              int64_t* total) {
+                                                              int64_t* total, StreamSegs* segs, int* seg_totals,
+                                                              int* wmap) {
   __shared__ int64_t part[kLayoutThreads];
+  __shared__ int64_t spart[kLayoutThreads];  // segments << 32 | 64-segment groups
   const int t = threadIdx.x;
   const int per = (nstreams + kLayoutThreads - 1) / kLayoutThreads;
   const int lo = min(t * per, nstreams), hi = min(lo + per, nstreams);
@@ -1547,22 +1676,52 @@ __global__ __launch_bounds__(kLayoutThreads) void ffv1_layout(const int* dcount,
     const int64_t n = (int64_t)dcount[3 * i + 1] + dcount[3 * i + 2];
     return chroma_start(dcount[3 * i]) + ((n + kStreamAlign - 1) / kStreamAlign * kStreamAlign) + kChainPad;
   };
-  int64_t sum = 0;
-  for (int i = lo; i < hi; i++) sum += len(i);
+  // the coder's segments: the luma chain's, then the chroma chain's (at
+  // least one segment, which carries the terminate)
+  auto nseg = [&](int i, int* sl) -> int {
+    const int64_t nc = (int64_t)dcount[3 * i + 1] + dcount[3 * i + 2];
+    const int a = (int)((dcount[3 * i] + kSeg - 1) / kSeg), b = (int)((nc + kSeg - 1) / kSeg);
+    *sl = a;
+    return max(1, a + b);
+  };
+  int64_t sum = 0, ssum = 0;
+  for (int i = lo; i < hi; i++) {
+    int sl;
+    const int n = nseg(i, &sl);
+    sum += len(i);
+    ssum += ((int64_t)n << 32) | (int64_t)((n + 63) / 64);
+  }
   part[t] = sum;
+  spart[t] = ssum;
   __syncthreads();
   for (int o = 1; o < kLayoutThreads; o <<= 1) {
     const int64_t y = t >= o ? part[t - o] : 0;
+    const int64_t z = t >= o ? spart[t - o] : 0;
     __syncthreads();
     part[t] += y;
+    spart[t] += z;
     __syncthreads();
   }
-  int64_t acc = part[t] - sum;
+  int64_t acc = part[t] - sum, sacc = spart[t] - ssum;
   for (int i = lo; i < hi; i++) {
     dbase[i] = acc;
     acc += len(i);
+    int sl;
+    const int n = nseg(i, &sl);
+    StreamSegs g;
+    g.seg_base = (int)(sacc >> 32);
+    g.wave_base = (int)(sacc & 0xFFFFFFFF);
+    g.s_luma = sl;
+    g.s_all = n;
+    segs[i] = g;
+    for (int k = 0; k < (n + 63) / 64; k++) wmap[g.wave_base + k] = i;
+    sacc += ((int64_t)n << 32) | (int64_t)((n + 63) / 64);
   }
-  if (t == kLayoutThreads - 1) *total = part[t];
+  if (t == kLayoutThreads - 1) {
+    *total = part[t];
+    seg_totals[0] = (int)(spart[t] >> 32);
+    seg_totals[1] = (int)(spart[t] & 0xFFFFFFFF);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2048,10 +2207,23 @@ int launch_code(const CodeArgs& a, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_dcode(const CodeArgs& a, void* stream) {
+int launch_range(const CodeArgs& a, void* stream) {
   const int64_t streams = (int64_t)a.nframes * a.nslices;
-  dim3 grid((unsigned)((streams + kCodeThreads - 1) / kCodeThreads)), block(kCodeThreads);
-  hipLaunchKernelGGL(ffv1_dcode, grid, block, dcode_lds_bytes(a.nopsets), reinterpret_cast<hipStream_t>(stream), a);
+  dim3 grid((unsigned)((streams + kRangeThreads - 1) / kRangeThreads)), block(kRangeThreads);
+  hipLaunchKernelGGL(ffv1_range, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_dseg(const CodeArgs& a, void* stream) {
+  hipLaunchKernelGGL(ffv1_dseg, dim3((unsigned)a.dseg_blocks), dim3(kDsegThreads), 0,
+                     reinterpret_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_dfix(const CodeArgs& a, void* stream) {
+  const int64_t streams = (int64_t)a.nframes * a.nslices;
+  dim3 grid((unsigned)((streams + kFixThreads - 1) / kFixThreads)), block(kFixThreads);
+  hipLaunchKernelGGL(ffv1_dfix, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2106,9 +2278,10 @@ int launch_bits(const BitsArgs& a, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_layout(const int* dcount, int nstreams, int64_t* dbase, int64_t* total, void* stream) {
+int launch_layout(const int* dcount, int nstreams, int64_t* dbase, int64_t* total, StreamSegs* segs,
+                  int* seg_totals, int* wmap, void* stream) {
   hipLaunchKernelGGL(ffv1_layout, dim3(1), dim3(kLayoutThreads), 0, reinterpret_cast<hipStream_t>(stream), dcount,
-                     nstreams, dbase, total);
+                     nstreams, dbase, total, segs, seg_totals, wmap);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -76,7 +76,9 @@ class KernelStats(ctypes.Structure):
                 ("states_launches", ctypes.c_int), ("layout_ms", ctypes.c_float),
                 ("bits_ms", ctypes.c_float), ("layout_launches", ctypes.c_int),
                 ("bits_launches", ctypes.c_int), ("sink_ms", ctypes.c_float),
-                ("sink_launches", ctypes.c_int)]
+                ("sink_launches", ctypes.c_int), ("dseg_ms", ctypes.c_float),
+                ("dfix_ms", ctypes.c_float), ("dseg_launches", ctypes.c_int),
+                ("dfix_launches", ctypes.c_int)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

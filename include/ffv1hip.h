@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define FFV1HIP_ABI_VERSION 3
+#define FFV1HIP_ABI_VERSION 4
 #define FFV1HIP_AVERROR_INVALIDDATA (-1094995529)
 
 /* AVCodecContext fields + codec private options that encode_init reads
@@ -187,11 +187,13 @@ int ffv1hip_last_kernel_ms(ffv1hip_ctx *ctx, float *encode_ms, float *assemble_m
 /* Per-kernel totals of every call since profiling was (re)enabled: summed
  * HIP-event durations (events on each kernel's own stream) and launch counts
  * of ffv1_symbols (prediction/context), the states walk (ffv1_walk,
- * frame-parallel mode), the range coder (ffv1_dcode; ffv1_code or
- * ffv1_code_golomb in the chained mode), ffv1_assemble_packets, and in
- * frame-parallel mode the decision layout (ffv1_layout) and decision bits
- * (ffv1_bits) and the coder's byte writer (ffv1_sink).  Frame-parallel mode launches each once per call; the chained
- * mode launches symbols and code once per frame index of the GOP. */
+ * frame-parallel mode), the range coder (frame-parallel mode: ffv1_range,
+ * the serial pass, in code_ms, then ffv1_dseg and ffv1_dfix; chained mode:
+ * ffv1_code or ffv1_code_golomb), ffv1_assemble_packets, and in
+ * frame-parallel mode the decision layout (ffv1_layout), the decision bits
+ * (ffv1_bits) and the coder's byte writer (ffv1_sink).  Frame-parallel mode
+ * launches each once per call; the chained mode launches symbols and code
+ * once per frame index of the GOP. */
 typedef struct ffv1hip_kernel_stats {
     float symbols_ms, code_ms, assemble_ms;
     int symbols_launches, code_launches, assemble_launches;
@@ -202,6 +204,9 @@ typedef struct ffv1hip_kernel_stats {
     int layout_launches, bits_launches;
     float sink_ms;                         /* frame-parallel mode: the coder's byte writer (ffv1_sink) */
     int sink_launches;
+    float dseg_ms, dfix_ms;                /* frame-parallel mode: the coder's segments (ffv1_dseg) and
+                                              their join (ffv1_dfix); code_ms is then ffv1_range */
+    int dseg_launches, dfix_launches;
 } ffv1hip_kernel_stats;
 int ffv1hip_last_kernel_stats(ffv1hip_ctx *ctx, ffv1hip_kernel_stats *out);
 

@@ -13,6 +13,14 @@ for p in (ROOT, PKG):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# torch first: the tests that stage frames in HBM use torch, whose bundled
+# HIP runtime must be the process's one before libffv1hip.so loads (loaded
+# the other way round, torch finds no GPU)
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
