@@ -210,6 +210,20 @@ std::string pass1_text(const uint64_t* rc_stat, const uint64_t* rc_stat2, int co
 
 }  // namespace ffv1hip
 
+// Host-only test hook (not part of include/ffv1hip.h): pass2_states on a
+// stats_in text, for the sanitizer build's parser checks
+// (tests/test_sanitize.py).  init0 / init1 receive 666 / 7563 x 32 states.
+extern "C" int ffv1hip_internal_pass2_states(const char* stats, int custom, uint8_t* stt,
+                                             const uint8_t* default_one, uint8_t* init0, uint8_t* init1) {
+  std::vector<uint8_t> init[2];
+  std::string err;
+  const int rc = ffv1hip::pass2_states(stats, custom != 0, stt, default_one, init, &err);
+  if (rc < 0) return rc;
+  std::memcpy(init0, init[0].data(), init[0].size());
+  std::memcpy(init1, init[1].data(), init[1].size());
+  return 0;
+}
+
 // Host-only test hook (not part of include/ffv1hip.h): sort_stt on
 // caller-given counts [256][2] and table, for the FFSWAP(int, ...)
 // truncation check in tests/test_twopass_host.py.

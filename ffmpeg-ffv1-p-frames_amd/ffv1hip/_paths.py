@@ -12,7 +12,9 @@ INCLUDE_DIR = os.path.join(REPO_DIR, "include")
 
 
 def synth_lib() -> str:
-    p = os.path.join(LIB_DIR, "libffv1synth.so")
+    # FFV1HIP_SYNTH_LIB: another build of the same source (the sanitizer
+    # build, oracle/Makefile `sanitize`)
+    p = os.environ.get("FFV1HIP_SYNTH_LIB") or os.path.join(LIB_DIR, "libffv1synth.so")
     if not os.path.exists(p):
         raise FileNotFoundError(f"{p} missing: run `python ffmpeg-ffv1-p-frames_amd/build.py`")
     return p

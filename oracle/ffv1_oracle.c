@@ -1809,10 +1809,12 @@ static void decode_row(void *coder, int golomb, plane_state *ps, const int16_t q
                 diff = vlc_get(b, &ps->vlc[ctx], bits);
             }
         }
+        /* a damaged stream can decode any int here (the reference's int
+         * arithmetic wraps on it); unsigned keeps that defined */
         if (sign)
-            diff = -diff;
+            diff = (int)(0u - (unsigned)diff);
         int pred = median3(t.L, t.L + t.T - t.LT, t.T);
-        P[(int64_t)y * w + x] = (int16_t)((unsigned)(pred + diff) & ((1u << bits) - 1));
+        P[(int64_t)y * w + x] = (int16_t)(((unsigned)pred + (unsigned)diff) & ((1u << bits) - 1));
     }
     *run_index_io = run_index;
 }

@@ -14,7 +14,9 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "libffv1_oracle.so")
+# FFV1_ORACLE_LIB: another build of the same source (the sanitizer build,
+# `make -C oracle sanitize`)
+_LIB_PATH = os.environ.get("FFV1_ORACLE_LIB") or os.path.join(_HERE, "libffv1_oracle.so")
 
 
 class Config(ctypes.Structure):
