@@ -1194,8 +1194,11 @@ __global__ __launch_bounds__(kSinkThreads) void ffv1_sink(CodeArgs a) {
   }
   if (lane == 0) {
     const int nbytes = pend < 0 ? 0 : pend;
-    if (nbytes > cap) atomicAdd(a.status, 1);
-    a.slice_bytes[st] = nbytes;
+    if (nbytes > cap) {  // the batch is encoded again; the assembly stays inside the slots
+      atomicAdd(a.status, 1);
+      atomicMax(a.status + 1, nbytes);
+    }
+    a.slice_bytes[st] = min(nbytes, cap);
   }
 }
 
