@@ -712,10 +712,67 @@ static int grow_decisions(ffv1hip_ctx* c, int k, int64_t need) {
   return 0;
 }
 
+// Decision-stream capacity of one set for a batch of nb frames: the worst
+// case when it is small, else ~12 per symbol (real content codes ~3; a batch
+// that needs more grows the set).
+static int64_t decision_cap(const ffv1hip_ctx* c, int64_t nb) {
+  const int64_t align = nb * c->nslices * kStreamSlack;
+  const int64_t worst = nb * c->frame_samples * c->wmax + align;
+  const int64_t guess = nb * c->frame_samples * 12 + align;
+  const int64_t cap = worst <= (int64_t(1) << 31) ? worst : std::min(worst, guess);
+  return (cap + 4095) & ~int64_t(4095);
+}
+
+// HBM the context's buffers take for a batch of nb frames (the second walk
+// records set, allocated only with room to spare, not counted).
+static int64_t device_bytes(const ffv1hip_ctx* c, int64_t nb) {
+  int64_t b = nb * (c->frame_bytes + c->slice_stride * c->nslices + c->packet_stride);
+  b += 2 * int64_t(2) * c->contexts * 32 * c->nslices;  // the P-frame carry
+  if (c->frames_mode) {
+    b += nb * (16 * c->frame_samples + 4 * int64_t(kChunkWords) * c->frame_chunks);  // walk records, chunk bits
+    const int64_t dcap = decision_cap(c, nb);
+    b += 2 * (dcap + dcap / 8);                                                      // two decision sets
+    int64_t segs = 0, groups = 0;
+    for (const SliceGeom& g : c->geom) {
+      const int64_t l = int64_t(g.pw[0]) * g.ph[0] * c->wmax;
+      const int64_t ch = (int64_t(g.pw[1]) * g.ph[1] + int64_t(g.pw[2]) * g.ph[2]) * c->wmax;
+      const int64_t n = std::max<int64_t>(1, (l + kSeg - 1) / kSeg + (ch + kSeg - 1) / kSeg);
+      segs += n;
+      groups += (n + 63) / 64;
+    }
+    b += nb * (2 * 8 * segs + 3 * 4 * groups);  // checkpoints, segment records, group maps
+  } else {
+    const int64_t slots = c->max_slots;
+    b += slots * (4 * c->frame_samples + int64_t(2) * c->contexts * 32 * c->nslices);
+  }
+  return b;
+}
+
 static int alloc_device(ffv1hip_ctx* c) {
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   const int nb = c->max_batch;
+  {  // a batch that cannot fit is refused up front, with the largest one that can
+    size_t free_b = 0, total_b = 0;
+    HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+    const int64_t need = device_bytes(c, nb);
+    const int64_t reserve = int64_t(1) << 30;  // streams, events, the runtime
+    if (need + reserve > int64_t(free_b)) {
+      int64_t fit = 0;
+      for (int64_t lo = 1, hi = nb; lo <= hi;) {
+        const int64_t mid = (lo + hi) / 2;
+        if (device_bytes(c, mid) + reserve <= int64_t(free_b)) {
+          fit = mid;
+          lo = mid + 1;
+        } else {
+          hi = mid - 1;
+        }
+      }
+      return set_err(-12, "a batch of %d frames needs %.1f GB of device memory, %.1f GB are free: "
+                          "at most %lld frames per batch fit", nb, double(need) / 1e9, double(free_b) / 1e9,
+                     (long long)fit);
+    }
+  }
+  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIP_TRY(hipMalloc(&c->d_frames, size_t(c->frame_bytes) * nb));
   HIP_TRY(hipMalloc(&c->d_qt, sizeof(c->qt)));
   HIP_TRY(hipMemcpy(c->d_qt, c->qt, sizeof(c->qt), hipMemcpyHostToDevice));
@@ -743,6 +800,7 @@ static int alloc_device(ffv1hip_ctx* c) {
   }
   HIP_TRY(hipEventCreateWithFlags(&c->dep_ev, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming));
+  for (hipEvent_t& e : c->entry) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   // the coder grid is padded to whole waves and idle lanes touch their own table
   if (c->frames_mode) {
     // double-buffered: the states walk of batch k+1 runs while batch k codes
@@ -756,7 +814,6 @@ static int alloc_device(ffv1hip_ctx* c) {
     HIP_TRY(hipMalloc(&c->d_dtotal, 3 * sizeof(int64_t)));
     HIP_TRY(hipHostMalloc(&c->h_dtotal, 3 * sizeof(int64_t), hipHostMallocDefault));
     for (hipEvent_t& e : c->coded3) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    for (hipEvent_t& e : c->entry) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->walk_a, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->zeroed, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->sym1, hipEventDisableTiming));
@@ -772,8 +829,6 @@ static int alloc_device(ffv1hip_ctx* c) {
     for (hipEvent_t& e : c->bitsed) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->walked) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->coded) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    // decision capacity: the worst case when it is small, else ~12 per symbol
-    // (real content codes ~10); a batch that needs more grows the set
     HIP_TRY(hipMalloc(&c->d_scratch, 4096));
     // the coder's segments: at most wmax decisions per sample
     c->max_segs = 0;
@@ -791,10 +846,7 @@ static int alloc_device(ffv1hip_ctx* c) {
     HIP_TRY(hipMalloc(&c->d_ck, sizeof(uint2) * size_t(c->max_segs)));
     HIP_TRY(hipMalloc(&c->d_segrec, sizeof(uint2) * size_t(c->max_segs)));
     if (upload_hdr(c) < 0) return -5;
-    const int64_t align = int64_t(nb) * c->nslices * kStreamSlack;
-    const int64_t worst = int64_t(nb) * c->frame_samples * c->wmax + align;
-    const int64_t guess = int64_t(nb) * c->frame_samples * 12 + align;
-    const int64_t cap = worst <= (int64_t(1) << 31) ? worst : std::min(worst, guess);
+    const int64_t cap = decision_cap(c, nb);
     for (int k = 0; k < 2; k++)
       if (grow_decisions(c, k, cap) < 0) return -5;
     // the second records set, only with room to spare (a later batch may
@@ -1030,8 +1082,13 @@ static int coded_bits(const ffv1hip_params& p) {
   return p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample;
 }
 
+// caller: the stream the frames were written on (their readiness is all the
+// batch takes from it), or null when they are complete already.  The
+// batch's own kernels run on the context's streams, so that a caller's
+// stream never orders them after the previous batch's states walk.
 static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_bytes,
-                     const int64_t plane_off[3], const int plane_stride[3], int n, hipStream_t st) {
+                     const int64_t plane_off[3], const int plane_stride[3], int n, hipStream_t caller) {
+  hipStream_t const st = c->stream;
   const ffv1hip_params& p = c->P;
   if (n <= 0 || n > c->max_batch) return set_err(-22, "batch of %d frames (max %d)", n, c->max_batch);
   // keyframes and state-chaining segments
@@ -1058,7 +1115,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     c->last.plane_stride[k] = plane_stride[k];
   }
   c->last.n = n;
-  c->last.st = st;
+  c->last.st = caller;
   c->last.pn0 = c->picture_number;
   c->last.have0 = c->have_states;
   c->last.pcur0 = c->pcur;
@@ -1094,14 +1151,17 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   const bool part = c->frames_mode && !c->two_rec && !serial && c->pass != 1 && part_env;
   hipStream_t const sst = c->frames_mode && (c->two_rec || part) && !serial ? c->bits_stream : st;
   hipStream_t const lst = part ? st : sst;  // the layout's stream
+  if (caller) {  // the frames, for the symbols
+    HIP_TRY(hipEventRecord(c->entry[fb], caller));
+    HIP_TRY(hipStreamWaitEvent(st, c->entry[fb], 0));
+    if (sst != st) HIP_TRY(hipStreamWaitEvent(sst, c->entry[fb], 0));
+  }
   if (sst != st) {
-    // the caller's work on st so far (the frames), then what the symbols
-    // rewrite: records set fb (read by the walk of batch k-2) and metadata
-    // set t3 (read by the coder of batch k-3); and they start once the first
-    // part of the previous batch's walk is done and its second part's waves
-    // are on the CUs (a short wait kernel, FFV1HIP_SYM_DELAY_US)
-    HIP_TRY(hipEventRecord(c->entry[fb], st));
-    HIP_TRY(hipStreamWaitEvent(sst, c->entry[fb], 0));
+    // what the symbols rewrite: records set fb (read by the walk of batch
+    // k-2) and metadata set t3 (read by the coder of batch k-3); and they
+    // start once the first part of the previous batch's walk is done and its
+    // second part's waves are on the CUs (a short wait kernel,
+    // FFV1HIP_SYM_DELAY_US)
     HIP_TRY(hipStreamWaitEvent(sst, c->walked[fb], 0));
     HIP_TRY(hipStreamWaitEvent(sst, c->coded3[t3], 0));
     if (c->walk_a_valid) {
@@ -1470,7 +1530,7 @@ int ffv1hip_encode_device(ffv1hip_ctx* c, const void* d_frames, int64_t frame_by
   if (!c || !d_frames) return set_err(-22, "null argument");
   HIP_TRY(hipSetDevice(c->device));
   return run_batch(c, static_cast<const uint8_t*>(d_frames), frame_bytes, plane_offset, plane_stride,
-                   n_frames, stream ? reinterpret_cast<hipStream_t>(stream) : c->stream);
+                   n_frames, reinterpret_cast<hipStream_t>(stream));
 }
 
 // A slice went over the byte budget: the reference would still have coded

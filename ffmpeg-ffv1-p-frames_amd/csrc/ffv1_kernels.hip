@@ -1000,17 +1000,30 @@ struct DigitOut {
 };
 constexpr int kBufDword3 = 0x00020000;  // gfx9-family raw buffer (32-bit data format)
 
+#ifndef FFV1_DSEG_STORE
+#define FFV1_DSEG_STORE 0  // 0: every lane stores, out of range without a shift; 1: exec-masked; 2: LDS ring
+#endif
+constexpr int kSRing = 32, kSRingStride = kSRing + 3;
+
 // put_rac + renorm_encoder's shift (rangecoder.h:52-102): the value of low
 // before a shift is stored as the lane's next digit.
-__device__ __forceinline__ void put_dec(int& low, int& range, DigitOut& o, int s, int m) {
+__device__ __forceinline__ void put_dec(int& low, int& range, DigitOut& o, int s, int m, lds_u32* ring = nullptr) {
   const int r1 = (int)(__umul24((unsigned)range, (unsigned)s) >> 8);
   const int d = range - r1;
   low += d & m;
   const int nr = (m & r1) | (~m & d);  // m ? r1 : d, one bitwise select
   // all ones when a byte shifts out: nr < 0x100 (24+ leading zeros, see range32)
   const int sm = __builtin_amdgcn_sbfe((int)__builtin_clz((unsigned)nr), 3, 1);
+#if FFV1_DSEG_STORE == 0
   __builtin_amdgcn_raw_buffer_store_b32((uint32_t)low, o.rs, o.kb | (~sm & (int)0x80000000), 0, 0);
   o.kb += sm & 4;
+#elif FFV1_DSEG_STORE == 1
+  if (sm) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)low, o.rs, o.kb, 0, 0);
+  o.kb += sm & 4;
+#else
+  ring[o.kb] = (uint32_t)low;  // kb: the ring head here
+  o.kb += sm & 1;
+#endif
   const int shifted = (int)__builtin_amdgcn_perm(0u, (uint32_t)low, 0x0c0c000cu);  // (low & 0xFF) << 8
   low = (sm & shifted) | (~sm & low);
   range = nr << (sm & 8);
@@ -1018,6 +1031,12 @@ __device__ __forceinline__ void put_dec(int& low, int& range, DigitOut& o, int s
 
 __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
   const int lane = threadIdx.x;
+#if FFV1_DSEG_STORE == 2
+  __shared__ uint32_t sring[kDsegThreads * kSRingStride];
+  lds_u32* const ring = (lds_u32*)(sring + lane * kSRingStride);
+#else
+  lds_u32* const ring = nullptr;
+#endif
   const int ngroups = a.seg_totals[1];
   for (int w = blockIdx.x; w < ngroups; w += gridDim.x) {
     const int st = a.wmap[w];  // wave-uniform
@@ -1034,13 +1053,30 @@ __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
     const int64_t pb = a.ds.dbase[st] + (part ? chroma_start(dc[0]) : 0) + off;  // multiple of 64
     const uint2 ck = act ? a.ck[ss.seg_base + s] : make_uint2(0x100u, 0u);
     int range = (int)ck.x, low = 0;
-    // the segment's digits: stream-wide shift index ck.y; a segment that
-    // could run past the slot writes to the dummy area (the fixup sees the
-    // overflow and the batch is encoded again with a larger budget)
+    // the segment's digits: stream-wide shift index ck.y; stores past the
+    // slot are dropped (the join sees the overflow and the batch is encoded
+    // again with a larger budget)
     DigitOut o;
     o.rs = __builtin_amdgcn_make_buffer_rsrc(a.slice_out + (int64_t)st * a.slice_stride, 0,
                                             (int)(a.digit_cap * 4), kBufDword3);
+#if FFV1_DSEG_STORE == 2
+    int gpos = (int)ck.y;  // digits flushed so far (stream-wide index of the ring's first)
+    o.kb = 0;
+    auto flush = [&]() {
+      const int nr = o.kb;
+      for (int t = 0; __ballot(t < nr); t += 4) {
+        const uint32_t d0 = ring[t], d1 = ring[t + 1], d2 = ring[t + 2], d3 = ring[t + 3];
+        if (t < nr) __builtin_amdgcn_raw_buffer_store_b32(d0, o.rs, (gpos + t) * 4, 0, 0);
+        if (t + 1 < nr) __builtin_amdgcn_raw_buffer_store_b32(d1, o.rs, (gpos + t + 1) * 4, 0, 0);
+        if (t + 2 < nr) __builtin_amdgcn_raw_buffer_store_b32(d2, o.rs, (gpos + t + 2) * 4, 0, 0);
+        if (t + 3 < nr) __builtin_amdgcn_raw_buffer_store_b32(d3, o.rs, (gpos + t + 3) * 4, 0, 0);
+      }
+      gpos += nr;
+      o.kb = 0;
+    };
+#else
     o.kb = (int)ck.y * 4;
+#endif
     const int kb0 = o.kb;
     const uint4* P = reinterpret_cast<const uint4*>(a.ds.pre + pb);
     const uint32_t* B = a.ds.bits + (pb >> 5);
@@ -1081,12 +1117,33 @@ __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
         static_for<0, 8>([&](auto jc) {
           constexpr int J = 8 * G + decltype(jc)::value;
           const uint32_t sw = state_word<J>(wa, wb);
-          put_dec(low, range, o, (int)((sw >> ((J & 3) * 8)) & 0xFFu), k.m[J & 7]);
+          put_dec(low, range, o, (int)((sw >> ((J & 3) * 8)) & 0xFFu), k.m[J & 7], ring);
+#if FFV1_DSEG_STORE == 2
+          if constexpr ((J & 15) == 15) {
+            if (__ballot(o.kb > 15)) flush();  // <= 16 shifts per 16 decisions
+          }
+#endif
         });
       });
     }
+#if FFV1_DSEG_STORE == 2
+    flush();
+    o.kb = gpos * 4;  // byte offset of the next digit, for the terminate
+    const int kb0b = (int)ck.y * 4;
+#else
+    const int kb0b = kb0;
+#endif
     if (last) {  // a 0 on state 129, then ff_rac_terminate (ffv1enc.c:1331-1334, rangecoder.c:104-116)
-      put_dec(low, range, o, 129, 0);
+      {  // the trailer decision: at most one shift
+        const int r1 = (int)(__umul24((unsigned)range, 129u) >> 8);
+        range -= r1;
+        if (range < 0x100) {
+          __builtin_amdgcn_raw_buffer_store_b32((uint32_t)low, o.rs, o.kb, 0, 0);
+          o.kb += 4;
+          low = (low & 0xFF) << 8;
+          range <<= 8;
+        }
+      }
       low += 0xFF;
       __builtin_amdgcn_raw_buffer_store_b32((uint32_t)low, o.rs, o.kb, 0, 0);  // range = 0xFF: one shift
       low = (low & 0xFF) << 8;
@@ -1094,7 +1151,8 @@ __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
       low = (low & 0xFF) << 8;
       o.kb += 8;
     }
-    if (act) a.segrec[ss.seg_base + s] = make_uint2((uint32_t)low, (uint32_t)((o.kb - kb0) >> 2));
+    if (act) a.segrec[ss.seg_base + s] = make_uint2((uint32_t)low, (uint32_t)((o.kb - kb0b) >> 2));
+    (void)kb0;
   }
 }
 

@@ -130,9 +130,10 @@ int ffv1hip_encode2(ffv1hip_ctx *ctx, const void *const planes[3],
 
 /* Device-resident variant: frames already in HBM at d_frames + i*frame_bytes
  * with plane p at byte offset plane_offset[p] and row stride plane_stride[p].
- * The frames are read on `stream` (a hipStream_t, may be NULL: the context's
- * own stream); the coding may continue on the context's internal streams so
- * that consecutive calls overlap.  Nothing is synchronised: the packets of
+ * `stream` (a hipStream_t) is the stream the frames were written on: the
+ * batch waits for the work queued on it so far, and for nothing else; NULL
+ * when the frames are complete already.  The coding runs on the context's
+ * internal streams, so that consecutive calls overlap.  Nothing is synchronised: the packets of
  * the LAST call are valid after ffv1hip_synchronize, ffv1hip_fetch or
  * ffv1hip_device_packets (each call's packets replace the previous call's).
  * Those three check the last call's slices against the slice byte budget: a

@@ -340,3 +340,19 @@ def test_full_size_configs_match_oracle(name):
     assert ex == ex_ref
     assert [len(p) for p, _ in got] == [len(p) for p, _ in ref]
     assert got == ref
+
+
+def test_batch_too_large_for_hbm_is_enomem():
+    """A batch that cannot fit in HBM is refused with -ENOMEM and the
+    largest batch that fits (not a HIP out-of-memory -EIO half way through
+    the allocations), and that batch can then be created."""
+    import re
+    from ffv1hip import FFV1Error, HipEncoder, configure
+    params = configure(3840, 2160, "yuv444p16", slices=64, coder=1, gop_size=12, bits_per_raw_sample=12)
+    with pytest.raises(FFV1Error) as e:
+        HipEncoder(params, 0, 5000)
+    assert e.value.code == -12
+    fit = int(re.search(r"at most (\d+) frames", str(e.value)).group(1))
+    assert 12 <= fit < 5000
+    enc = HipEncoder(params, 0, min(fit, 48))
+    enc.close()

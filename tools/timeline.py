@@ -5,7 +5,8 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 ks = []
 for r in rows:
     n = r["Kernel_Name"]
-    for k in ("ffv1_symbols", "ffv1_layout", "ffv1_bits", "ffv1_walk", "ffv1_dcode", "ffv1_sink", "ffv1_assemble"):
+    for k in ("ffv1_symbols", "ffv1_layout", "ffv1_bits", "ffv1_walk", "ffv1_range", "ffv1_dseg", "ffv1_dfix",
+              "ffv1_sink", "ffv1_assemble", "ffv1_delay"):
         if k in n:
             ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), k))
 ks.sort()
