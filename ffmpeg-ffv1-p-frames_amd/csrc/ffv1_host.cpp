@@ -10,6 +10,11 @@
 #include <cstring>
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -37,6 +42,92 @@ int set_err(int code, const char* fmt, ...) {
     if (e_ != hipSuccess)                                                     \
       return set_err(-5, "%s failed: %s", #expr, hipGetErrorString(e_));      \
   } while (0)
+
+// A few host threads for the copies between pageable caller memory and the
+// pinned staging buffers of the host-frame path: run(fn) calls fn(part,
+// nparts) on every worker and on the caller, and returns when all are done.
+class CopyPool {
+ public:
+  explicit CopyPool(int n) : n_(std::max(1, n)) {
+    for (int i = 1; i < n_; i++) th_.emplace_back([this, i] { loop(i); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (std::thread& t : th_) t.join();
+  }
+  int size() const { return n_; }
+  void run(const std::function<void(int, int)>& fn) {
+    if (n_ == 1) {
+      fn(0, 1);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_ = &fn;
+      pending_ = n_ - 1;
+      gen_++;
+    }
+    cv_.notify_all();
+    fn(0, n_);
+    std::unique_lock<std::mutex> g(m_);
+    done_.wait(g, [&] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void loop(int i) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int, int)>* job;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        job = job_;
+      }
+      (*job)(i, n_);
+      std::lock_guard<std::mutex> g(m_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  int n_;
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int, int)>* job_ = nullptr;
+  uint64_t gen_ = 0;
+  int pending_ = 0;
+  bool stop_ = false;
+};
+
+// rows of wb bytes from src (pitch sp) to dst (pitch dp), split over the pool
+void pool_copy2d(CopyPool& pool, uint8_t* dst, int64_t dp, const uint8_t* src, int64_t sp, int64_t wb, int64_t rows) {
+  if (rows <= 0 || wb <= 0) return;
+  const bool flat = dp == wb && sp == wb;
+  if (wb * rows < (int64_t(1) << 20) || pool.size() == 1) {
+    if (flat) {
+      std::memcpy(dst, src, size_t(wb * rows));
+    } else {
+      for (int64_t r = 0; r < rows; r++) std::memcpy(dst + r * dp, src + r * sp, size_t(wb));
+    }
+    return;
+  }
+  pool.run([&](int part, int np) {
+    if (flat) {  // 4 KiB-aligned byte ranges
+      const int64_t n = wb * rows, per = ((n + np - 1) / np + 4095) & ~int64_t(4095);
+      const int64_t a = std::min(n, per * part), b = std::min(n, a + per);
+      if (b > a) std::memcpy(dst + a, src + a, size_t(b - a));
+    } else {
+      const int64_t a = rows * part / np, b = rows * (part + 1) / np;
+      for (int64_t r = a; r < b; r++) std::memcpy(dst + r * dp, src + r * sp, size_t(wb));
+    }
+  });
+}
 
 // ---------------------------------------------------------------------------
 // Transition tables.  Default: ff_build_rac_states(c, 0.05*2^32, 256-8)
@@ -234,7 +325,9 @@ struct ffv1hip_ctx {
   int64_t slice_stride = 0;  // bytes per slice slot of d_slice_out
   int64_t packet_stride = 0;
   int64_t frame_bytes = 0;  // host-layout batch buffer stride
-  int64_t plane_bytes[3]{};
+  int64_t plane_bytes[kMaxPlanes]{};  // input planes of a frame slot (YUVA: Y, Cb, Cr, A)
+  int pcount = 2;                     // plane contexts: plane_count, 2 + transparency (ffv1enc.c:720, 890-891)
+  int ncoded = 3;                     // coded planes of a slice (symbols kernel z, chained coders)
   int64_t picture_number = 0;
   bool have_states = false;  // persistent states valid (a frame was coded)
   int max_slots = 0;          // segments (= frame slots) per call
@@ -314,13 +407,6 @@ struct ffv1hip_ctx {
   hipEvent_t entry[2] = {nullptr, nullptr};  // set k's batch: the launch stream's work so far
   hipEvent_t walk_a = nullptr;               // the first part of the last batch's walk is done
   bool walk_a_valid = false;
-  // With one records set the same overlap is partial: the next batch's
-  // symbols beside part B skip the plane group and frames part B reads
-  // (frames from part_b_f0 of group part_b_grp, all groups when part_b_all);
-  // those run on the walk's stream after part B
-  int part_b_f0 = 0, part_b_grp = 0;
-  bool part_b_all = true;
-  hipEvent_t zeroed = nullptr, sym1 = nullptr;  // the stream counts are zeroed / part 1 of the symbols is done
   SliceGeom* d_geom = nullptr;
   int* d_slot_frames = nullptr;  // [j][slot]
   int* d_status = nullptr;       // [set][4]: [0] slices over budget, [1] most bytes one needed
@@ -339,23 +425,35 @@ struct ffv1hip_ctx {
   // ffv1hip_synchronize waits for `done` (the previous batch's last kernel)
   hipEvent_t dep_ev = nullptr, done_ev = nullptr;
   bool dep_valid = false;
-  // the last batch, kept so that a slice over the byte budget can be
-  // encoded again with a larger budget (ffv1hip_fetch)
+  // The last two batches (slot b & 1 for batch b), kept so that a slice over
+  // the byte budget can be encoded again with a larger budget
+  // (settle_batch): the inputs, and the state before the batch.
   struct LastBatch {
     bool valid = false;
     const uint8_t* frames = nullptr;
     int64_t frame_bytes = 0;
-    int64_t plane_off[3]{};
-    int plane_stride[3]{};
+    int64_t plane_off[kMaxPlanes]{};
+    int plane_stride[kMaxPlanes]{};
     int n = 0;
     hipStream_t st = nullptr;
     int64_t pn0 = 0;
     bool have0 = false;
-    int pcur0 = 0, buf0 = 0, tri0 = 0, status_set = 0;
+    int pcur0 = 0, buf0 = 0, tri0 = 0, pk0 = 0, status_set = 0;
+    int pk = 0;  // the packet set its packets are in
     int64_t gob0 = 0;
-  } last;
-  int last_n = 0;
-  std::vector<int> last_keys;
+    std::vector<int> keys;
+  } hist[2];
+  hipEvent_t hist_done[2] = {nullptr, nullptr};  // batch slot k's last kernel
+  int64_t nsub = 0;                              // batches submitted
+  // packet slots: set 0 always; a second set (two_pk) for the host-frame
+  // path, so that batch k's packets are copied out while batch k+1 codes
+  uint8_t* d_packets2 = nullptr;
+  int64_t* d_packet_size2 = nullptr;
+  bool two_pk = false;
+  int pk = 0;  // packet set of the next batch
+  uint8_t* pkts(int set) const { return set ? d_packets2 : d_packets; }
+  int64_t* psize(int set) const { return set ? d_packet_size2 : d_packet_size; }
+  const LastBatch& last() const { return hist[(nsub + 1) & 1]; }
   bool profiling = false;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> kev;  // [2 * launches]: start/stop per kernel launch
@@ -367,11 +465,39 @@ struct ffv1hip_ctx {
   // 0..q_pts.size()-1, and encoded packets not yet handed out
   std::vector<int64_t> q_pts;
   struct Ready {
-    std::vector<uint8_t> data;
+    const uint8_t* base = nullptr;  // the pinned packets of its packet set
     std::vector<int64_t> off, size, pts;
     std::vector<int> key;
     size_t next = 0;
   } ready;
+  // The host-frame path (ffv1hip_encode / ffv1hip_encode2): frames are
+  // copied in through pinned staging slots by the pool's threads, on a
+  // transfer stream of its own, into one of two frame sets (d_frames,
+  // d_frames2); packets come back through a pinned buffer per packet set.
+  struct HostPipe {
+    bool on = false;
+    bool overlap = false;  // two frame sets and two packet sets: batch k+1 stages while batch k codes
+    std::unique_ptr<CopyPool> pool;
+    hipStream_t xfer = nullptr;
+    static constexpr int kSlots = 6;
+    int64_t slot_bytes = 0;
+    uint8_t* h_slot[kSlots]{};
+    hipEvent_t slot_ev[kSlots]{};
+    bool slot_busy[kSlots]{};
+    int next = 0;
+    int64_t fill = 0;
+    uint8_t* h_pk[2]{};  // pinned packets of a collected batch, per packet set
+    int64_t h_pk_cap[2]{};
+  } pipe;
+  uint8_t* d_frames2 = nullptr;
+  // encode2 with the pipe: the set being filled and the launched batches
+  // whose packets are not handed out yet (batch id, pts)
+  int q_set = 0;
+  struct Launched {
+    int64_t b;
+    std::vector<int64_t> pts;
+  };
+  std::deque<Launched> launched;
 };
 
 extern "C" {
@@ -382,7 +508,8 @@ int ffv1hip_abi_version(void) { return FFV1HIP_ABI_VERSION; }
 int ffv1hip_configure(ffv1hip_params* out, const ffv1hip_options* o) {
   if (!out || !o || !o->pix_fmt || o->width <= 0 || o->height <= 0)
     return set_err(-22, "invalid arguments");
-  // rgb: 1 AV_PIX_FMT_0RGB32 (bgr0 bytes), 2 GBRP9..14 (ffv1enc.c:787-814)
+  // rgb: 1 AV_PIX_FMT_0RGB32 (bgr0 bytes) / RGB32 (bgra bytes), 2 GBRP9..14
+  // (ffv1enc.c:780-814); planes = the format's components (2 and 4: alpha)
   struct Fmt { const char* name; int planes, hs, vs, depth, rgb; };
   static const Fmt fmts[] = {
       {"yuv420p", 3, 1, 1, 8, 0},    {"yuv422p", 3, 1, 0, 8, 0},    {"yuv444p", 3, 0, 0, 8, 0},
@@ -393,6 +520,12 @@ int ffv1hip_configure(ffv1hip_params* out, const ffv1hip_options* o) {
       {"yuv444p16", 3, 0, 0, 16, 0}, {"gray16", 1, 0, 0, 16, 0},    {"bgr0", 3, 0, 0, 8, 1},
       {"0rgb32", 3, 0, 0, 8, 1},     {"gbrp9", 3, 0, 0, 9, 2},      {"gbrp10", 3, 0, 0, 10, 2},
       {"gbrp12", 3, 0, 0, 12, 2},    {"gbrp14", 3, 0, 0, 14, 2},
+      // with alpha (ffv1enc.c:725-786)
+      {"yuva420p", 4, 1, 1, 8, 0},   {"yuva422p", 4, 1, 0, 8, 0},   {"yuva444p", 4, 0, 0, 8, 0},
+      {"ya8", 2, 0, 0, 8, 0},        {"yuva420p9", 4, 1, 1, 9, 0},  {"yuva422p9", 4, 1, 0, 9, 0},
+      {"yuva444p9", 4, 0, 0, 9, 0},  {"yuva420p10", 4, 1, 1, 10, 0}, {"yuva422p10", 4, 1, 0, 10, 0},
+      {"yuva444p10", 4, 0, 0, 10, 0}, {"yuva420p16", 4, 1, 1, 16, 0}, {"yuva422p16", 4, 1, 0, 16, 0},
+      {"yuva444p16", 4, 0, 0, 16, 0}, {"bgra", 4, 0, 0, 8, 1},      {"rgb32", 4, 0, 0, 8, 1},
   };
   const Fmt* f = nullptr;
   for (const Fmt& c : fmts)
@@ -445,9 +578,12 @@ int ffv1hip_configure(ffv1hip_params* out, const ffv1hip_options* o) {
   }
   if (!bits) bits = 8;
   if (o->context < 0 || o->context > 1) return set_err(-22, "context model %d", o->context);
-  p.chroma_planes = f->planes == 3;
-  p.chroma_h_shift = f->planes == 3 ? f->hs : 0;
-  p.chroma_v_shift = f->planes == 3 ? f->vs : 0;
+  // chroma_planes = nb_components >= 3, transparency = 4 or 2 components
+  // (ffv1enc.c:772-774, 782)
+  p.chroma_planes = f->planes >= 3;
+  p.chroma_h_shift = f->planes >= 3 ? f->hs : 0;
+  p.chroma_v_shift = f->planes >= 3 ? f->vs : 0;
+  p.transparency = f->planes == 4 || f->planes == 2;
   p.bits_per_raw_sample = bits;
   p.packed_at_lsb = packed;
   p.sample_bytes = f->rgb == 1 ? 4 : f->depth > 8 ? 2 : 1;
@@ -476,6 +612,17 @@ int ffv1hip_configure(ffv1hip_params* out, const ffv1hip_options* o) {
   return 0;
 }
 
+// YA8: gray with alpha, Y and A bytes interleaved in one plane
+// (ffv1enc.c:1199-1201)
+static bool is_ya8(const ffv1hip_params& p) { return p.transparency && !p.chroma_planes && !p.colorspace; }
+
+// Input planes of a frame (the caller's plane arrays): Y, Cb, Cr (+ A); one
+// for gray, YA8, bgr0 and RGB32.
+static int input_planes(const ffv1hip_params& p) {
+  if (p.colorspace) return p.sample_bytes == 4 ? 1 : 3;
+  return p.chroma_planes ? 3 + (p.transparency != 0) : 1;
+}
+
 static int build_extradata(ffv1hip_ctx* c) {
   const ffv1hip_params& p = c->P;
   c->extradata.clear();
@@ -493,7 +640,7 @@ static int build_extradata(ffv1hip_ctx* c) {
   r.put(st, p.chroma_planes);
   r.symbol(st, p.chroma_h_shift, false);
   r.symbol(st, p.chroma_v_shift, false);
-  r.put(st, 0);  // transparency
+  r.put(st, p.transparency);
   r.symbol(st, p.num_h_slices - 1, false);
   r.symbol(st, p.num_v_slices - 1, false);
   r.symbol(st, 2, false);  // quant_table_count
@@ -559,7 +706,7 @@ static void build_ops(ffv1hip_ctx* c) {
           L.bit(kSetHdr, 0, p.chroma_planes);
           L.sym(kSetHdr, 0, p.chroma_h_shift, false);
           L.sym(kSetHdr, 0, p.chroma_v_shift, false);
-          L.bit(kSetHdr, 0, 0);
+          L.bit(kSetHdr, 0, p.transparency);
           for (int t = 0; t < 5; t++) {
             int last = 0, i;
             for (i = 1; i < 128; i++)
@@ -577,7 +724,7 @@ static void build_ops(ffv1hip_ctx* c) {
         L.sym(kSetSlice, 1, int(int64_t(y0 + 1) * nv / p.height), false);
         L.sym(kSetSlice, 1, int(int64_t(x1 - x0 + 1) * nh / p.width) - 1, false);
         L.sym(kSetSlice, 1, int(int64_t(y1 - y0 + 1) * nv / p.height) - 1, false);
-        for (int j = 0; j < 2; j++) L.sym(kSetSlice, 1, p.context_model, false);
+        for (int j = 0; j < c->pcount; j++) L.sym(kSetSlice, 1, p.context_model, false);
         L.sym(kSetSlice, 1, 3, false);  // progressive
         L.sym(kSetSlice, 1, p.sar_num, false);
         L.sym(kSetSlice, 1, p.sar_den, false);
@@ -658,7 +805,10 @@ static int upload_hdr(ffv1hip_ctx* c) {
   return 0;
 }
 
+static void pipe_close(ffv1hip_ctx* c);
+
 static void free_device(ffv1hip_ctx* c) {
+  pipe_close(c);
   void* ptrs[] = {c->d_frames, c->d_qt, c->d_tabs, c->d_ops, c->d_nops, c->d_segs, c->d_keys,
                   c->d_slice_out, c->d_slice_bytes, c->d_packets, c->d_packet_size, c->d_persist[0],
                   c->d_persist[1], c->d_tables, c->d_sym, c->d_keys2, c->d_cbits, c->d_dcount, c->d_dbase, c->d_dtotal, c->d_pre[0],
@@ -692,8 +842,8 @@ static void free_device(ffv1hip_ctx* c) {
   for (hipEvent_t& e : c->entry)
     if (e) (void)hipEventDestroy(e);
   if (c->walk_a) (void)hipEventDestroy(c->walk_a);
-  if (c->zeroed) (void)hipEventDestroy(c->zeroed);
-  if (c->sym1) (void)hipEventDestroy(c->sym1);
+  for (hipEvent_t& e : c->hist_done)
+    if (e) (void)hipEventDestroy(e);
 }
 
 // Decision-stream buffers of set k for `need` decisions.  The set's previous
@@ -724,10 +874,11 @@ static int64_t decision_cap(const ffv1hip_ctx* c, int64_t nb) {
 }
 
 // HBM the context's buffers take for a batch of nb frames (the second walk
-// records set, allocated only with room to spare, not counted).
+// records set, allocated only with room to spare, and the host-frame path's
+// frame slots, allocated on its first use, not counted).
 static int64_t device_bytes(const ffv1hip_ctx* c, int64_t nb) {
-  int64_t b = nb * (c->frame_bytes + c->slice_stride * c->nslices + c->packet_stride);
-  b += 2 * int64_t(2) * c->contexts * 32 * c->nslices;  // the P-frame carry
+  int64_t b = nb * (c->slice_stride * c->nslices + c->packet_stride);
+  b += 2 * int64_t(c->pcount) * c->contexts * 32 * c->nslices;  // the P-frame carry
   if (c->frames_mode) {
     b += nb * (16 * c->frame_samples + 4 * int64_t(kChunkWords) * c->frame_chunks);  // walk records, chunk bits
     const int64_t dcap = decision_cap(c, nb);
@@ -743,7 +894,7 @@ static int64_t device_bytes(const ffv1hip_ctx* c, int64_t nb) {
     b += nb * (2 * 8 * segs + 3 * 4 * groups);  // checkpoints, segment records, group maps
   } else {
     const int64_t slots = c->max_slots;
-    b += slots * (4 * c->frame_samples + int64_t(2) * c->contexts * 32 * c->nslices);
+    b += slots * (4 * c->frame_samples + int64_t(c->pcount) * c->contexts * 32 * c->nslices);
   }
   return b;
 }
@@ -773,7 +924,7 @@ static int alloc_device(ffv1hip_ctx* c) {
     }
   }
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HIP_TRY(hipMalloc(&c->d_frames, size_t(c->frame_bytes) * nb));
+  for (hipEvent_t& e : c->hist_done) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_TRY(hipMalloc(&c->d_qt, sizeof(c->qt)));
   HIP_TRY(hipMemcpy(c->d_qt, c->qt, sizeof(c->qt), hipMemcpyHostToDevice));
   uint8_t tabs[1024];
@@ -793,7 +944,7 @@ static int alloc_device(ffv1hip_ctx* c) {
   HIP_TRY(hipMalloc(&c->d_slice_bytes, sizeof(int64_t) * c->nslices * nb));
   HIP_TRY(hipMalloc(&c->d_packets, size_t(c->packet_stride) * nb));
   HIP_TRY(hipMalloc(&c->d_packet_size, sizeof(int64_t) * nb));
-  const size_t state_bytes = size_t(2) * c->contexts * 32;
+  const size_t state_bytes = size_t(c->pcount) * c->contexts * 32;
   for (uint8_t*& pb : c->d_persist) {
     HIP_TRY(hipMalloc(&pb, state_bytes * c->nslices));
     HIP_TRY(hipMemset(pb, 128, state_bytes * c->nslices));
@@ -815,8 +966,6 @@ static int alloc_device(ffv1hip_ctx* c) {
     HIP_TRY(hipHostMalloc(&c->h_dtotal, 3 * sizeof(int64_t), hipHostMallocDefault));
     for (hipEvent_t& e : c->coded3) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->walk_a, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&c->zeroed, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&c->sym1, hipEventDisableTiming));
     {
       std::vector<int> ident(nb);
       for (int i = 0; i < nb; i++) ident[i] = i;
@@ -890,7 +1039,7 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
                      : p.colorspace == 1 ? p.chroma_planes && !p.chroma_h_shift && !p.chroma_v_shift &&
                                                (p.sample_bytes == 4 ? p.bits_per_raw_sample == 8
                                                                     : p.sample_bytes == 2 && p.packed_at_lsb &&
-                                                                          p.bits_per_raw_sample <= 14)
+                                                                          p.bits_per_raw_sample <= 14 && !p.transparency)
                                          : false;
   if (p.version == 2 || p.version > 3 || p.num_h_slices * p.num_v_slices > 256 ||
       p.bits_per_raw_sample < 8 || p.bits_per_raw_sample > 16 || p.width <= 0 || p.height <= 0 || !fmt_ok)
@@ -903,18 +1052,25 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
   c->max_batch = max_batch_frames;
   c->nslices = p.num_h_slices * p.num_v_slices;
   c->contexts = contexts_of(p.context_model);
+  c->pcount = 2 + (p.transparency != 0);
+  c->ncoded = p.colorspace ? 3 + (p.transparency != 0)
+                           : p.chroma_planes ? 3 + (p.transparency != 0) : 1 + (p.transparency != 0);
   c->dflt = default_tables();
   c->frame = p.ac == 2 ? custom_tables(c->dflt) : c->dflt;
   quant_set(c->qt, p.context_model, p.bits_per_raw_sample);
   build_extradata(c);
   build_ops(c);
   build_hdr(c);
-  // layout of a frame in the batch buffer (planar, tightly packed)
+  // layout of a frame in the batch buffer (planar, tightly packed): Y, Cb,
+  // Cr, A (YUVA); YA8 one plane of Y, A byte pairs; bgr0 / RGB32 one plane
+  // of 4-byte pixels
+  const bool ya8 = is_ya8(p);
   const int cw = p.chroma_planes ? -((-p.width) >> p.chroma_h_shift) : 0;
   const int ch = p.chroma_planes ? -((-p.height) >> p.chroma_v_shift) : 0;
-  c->plane_bytes[0] = int64_t(p.width) * p.height * p.sample_bytes;
+  c->plane_bytes[0] = int64_t(p.width) * p.height * p.sample_bytes * (ya8 ? 2 : 1);
   c->plane_bytes[1] = c->plane_bytes[2] = p.sample_bytes == 4 ? 0 : int64_t(cw) * ch * p.sample_bytes;
-  c->frame_bytes = (c->plane_bytes[0] + 2 * c->plane_bytes[1] + 255) & ~int64_t(255);
+  c->plane_bytes[3] = p.transparency && !p.colorspace && p.chroma_planes ? int64_t(p.width) * p.height * p.sample_bytes : 0;
+  c->frame_bytes = (c->plane_bytes[0] + 2 * c->plane_bytes[1] + c->plane_bytes[3] + 255) & ~int64_t(255);
   // Per-slice geometry and symbol-stream layout (ffv1.c:117-145,
   // ffv1enc.c:1185-1196); each slice's stream is padded to 4 symbols.
   c->geom.resize(c->nslices);
@@ -933,8 +1089,13 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
       g.px[k] = x0 >> p.chroma_h_shift;
       g.py[k] = y0 >> p.chroma_v_shift;
     }
+    g.px[3] = g.py[3] = g.pw[3] = g.ph[3] = 0;
+    if (p.transparency) {  // A at the luma rectangle: plane 3, or plane 1 of YA8
+      const int k = ya8 ? 1 : 3;
+      g.px[k] = x0; g.py[k] = y0; g.pw[k] = sw; g.ph[k] = sh;
+    }
     int64_t n = 0;
-    for (int k = 0; k < 3; k++) {
+    for (int k = 0; k < kMaxPlanes; k++) {
       g.plane_sym_off[k] = n;
       n += int64_t(g.pw[k]) * g.ph[k];
       g.chunk_off[k] = c->frame_chunks;
@@ -970,7 +1131,9 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
     const char* mode = std::getenv("FFV1HIP_CODER");
     const int64_t lds = walk_lds_bytes(int64_t(2) * c->contexts * 32);
     // RGB interleaves the three planes' rows (encode_rgb_frame): chained
-    c->frames_mode = p.ac && !p.colorspace && lds <= kWalkLdsMax && !(mode && std::strcmp(mode, "chain") == 0);
+    // alpha: the chained coders (a third plane context)
+    c->frames_mode = p.ac && !p.colorspace && !p.transparency && lds <= kWalkLdsMax &&
+                     !(mode && std::strcmp(mode, "chain") == 0);
     c->wmax = 2 * (p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample) + 1;
     // the decision-stream coder writes a slice's digits (2 bytes each) where
     // ffv1_sink then writes its bytes
@@ -1087,7 +1250,7 @@ static int coded_bits(const ffv1hip_params& p) {
 // batch's own kernels run on the context's streams, so that a caller's
 // stream never orders them after the previous batch's states walk.
 static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_bytes,
-                     const int64_t plane_off[3], const int plane_stride[3], int n, hipStream_t caller) {
+                     const int64_t plane_off[kMaxPlanes], const int plane_stride[kMaxPlanes], int n, hipStream_t caller) {
   hipStream_t const st = c->stream;
   const ffv1hip_params& p = c->P;
   if (n <= 0 || n > c->max_batch) return set_err(-22, "batch of %d frames (max %d)", n, c->max_batch);
@@ -1107,21 +1270,26 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   const int nsegs = int(segs.size());
   if (nsegs > c->max_slots) return set_err(-22, "batch spans %d GOPs (max %d)", nsegs, c->max_slots);
   // what to restore if this batch has to be encoded again (ffv1hip_fetch)
-  c->last.valid = true;
-  c->last.frames = d_frames;
-  c->last.frame_bytes = frame_bytes;
-  for (int k = 0; k < 3; k++) {
-    c->last.plane_off[k] = plane_off[k];
-    c->last.plane_stride[k] = plane_stride[k];
+  ffv1hip_ctx::LastBatch& L = c->hist[c->nsub & 1];
+  L.valid = true;
+  L.frames = d_frames;
+  L.frame_bytes = frame_bytes;
+  const int nin = input_planes(p);
+  for (int k = 0; k < kMaxPlanes; k++) {
+    L.plane_off[k] = k < nin ? plane_off[k] : 0;
+    L.plane_stride[k] = k < nin ? plane_stride[k] : 0;
   }
-  c->last.n = n;
-  c->last.st = caller;
-  c->last.pn0 = c->picture_number;
-  c->last.have0 = c->have_states;
-  c->last.pcur0 = c->pcur;
-  c->last.buf0 = c->buf;
-  c->last.tri0 = c->tri;
-  c->last.gob0 = c->gob_count;
+  L.n = n;
+  L.st = caller;
+  L.pn0 = c->picture_number;
+  L.have0 = c->have_states;
+  L.pcur0 = c->pcur;
+  L.buf0 = c->buf;
+  L.tri0 = c->tri;
+  L.pk0 = c->pk;
+  L.pk = c->two_pk ? c->pk : 0;
+  L.gob0 = c->gob_count;
+  L.keys.assign(keys.begin(), keys.end());
   for (uint8_t k : keys) c->gob_count += k;
   if (c->pass == 1) {
     // the previous batch's state counts (ffv1_stats_states, on the coder
@@ -1140,17 +1308,9 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   // FFV1HIP_SERIAL=1 (measurement hook): no walk/code overlap
   static const bool serial = std::getenv("FFV1HIP_SERIAL") && std::atoi(std::getenv("FFV1HIP_SERIAL"));
   hipStream_t const cst = c->frames_mode && !serial ? c->code_stream : st;
-  // the split schedule: symbols, layout and bits on the bits stream; with one
-  // records set (part), the symbols the previous batch's walk part B does
-  // not read on the bits stream, the rest and the layout on st after the walk
-  // (not in pass 1, whose slot counts read all of a batch's records after
-  // its walk).  Off unless FFV1HIP_PARTIAL=1 (read per batch): measured
-  // slower (c4 5.7 -> 4.9, c3 with one set 11.6 -> 10.9 Gpix/s), the walk's
-  // second part slows beside the symbols
-  const bool part_env = std::getenv("FFV1HIP_PARTIAL") && std::atoi(std::getenv("FFV1HIP_PARTIAL")) == 1;
-  const bool part = c->frames_mode && !c->two_rec && !serial && c->pass != 1 && part_env;
-  hipStream_t const sst = c->frames_mode && (c->two_rec || part) && !serial ? c->bits_stream : st;
-  hipStream_t const lst = part ? st : sst;  // the layout's stream
+  // the split schedule (two records sets): symbols, layout and bits on the
+  // bits stream, beside the previous batch's walk
+  hipStream_t const sst = c->frames_mode && c->two_rec && !serial ? c->bits_stream : st;
   if (caller) {  // the frames, for the symbols
     HIP_TRY(hipEventRecord(c->entry[fb], caller));
     HIP_TRY(hipStreamWaitEvent(st, c->entry[fb], 0));
@@ -1192,14 +1352,21 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   SymbolArgs sa{};
   sa.frames = d_frames;
   sa.frame_bytes = frame_bytes;
-  for (int k = 0; k < 3; k++) {
-    sa.plane_off[k] = plane_off[k];
-    sa.plane_stride[k] = plane_stride[k];
+  // coded plane k: input plane k (YA8: Y and A both from input plane 0, one
+  // byte apart, every second byte); context sets Y 0, Cb / Cr 1, A 2 (YA8's
+  // A: 1), ffv1enc.c:1191-1201, (p + 1) / 2 for RGB (:460-467)
+  const bool ya8 = is_ya8(p);
+  for (int k = 0; k < kMaxPlanes; k++) {
+    const int src = ya8 ? 0 : (k < nin ? k : 0);
+    sa.plane_off[k] = plane_off[src] + (ya8 && k == 1 ? 1 : 0);
+    sa.plane_stride[k] = plane_stride[src];
+    sa.pstep[k] = ya8 ? 2 : 1;
+    sa.pset[k] = ya8 ? k : (k + 1) / 2;
   }
   sa.nslots = nsegs;
   sa.geom = c->d_geom;
   sa.nslices = c->nslices;
-  sa.nplanes = p.chroma_planes ? 3 : 1;
+  sa.nplanes = c->ncoded;
   sa.sample_bytes = p.sample_bytes;
   sa.packed_at_lsb = p.packed_at_lsb;
   sa.msb_shift = 16 - p.bits_per_raw_sample;
@@ -1234,14 +1401,14 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   ca.nops = c->d_nops;
   ca.max_ops = c->max_ops;
   ca.tabs = c->d_tabs;
-  ca.state_bytes = int64_t(2) * c->contexts * 32;
+  ca.state_bytes = int64_t(c->pcount) * c->contexts * 32;
   ca.tables = c->d_tables;
   ca.persist_in = c->d_persist[c->pcur];
   ca.persist_out = c->d_persist[c->pcur ^ 1];
   // overflow report of this batch (per buffer set: the coder of the
   // previous batch may still write the other one)
-  const int sset = c->frames_mode ? fb : 0;
-  c->last.status_set = sset;
+  const int sset = c->frames_mode ? fb : L.pk;
+  L.status_set = sset;
   ca.status = c->d_status + 4 * sset;
   ca.slice_out = c->d_slice_out;
   ca.slice_cap = c->slice_cap;
@@ -1250,6 +1417,9 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   ca.version = p.version;
   ca.coded_bits = coded_bits(p);
   ca.rgb = p.colorspace;
+  ca.nplanes = c->ncoded;
+  ca.pcount = c->pcount;
+  for (int k = 0; k < kMaxPlanes; k++) ca.pset[k] = sa.pset[k];
   ca.init = c->d_init;
 
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev[0], st));
@@ -1284,51 +1454,23 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     // one set: the previous batch's bits kernel (its own stream) has read the chunk bits
     if (sst == st) HIP_TRY(hipStreamWaitEvent(st, c->bitsed[fb ^ 1], 0));
     sa.frame_chunks = c->frame_chunks;
-    if (!part) {
-      if (timed(0, sst, [&] { return launch_symbols(sa, sst); }) < 0)
-        return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
-    } else {
-      // part 1 on the bits stream: the plane group part B does not read, and
-      // part B's group in the frames before part_b_f0; part 2 on st
-      const int np = p.chroma_planes ? 3 : 1;
-      const int f0 = c->part_b_all ? 0 : std::min(n, c->part_b_f0);
-      const int g2 = c->part_b_grp;
-      const int g2lo = g2 ? 1 : 0, g2hi = g2 ? np : 1;  // planes of the group part B reads
-      const int g1lo = g2 ? 0 : 1, g1hi = g2 ? 1 : np;
-      auto launch_part = [&](hipStream_t q, int plo, int phi, int flo, int fhi) -> int {
-        if (phi <= plo || fhi <= flo) return 0;
-        SymbolArgs b = sa;
-        b.p_lo = plo;
-        b.p_hi = phi;
-        b.frame_of_slot = c->d_ident + flo;
-        b.nslots = fhi - flo;
-        return timed(0, q, [&] { return launch_symbols(b, q); });
-      };
-      HIP_TRY(hipEventRecord(c->zeroed, sst));
-      if ((c->part_b_all ? 0 : launch_part(sst, g1lo, g1hi, 0, n)) < 0 || launch_part(sst, g2lo, g2hi, 0, f0) < 0)
-        return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
-      HIP_TRY(hipEventRecord(c->sym1, sst));
-      HIP_TRY(hipStreamWaitEvent(st, c->zeroed, 0));
-      if ((c->part_b_all ? launch_part(st, 0, np, 0, n) : launch_part(st, g2lo, g2hi, f0, n)) < 0)
-        return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
-      HIP_TRY(hipStreamWaitEvent(st, c->sym1, 0));
-    }
-    if (timed(4, lst, [&] {
-          return launch_layout(d_dcount, n * c->nslices, d_dbase, c->d_dtotal + t3, d_segs, d_segtot, d_wmap, lst);
+    if (timed(0, sst, [&] { return launch_symbols(sa, sst); }) < 0)
+      return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (timed(4, sst, [&] {
+          return launch_layout(d_dcount, n * c->nslices, d_dbase, c->d_dtotal + t3, d_segs, d_segtot, d_wmap, sst);
         }) < 0)
       return set_err(-5, "layout launch failed: %s", hipGetErrorString(hipGetLastError()));
     // decisions of this batch: the worst case fits without asking the device
     int64_t need = int64_t(n) * c->frame_samples * c->wmax + int64_t(n) * c->nslices * kStreamSlack;
     if (need > c->dcap[fb]) {
-      HIP_TRY(hipMemcpyAsync(c->h_dtotal + t3, c->d_dtotal + t3, sizeof(int64_t), hipMemcpyDeviceToHost, lst));
-      HIP_TRY(hipStreamSynchronize(lst));
+      HIP_TRY(hipMemcpyAsync(c->h_dtotal + t3, c->d_dtotal + t3, sizeof(int64_t), hipMemcpyDeviceToHost, sst));
+      HIP_TRY(hipStreamSynchronize(sst));
       HIP_TRY(hipEventSynchronize(c->coded[fb]));  // set fb's previous coder is done
       need = c->h_dtotal[t3];
       if (need > c->dcap[fb] && grow_decisions(c, fb, need + need / 8) < 0)
         return set_err(-12, "decision buffers for %lld decisions: %s", (long long)need, g_err);
     }
-    HIP_TRY(hipEventRecord(c->laid[fb], lst));  // the records and the stream layout: the walk may start
-    if (lst != sst) HIP_TRY(hipStreamWaitEvent(sst, c->laid[fb], 0));
+    HIP_TRY(hipEventRecord(c->laid[fb], sst));  // the records and the stream layout: the walk may start
     if (sst != st) HIP_TRY(hipStreamWaitEvent(sst, c->coded[fb], 0));  // d_bits[fb]: the coder of batch k-2
     HIP_TRY(hipMemsetAsync(c->d_bits[fb], 0, size_t((need + 31) / 32) * 4, sst));
     DecisionStream ds{d_dcount, d_dbase, c->d_pre[fb], c->d_bits[fb]};
@@ -1339,26 +1481,11 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     ba.nslices = c->nslices;
     ba.nframes = n;
     ba.ds = ds;
-    // the bits run beside the walk, on their own stream; the coder waits for both
-    // FFV1HIP_BITS_INLINE=1 (measurement hook): the bits kernel before the walk, on its stream
-    // FFV1HIP_BITS (measurement hook): side (its own stream, beside the
-    // walk), code (on the coder stream, after the previous batch's packets:
-    // by then the walk's waves are all on the CUs), inline (before the walk)
-    static const int bits_mode = [] {
-      const char* e = std::getenv("FFV1HIP_BITS");
-      if (std::getenv("FFV1HIP_BITS_INLINE") && std::atoi(std::getenv("FFV1HIP_BITS_INLINE"))) return 1;
-      if (!e) return 0;
-      return std::strcmp(e, "inline") == 0 ? 1 : std::strcmp(e, "code") == 0 ? 2 : 0;
-    }();
-    hipStream_t const bst = sst != st ? (bits_mode == 2 && !part ? cst : sst)
-                                      : serial || bits_mode == 1 ? st : bits_mode == 2 ? cst : c->bits_stream;
+    // the bits run beside the walk, on their own stream (after the layout
+    // and the memset with the split schedule); the coder waits for both
+    hipStream_t const bst = sst != st ? sst : serial ? st : c->bits_stream;
     if (sst == st) HIP_TRY(hipEventRecord(c->laid[fb], st));  // after the bits memset
-    if (sst != st && bst != sst) {  // split schedule, bits on the coder stream: after the memset
-      HIP_TRY(hipEventRecord(c->zeroed, sst));
-      HIP_TRY(hipStreamWaitEvent(bst, c->zeroed, 0));
-    } else if (bst != sst) {
-      HIP_TRY(hipStreamWaitEvent(bst, c->laid[fb], 0));
-    }
+    if (bst != sst) HIP_TRY(hipStreamWaitEvent(bst, c->laid[fb], 0));
     if (sst != st) HIP_TRY(hipStreamWaitEvent(st, c->laid[fb], 0));
     if (timed(5, bst, [&] { return launch_bits(ba, bst); }) < 0)
       return set_err(-5, "bits launch failed: %s", hipGetErrorString(hipGetLastError()));
@@ -1412,17 +1539,6 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       return set_err(-5, "walk launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (!two_parts) HIP_TRY(hipEventRecord(c->walk_a, st));
     c->walk_a_valid = sst != st;
-    // what part B reads, for the next batch's partial split: items from nblk
-    // on are the second-dispatched plane group, segment by segment
-    {
-      const int nblk = nitems / 2, npairs = (c->nslices + 1) / 2;
-      const bool chroma_first = 2 * int64_t(c->geom[0].pw[1]) * c->geom[0].ph[1] >
-                                int64_t(c->geom[0].pw[0]) * c->geom[0].ph[0];
-      c->part_b_all = two_parts && first < nblk;
-      c->part_b_grp = chroma_first ? 0 : 1;
-      c->part_b_f0 = !two_parts ? n : segs[std::min(nsegs - 1, (first - nblk) / npairs)].first_frame;
-      if (two_parts && first >= nblk && !(p.chroma_planes) && c->part_b_grp == 1) c->part_b_f0 = n;
-    }
     StatsArgs sta{};
     if (c->pass == 1) {  // slot counts from the records, before the next batch's symbols rewrite them
       sta.rec = d_rec;
@@ -1497,9 +1613,9 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   b.slice_cap = c->slice_cap;
   b.slice_stride = c->slice_stride;
   b.slice_bytes = c->d_slice_bytes;
-  b.packets = c->d_packets;
+  b.packets = c->pkts(L.pk);
   b.packet_stride = c->packet_stride;
-  b.packet_size = c->d_packet_size;
+  b.packet_size = c->psize(L.pk);
   b.nslices = c->nslices;
   b.version = p.version;
   b.ec = p.ec;
@@ -1519,13 +1635,14 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
 
   c->picture_number += n;
   c->have_states = true;
-  c->last_n = n;
-  c->last_keys.assign(keys.begin(), keys.end());
+  HIP_TRY(hipEventRecord(c->hist_done[c->nsub & 1], cst));
+  if (c->two_pk) c->pk ^= 1;
+  c->nsub++;
   return 0;
 }
 
 int ffv1hip_encode_device(ffv1hip_ctx* c, const void* d_frames, int64_t frame_bytes,
-                          const int64_t plane_offset[3], const int plane_stride[3], int n_frames,
+                          const int64_t plane_offset[4], const int plane_stride[4], int n_frames,
                           void* stream) {
   if (!c || !d_frames) return set_err(-22, "null argument");
   HIP_TRY(hipSetDevice(c->device));
@@ -1534,59 +1651,79 @@ int ffv1hip_encode_device(ffv1hip_ctx* c, const void* d_frames, int64_t frame_by
 }
 
 // A slice went over the byte budget: the reference would still have coded
-// it (its buffer is ~w*h*140 bytes, ffv1enc.c:1232), so the last batch is
-// rolled back (picture number, P-frame carry, buffer set) and encoded again
-// with a budget sized from what the slice needed.  The batch's input frames
-// must still be where the call found them.
+// it (its buffer is ~w*h*140 bytes, ffv1enc.c:1232), so the batch is rolled
+// back (picture number, P-frame carry, buffer sets) and encoded again with a
+// budget sized from what the slice needed.  The batch's input frames must
+// still be where the call found them.
 static int grow_slice_budget(ffv1hip_ctx* c, int64_t needed) {
   const int64_t cap = ((needed + needed / 4 + 4096) + 255) & ~int64_t(255);
   if (cap <= c->slice_cap) return set_err(-28, "slice byte budget %lld not enough", (long long)c->slice_cap);
   HIP_TRY(hipDeviceSynchronize());
-  if (c->d_slice_out) HIP_TRY(hipFree(c->d_slice_out));
-  if (c->d_packets) HIP_TRY(hipFree(c->d_packets));
-  c->d_slice_out = nullptr;
-  c->d_packets = nullptr;
+  for (uint8_t** q : {&c->d_slice_out, &c->d_packets, &c->d_packets2}) {
+    if (*q) HIP_TRY(hipFree(*q));
+    *q = nullptr;
+  }
   c->slice_cap = cap;
   c->slice_stride = c->frames_mode ? slice_stride_frames(cap) : cap;
   c->packet_stride = ((cap + 16) * c->nslices + 255) & ~int64_t(255);
+  const size_t pk_bytes = size_t(c->packet_stride) * c->max_batch;
   if (hipMalloc(&c->d_slice_out, size_t(c->slice_stride) * c->nslices * c->max_batch) != hipSuccess ||
-      hipMalloc(&c->d_packets, size_t(c->packet_stride) * c->max_batch) != hipSuccess)
+      hipMalloc(&c->d_packets, pk_bytes) != hipSuccess ||
+      (c->two_pk && hipMalloc(&c->d_packets2, pk_bytes) != hipSuccess))
     return set_err(-12, "slice buffers for a %lld-byte budget", (long long)cap);
   return 0;
 }
 
-// With the device idle: if a slice of the last batch (the one whose packets
-// d_packets holds) went over the byte budget, roll the batch back and encode
-// it again with a larger budget, so that no caller ever sees a truncated
-// slice (the reference fails a frame it cannot fit, ffv1enc.c:283-292; its
-// buffer is large enough for any slice, :1232).  Every batch reports into
-// its own status set, cleared when the batch starts, so the set read here is
-// the last batch's.
-static int settle_last_batch(ffv1hip_ctx* c) {
+// Once batch b (one of the last two submitted) is done: if a slice of it
+// went over the byte budget, roll it back and encode it again with a larger
+// budget, then encode the batch submitted after it again too (it carried
+// b's P-frame states and may use b's buffer sets), so that no caller ever
+// sees a truncated slice (the reference fails a frame it cannot fit,
+// ffv1enc.c:283-292; its buffer is large enough for any slice, :1232).
+// Every batch reports into its own status set, cleared when the batch
+// starts; the last two batches' sets are intact.
+static int settle_batch(ffv1hip_ctx* c, int64_t b) {
+  if (b < 0 || b < c->nsub - 2 || b >= c->nsub) return 0;
+  bool redo_next = false;
+  ffv1hip_ctx::LastBatch next;
   for (int attempt = 0;; attempt++) {
+    const ffv1hip_ctx::LastBatch& L = c->hist[b & 1];
+    HIP_TRY(hipEventSynchronize(c->hist_done[b & 1]));
     int status[4];
-    HIP_TRY(hipMemcpy(status, c->d_status + 4 * c->last.status_set, sizeof(status), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(status, c->d_status + 4 * L.status_set, sizeof(status), hipMemcpyDeviceToHost));
     if (!status[0]) break;
-    if (attempt >= 2 || !c->last.valid)
+    if (attempt >= 2 || !L.valid)
       return set_err(-28, "%d slices exceeded the slice byte budget", status[0]);
-    const ffv1hip_ctx::LastBatch L = c->last;
-    c->picture_number = L.pn0;
-    c->have_states = L.have0;
-    c->pcur = L.pcur0;
-    c->buf = L.buf0;
-    c->tri = L.tri0;
+    if (!redo_next && b + 1 < c->nsub) {
+      // pass 1 keeps one count snapshot, from before the last batch
+      if (c->pass == 1) return set_err(-28, "pass 1: a slice of batch %lld went over the byte budget after a "
+                                            "later batch was submitted", (long long)b);
+      next = c->hist[(b + 1) & 1];
+      redo_next = true;
+    }
+    HIP_TRY(hipDeviceSynchronize());
+    const ffv1hip_ctx::LastBatch R = L;  // run_batch rewrites the slot
+    c->picture_number = R.pn0;
+    c->have_states = R.have0;
+    c->pcur = R.pcur0;
+    c->buf = R.buf0;
+    c->tri = R.tri0;
+    c->pk = R.pk0;
     c->walk_a_valid = false;
-    c->part_b_all = true;
-    c->gob_count = L.gob0;
+    c->gob_count = R.gob0;
     if (c->pass == 1)
       HIP_TRY(hipMemcpy(c->d_rcstat, c->d_rcstat_bak, sizeof(unsigned long long) * (512 + size_t(64) * c->contexts),
                         hipMemcpyDeviceToDevice));
     c->dep_valid = false;  // synchronised above
+    c->nsub = b;
     int rc = grow_slice_budget(c, status[1]);
     if (rc < 0) return rc;
-    rc = run_batch(c, L.frames, L.frame_bytes, L.plane_off, L.plane_stride, L.n, L.st);
+    rc = run_batch(c, R.frames, R.frame_bytes, R.plane_off, R.plane_stride, R.n, nullptr);
     if (rc < 0) return rc;
-    HIP_TRY(hipDeviceSynchronize());
+  }
+  if (redo_next) {
+    const int rc = run_batch(c, next.frames, next.frame_bytes, next.plane_off, next.plane_stride, next.n, nullptr);
+    if (rc < 0) return rc;
   }
   return 0;
 }
@@ -1595,20 +1732,22 @@ int ffv1hip_fetch(ffv1hip_ctx* c, uint8_t* out, int64_t out_cap, int64_t* sizes,
   if (!c) return set_err(-22, "null ctx");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipDeviceSynchronize());
-  const int rc = settle_last_batch(c);
+  const int rc = settle_batch(c, c->nsub - 1);
   if (rc < 0) return rc;
-  const int n = c->last_n;
+  if (!c->nsub) return 0;
+  const ffv1hip_ctx::LastBatch& L = c->last();
+  const int n = L.n;
   std::vector<int64_t> sz(n);
-  HIP_TRY(hipMemcpy(sz.data(), c->d_packet_size, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(sz.data(), c->psize(L.pk), sizeof(int64_t) * n, hipMemcpyDeviceToHost));
   int64_t pos = 0;
   for (int i = 0; i < n; i++) {
     if (out) {
       if (pos + sz[i] > out_cap) return set_err(-22, "output buffer too small");
-      HIP_TRY(hipMemcpy(out + pos, c->d_packets + int64_t(i) * c->packet_stride, sz[i], hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(out + pos, c->pkts(L.pk) + int64_t(i) * c->packet_stride, sz[i], hipMemcpyDeviceToHost));
     }
     pos += sz[i];
     if (sizes) sizes[i] = sz[i];
-    if (key_flags) key_flags[i] = c->last_keys[i];
+    if (key_flags) key_flags[i] = L.keys[i];
   }
   return 0;
 }
@@ -1620,7 +1759,7 @@ int ffv1hip_synchronize(ffv1hip_ctx* c) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (c->code_stream) HIP_TRY(hipStreamSynchronize(c->code_stream));
   if (c->bits_stream) HIP_TRY(hipStreamSynchronize(c->bits_stream));
-  return settle_last_batch(c);
+  return settle_batch(c, c->nsub - 1);
 }
 
 int ffv1hip_device_packets(ffv1hip_ctx* c, void** d_packets, int64_t* packet_stride, void** d_sizes) {
@@ -1628,139 +1767,327 @@ int ffv1hip_device_packets(ffv1hip_ctx* c, void** d_packets, int64_t* packet_str
   // the packets are only valid once settled; a re-encode may also move them
   const int rc = ffv1hip_synchronize(c);
   if (rc < 0) return rc;
-  if (d_packets) *d_packets = c->d_packets;
+  const int pk = c->nsub ? c->last().pk : 0;
+  if (d_packets) *d_packets = c->pkts(pk);
   if (packet_stride) *packet_stride = c->packet_stride;
-  if (d_sizes) *d_sizes = c->d_packet_size;
+  if (d_sizes) *d_sizes = c->psize(pk);
   return 0;
 }
 
 // Where the planes of one frame sit in a batch slot of d_frames (tightly
 // packed rows): np planes, plane k at off[k] with rows[k] rows of pst[k]
 // bytes.  bgr0 is one packed plane.
-static void slot_layout(const ffv1hip_ctx* c, int64_t off[3], int pst[3], int rows[3], int* np) {
+static void slot_layout(const ffv1hip_ctx* c, int64_t off[kMaxPlanes], int pst[kMaxPlanes], int rows[kMaxPlanes],
+                        int* np) {
   const ffv1hip_params& p = c->P;
   const int cw = -((-p.width) >> p.chroma_h_shift), ch = -((-p.height) >> p.chroma_v_shift);
-  *np = p.sample_bytes == 4 ? 1 : p.chroma_planes ? 3 : 1;
+  *np = input_planes(p);
   off[0] = 0;
   off[1] = c->plane_bytes[0];
   off[2] = c->plane_bytes[0] + c->plane_bytes[1];
-  pst[0] = p.width * p.sample_bytes;
+  off[3] = off[2] + c->plane_bytes[2];
+  pst[0] = p.width * p.sample_bytes * (is_ya8(p) ? 2 : 1);
   pst[1] = pst[2] = cw * p.sample_bytes;
-  rows[0] = p.height;
+  pst[3] = p.width * p.sample_bytes;
+  rows[0] = rows[3] = p.height;
   rows[1] = rows[2] = ch;
+}
+
+// ---------------------------------------------------------------------------
+// The host-frame path (ffv1hip_encode, ffv1hip_encode2).  On first use: the
+// batch's frame slots (not needed by ffv1hip_encode_device), the transfer
+// stream, the pinned staging slots and the copy threads; and, with HBM to
+// spare and outside pass 1, a second frame set and a second packet set, so
+// that batch k+1's frames are copied in while batch k codes and batch k-1's
+// packets are copied out (PCIe both ways beside the kernels).
+static int pipe_open(ffv1hip_ctx* c) {
+  ffv1hip_ctx::HostPipe& P = c->pipe;
+  if (P.on) return 0;
+  const size_t fset = size_t(c->frame_bytes) * c->max_batch;
+  if (!c->d_frames && hipMalloc(&c->d_frames, fset) != hipSuccess) {
+    (void)hipGetLastError();
+    c->d_frames = nullptr;
+    return set_err(-12, "the frame slots of a %d-frame batch (%.1f GB) do not fit in device memory", c->max_batch,
+                   double(fset) / 1e9);
+  }
+  HIP_TRY(hipStreamCreateWithFlags(&P.xfer, hipStreamNonBlocking));
+  int nt = int(std::thread::hardware_concurrency());
+  if (const char* e = std::getenv("OMP_NUM_THREADS"))  // the host's CPU share where it is set
+    if (std::atoi(e) > 0) nt = std::min(nt, std::atoi(e));
+  if (const char* e = std::getenv("FFV1HIP_COPY_THREADS")) nt = std::atoi(e);
+  P.pool = std::make_unique<CopyPool>(std::max(1, std::min(nt, 16)));
+  P.slot_bytes = std::max<int64_t>(int64_t(32) << 20, int64_t(c->P.width) * 4);
+  for (int k = 0; k < ffv1hip_ctx::HostPipe::kSlots; k++) {
+    HIP_TRY(hipHostMalloc(&P.h_slot[k], size_t(P.slot_bytes), hipHostMallocDefault));
+    HIP_TRY(hipEventCreateWithFlags(&P.slot_ev[k], hipEventDisableTiming));
+  }
+  if (c->pass != 1) {
+    size_t free_b = 0, total_b = 0;
+    HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+    const size_t pk_bytes = size_t(c->packet_stride) * c->max_batch;
+    if (free_b > fset + pk_bytes + (size_t(2) << 30) && hipMalloc(&c->d_frames2, fset) == hipSuccess &&
+        hipMalloc(&c->d_packets2, pk_bytes) == hipSuccess &&
+        hipMalloc(&c->d_packet_size2, sizeof(int64_t) * c->max_batch) == hipSuccess) {
+      c->two_pk = true;
+      P.overlap = true;
+    } else {
+      (void)hipGetLastError();
+      for (void** q : {(void**)&c->d_frames2, (void**)&c->d_packets2, (void**)&c->d_packet_size2}) {
+        if (*q) (void)hipFree(*q);
+        *q = nullptr;
+      }
+    }
+  }
+  P.on = true;
+  return 0;
+}
+
+static void pipe_close(ffv1hip_ctx* c) {
+  ffv1hip_ctx::HostPipe& P = c->pipe;
+  if (P.xfer) (void)hipStreamSynchronize(P.xfer);
+  P.pool.reset();
+  for (int k = 0; k < ffv1hip_ctx::HostPipe::kSlots; k++) {
+    if (P.h_slot[k]) (void)hipHostFree(P.h_slot[k]);
+    if (P.slot_ev[k]) (void)hipEventDestroy(P.slot_ev[k]);
+  }
+  for (uint8_t* h : P.h_pk)
+    if (h) (void)hipHostFree(h);
+  if (P.xfer) (void)hipStreamDestroy(P.xfer);
+  for (void* q : {(void*)c->d_frames2, (void*)c->d_packets2, (void*)c->d_packet_size2})
+    if (q) (void)hipFree(q);
+}
+
+// The current staging slot's copies are all queued: mark it busy until they
+// are done.
+static int stage_flush(ffv1hip_ctx* c) {
+  ffv1hip_ctx::HostPipe& P = c->pipe;
+  if (P.fill == 0) return 0;
+  HIP_TRY(hipEventRecord(P.slot_ev[P.next], P.xfer));
+  P.slot_busy[P.next] = true;
+  P.next = (P.next + 1) % ffv1hip_ctx::HostPipe::kSlots;
+  P.fill = 0;
+  return 0;
+}
+
+// rows of wb bytes of a host plane (pitch sp) to device memory with tight
+// rows at dst: piece by piece, copied into a pinned slot by the pool and
+// sent with one async copy on the transfer stream; a slot is reused once
+// its copies are done.
+static int stage_rows(ffv1hip_ctx* c, uint8_t* dst, const uint8_t* src, int64_t sp, int64_t wb, int64_t rows) {
+  ffv1hip_ctx::HostPipe& P = c->pipe;
+  for (int64_t r = 0; r < rows;) {
+    if (P.fill + wb > P.slot_bytes) {
+      const int rc = stage_flush(c);
+      if (rc < 0) return rc;
+    }
+    if (P.fill == 0 && P.slot_busy[P.next]) {
+      HIP_TRY(hipEventSynchronize(P.slot_ev[P.next]));
+      P.slot_busy[P.next] = false;
+    }
+    const int64_t nr = std::min(rows - r, (P.slot_bytes - P.fill) / wb);
+    uint8_t* const h = P.h_slot[P.next] + P.fill;
+    pool_copy2d(*P.pool, h, wb, src + r * sp, sp, wb, nr);
+    HIP_TRY(hipMemcpyAsync(dst + r * wb, h, size_t(nr * wb), hipMemcpyHostToDevice, P.xfer));
+    P.fill += nr * wb;
+    r += nr;
+  }
+  return 0;
+}
+
+// One host frame into batch slot `slot` of frame set `set`.
+static int stage_frame(ffv1hip_ctx* c, int set, int64_t slot, const void* const* planes, const int* strides) {
+  int64_t off[kMaxPlanes];
+  int pst[kMaxPlanes], rows[kMaxPlanes], np;
+  slot_layout(c, off, pst, rows, &np);
+  uint8_t* const base = (set ? c->d_frames2 : c->d_frames) + slot * c->frame_bytes;
+  for (int k = 0; k < np; k++) {
+    if (!planes[k]) return set_err(-22, "null plane %d", k);
+    const int rc = stage_rows(c, base + off[k], static_cast<const uint8_t*>(planes[k]), strides[k], pst[k], rows[k]);
+    if (rc < 0) return rc;
+  }
+  return 0;
+}
+
+// Batch `set`'s queued frames (staged) as one batch.
+static int launch_staged(ffv1hip_ctx* c, int set, int n) {
+  int rc = stage_flush(c);
+  if (rc < 0) return rc;
+  int64_t off[kMaxPlanes];
+  int pst[kMaxPlanes], rows[kMaxPlanes], np;
+  slot_layout(c, off, pst, rows, &np);
+  return run_batch(c, set ? c->d_frames2 : c->d_frames, c->frame_bytes, off, pst, n, c->pipe.xfer);
+}
+
+// Batch b's packets (its slice budget settled first) into the pinned buffer
+// of its packet set: sizes, offsets and the buffer out.
+static int collect(ffv1hip_ctx* c, int64_t b, std::vector<int64_t>& sz, std::vector<int64_t>& off,
+                   const uint8_t** data) {
+  int rc = settle_batch(c, b);
+  if (rc < 0) return rc;
+  ffv1hip_ctx::HostPipe& P = c->pipe;
+  const ffv1hip_ctx::LastBatch& L = c->hist[b & 1];
+  const int n = L.n;
+  sz.resize(n);
+  off.resize(n);
+  HIP_TRY(hipEventSynchronize(c->hist_done[b & 1]));
+  HIP_TRY(hipMemcpy(sz.data(), c->psize(L.pk), sizeof(int64_t) * n, hipMemcpyDeviceToHost));
+  int64_t total = 0;
+  for (int i = 0; i < n; i++) {
+    off[i] = total;
+    total += sz[i];
+  }
+  if (total > P.h_pk_cap[L.pk]) {
+    if (P.h_pk[L.pk]) HIP_TRY(hipHostFree(P.h_pk[L.pk]));
+    P.h_pk[L.pk] = nullptr;
+    P.h_pk_cap[L.pk] = 0;
+    const int64_t cap = (total + total / 4 + (int64_t(1) << 20)) & ~int64_t(4095);
+    HIP_TRY(hipHostMalloc(&P.h_pk[L.pk], size_t(cap), hipHostMallocDefault));
+    P.h_pk_cap[L.pk] = cap;
+  }
+  uint8_t* const h = P.h_pk[L.pk];
+  const uint8_t* const d = c->pkts(L.pk);
+  for (int i = 0; i < n; i++)
+    if (sz[i]) HIP_TRY(hipMemcpyAsync(h + off[i], d + int64_t(i) * c->packet_stride, size_t(sz[i]),
+                                      hipMemcpyDeviceToHost, P.xfer));
+  HIP_TRY(hipStreamSynchronize(P.xfer));
+  *data = h;
+  return 0;
 }
 
 int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides, int n_frames,
                    uint8_t* out, int64_t out_cap, int64_t* sizes, int* key_flags) {
   if (!c || !planes || !strides) return set_err(-22, "null argument");
+  if (!c->q_pts.empty() || !c->launched.empty() || c->ready.next < c->ready.size.size())
+    return set_err(-22, "ffv1hip_encode2 has frames or packets pending: flush it first");
   HIP_TRY(hipSetDevice(c->device));
-  int64_t off[3];
-  int pst[3], rows[3], np;
-  slot_layout(c, off, pst, rows, &np);
+  int rc = pipe_open(c);
+  if (rc < 0) return rc;
+  ffv1hip_ctx::HostPipe& P = c->pipe;
   int64_t used = 0;
-  std::vector<int64_t> local_sizes(size_t(c->max_batch));
-  for (int base = 0; base < n_frames; base += c->max_batch) {
-    const int n = std::min(c->max_batch, n_frames - base);
-    for (int i = 0; i < n; i++)
-      for (int k = 0; k < np; k++)
-        HIP_TRY(hipMemcpy2DAsync(c->d_frames + int64_t(i) * c->frame_bytes + off[k], pst[k],
-                                 planes[3 * (base + i) + k], strides[3 * (base + i) + k], pst[k], rows[k],
-                                 hipMemcpyHostToDevice, c->stream));
-    int rc = run_batch(c, c->d_frames, c->frame_bytes, off, pst, n, c->stream);
-    if (rc < 0) return rc;
-    rc = ffv1hip_fetch(c, out ? out + used : nullptr, out_cap - used, local_sizes.data(),
-                       key_flags ? key_flags + base : nullptr);
-    if (rc < 0) return rc;
-    for (int i = 0; i < n; i++) {
-      if (sizes) sizes[base + i] = local_sizes[i];
-      used += local_sizes[i];
+  // batch b's packets out, frames base.. of this call
+  auto finish = [&](int64_t b, int base) -> int {
+    std::vector<int64_t> sz, off;
+    const uint8_t* h = nullptr;
+    int r = collect(c, b, sz, off, &h);
+    if (r < 0) return r;
+    int64_t total = 0;
+    for (int64_t v : sz) total += v;
+    if (out) {
+      if (used + total > out_cap) return set_err(-22, "output buffer too small");
+      pool_copy2d(*P.pool, out + used, total, h, total, total, 1);
     }
+    const std::vector<int>& keys = c->hist[b & 1].keys;
+    for (size_t i = 0; i < sz.size(); i++) {
+      if (sizes) sizes[base + i] = sz[i];
+      if (key_flags) key_flags[base + i] = keys[i];
+    }
+    used += total;
+    return 0;
+  };
+  int64_t prev = -1;
+  int prev_base = 0;
+  const int fstep = input_planes(c->P) == 4 ? FFV1HIP_PLANES_YUVA : FFV1HIP_PLANES;  // plane pointers per frame
+  for (int j = 0, base = 0; base < n_frames; j++, base += c->max_batch) {
+    const int n = std::min(c->max_batch, n_frames - base);
+    // set j % 2 was last read by batch j - 2, collected in iteration j - 1
+    const int set = P.overlap ? (j & 1) : 0;
+    for (int i = 0; i < n; i++)
+      if ((rc = stage_frame(c, set, i, planes + fstep * (base + i), strides + fstep * (base + i))) < 0) return rc;
+    if ((rc = launch_staged(c, set, n)) < 0) return rc;
+    if (!P.overlap) {
+      if ((rc = finish(c->nsub - 1, base)) < 0) return rc;
+      continue;
+    }
+    if (prev >= 0 && (rc = finish(prev, prev_base)) < 0) return rc;
+    prev = c->nsub - 1;
+    prev_base = base;
   }
+  if (prev >= 0 && (rc = finish(prev, prev_base)) < 0) return rc;
   return 0;
 }
 
-// The queued frames as one batch: encode, fetch the packets into `ready`.
-static int encode_queue(ffv1hip_ctx* c) {
-  const int n = int(c->q_pts.size());
-  int64_t off[3];
-  int pst[3], rows[3], np;
-  slot_layout(c, off, pst, rows, &np);
-  int rc = run_batch(c, c->d_frames, c->frame_bytes, off, pst, n, c->stream);
+int ffv1hip_encode2_delay(ffv1hip_ctx* c) {
+  if (!c) return set_err(-22, "null ctx");
+  HIP_TRY(hipSetDevice(c->device));
+  const int rc = pipe_open(c);
   if (rc < 0) return rc;
-  std::vector<int64_t> sz(n);
-  std::vector<int> keys(n);
-  rc = ffv1hip_fetch(c, nullptr, 0, sz.data(), keys.data());  // sizes (and any budget re-encode)
-  if (rc < 0) return rc;
-  int64_t total = 0;
-  for (int64_t v : sz) total += v;
+  return (c->pipe.overlap ? 2 : 1) * c->max_batch - 1;
+}
+
+// The oldest launched batch's packets become the ones handed out.
+static int collect_ready(ffv1hip_ctx* c) {
+  ffv1hip_ctx::Launched l = c->launched.front();
+  c->launched.pop_front();
   ffv1hip_ctx::Ready& R = c->ready;
-  R.data.resize(size_t(total));
-  rc = ffv1hip_fetch(c, R.data.data(), total, nullptr, nullptr);
+  const uint8_t* h = nullptr;
+  const int rc = collect(c, l.b, R.size, R.off, &h);
   if (rc < 0) return rc;
-  R.off.assign(n, 0);
-  for (int i = 1; i < n; i++) R.off[i] = R.off[i - 1] + sz[i - 1];
-  R.size.assign(sz.begin(), sz.end());
-  R.key.assign(keys.begin(), keys.end());
-  R.pts = c->q_pts;
+  R.base = h;
+  R.key = c->hist[l.b & 1].keys;
+  R.pts = std::move(l.pts);
   R.next = 0;
-  c->q_pts.clear();
   return 0;
 }
 
-int ffv1hip_encode2(ffv1hip_ctx* c, const void* const planes[3], const int strides[3], int64_t pts,
+int ffv1hip_encode2(ffv1hip_ctx* c, const void* const planes[4], const int strides[4], int64_t pts,
                     uint8_t* out, int64_t out_cap, int64_t* size, int64_t* pts_out, int* key, int* got_packet) {
   if (!c || !got_packet) return set_err(-22, "null argument");
   *got_packet = 0;
   HIP_TRY(hipSetDevice(c->device));
+  int rc = pipe_open(c);
+  if (rc < 0) return rc;
   ffv1hip_ctx::Ready& R = c->ready;
-  // the packet this call hands out, if one is ready, must fit before the
-  // frame is taken (an error return leaves the queue as it was)
-  if (out && R.next < R.size.size() && R.size[R.next] > out_cap)
-    return set_err(-22, "packet of %lld bytes, buffer %lld", (long long)R.size[R.next], (long long)out_cap);
+  // with two frame sets a batch codes while the next one queues: batches are
+  // collected once two are in flight (the encoder's delay is two batches)
+  const size_t inflight = c->pipe.overlap ? 2 : 1;
+  const bool drained = R.next >= R.size.size();
   if (planes) {
     if (!strides) return set_err(-22, "null strides");
-    // a full queue is encoded as soon as the previous packets are out; one
-    // that is still full (its encode failed) takes no more frames
     if (int64_t(c->q_pts.size()) >= c->max_batch)
       return set_err(-11, "frame queue full (%d frames): drain the packets first", c->max_batch);
+    // the set this frame goes to must not hold a launched batch's frames
+    // (a budget re-encode reads them): that batch is collected first
+    if (c->q_pts.empty() && c->launched.size() >= inflight) {
+      if (!drained) return set_err(-11, "packets pending: drain them first");
+      if ((rc = collect_ready(c)) < 0) return rc;
+    }
     // the frame is copied into the next batch slot (the caller keeps
     // ownership: it may reuse the buffer once the call returns)
-    int64_t off[3];
-    int pst[3], rows[3], np;
-    slot_layout(c, off, pst, rows, &np);
-    const int64_t slot = int64_t(c->q_pts.size());
-    for (int k = 0; k < np; k++) {
-      if (!planes[k]) return set_err(-22, "null plane %d", k);
-      HIP_TRY(hipMemcpy2D(c->d_frames + slot * c->frame_bytes + off[k], pst[k], planes[k], strides[k], pst[k],
-                          rows[k], hipMemcpyHostToDevice));
-    }
+    if ((rc = stage_frame(c, c->q_set, int64_t(c->q_pts.size()), planes, strides)) < 0) return rc;
     c->q_pts.push_back(pts);
-    // a full queue is encoded once the packets of the previous batch are out
-    if (int(c->q_pts.size()) == c->max_batch && R.next >= R.size.size()) {
-      const int rc = encode_queue(c);
-      if (rc < 0) return rc;
+    if (int(c->q_pts.size()) == c->max_batch) {
+      if ((rc = launch_staged(c, c->q_set, c->max_batch)) < 0) return rc;
+      c->launched.push_back(ffv1hip_ctx::Launched{c->nsub - 1, std::move(c->q_pts)});
+      c->q_pts.clear();
+      if (c->pipe.overlap) c->q_set ^= 1;
     }
-  } else if (R.next >= R.size.size() && !c->q_pts.empty()) {  // flush: what is queued
-    const int rc = encode_queue(c);
-    if (rc < 0) return rc;
+    if (R.next >= R.size.size() && c->launched.size() >= inflight && (rc = collect_ready(c)) < 0) return rc;
+  } else if (R.next >= R.size.size()) {  // flush: what is launched, then what is queued
+    if (c->launched.empty() && !c->q_pts.empty()) {
+      if ((rc = launch_staged(c, c->q_set, int(c->q_pts.size()))) < 0) return rc;
+      c->launched.push_back(ffv1hip_ctx::Launched{c->nsub - 1, std::move(c->q_pts)});
+      c->q_pts.clear();
+      if (c->pipe.overlap) c->q_set ^= 1;
+    }
+    if (!c->launched.empty() && (rc = collect_ready(c)) < 0) return rc;
   }
   if (R.next >= R.size.size()) return 0;
   const size_t i = R.next;
   if (out) {
-    if (R.size[i] > out_cap) return set_err(-22, "packet of %lld bytes, buffer %lld", (long long)R.size[i],
-                                            (long long)out_cap);
-    std::memcpy(out, R.data.data() + R.off[i], size_t(R.size[i]));
+    // a slice budget re-encode can make packets larger than the
+    // ffv1hip_max_packet_size the buffer was sized for: the frame is taken,
+    // the packet waits for a call with a larger buffer
+    if (R.size[i] > out_cap) {
+      if (size) *size = R.size[i];
+      return set_err(-28, "packet of %lld bytes, buffer %lld", (long long)R.size[i], (long long)out_cap);
+    }
+    std::memcpy(out, R.base + R.off[i], size_t(R.size[i]));
   }
   if (size) *size = R.size[i];
   if (pts_out) *pts_out = R.pts[i];
   if (key) *key = R.key[i];
   *got_packet = 1;
   R.next++;
-  // the queue filled while packets were still being handed out
-  if (R.next >= R.size.size() && int(c->q_pts.size()) == c->max_batch) {
-    const int rc = encode_queue(c);
-    if (rc < 0) return rc;
-  }
   return 0;
 }
 
@@ -1813,7 +2140,7 @@ int ffv1hip_last_kernel_stats(ffv1hip_ctx* c, ffv1hip_kernel_stats* out) {
 
 int64_t ffv1hip_get_slice_states(ffv1hip_ctx* c, uint8_t* buf, int64_t cap) {
   if (!c) return set_err(-22, "null ctx");
-  const int64_t n = int64_t(2) * c->contexts * 32 * c->nslices;
+  const int64_t n = int64_t(c->pcount) * c->contexts * 32 * c->nslices;
   if (!buf) return n;
   if (cap < n) return set_err(-22, "buffer too small");
   HIP_TRY(hipSetDevice(c->device));
@@ -1832,7 +2159,7 @@ int ffv1hip_set_picture_number(ffv1hip_ctx* c, int64_t picture_number) {
 
 int ffv1hip_set_slice_states(ffv1hip_ctx* c, const uint8_t* buf, int64_t size) {
   if (!c || !buf) return set_err(-22, "null argument");
-  const int64_t n = int64_t(2) * c->contexts * 32 * c->nslices;
+  const int64_t n = int64_t(c->pcount) * c->contexts * 32 * c->nslices;
   if (size != n) return set_err(-22, "state blob is %lld bytes, expected %lld", (long long)size, (long long)n);
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipDeviceSynchronize());
@@ -2024,6 +2351,8 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
       (p.version < 2 && p.num_h_slices * p.num_v_slices != 1) || p.context_model < 0 || p.context_model > 1 ||
       p.colorspace < 0 || p.colorspace > 1 || p.ac < 0 || p.ac > 2)
     return fail(set_err(-38, "GPU decoder: unsupported parameter set"));
+  if (p.transparency)  // the oracle decoder reads these streams (tests/test_alpha.py)
+    return fail(set_err(-38, "GPU decoder: alpha planes are not decoded on the GPU"));
   // The stream's extradata must be the one these parameters produce
   // (read_extradata, ffv1dec.c:509-631, would derive the same parameters);
   // versions 0 and 1 have none, their header is in band.

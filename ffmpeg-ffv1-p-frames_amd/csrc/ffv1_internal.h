@@ -37,14 +37,18 @@ struct Segment {
   int save_states;  // 1: store the final states for the next call
 };
 
+// Coded planes of a slice: Y, Cb, Cr, then A (YUVA: ffv1enc.c:1191-1198);
+// YA8 codes Y and A of one packed plane (:1199-1201).
+constexpr int kMaxPlanes = 4;
+
 // Per-slice geometry (ffv1.c:117-145 + the chroma rounding of
 // ffv1enc.c:1185-1196) and the slice's place in a frame's symbol stream.
 struct SliceGeom {
-  int px[3], py[3], pw[3], ph[3];  // plane rectangles
-  int64_t sym_off;                 // first symbol of this slice in the frame stream
-  int64_t plane_sym_off[3];        // first symbol of each plane, relative to sym_off
-  int64_t nsym;                    // all planes
-  int64_t chunk_off[3];            // first 64-sample walk chunk of each plane in the frame
+  int px[kMaxPlanes], py[kMaxPlanes], pw[kMaxPlanes], ph[kMaxPlanes];  // plane rectangles
+  int64_t sym_off;                      // first symbol of this slice in the frame stream
+  int64_t plane_sym_off[kMaxPlanes];    // first symbol of each plane, relative to sym_off
+  int64_t nsym;                         // all planes
+  int64_t chunk_off[kMaxPlanes];        // first 64-sample walk chunk of each plane in the frame
 };
 
 // Per walk chunk (64 consecutive samples of a plane), written by ffv1_symbols:
@@ -60,8 +64,10 @@ constexpr uint32_t kChunkFlags = kChunkLong | kChunkMulti;
 struct SymbolArgs {
   const uint8_t* frames;
   int64_t frame_bytes;
-  int64_t plane_off[3];
-  int plane_stride[3];
+  int64_t plane_off[kMaxPlanes];   // coded plane p's first sample (YA8's A: Y's + 1)
+  int plane_stride[kMaxPlanes];
+  int pstep[kMaxPlanes];           // samples between a plane's pixels (YA8: 2)
+  int pset[kMaxPlanes];            // plane context set of coded plane p (ffv1enc.c:1191-1201, (p+1)/2 for RGB)
   const int* frame_of_slot;   // [slot] batch frame index coded in this launch, -1 = none
   int nslots;
   const SliceGeom* geom;
@@ -150,7 +156,7 @@ struct CodeArgs {
   const int* nops;            // [key][slice]
   int max_ops;
   const uint8_t* tabs;        // [default to0|to1][frame to0|to1]
-  int64_t state_bytes;        // 2 * contexts * 32
+  int64_t state_bytes;        // pcount * contexts * 32
   uint8_t* tables;            // [chain][state_bytes] working context states (grid-padded)
   const uint8_t* persist_in;  // [slice][state_bytes]: the carry the batch starts from
   uint8_t* persist_out;       // [slice][state_bytes]: the carry it leaves (the other buffer)
@@ -162,7 +168,10 @@ struct CodeArgs {
   int* status;                // [0] slices over the byte budget, [1] most bytes a slice needed
   int version;                // bitstream version (Golomb: v3 adds a 129/0 decision)
   int coded_bits;             // "bits" of encode_line (8 for <=8-bit)
-  int rgb;                    // RGB: a slice's three planes are row-interleaved (chained coders)
+  int rgb;                    // RGB: a slice's planes are row-interleaved (chained coders)
+  int nplanes;                // coded planes (1 gray, 2 YA8, 3, 4 with alpha)
+  int pset[kMaxPlanes];       // plane context set of each coded plane
+  int pcount;                 // plane contexts (plane_count: 2, 3 with alpha)
   int nframes;                // decision-stream mode: frames of the batch
   DecisionStream ds;
   const uint8_t* init;        // chained range coder: 2-pass initial states [contexts][32], or null

@@ -139,13 +139,15 @@ __device__ __forceinline__ int wave_next(int x) { return __builtin_amdgcn_update
 
 // RGB (encode_rgb_frame, ffv1enc.c:413-459): pixel (x, y) of the frame as
 // coded plane p of the reversible colour transform, G' = g + (b' + r') >> 2,
-// B' = b - g + off, R' = r - g + off.  bgr0: one u32 per pixel (B, G, R, X
-// bytes); gbrp: three u16 planes read in AVFrame data[] order as b, g, r.
+// B' = b - g + off, R' = r - g + off, and A (p = 3, RGB32) as it is.  bgr0 /
+// RGB32: one u32 per pixel (B, G, R, X / A bytes); gbrp: three u16 planes
+// read in AVFrame data[] order as b, g, r.
 template <int SB>
 __device__ __forceinline__ int rct_sample(const SymbolArgs& a, const uint8_t* fr, int p, int x, int y) {
   int b, g, r;
   if constexpr (SB == 4) {
     const uint32_t v = reinterpret_cast<const uint32_t*>(fr + a.plane_off[0] + (int64_t)y * a.plane_stride[0])[x];
+    if (p == 3) return (int)(v >> 24);
     b = v & 0xFF;
     g = (v >> 8) & 0xFF;
     r = (v >> 16) & 0xFF;
@@ -182,9 +184,10 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   const int pw = g.pw[p], ph = g.ph[p], px = g.px[p], py = g.py[p];
   const uint8_t* base = a.frames + (int64_t)f * a.frame_bytes + a.plane_off[p];
   const int stride = a.plane_stride[p];
-  // RGB: the slice's G', B', R' rows interleave (ffv1enc.c:428-471)
+  // RGB: the slice's G', B', R' (A) rows interleave (ffv1enc.c:428-471)
   uint32_t* out = a.sym + (int64_t)slot * a.frame_samples + g.sym_off + (RGB ? 0 : g.plane_sym_off[p]);
-  const int row0 = p ? a.contexts : 0;  // plane context 1 rows follow plane 0's
+  const int row0 = a.pset[p] * a.contexts;  // the plane context's rows follow the previous ones'
+  const int step = a.pstep[p];
 
   // sample of the slice plane as int16 (ffv1enc.c:390-407), at in-plane
   // coordinates: every load is unconditional, so the loads of a step are
@@ -197,7 +200,7 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
     } else {
       if constexpr (SB == 2 && RGB) return rct_sample<2>(a, fr, p, px + x, py + y);
       const uint8_t* r = base + (int64_t)(py + y) * stride;
-      if constexpr (SB == 1) return r[px + x];
+      if constexpr (SB == 1) return r[(px + x) * step];
       else return (int16_t)(reinterpret_cast<const uint16_t*>(r)[px + x] >> sh);
     }
   };
@@ -302,7 +305,7 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
         if (lane < kChunkWords - kWave) dst[kWave + lane] = cs[kWave + lane];
       }
     } else if (valid) {
-      out[RGB ? ((int64_t)y * 3 + p) * pw + x : idx] = ((uint32_t)(row0 + ctx) << 16) | (uint16_t)diff;
+      out[RGB ? ((int64_t)y * a.nplanes + p) * pw + x : idx] = ((uint32_t)(row0 + ctx) << 16) | (uint16_t)diff;
     }
   }
   if (count && b0 < b1) {
@@ -727,8 +730,8 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
       for (int64_t i = 0; i < a.state_bytes / 16; i++) reinterpret_cast<uint4*>(table)[i] = src[i];
     } else if (key && a.init) {  // ff_ffv1_clear_slice_state with 2-pass initial states
       const uint4* src = reinterpret_cast<const uint4*>(a.init);
-      const int64_t half = a.state_bytes / 32;  // uint4s of one plane context's table
-      for (int64_t i = 0; i < a.state_bytes / 16; i++) reinterpret_cast<uint4*>(table)[i] = src[i % half];
+      const int64_t per = a.state_bytes / (16 * a.pcount);  // uint4s of one plane context's table
+      for (int64_t i = 0; i < a.state_bytes / 16; i++) reinterpret_cast<uint4*>(table)[i] = src[i % per];
     } else if (key) {
       const uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
       for (int64_t i = 0; i < a.state_bytes / 16; i++) reinterpret_cast<uint4*>(table)[i] = v;
@@ -1564,10 +1567,6 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
     case 3: __builtin_amdgcn_s_setprio(3); break;
     default: __builtin_amdgcn_s_setprio(2); break;
   }
-#ifdef FFV1_WALK_FAT
-  // the whole register file of a SIMD: no other wave shares this one's SIMD
-  asm volatile("" ::: "v255", "a255");
-#endif
   uint64_t t_loop = 0, n_steps = 0;
   const uint64_t t_all = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
   for (int j = 0; j < seg.nframes; j++) {
@@ -1981,7 +1980,8 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
   const int f = seg.first_frame + a.j;
   const int key = live ? a.keyflags[f] : 0;
   uint64_t* table = reinterpret_cast<uint64_t*>(a.tables + chain * a.state_bytes);
-  const int64_t nrec = a.state_bytes / 32;  // 2 * contexts records
+  const int64_t nrec = a.state_bytes / 32;  // pcount * contexts records
+  const int contexts = (int)(nrec / a.pcount);
 
   if (live) {
     if (a.j == 0 && seg.load_states) {
@@ -2010,12 +2010,12 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
   int64_t idx = 0;
   int run_index = 0;
   // one row of encode_line's Golomb branch (ffv1enc.c:318-368)
-  auto code_row = [&](int pw, bool chroma) {
+  auto code_row = [&](int pw, int set) {
     int run_count = 0, run_mode = 0;
     for (int x = 0; x < pw; x++, idx++) {
       const uint32_t sv = sp[idx];
       const int row = (int)(sv >> 16);
-      const int ctx = chroma ? row - a.state_bytes / 64 : row;  // context inside its plane
+      const int ctx = row - set * contexts;  // context inside its plane context
       int diff = (int16_t)(sv & 0xFFFF);
       if (ctx == 0) run_mode = 1;
       if (run_mode) {
@@ -2045,13 +2045,13 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
       if (run_count) b.put(1, 1);
     }
   };
-  if (a.rgb) {  // rows of G', B', R' in turn, one run index per slice (ffv1enc.c:423)
+  if (a.rgb) {  // rows of G', B', R' (A) in turn, one run index per slice (ffv1enc.c:423)
     for (int y = 0; y < g.ph[0]; y++)
-      for (int p = 0; p < 3; p++) code_row(g.pw[0], p != 0);
+      for (int p = 0; p < a.nplanes; p++) code_row(g.pw[0], a.pset[p]);
   } else {
-    for (int p = 0; p < 3; p++) {
+    for (int p = 0; p < a.nplanes; p++) {
       run_index = 0;  // per plane (ffv1enc.c:379)
-      for (int y = 0; y < g.ph[p]; y++) code_row(g.pw[p], p != 0);
+      for (int y = 0; y < g.ph[p]; y++) code_row(g.pw[p], a.pset[p]);
     }
   }
   b.flush();

@@ -35,7 +35,7 @@ class Params(ctypes.Structure):
         "width", "height", "chroma_planes", "chroma_h_shift", "chroma_v_shift",
         "bits_per_raw_sample", "packed_at_lsb", "sample_bytes", "version", "ac", "ec",
         "context_model", "num_h_slices", "num_v_slices", "gop_size", "sar_num", "sar_den",
-        "colorspace")]
+        "colorspace", "transparency")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -45,14 +45,25 @@ class Params(ctypes.Structure):
         return self.num_h_slices * self.num_v_slices
 
     def plane_shapes(self):
-        if self.sample_bytes == 4:  # bgr0: one packed B, G, R, X plane
+        """(rows, samples) of each host plane: Y, Cb, Cr (+ A for YUVA); one
+        packed plane for bgr0 / RGB32 (4 bytes a pixel) and YA8 (Y, A bytes)."""
+        if self.sample_bytes == 4:  # bgr0 / RGB32: one packed B, G, R, X / A plane
             return [(self.height, 4 * self.width)]
+        if self.transparency and not self.chroma_planes:  # YA8
+            return [(self.height, 2 * self.width)]
         cw = -((-self.width) >> self.chroma_h_shift)
         ch = -((-self.height) >> self.chroma_v_shift)
         shapes = [(self.height, self.width)]
         if self.chroma_planes:
             shapes += [(ch, cw), (ch, cw)]
+        if self.transparency:
+            shapes.append((self.height, self.width))
         return shapes
+
+    @property
+    def planes_per_frame(self):
+        """Plane pointers per frame in the C-ABI's arrays (FFV1HIP_PLANES[_YUVA])."""
+        return 4 if len(self.plane_shapes()) == 4 else 3
 
 
 EXPORTED_SYMBOLS = (
@@ -63,7 +74,7 @@ EXPORTED_SYMBOLS = (
     "ffv1hip_abi_version", "ffv1hip_set_profiling", "ffv1hip_last_kernel_ms",
     "ffv1hip_last_kernel_stats", "ffv1hip_synchronize",
     "ffv1hip_dec_create", "ffv1hip_dec_destroy", "ffv1hip_decode", "ffv1hip_dec_reset",
-    "ffv1hip_set_picture_number", "ffv1hip_encode2", "ffv1hip_dec_damaged_slices",
+    "ffv1hip_set_picture_number", "ffv1hip_encode2", "ffv1hip_encode2_delay", "ffv1hip_dec_damaged_slices",
     "ffv1hip_set_pass", "ffv1hip_stats_out",
 )
 
@@ -109,6 +120,8 @@ def load_library():
     L.ffv1hip_encode2.argtypes = [vp, P(vp), P(ctypes.c_int), i64, u8p, i64, P(i64), P(i64),
                                   P(ctypes.c_int), P(ctypes.c_int)]
     L.ffv1hip_encode2.restype = ctypes.c_int
+    L.ffv1hip_encode2_delay.argtypes = [vp]
+    L.ffv1hip_encode2_delay.restype = ctypes.c_int
     L.ffv1hip_set_pass.argtypes = [vp, ctypes.c_int, ctypes.c_char_p]
     L.ffv1hip_set_pass.restype = ctypes.c_int
     L.ffv1hip_stats_out.argtypes = [vp, ctypes.c_char_p, i64]
@@ -250,6 +263,13 @@ class HipEncoder:
     def max_packet_size(self) -> int:
         return load_library().ffv1hip_max_packet_size(self._h)
 
+    def encode2_delay(self) -> int:
+        """Frames ffv1hip_encode2 holds back (avctx->delay)."""
+        rc = load_library().ffv1hip_encode2_delay(self._h)
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_encode2_delay")
+        return rc
+
     def encode(self, frames: Sequence[Sequence[np.ndarray]]) -> List[Tuple[bytes, bool]]:
         """Encode host frames (each a list of 2-D uint8/uint16 planes) in order."""
         L = load_library()
@@ -257,16 +277,17 @@ class HipEncoder:
         np_planes = len(self.params.plane_shapes())
         for fr in frames:
             check_planes(self.params, fr)
-        ptrs = (ctypes.c_void_p * (3 * n))()
-        strides = (ctypes.c_int * (3 * n))()
+        ppf = self.params.planes_per_frame
+        ptrs = (ctypes.c_void_p * (ppf * n))()
+        strides = (ctypes.c_int * (ppf * n))()
         keep = []
         for i, fr in enumerate(frames):
-            for k in range(3):
+            for k in range(ppf):
                 a = fr[min(k, np_planes - 1)]
                 a = np.ascontiguousarray(a)
                 keep.append(a)
-                ptrs[3 * i + k] = a.ctypes.data
-                strides[3 * i + k] = a.strides[0]
+                ptrs[ppf * i + k] = a.ctypes.data
+                strides[ppf * i + k] = a.strides[0]
         total_in = sum(a.nbytes for a in keep)
         cap = total_in * 4 + 65536 * n
         out = np.empty(cap, np.uint8)
@@ -284,8 +305,8 @@ class HipEncoder:
     def encode_device(self, d_frames: int, frame_bytes: int, plane_offset, plane_stride,
                       n_frames: int, stream: int = 0):
         L = load_library()
-        off = (ctypes.c_int64 * 3)(*plane_offset)
-        st = (ctypes.c_int * 3)(*plane_stride)
+        off = (ctypes.c_int64 * 4)(*plane_offset)
+        st = (ctypes.c_int * 4)(*plane_stride)
         rc = L.ffv1hip_encode_device(self._h, ctypes.c_void_p(d_frames), frame_bytes, off, st,
                                      n_frames, ctypes.c_void_p(stream) if stream else None)
         if rc < 0:
@@ -404,6 +425,7 @@ class AVCodecContext:
     flags: int = 0                   # AV_CODEC_FLAG_PASS1 / PASS2
     stats_in: Optional[str] = None   # pass 2: what pass 1 left in stats_out
     stats_out: str = ""              # pass 1: written at the flush (ffv1enc.c:1236-1277)
+    delay: int = 0                   # frames encode2 holds back, set by init
     priv: dict = field(default_factory=dict)
 
 
@@ -420,8 +442,9 @@ class FFV1Encoder:
     and returns at most one packet (``got_packet``), or ``None``.  The
     queueing is the library's (``ffv1hip_encode2``, the entry point an
     AVCodec shim's encode2 forwards to): frames are encoded
-    on the GPU ``batch`` at a time, so the first packet comes out with the
-    batch-th frame and the encoder then returns one packet per call; a
+    on the GPU ``batch`` at a time, one batch coding while the next queues,
+    so the first packet comes out with frame ``avctx.delay`` + 1 (2 x batch
+    - 1 frames of delay) and the encoder then returns one packet per call; a
     ``None`` frame encodes what is queued and the caller keeps flushing until
     ``None`` comes back (ffmpeg.c:1699-1776).  Every packet carries pts = dts
     = its frame's pts and the KEY flag (ffv1enc.c:1365-1370).
@@ -433,7 +456,9 @@ class FFV1Encoder:
     pix_fmts = ("yuv420p", "yuv422p", "yuv444p", "yuv440p", "yuv411p", "yuv410p", "gray",
                 "yuv420p9", "yuv422p9", "yuv444p9", "yuv420p10", "yuv422p10", "yuv444p10",
                 "yuv420p16", "yuv422p16", "yuv444p16", "gray16", "bgr0", "0rgb32", "gbrp9",
-                "gbrp10", "gbrp12", "gbrp14")
+                "gbrp10", "gbrp12", "gbrp14", "yuva420p", "yuva422p", "yuva444p", "yuva420p9",
+                "yuva422p9", "yuva444p9", "yuva420p10", "yuva422p10", "yuva444p10", "yuva420p16",
+                "yuva422p16", "yuva444p16", "ya8", "bgra", "rgb32")
 
     def __init__(self, batch: int = 12, device: int = 0):
         if batch < 1:
@@ -459,6 +484,7 @@ class FFV1Encoder:
         if pass_ == 1 or (pass_ == 2 and avctx.stats_in is not None):
             self._enc.set_pass(pass_, avctx.stats_in)
         avctx.extradata = self._enc.extradata()
+        avctx.delay = self._enc.encode2_delay()
         self._out = np.empty(self._enc.max_packet_size(), np.uint8)
         return 0
 
@@ -466,13 +492,13 @@ class FFV1Encoder:
         if self._enc is None:
             raise FFV1Error(-22, "encode2 before init")
         L = load_library()
-        ptrs = (ctypes.c_void_p * 3)()
-        strides = (ctypes.c_int * 3)()
+        ptrs = (ctypes.c_void_p * 4)()
+        strides = (ctypes.c_int * 4)()
         keep = []
         if frame is not None:
             check_planes(self.params, frame)
             np_planes = len(self.params.plane_shapes())
-            for k in range(3):
+            for k in range(np_planes):
                 a = np.ascontiguousarray(frame[min(k, np_planes - 1)])
                 keep.append(a)
                 ptrs[k] = a.ctypes.data
@@ -486,6 +512,10 @@ class FFV1Encoder:
                                strides if frame is not None else None, pts or 0, _u8p(self._out),
                                self._out.size, ctypes.byref(size), ctypes.byref(pts_out),
                                ctypes.byref(key), ctypes.byref(got))
+        if rc == -28:  # the packet outgrew the buffer (a budget re-encode): the frame was taken
+            self._out = np.empty(max(size.value, self._enc.max_packet_size()), np.uint8)
+            rc = L.ffv1hip_encode2(self._enc._h, None, None, 0, _u8p(self._out), self._out.size,
+                                   ctypes.byref(size), ctypes.byref(pts_out), ctypes.byref(key), ctypes.byref(got))
         if rc < 0:
             raise FFV1Error(rc, "ffv1hip_encode2")
         if not got.value:

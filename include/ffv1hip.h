@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define FFV1HIP_ABI_VERSION 4
+#define FFV1HIP_ABI_VERSION 5
 #define FFV1HIP_AVERROR_INVALIDDATA (-1094995529)
 
 /* AVCodecContext fields + codec private options that encode_init reads
@@ -31,7 +31,9 @@ extern "C" {
 typedef struct ffv1hip_options {
     int width, height;
     const char *pix_fmt;      /* "yuv420p", "yuv420p10", "yuv444p16", ...,
-                                 "bgr0" / "gbrp9".."gbrp14" (RGB)          */
+                                 "bgr0" / "gbrp9".."gbrp14" (RGB); with
+                                 alpha "yuva420p".."yuva444p16", "ya8",
+                                 "bgra" / "rgb32" (ffv1enc.c:725-786)      */
     int slices;               /* avctx->slices (0 = auto)                   */
     int level;                /* avctx->level (-1 = unset)                  */
     int coder;                /* -1 default, 0 rice, 1/2 range_tab, -2 range_def */
@@ -65,7 +67,18 @@ typedef struct ffv1hip_params {
     int colorspace;           /* 0 YCbCr; 1 RGB through the reversible colour
                                  transform (ffv1enc.c:413-473): bgr0 or
                                  gbrp planes in AVFrame data[] order        */
+    int transparency;         /* alpha (ffv1enc.c:774, 782): YUVA's plane 3
+                                 (plane context 2), YA8's packed A bytes
+                                 (plane context 1), RGB32's A byte; coded by
+                                 the chained coders                         */
 } ffv1hip_params;
+
+/* Host planes per frame in the plane / stride arrays of ffv1hip_encode,
+ * ffv1hip_encode2 and ffv1hip_encode_device: 4 (Y, Cb, Cr, A) for the YUVA
+ * formats, else 3 (entries past the format's planes are not read: gray,
+ * YA8, bgr0 and RGB32 use plane 0 only). */
+#define FFV1HIP_PLANES_YUVA 4
+#define FFV1HIP_PLANES 3
 
 typedef struct ffv1hip_ctx ffv1hip_ctx;
 
@@ -103,10 +116,13 @@ int ffv1hip_extradata(ffv1hip_ctx *ctx, uint8_t *buf, int cap);
 int64_t ffv1hip_max_packet_size(const ffv1hip_ctx *ctx);
 
 /* AVCodec.encode2 over a batch (ffv1enc.c:1222 encode_frame, called once
- * per frame in order).  planes[3*i + p] / strides[3*i + p] describe plane p
- * of frame i in HOST memory.  Packets are written back to back into `out`;
+ * per frame in order).  planes[np*i + p] / strides[np*i + p] describe plane
+ * p of frame i in HOST memory (np = 4 for the YUVA formats, else 3).  Packets are written back to back into `out`;
  * sizes[i] and key_flags[i] describe packet i.  P-frame context state
- * carries across calls exactly as across encode_frame calls. */
+ * carries across calls exactly as across encode_frame calls.  Frames go in
+ * max_batch_frames at a time through pinned staging buffers; with HBM for
+ * two batches, batch k+1 is copied in while batch k codes and batch k-1's
+ * packets are copied out (ffv1hip_encode2_delay). */
 int ffv1hip_encode(ffv1hip_ctx *ctx, const void *const *planes,
                    const int *strides, int n_frames, uint8_t *out,
                    int64_t out_cap, int64_t *sizes, int *key_flags);
@@ -117,16 +133,28 @@ int ffv1hip_encode(ffv1hip_ctx *ctx, const void *const *planes,
  * planes in HOST memory (copied before the call returns), or planes == NULL
  * to flush (ffmpeg.c:1699-1776 passes NULL frames until no packet comes
  * back).  Frames queue up to the context's max_batch_frames and are encoded
- * together; each call then hands out at most one packet in input order, so
- * the first packet comes with frame max_batch_frames (the encoder's delay is
- * max_batch_frames - 1 frames).  A returned packet has pts = dts = its
- * frame's pts and the key flag (ffv1enc.c:1365-1370).  out must hold
- * ffv1hip_max_packet_size bytes.  *got_packet = 1 when a packet was
+ * together, on the GPU while the next batch queues: each call then hands
+ * out at most one packet in input order, and the first packet comes with
+ * frame ffv1hip_encode2_delay + 1.  Frames go to HBM through pinned staging
+ * buffers (a few host threads copy into them, DMA on a transfer stream of
+ * the context) and packets come back through a pinned buffer.  A returned
+ * packet has pts = dts = its frame's pts and the key flag
+ * (ffv1enc.c:1365-1370).  out should hold ffv1hip_max_packet_size bytes,
+ * which grows after a slice byte budget re-encode: a packet larger than
+ * out_cap makes the call return -ENOSPC with *size = the packet's size,
+ * having taken the frame; a call with planes = NULL and a large enough
+ * buffer then hands the packet out.  *got_packet = 1 when a packet was
  * written. */
-int ffv1hip_encode2(ffv1hip_ctx *ctx, const void *const planes[3],
-                    const int strides[3], int64_t pts, uint8_t *out,
+int ffv1hip_encode2(ffv1hip_ctx *ctx, const void *const planes[4],
+                    const int strides[4], int64_t pts, uint8_t *out,
                     int64_t out_cap, int64_t *size, int64_t *pts_out,
                     int *key, int *got_packet);
+
+/* The encoder's delay in frames (avctx->delay): 2 * max_batch_frames - 1
+ * when two batches fit in HBM side by side (one codes while the next
+ * queues), else max_batch_frames - 1.  Allocates the host-frame path's
+ * buffers if they are not yet. */
+int ffv1hip_encode2_delay(ffv1hip_ctx *ctx);
 
 /* Device-resident variant: frames already in HBM at d_frames + i*frame_bytes
  * with plane p at byte offset plane_offset[p] and row stride plane_stride[p].
@@ -141,8 +169,8 @@ int ffv1hip_encode2(ffv1hip_ctx *ctx, const void *const planes[3],
  * input frames must still be in place), so no truncated slice is ever
  * handed out; if even that fails they return -ENOSPC. */
 int ffv1hip_encode_device(ffv1hip_ctx *ctx, const void *d_frames,
-                          int64_t frame_bytes, const int64_t plane_offset[3],
-                          const int plane_stride[3], int n_frames,
+                          int64_t frame_bytes, const int64_t plane_offset[4],
+                          const int plane_stride[4], int n_frames,
                           void *stream);
 
 /* Waits for all work of the context (every stream it uses), then settles

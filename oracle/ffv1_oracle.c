@@ -526,7 +526,8 @@ static const uint8_t CUSTOM_STT[256] = {
 
 typedef struct pixfmt_info {
     const char *name;
-    int planes;        /* 1 gray, 3 yuv / rgb */
+    int planes;        /* components: 1 gray, 2 gray + alpha (YA8), 3 yuv /
+                          rgb, 4 yuva / rgb32 (desc->nb_components) */
     int hs, vs;
     int depth;         /* nominal depth of the storage format */
     int family;        /* 9, 10, 16 or 8: which switch group it enters;
@@ -548,6 +549,16 @@ static const pixfmt_info PIXFMTS[] = {
     {"bgr0", 3, 0, 0, 8, 32},       {"0rgb32", 3, 0, 0, 8, 32},
     {"gbrp9", 3, 0, 0, 9, 109},     {"gbrp10", 3, 0, 0, 10, 110},
     {"gbrp12", 3, 0, 0, 12, 112},   {"gbrp14", 3, 0, 0, 14, 114},
+    /* with alpha (ffv1enc.c:725-774, 780-786) */
+    {"yuva420p", 4, 1, 1, 8, 8},    {"yuva422p", 4, 1, 0, 8, 8},
+    {"yuva444p", 4, 0, 0, 8, 8},    {"ya8", 2, 0, 0, 8, 8},
+    {"yuva420p9", 4, 1, 1, 9, 9},   {"yuva422p9", 4, 1, 0, 9, 9},
+    {"yuva444p9", 4, 0, 0, 9, 9},
+    {"yuva420p10", 4, 1, 1, 10, 10}, {"yuva422p10", 4, 1, 0, 10, 10},
+    {"yuva444p10", 4, 0, 0, 10, 10},
+    {"yuva420p16", 4, 1, 1, 16, 16}, {"yuva422p16", 4, 1, 0, 16, 16},
+    {"yuva444p16", 4, 0, 0, 16, 16},
+    {"bgra", 4, 0, 0, 8, 32},       {"rgb32", 4, 0, 0, 8, 32},
 };
 
 int ffv1o_configure(ffv1o_config *cfg, int width, int height,
@@ -648,10 +659,12 @@ int ffv1o_configure2(ffv1o_config *cfg, int width, int height,
     if (context < 0 || context > 1)
         return AVERR_EINVAL;
 
-    cfg->chroma_planes = pf->planes == 3;
-    cfg->chroma_h_shift = pf->planes == 3 ? pf->hs : 0;
-    cfg->chroma_v_shift = pf->planes == 3 ? pf->vs : 0;
-    cfg->transparency = 0;
+    /* chroma_planes = nb_components >= 3, transparency = 4 or 2 components
+     * (ffv1enc.c:772-774); RGB32 has alpha, 0RGB32 not (:780-792) */
+    cfg->chroma_planes = pf->planes >= 3;
+    cfg->chroma_h_shift = pf->planes >= 3 ? pf->hs : 0;
+    cfg->chroma_v_shift = pf->planes >= 3 ? pf->vs : 0;
+    cfg->transparency = pf->planes == 4 || pf->planes == 2;
     cfg->bits_per_raw_sample = bits;
     cfg->packed_at_lsb = packed;
     cfg->sample_bytes = pf->family == 32 ? 4 : pf->depth > 8 ? 2 : 1;
@@ -688,7 +701,7 @@ typedef struct plane_state {
 
 typedef struct slice_ctx {
     int x0, y0, w, h;   /* luma rectangle, ffv1.c:117-145 */
-    plane_state ps[2];  /* plane_count == 2 (no alpha), ffv1enc.c:890-891 */
+    plane_state ps[3];  /* plane_count: 2, 3 with alpha (ffv1enc.c:720, 890-891) */
     uint8_t *buf;
     int64_t cap;
     int64_t bytes;
@@ -705,6 +718,7 @@ struct ffv1o_enc {
     int nslices;
     slice_ctx *sl;
     int64_t picture_number;
+    int plane_count;    /* 2 + transparency (ffv1enc.c:720, 890-891) */
     int16_t *scratch;   /* one slice plane of samples */
     /* 2-pass (ffv1enc.c:898-986, 1236-1277) */
     int pass1;
@@ -728,12 +742,13 @@ static void slice_rects(const ffv1o_config *cfg, int i, int *x0, int *y0,
 
 ffv1o_enc *ffv1o_enc_new(const ffv1o_config *cfg)
 {
-    if (cfg->transparency || cfg->num_h_slices * cfg->num_v_slices > 256)
+    if (cfg->num_h_slices * cfg->num_v_slices > 256)
         return NULL;
     ffv1o_enc *e = calloc(1, sizeof(*e));
     if (!e)
         return NULL;
     e->cfg = *cfg;
+    e->plane_count = 2 + (cfg->transparency != 0);
     build_quant_set(e->qt, cfg->context_model, cfg->bits_per_raw_sample);
     e->contexts = context_count_of(cfg->context_model);
     /* encode_line's bits: RGB samples after the RCT carry one bit more
@@ -763,12 +778,12 @@ ffv1o_enc *ffv1o_enc_new(const ffv1o_config *cfg)
          * 1317-1322); malloc'd pages are only touched as far as used */
         s->cap = (16384 + (int64_t)cfg->width * cfg->height * 140) / e->nslices;
         s->buf = malloc(s->cap);
-        for (int p = 0; p < 2; p++) {
+        for (int p = 0; p < e->plane_count; p++) {
             s->ps[p].rac = malloc((size_t)e->contexts * 32);
             s->ps[p].vlc = malloc((size_t)e->contexts * sizeof(vlc_ctx));
         }
     }
-    e->scratch = malloc(3 * (size_t)maxw * sizeof(int16_t) + 16);
+    e->scratch = malloc(4 * (size_t)maxw * sizeof(int16_t) + 16);
     return e;
 }
 
@@ -1015,7 +1030,7 @@ void ffv1o_enc_free(ffv1o_enc *e)
         return;
     for (int i = 0; i < e->nslices; i++) {
         free(e->sl[i].buf);
-        for (int p = 0; p < 2; p++) {
+        for (int p = 0; p < e->plane_count; p++) {
             free(e->sl[i].ps[p].rac);
             free(e->sl[i].ps[p].vlc);
         }
@@ -1138,7 +1153,7 @@ static void put_slice_header(const ffv1o_enc *e, const slice_ctx *s, rc_enc *c)
     rc_put_symbol(c, st, (int)((int64_t)(s->y0 + 1) * nv / cfg->height), 0);
     rc_put_symbol(c, st, (int)((int64_t)(s->w + 1) * nh / cfg->width) - 1, 0);
     rc_put_symbol(c, st, (int)((int64_t)(s->h + 1) * nv / cfg->height) - 1, 0);
-    for (int j = 0; j < 2; j++)
+    for (int j = 0; j < e->plane_count; j++)
         rc_put_symbol(c, st, cfg->context_model, 0);
     rc_put_symbol(c, st, 3, 0); /* progressive picture structure */
     rc_put_symbol(c, st, cfg->sar_num, 0);
@@ -1150,12 +1165,15 @@ static void put_slice_header(const ffv1o_enc *e, const slice_ctx *s, rc_enc *c)
 static void load_plane(const ffv1o_config *cfg, const uint8_t *src,
                        int stride, int x0, int y0, int w, int h, int16_t *dst)
 {
+    /* YA8: Y and A bytes interleaved, encode_plane's pixel_stride 2
+     * (ffv1enc.c:1199-1201); src points at the component's first byte */
+    const int ps = cfg->transparency && !cfg->chroma_planes && !cfg->colorspace ? 2 : 1;
     for (int y = 0; y < h; y++) {
         const uint8_t *row = src + (int64_t)(y0 + y) * stride;
         for (int x = 0; x < w; x++) {
             int v;
             if (cfg->sample_bytes == 1) {
-                v = row[x0 + x];
+                v = row[ps * (x0 + x)];
             } else {
                 v = row[2 * (x0 + x)] | (row[2 * (x0 + x) + 1] << 8);
                 if (!cfg->packed_at_lsb)
@@ -1326,16 +1344,18 @@ static void code_plane(ffv1o_enc *e, void *coder, int golomb, plane_state *ps,
  * pixel (x, y) of the slice as the three coded samples G', B', R'.  bgr0 is
  * one packed plane (B, G, R, X bytes); gbrp is three u16 planes whose first
  * is read as "b", second as "g", third as "r", as the reference does. */
-static void rct_sample(const ffv1o_config *cfg, const uint8_t *const planes[3],
-                       const int strides[3], int x, int y, int out[3])
+static void rct_sample(const ffv1o_config *cfg, const uint8_t *const planes[4],
+                       const int strides[4], int x, int y, int out[4])
 {
     int b, g, r;
     int bits = cfg->bits_per_raw_sample;
+    out[3] = 0;
     if (cfg->sample_bytes == 4) {
         const uint8_t *px = planes[0] + (int64_t)y * strides[0] + 4 * (int64_t)x;
         b = px[0];
         g = px[1];
         r = px[2];
+        out[3] = px[3]; /* RGB32: a = v >> 24 (ffv1enc.c:440) */
     } else {
         const uint8_t *q0 = planes[0] + (int64_t)y * strides[0] + 2 * (int64_t)x;
         const uint8_t *q1 = planes[1] + (int64_t)y * strides[1] + 2 * (int64_t)x;
@@ -1352,24 +1372,26 @@ static void rct_sample(const ffv1o_config *cfg, const uint8_t *const planes[3],
     out[2] = r + (1 << bits);
 }
 
-/* encode_rgb_frame (ffv1enc.c:413-473): the lines of G', B', R' interleaved
- * (row y of each plane in turn), plane contexts 0, 1, 1; one run index for
- * the whole slice. */
-static void code_rgb_slice(ffv1o_enc *e, slice_ctx *s, const uint8_t *const planes[3],
-                           const int strides[3], void *coder, int golomb)
+/* encode_rgb_frame (ffv1enc.c:413-473): the lines of G', B', R' (and A
+ * for RGB32) interleaved (row y of each plane in turn), plane contexts 0,
+ * 1, 1, 2 ((p + 1) / 2); one run index for the whole slice; every plane
+ * coded at 9 bits at 8-bit depth, alpha included (:464-465). */
+static void code_rgb_slice(ffv1o_enc *e, slice_ctx *s, const uint8_t *const planes[4],
+                           const int strides[4], void *coder, int golomb)
 {
     int64_t n = (int64_t)s->w * s->h;
-    int16_t *P[3] = {e->scratch, e->scratch + n, e->scratch + 2 * n};
+    int16_t *P[4] = {e->scratch, e->scratch + n, e->scratch + 2 * n, e->scratch + 3 * n};
+    const int np = 3 + (e->cfg.transparency != 0);
     for (int y = 0; y < s->h; y++)
         for (int x = 0; x < s->w; x++) {
-            int v[3];
+            int v[4];
             rct_sample(&e->cfg, planes, strides, s->x0 + x, s->y0 + y, v);
-            for (int p = 0; p < 3; p++)
+            for (int p = 0; p < np; p++)
                 P[p][(int64_t)y * s->w + x] = (int16_t)v[p];
         }
     int run_index = 0;
     for (int y = 0; y < s->h; y++)
-        for (int p = 0; p < 3; p++) {
+        for (int p = 0; p < np; p++) {
             plane_state *ps = &s->ps[(p + 1) / 2];
             if (golomb)
                 code_row_golomb(e, (bitw *)coder, ps, P[p], s->w, y, &run_index);
@@ -1381,7 +1403,7 @@ static void code_rgb_slice(ffv1o_enc *e, slice_ctx *s, const uint8_t *const plan
 static void reset_slice_states(ffv1o_enc *e, slice_ctx *s)
 {
     const uint8_t *is = e->init_states[e->cfg.context_model];
-    for (int p = 0; p < 2; p++) {
+    for (int p = 0; p < e->plane_count; p++) {
         if (is) /* ff_ffv1_clear_slice_state (ffv1.c:185-189) */
             memcpy(s->ps[p].rac, is, (size_t)e->contexts * 32);
         else
@@ -1392,15 +1414,25 @@ static void reset_slice_states(ffv1o_enc *e, slice_ctx *s)
 }
 
 /* Planes of one slice in coding order: Y (plane context 0) then Cb, Cr
- * (both plane context 1), ffv1enc.c:1185-1196. */
+ * (both plane context 1), then A (plane context 2) at the luma size
+ * (ffv1enc.c:1185-1198); YA8: Y and A of the one packed plane, A with plane
+ * context 1 (:1199-1201).  planes[3] is the alpha plane of the YUVA
+ * formats. */
 typedef void (*plane_fn)(ffv1o_enc *, void *, plane_state *, const int16_t *,
                          int, int);
 
 static void for_each_plane(ffv1o_enc *e, slice_ctx *s,
-                           const uint8_t *const planes[3], const int strides[3],
+                           const uint8_t *const planes[4], const int strides[4],
                            void *coder, int golomb)
 {
     const ffv1o_config *cfg = &e->cfg;
+    if (cfg->transparency && !cfg->chroma_planes) { /* YA8 */
+        for (int p = 0; p < 2; p++) {
+            load_plane(cfg, planes[0] + p, strides[0], s->x0, s->y0, s->w, s->h, e->scratch);
+            code_plane(e, coder, golomb, &s->ps[p], e->scratch, s->w, s->h);
+        }
+        return;
+    }
     int np = cfg->chroma_planes ? 3 : 1;
     for (int p = 0; p < np; p++) {
         int x0 = s->x0, y0 = s->y0, w = s->w, h = s->h;
@@ -1413,10 +1445,14 @@ static void for_each_plane(ffv1o_enc *e, slice_ctx *s,
         load_plane(cfg, planes[p], strides[p], x0, y0, w, h, e->scratch);
         code_plane(e, coder, golomb, &s->ps[p ? 1 : 0], e->scratch, w, h);
     }
+    if (cfg->transparency) {
+        load_plane(cfg, planes[3], strides[3], s->x0, s->y0, s->w, s->h, e->scratch);
+        code_plane(e, coder, golomb, &s->ps[2], e->scratch, s->w, s->h);
+    }
 }
 
-static void code_slice_planes(ffv1o_enc *e, slice_ctx *s, const uint8_t *const planes[3],
-                              const int strides[3], void *coder, int golomb)
+static void code_slice_planes(ffv1o_enc *e, slice_ctx *s, const uint8_t *const planes[4],
+                              const int strides[4], void *coder, int golomb)
 {
     if (e->cfg.colorspace)
         code_rgb_slice(e, s, planes, strides, coder, golomb);
@@ -1424,8 +1460,8 @@ static void code_slice_planes(ffv1o_enc *e, slice_ctx *s, const uint8_t *const p
         for_each_plane(e, s, planes, strides, coder, golomb);
 }
 
-int64_t ffv1o_enc_frame(ffv1o_enc *e, const uint8_t *const planes[3],
-                        const int strides[3], uint8_t *out, int64_t cap,
+int64_t ffv1o_enc_frame(ffv1o_enc *e, const uint8_t *const planes[4],
+                        const int strides[4], uint8_t *out, int64_t cap,
                         int *key_out)
 {
     const ffv1o_config *cfg = &e->cfg;
@@ -1511,26 +1547,28 @@ int64_t ffv1o_enc_frame(ffv1o_enc *e, const uint8_t *const planes[3],
  * stream mid-GOP in another encoder (the multi-rank exchange step). */
 int64_t ffv1o_enc_get_states(const ffv1o_enc *e, uint8_t *buf, int64_t cap)
 {
-    int64_t per = (int64_t)e->contexts * 32, n = 2 * per * e->nslices;
+    const int pc = e->plane_count;
+    int64_t per = (int64_t)e->contexts * 32, n = pc * per * e->nslices;
     if (!buf)
         return n;
     if (cap < n)
         return -1;
     for (int i = 0; i < e->nslices; i++)
-        for (int p = 0; p < 2; p++)
-            memcpy(buf + (2 * (int64_t)i + p) * per, e->sl[i].ps[p].rac, (size_t)per);
+        for (int p = 0; p < pc; p++)
+            memcpy(buf + ((int64_t)pc * i + p) * per, e->sl[i].ps[p].rac, (size_t)per);
     return n;
 }
 
 int ffv1o_enc_set_states(ffv1o_enc *e, const uint8_t *buf, int64_t size,
                          int64_t picture_number)
 {
+    const int pc = e->plane_count;
     int64_t per = (int64_t)e->contexts * 32;
-    if (size != 2 * per * e->nslices)
+    if (size != pc * per * e->nslices)
         return -1;
     for (int i = 0; i < e->nslices; i++)
-        for (int p = 0; p < 2; p++)
-            memcpy(e->sl[i].ps[p].rac, buf + (2 * (int64_t)i + p) * per, (size_t)per);
+        for (int p = 0; p < pc; p++)
+            memcpy(e->sl[i].ps[p].rac, buf + ((int64_t)pc * i + p) * per, (size_t)per);
     e->picture_number = picture_number;
     return 0;
 }
@@ -1543,8 +1581,8 @@ int ffv1o_enc_last_slice_bytes(const ffv1o_enc *e, int *bytes, int n)
 }
 
 int64_t ffv1o_slice_symbols(const ffv1o_config *cfg,
-                            const uint8_t *const planes[3],
-                            const int strides[3], int slice, int32_t *out,
+                            const uint8_t *const planes[4],
+                            const int strides[4], int slice, int32_t *out,
                             int64_t cap)
 {
     int16_t qt[5][256];
@@ -1585,13 +1623,14 @@ int64_t ffv1o_slice_symbols(const ffv1o_config *cfg,
 
 typedef struct dslice {
     int x0, y0, w, h;
-    plane_state ps[2];
+    plane_state ps[3];
     int damaged; /* slice_damaged: set by a CRC / header / end mismatch, cleared by read_header */
 } dslice;
 
 struct ffv1o_dec {
     ffv1o_config cfg;
     int version, micro_version, ac, ec, bits, chroma_planes, hs, vs, colorspace;
+    int transparency, plane_count; /* ffv1dec.c:558-559, 693-695 */
     int num_h, num_v;
     int16_t qsets[2][5][256];
     int ctx_count[2];
@@ -1604,23 +1643,34 @@ struct ffv1o_dec {
     int key_ok;
     int16_t *scratch;
     /* last_picture for the concealment copy (ffv1dec.c:998-1021) */
-    uint8_t *last[3];
-    int last_row[3], last_rows[3];
+    uint8_t *last[4];
+    int last_row[4], last_rows[4];
     int have_last;
     uint8_t *init_states[2]; /* per quant set from the extradata, NULL = all 128 */
 };
 
-/* Rows and row bytes of the output planes (the encoder's input layout). */
-static int out_planes(const ffv1o_dec *d, int row[3], int rows[3])
+/* Planes of the output picture (the encoder's input layout): row bytes,
+ * rows and bytes per pixel; YUVA's alpha is plane 3 at the luma size, YA8
+ * one plane of Y and A bytes, bgr0 / RGB32 one plane of 4-byte pixels. */
+static int out_planes(const ffv1o_dec *d, int row[4], int rows[4], int step[4])
 {
     const ffv1o_config *c = &d->cfg;
     int sb = c->sample_bytes;
-    row[0] = c->width * sb;
-    rows[0] = c->height;
     int np = c->chroma_planes && sb != 4 ? 3 : 1;
+    step[0] = np == 1 && c->transparency && !c->colorspace ? 2 : sb;
+    row[0] = c->width * step[0];
+    rows[0] = c->height;
     for (int k = 1; k < 3; k++) {
+        step[k] = sb;
         row[k] = k < np ? ceil_rshift(c->width, c->chroma_h_shift) * sb : 0;
         rows[k] = k < np ? ceil_rshift(c->height, c->chroma_v_shift) : 0;
+    }
+    step[3] = sb;
+    row[3] = rows[3] = 0;
+    if (np == 3 && c->transparency) {
+        row[3] = c->width * sb;
+        rows[3] = c->height;
+        np = 4;
     }
     return np;
 }
@@ -1658,7 +1708,7 @@ static void dec_alloc_slices(ffv1o_dec *d)
     for (int i = 0; i < d->nslices; i++) {
         slice_rects(&d->cfg, i, &d->sl[i].x0, &d->sl[i].y0, &d->sl[i].w,
                     &d->sl[i].h);
-        for (int p = 0; p < 2; p++) {
+        for (int p = 0; p < 3; p++) {
             d->sl[i].ps[p].rac = malloc((size_t)maxctx * 32);
             d->sl[i].ps[p].vlc = malloc((size_t)maxctx * sizeof(vlc_ctx));
         }
@@ -1673,7 +1723,9 @@ ffv1o_dec *ffv1o_dec_new(const ffv1o_config *cfg, const uint8_t *ex, int exn)
     d->frame_tab = d->dflt;
     d->version = cfg->version;
     d->num_h = d->num_v = 1;
-    d->scratch = malloc(3 * (size_t)cfg->width * cfg->height * sizeof(int16_t) + 16);
+    d->scratch = malloc(4 * (size_t)cfg->width * cfg->height * sizeof(int16_t) + 16);
+    d->transparency = cfg->transparency;
+    d->plane_count = 2 + (cfg->transparency != 0);
     if (exn > 0) { /* read_extra_header, ffv1dec.c:517-636 */
         if (ffv1o_crc32(0, ex, exn) != 0)
             goto fail;
@@ -1697,8 +1749,8 @@ ffv1o_dec *ffv1o_dec_new(const ffv1o_config *cfg, const uint8_t *ex, int exn)
         d->chroma_planes = rc_get(&c, &st[0]);
         d->hs = rc_get_symbol(&c, st, 0);
         d->vs = rc_get_symbol(&c, st, 0);
-        if (rc_get(&c, &st[0])) /* transparency */
-            goto fail;
+        d->transparency = rc_get(&c, &st[0]);
+        d->plane_count = 1 + (d->chroma_planes || d->version < 4) + d->transparency;
         d->num_h = 1 + rc_get_symbol(&c, st, 0);
         d->num_v = 1 + rc_get_symbol(&c, st, 0);
         int nq = rc_get_symbol(&c, st, 0);
@@ -1743,11 +1795,11 @@ void ffv1o_dec_free(ffv1o_dec *d)
     if (!d)
         return;
     for (int i = 0; i < d->nslices; i++)
-        for (int p = 0; p < 2; p++) {
+        for (int p = 0; p < 3; p++) {
             free(d->sl[i].ps[p].rac);
             free(d->sl[i].ps[p].vlc);
         }
-    for (int k = 0; k < 3; k++)
+    for (int k = 0; k < 4; k++)
         free(d->last[k]);
     free(d->init_states[0]);
     free(d->init_states[1]);
@@ -1824,7 +1876,7 @@ static void decode_row(void *coder, int golomb, plane_state *ps, const int16_t q
 static void decode_plane_any(ffv1o_dec *d, void *coder, int golomb,
                              plane_state *ps, const int16_t qt[5][256],
                              int model1, int w, int h, uint8_t *dst,
-                             int stride, int x0, int y0)
+                             int stride, int x0, int y0, int pixel_stride)
 {
     int bits = d->bits <= 8 ? 8 : d->bits;
     int16_t *P = d->scratch;
@@ -1836,7 +1888,7 @@ static void decode_plane_any(ffv1o_dec *d, void *coder, int golomb,
         for (int x = 0; x < w; x++) {
             unsigned v = (uint16_t)P[(int64_t)y * w + x];
             if (d->cfg.sample_bytes == 1) {
-                row[x0 + x] = (uint8_t)v;
+                row[pixel_stride * (x0 + x)] = (uint8_t)v;
             } else {
                 if (!d->cfg.packed_at_lsb)
                     v = (v << (16 - d->bits)) & 0xFFFF;
@@ -1851,16 +1903,17 @@ static void decode_plane_any(ffv1o_dec *d, void *coder, int golomb,
  * the inverse RCT; bgr0 gets B, G, R and a zero fourth byte. */
 static void decode_rgb_slice(ffv1o_dec *d, void *coder, int golomb, dslice *s,
                              const int16_t qt[5][256], int model1,
-                             uint8_t *const planes[3], const int strides[3])
+                             uint8_t *const planes[4], const int strides[4])
 {
     int lbd = d->bits <= 8;
     int bits = lbd ? 9 : d->bits + 1;
     int offset = 1 << (lbd ? 8 : d->bits);
     int64_t n = (int64_t)s->w * s->h;
-    int16_t *P[3] = {d->scratch, d->scratch + n, d->scratch + 2 * n};
+    int16_t *P[4] = {d->scratch, d->scratch + n, d->scratch + 2 * n, d->scratch + 3 * n};
+    const int np = 3 + (d->transparency != 0);
     int run_index = 0;
     for (int y = 0; y < s->h; y++)
-        for (int p = 0; p < 3; p++)
+        for (int p = 0; p < np; p++)
             decode_row(coder, golomb, &s->ps[(p + 1) / 2], qt, model1, P[p], s->w, y, bits,
                        &run_index);
     for (int y = 0; y < s->h; y++)
@@ -1871,9 +1924,10 @@ static void decode_rgb_slice(ffv1o_dec *d, void *coder, int golomb, dslice *s,
             b += g;
             r += g;
             int X = s->x0 + x, Y = s->y0 + y;
-            if (lbd) { /* one 32-bit store of b + (g << 8) + (r << 16): carries cross bytes */
+            if (lbd) { /* one 32-bit store of b + (g << 8) + (r << 16) + (a << 24): carries cross bytes */
                 uint8_t *px = planes[0] + (int64_t)Y * strides[0] + 4 * (int64_t)X;
-                uint32_t v = (uint32_t)b + ((uint32_t)g << 8) + ((uint32_t)r << 16);
+                const uint32_t a = np > 3 ? (uint32_t)P[3][i] : 0u;
+                uint32_t v = (uint32_t)b + ((uint32_t)g << 8) + ((uint32_t)r << 16) + (a << 24);
                 px[0] = (uint8_t)v;
                 px[1] = (uint8_t)(v >> 8);
                 px[2] = (uint8_t)(v >> 16);
@@ -1890,7 +1944,7 @@ static void decode_rgb_slice(ffv1o_dec *d, void *coder, int golomb, dslice *s,
 }
 
 int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
-                    uint8_t *const planes[3], const int strides[3], int *key_out)
+                    uint8_t *const planes[4], const int strides[4], int *key_out)
 {
     rc_dec c0;
     uint8_t ks = 128;
@@ -1914,7 +1968,8 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
             d->chroma_planes = rc_get(&c0, &st[0]);
             d->hs = rc_get_symbol(&c0, st, 0);
             d->vs = rc_get_symbol(&c0, st, 0);
-            (void)rc_get(&c0, &st[0]);
+            d->transparency = rc_get(&c0, &st[0]);
+            d->plane_count = 2 + d->transparency; /* ffv1dec.c:695 */
             d->contexts = get_quant_tables(&c0, d->qt);
             if (d->contexts < 0)
                 return -1;
@@ -1973,7 +2028,9 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
         }
         c.t = &d->frame_tab;
         const int16_t(*qt)[256] = (const int16_t(*)[256])d->qt;
-        int model1 = 0;
+        /* get_context takes the LL / TT terms when the table has them
+         * (ffv1.h:161-176): context model 1's in-band v0/v1 tables */
+        int model1 = d->qt[3][127] != 0;
         int contexts = d->contexts;
         d->sl[i].damaged |= crc_bad[i];
         if (d->version > 2) { /* decode_slice_header, ffv1dec.c:282-359 */
@@ -1990,7 +2047,7 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
             int ok = (uint32_t)sw <= W && (uint32_t)sh <= H && (uint32_t)sx + (uint64_t)(uint32_t)sw <= (uint64_t)W &&
                      (uint32_t)sy + (uint64_t)(uint32_t)sh <= (uint64_t)H;
             int qi = 0;
-            for (int j = 0; ok && j < 2; j++) {
+            for (int j = 0; ok && j < d->plane_count; j++) {
                 unsigned idx = (unsigned)rc_get_symbol(&c, st, 0);
                 ok = idx < 2;
                 qi = (int)idx; /* plane 0 and plane 1 read their own index; ours agree */
@@ -2009,7 +2066,7 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
             contexts = d->ctx_count[qi];
         }
         if (key)
-            for (int pp = 0; pp < 2; pp++) {
+            for (int pp = 0; pp < d->plane_count; pp++) {
                 if (d->version > 2 && d->init_states[model1])
                     memcpy(s->ps[pp].rac, d->init_states[model1], (size_t)contexts * 32);
                 else
@@ -2036,19 +2093,26 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
         }
         if (d->colorspace) {
             decode_rgb_slice(d, coder, golomb, s, qt, model1, planes, strides);
-        } else {
-        int np = d->chroma_planes ? 3 : 1;
-        for (int pl = 0; pl < np; pl++) {
-            int x0 = s->x0, y0 = s->y0, w = s->w, h = s->h;
-            if (pl) {
-                w = ceil_rshift(s->w, d->hs);
-                h = ceil_rshift(s->h, d->vs);
-                x0 = s->x0 >> d->hs;
-                y0 = s->y0 >> d->vs;
+        } else if (d->chroma_planes || !d->transparency) { /* ffv1dec.c:437-449 */
+            int np = d->chroma_planes ? 3 : 1;
+            for (int pl = 0; pl < np; pl++) {
+                int x0 = s->x0, y0 = s->y0, w = s->w, h = s->h;
+                if (pl) {
+                    w = ceil_rshift(s->w, d->hs);
+                    h = ceil_rshift(s->h, d->vs);
+                    x0 = s->x0 >> d->hs;
+                    y0 = s->y0 >> d->vs;
+                }
+                decode_plane_any(d, coder, golomb, &s->ps[pl ? 1 : 0], qt, model1,
+                                 w, h, planes[pl], strides[pl], x0, y0, 1);
             }
-            decode_plane_any(d, coder, golomb, &s->ps[pl ? 1 : 0], qt, model1,
-                             w, h, planes[pl], strides[pl], x0, y0);
-        }
+            if (d->transparency)
+                decode_plane_any(d, coder, golomb, &s->ps[d->version >= 4 && !d->chroma_planes ? 1 : 2], qt,
+                                 model1, s->w, s->h, planes[3], strides[3], s->x0, s->y0, 1);
+        } else { /* YA8, ffv1dec.c:450-453 */
+            for (int pl = 0; pl < 2; pl++)
+                decode_plane_any(d, coder, golomb, &s->ps[pl], qt, model1, s->w, s->h, planes[0] + pl,
+                                 strides[0], s->x0, s->y0, 2);
         }
         if (!golomb && d->version > 2) { /* ffv1dec.c:461-467 */
             uint8_t st = 129;
@@ -2060,17 +2124,17 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
 
     /* concealment (ffv1dec.c:998-1021): a damaged slice's rectangle comes
      * from the previous picture; the x offset is in samples << (depth > 8),
-     * which for packed bgr0 is x bytes (not 4x) */
-    int row[3], rows[3];
-    int np = out_planes(d, row, rows);
+     * which for packed bgr0 / RGB32 / YA8 is x bytes (not 4x / 2x) */
+    int row[4], rows[4], step[4];
+    int np = out_planes(d, row, rows, step);
     for (int i = n - 1; i >= 0 && d->have_last; i--) {
         dslice *s = &d->sl[i];
         if (!s->damaged || !s->w || !s->h)
             continue;
         for (int k = 0; k < np; k++) {
-            int hs = k ? d->cfg.chroma_h_shift : 0, vs = k ? d->cfg.chroma_v_shift : 0;
+            int hs = k == 1 || k == 2 ? d->cfg.chroma_h_shift : 0, vs = k == 1 || k == 2 ? d->cfg.chroma_v_shift : 0;
             int pix = d->cfg.sample_bytes == 2;
-            int bpp = d->cfg.sample_bytes;
+            int bpp = step[k];
             int64_t xoff = (int64_t)(s->x0 >> hs) << pix;
             int64_t bytes = (int64_t)ceil_rshift(s->w, hs) * bpp;
             for (int y = 0; y < ceil_rshift(s->h, vs); y++) {

@@ -40,7 +40,7 @@ typedef struct ffv1o_config {
     int chroma_planes;        /* 1 = Y+Cb+Cr, 0 = gray                        */
     int chroma_h_shift;
     int chroma_v_shift;
-    int transparency;         /* must be 0 (alpha is out of scope)            */
+    int transparency;         /* alpha: YUVA (plane 3), YA8 (packed Y, A), RGB32 */
     int bits_per_raw_sample;  /* 8..16                                         */
     int packed_at_lsb;        /* 1: u16 samples hold the value in the LSBs     */
     int sample_bytes;         /* 1 (8-bit formats) or 2                        */
@@ -60,6 +60,9 @@ typedef struct ffv1o_config {
  * pix_fmt: "yuv420p" "yuv422p" "yuv444p" "yuv440p" "yuv411p" "yuv410p"
  *          "gray" "yuv420p9" "yuv422p9" "yuv444p9" "yuv420p10" "yuv422p10"
  *          "yuv444p10" "yuv420p16" "yuv422p16" "yuv444p16" "gray16"
+ *          "bgr0" "0rgb32" "gbrp9" "gbrp10" "gbrp12" "gbrp14"
+ *          with alpha: "yuva420p" "yuva422p" "yuva444p" (and 9, 10, 16 bit)
+ *          "ya8" "bgra" "rgb32"
  * coder: -1 (default), 0, 1 (custom table), 2, -2 ; level: -1 default.
  * bits_per_raw_sample: 0 = default from pix_fmt.  slicecrc: -1 default.
  * Returns 0 or a negative errno-style code (-22 EINVAL, -38 ENOSYS,
@@ -87,10 +90,11 @@ int64_t    ffv1o_enc_stats_out(const ffv1o_enc *e, char *buf, int64_t cap);
 void       ffv1o_enc_free(ffv1o_enc *e);
 /* Writes the v>=2 extradata (incl. CRC) and returns its size (0 for v<2). */
 int        ffv1o_enc_extradata(ffv1o_enc *e, uint8_t *buf, int cap);
-/* Encodes one frame; planes are Y, Cb, Cr with byte strides.  Returns the
+/* Encodes one frame; planes are Y, Cb, Cr (and A for YUVA) with byte
+ * strides; entries past the format's planes are not read.  Returns the
  * packet size or a negative error; *key receives the keyframe flag. */
-int64_t    ffv1o_enc_frame(ffv1o_enc *e, const uint8_t *const planes[3],
-                           const int strides[3], uint8_t *out, int64_t cap,
+int64_t    ffv1o_enc_frame(ffv1o_enc *e, const uint8_t *const planes[4],
+                           const int strides[4], uint8_t *out, int64_t cap,
                            int *key);
 /* Per-slice byte counts of the last frame (before the trailer). */
 int64_t    ffv1o_enc_get_states(const ffv1o_enc *e, uint8_t *buf, int64_t cap);
@@ -102,8 +106,8 @@ int        ffv1o_enc_last_slice_bytes(const ffv1o_enc *e, int *bytes, int n);
  * context already made non-negative and diff folded (ffv1enc.c:306-317).
  * Returns the number of samples written. */
 int64_t    ffv1o_slice_symbols(const ffv1o_config *cfg,
-                               const uint8_t *const planes[3],
-                               const int strides[3], int slice,
+                               const uint8_t *const planes[4],
+                               const int strides[4], int slice,
                                int32_t *out, int64_t cap);
 
 typedef struct ffv1o_dec ffv1o_dec;
@@ -117,7 +121,7 @@ void       ffv1o_dec_free(ffv1o_dec *d);
  * Returns 0, or a negative code: -1 bad packet, -2 slice CRC mismatch,
  * -3 P-frame without keyframe. */
 int        ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
-                           uint8_t *const planes[3], const int strides[3],
+                           uint8_t *const planes[4], const int strides[4],
                            int *key);
 
 /* MSB-first CRC-32, poly 0x04C11DB7, init 0, no final xor (crc.c:357). */

@@ -98,25 +98,31 @@ def configure(width, height, pix_fmt, slices=0, level=-1, coder=-1, context=0,
 
 
 def plane_shapes(cfg: Config):
+    """(rows, samples) of each input plane: Y, Cb, Cr, then A for YUVA; YA8
+    one plane of interleaved Y, A bytes; bgr0 / RGB32 one of 4-byte pixels."""
     w, h = cfg.width, cfg.height
-    if cfg.colorspace and cfg.sample_bytes == 4:  # bgr0: one packed plane
+    if cfg.colorspace and cfg.sample_bytes == 4:  # bgr0 / RGB32: one packed plane
         return [(h, 4 * w)]
+    if cfg.transparency and not cfg.chroma_planes:  # YA8
+        return [(h, 2 * w)]
     cw = -((-w) >> cfg.chroma_h_shift)
     ch = -((-h) >> cfg.chroma_v_shift)
     shapes = [(h, w)]
     if cfg.chroma_planes:
         shapes += [(ch, cw), (ch, cw)]
+    if cfg.transparency:
+        shapes.append((h, w))
     return shapes
 
 
 def _plane_ptrs(planes):
-    arr = (ctypes.POINTER(ctypes.c_uint8) * 3)()
-    strides = (ctypes.c_int * 3)()
+    arr = (ctypes.POINTER(ctypes.c_uint8) * 4)()
+    strides = (ctypes.c_int * 4)()
     for i, p in enumerate(planes):
         assert p.flags["C_CONTIGUOUS"]
         arr[i] = _u8p(p.view(np.uint8))
         strides[i] = p.strides[0]
-    for i in range(len(planes), 3):
+    for i in range(len(planes), 4):
         arr[i] = arr[0]
         strides[i] = strides[0]
     return arr, strides

@@ -32,12 +32,12 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), f"{n} declared in include/ffv1hip.h but not exported"
     assert set(names) == set(EXPORTED_SYMBOLS)
-    assert lib.ffv1hip_abi_version() == 4
+    assert lib.ffv1hip_abi_version() == 5
 
 
 FIELDS = ["width", "height", "chroma_planes", "chroma_h_shift", "chroma_v_shift",
           "bits_per_raw_sample", "packed_at_lsb", "sample_bytes", "version", "ac", "ec",
-          "context_model", "num_h_slices", "num_v_slices", "gop_size", "colorspace"]
+          "context_model", "num_h_slices", "num_v_slices", "gop_size", "colorspace", "transparency"]
 
 OPTION_GRID = [
     (352, 288, "yuv420p", 0, -1, -1, 0, 12, 0),
@@ -57,6 +57,13 @@ OPTION_GRID = [
     (352, 288, "bgr0", 0, -1, 1, 1, 12, 0),
     (176, 144, "0rgb32", 0, 1, 0, 0, 12, 0),
     (352, 288, "gbrp9", 4, -1, 0, 0, 12, 0),
+    (352, 288, "yuva420p", 4, -1, 1, 0, 12, 0),
+    (352, 288, "yuva420p", 0, -1, 0, 0, 12, 0),
+    (352, 288, "yuva444p10", 0, 3, 1, 1, 12, 0),
+    (720, 576, "yuva422p16", 0, -1, -1, 0, 12, 0),
+    (176, 144, "ya8", 0, 1, 1, 0, 12, 0),
+    (352, 288, "bgra", 0, 3, 0, 0, 12, 0),
+    (352, 288, "rgb32", 4, -1, 1, 0, 12, 0),
     (1920, 1080, "gbrp10", 0, -1, -1, 0, 12, 0),
     (352, 288, "gbrp12", 0, 3, 1, 0, 12, 0),
     (352, 288, "gbrp14", 0, 3, 1, 0, 12, 13),

@@ -81,10 +81,9 @@ def test_chained_coder_matches_oracle(stream, monkeypatch):
 def test_split_walk_matches_oracle(stream, recsets, monkeypatch):
     """The split schedule with a walk in two launches (first part 3 waves,
     forced by the test hooks) and the next batch's symbols beside its second
-    part (two records sets: all of them; one set: those part B does not read,
-    the rest after it): the same bytes as the oracle across batches."""
+    part (two records sets), and one records set (symbols, walk, bits beside
+    it): the same bytes as the oracle across batches."""
     monkeypatch.setenv("FFV1HIP_RECSETS", str(recsets))
-    monkeypatch.setenv("FFV1HIP_PARTIAL", "1")
     monkeypatch.setenv("FFV1HIP_WALK_PART_A", "3")
     monkeypatch.setenv("FFV1HIP_SPLIT_MAX", "100000")
     frames = list(stream.frames())
@@ -254,7 +253,9 @@ def test_avcodec_mirror_c3_known_answer(batch):
     assert enc.close() == 0
     assert len(pkts) == pin["frames"]
     n = pin["frames"]
-    assert got == [i >= batch - 1 for i in range(n)]  # the delay: batch - 1 frames
+    # the delay: two batches (one codes while the next queues)
+    assert avctx.delay == 2 * batch - 1
+    assert got == [i >= avctx.delay for i in range(n)]
     assert [p.pts for p in pkts] == [1000 + i for i in range(len(pkts))]
     assert [p.dts for p in pkts] == [p.pts for p in pkts]
     assert [p.key for p in pkts] == [i % 12 == 0 for i in range(len(pkts))]
@@ -262,6 +263,46 @@ def test_avcodec_mirror_c3_known_answer(batch):
     for p in pkts:
         h.update(p.data)
     assert h.hexdigest() == pin["stream_md5"]
+
+
+@pytest.mark.parametrize("batch", [3, 4])
+def test_encode2_pipelined_budget_reencode(batch, monkeypatch):
+    """encode2 one frame per call with a 512-byte starting slice budget: every
+    batch goes over it while the next one is already coding, so the re-encode
+    rolls back two batches in flight; packets, pts and keys equal the
+    oracle's stream."""
+    from ffv1hip import AVCodecContext, FFV1Encoder
+    monkeypatch.setenv("FFV1HIP_SLICE_CAP", "512")
+    s = PARITY_STREAMS[1]
+    frames = list(s.frames())
+    _, ex_ref, ref = oracle_encode(s, frames)
+    avctx = AVCodecContext(s.width, s.height, s.pix_fmt, gop_size=s.gop_size, slices=s.slices, coder=s.coder)
+    enc = FFV1Encoder(batch=batch)
+    assert enc.init(avctx) == 0
+    assert avctx.extradata == ex_ref
+    pkts = [enc.encode2(f, pts=i) for i, f in enumerate(frames)]
+    pkts = [p for p in pkts if p is not None]
+    while (p := enc.encode2(None)) is not None:
+        pkts.append(p)
+    enc.close()
+    assert [p.pts for p in pkts] == list(range(len(frames)))
+    assert [(p.data, p.key) for p in pkts] == ref
+
+
+@pytest.mark.parametrize("cap", [None, "512"])
+def test_host_encode_many_batches(cap, monkeypatch):
+    """ffv1hip_encode over several batches in one call (frames staged while
+    the previous batch codes), with and without the budget re-encode."""
+    if cap:
+        monkeypatch.setenv("FFV1HIP_SLICE_CAP", cap)
+    from ffv1hip import HipEncoder
+    s = PARITY_STREAMS[1]
+    frames = list(s.frames())
+    _, _, ref = oracle_encode(s, frames)
+    enc = HipEncoder(hip_params(s), 0, 3)
+    got = enc.encode(frames)
+    enc.close()
+    assert got == ref
 
 
 def _d2h(ptr, nbytes):
