@@ -410,6 +410,7 @@ struct ffv1hip_ctx {
   SliceGeom* d_geom = nullptr;
   int* d_slot_frames = nullptr;  // [j][slot]
   int* d_status = nullptr;       // [set][4]: [0] slices over budget, [1] most bytes one needed
+  int2* d_rct = nullptr;         // v4: [batch frame][slice] RCT coefficients (choose_rct_params)
   hipStream_t stream = nullptr;
   // 2-pass (ffv1enc.c:898-986): pass 1 counts into d_rcstat ([256][2] state
   // counts, then [contexts][32][2] slot counts); pass 2 starts keyframes
@@ -548,8 +549,9 @@ int ffv1hip_configure(ffv1hip_params* out, const ffv1hip_options* o) {
     version = o->level;
   }
   p.ec = o->slicecrc < 0 ? (version >= 3) : o->slicecrc;
-  if (version == 2 || version > 3)
+  if ((version == 2 || version > 3) && !o->experimental)
     return set_err(FFV1HIP_AVERROR_INVALIDDATA, "version %d is experimental in the reference", version);
+  if (version == 2) return set_err(-38, "version 2 (in-band slice layout) is not supported");
   // coder (ffv1enc.c:708-718)
   int ac = 0;
   if (o->coder != -1) ac = o->coder > 0 ? 2 : 0;
@@ -592,6 +594,12 @@ int ffv1hip_configure(ffv1hip_params* out, const ffv1hip_options* o) {
   p.ac = ac;
   p.context_model = o->context;
   p.num_h_slices = p.num_v_slices = 1;
+  // v4 runs choose_rct_params on every slice (ffv1enc.c:1163-1164): it reads
+  // plane 0 as 32-bit B, G, R words at 8 bit, planes 0-2 as u16 at the luma
+  // position above; inside the frame for RGB and >8-bit 4:4:4 YCbCr only
+  if (version > 3 && !p.colorspace &&
+      !(p.chroma_planes && !p.chroma_h_shift && !p.chroma_v_shift && p.sample_bytes == 2))
+    return set_err(-38, "version 4 with %s: the reference reads outside the frame (choose_rct_params)", o->pix_fmt);
   // slice grid (ffv1enc.c:988-1000); allow_large_grid extends it to the
   // decoder's MAX_SLICES=256 (ffv1.h:77) for 8K.
   if (version > 1) {
@@ -728,6 +736,12 @@ static void build_ops(ffv1hip_ctx* c) {
         L.sym(kSetSlice, 1, 3, false);  // progressive
         L.sym(kSetSlice, 1, p.sar_num, false);
         L.sym(kSetSlice, 1, p.sar_den, false);
+        if (p.version > 3) {  // ffv1enc.c:1052-1061: slice_coding_mode 0, the frame's RCT coefficients
+          L.bit(kSetSlice, 1, 0);
+          L.sym(kSetSlice, 1, 0, false);
+          L.ops.push_back(Op{int16_t(kOpSymRct), uint8_t(kSetSlice), 1, 0});
+          L.ops.push_back(Op{int16_t(kOpSymRct), uint8_t(kSetSlice), 1, 1});
+        }
       }
       const size_t sel = size_t(key) * c->nslices + s;
       c->nops[sel] = int(L.ops.size());
@@ -814,7 +828,7 @@ static void free_device(ffv1hip_ctx* c) {
                   c->d_persist[1], c->d_tables, c->d_sym, c->d_keys2, c->d_cbits, c->d_dcount, c->d_dbase, c->d_dtotal, c->d_pre[0],
                   c->d_pre[1], c->d_bits[0], c->d_bits[1], c->d_scratch, c->d_hdr, c->d_hdr_digits, c->d_geom, c->d_slot_frames, c->d_status,
                   c->d_rec2, c->d_cbits2, c->d_ident, c->d_segs_info, c->d_seg_totals, c->d_wmap, c->d_ck,
-                  c->d_segrec};
+                  c->d_segrec, c->d_rct};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_dtotal) (void)hipHostFree(c->h_dtotal);
@@ -1023,6 +1037,7 @@ static int alloc_device(ffv1hip_ctx* c) {
   HIP_TRY(hipMalloc(&c->d_geom, sizeof(SliceGeom) * c->nslices));
   HIP_TRY(hipMemcpy(c->d_geom, c->geom.data(), sizeof(SliceGeom) * c->nslices, hipMemcpyHostToDevice));
   HIP_TRY(hipMalloc(&c->d_slot_frames, sizeof(int) * size_t(c->max_slots) * (nb + 1)));
+  if (c->P.version > 3) HIP_TRY(hipMalloc(&c->d_rct, sizeof(int2) * size_t(nb) * c->nslices));
   HIP_TRY(hipMalloc(&c->d_status, sizeof(int) * 8));
   HIP_TRY(hipMemset(c->d_status, 0, sizeof(int) * 8));
   return 0;
@@ -1041,7 +1056,7 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
                                                                     : p.sample_bytes == 2 && p.packed_at_lsb &&
                                                                           p.bits_per_raw_sample <= 14 && !p.transparency)
                                          : false;
-  if (p.version == 2 || p.version > 3 || p.num_h_slices * p.num_v_slices > 256 ||
+  if (p.version == 2 || p.version > 4 || p.num_h_slices * p.num_v_slices > 256 ||
       p.bits_per_raw_sample < 8 || p.bits_per_raw_sample > 16 || p.width <= 0 || p.height <= 0 || !fmt_ok)
     return fail(set_err(-38, "unsupported parameter set"));
   if (p.num_h_slices > p.width || p.num_v_slices > p.height)
@@ -1131,8 +1146,9 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
     const char* mode = std::getenv("FFV1HIP_CODER");
     const int64_t lds = walk_lds_bytes(int64_t(2) * c->contexts * 32);
     // RGB interleaves the three planes' rows (encode_rgb_frame): chained
-    // alpha: the chained coders (a third plane context)
-    c->frames_mode = p.ac && !p.colorspace && !p.transparency && lds <= kWalkLdsMax &&
+    // alpha (a third plane context) and v4 (per-frame slice header values):
+    // the chained coders
+    c->frames_mode = p.ac && !p.colorspace && !p.transparency && p.version <= 3 && lds <= kWalkLdsMax &&
                      !(mode && std::strcmp(mode, "chain") == 0);
     c->wmax = 2 * (p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample) + 1;
     // the decision-stream coder writes a slice's digits (2 bytes each) where
@@ -1367,6 +1383,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   sa.geom = c->d_geom;
   sa.nslices = c->nslices;
   sa.nplanes = c->ncoded;
+  sa.rct = c->d_rct;
   sa.sample_bytes = p.sample_bytes;
   sa.packed_at_lsb = p.packed_at_lsb;
   sa.msb_shift = 16 - p.bits_per_raw_sample;
@@ -1419,6 +1436,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   ca.rgb = p.colorspace;
   ca.nplanes = c->ncoded;
   ca.pcount = c->pcount;
+  ca.rct = c->d_rct;
   for (int k = 0; k < kMaxPlanes; k++) ca.pset[k] = sa.pset[k];
   ca.init = c->d_init;
 
@@ -1597,6 +1615,21 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       return set_err(-5, "sink launch failed: %s", hipGetErrorString(hipGetLastError()));
   } else {
     HIP_TRY(hipMemsetAsync(ca.status, 0, sizeof(int) * 4, st));
+    if (p.version > 3) {  // every (frame, slice)'s RCT coefficients, before the symbols and headers
+      RctArgs ra{};
+      ra.frames = d_frames;
+      ra.frame_bytes = frame_bytes;
+      for (int k = 0; k < 3; k++) {
+        ra.plane_off[k] = plane_off[k < nin ? k : 0];
+        ra.plane_stride[k] = plane_stride[k < nin ? k : 0];
+      }
+      ra.sample_bytes = p.sample_bytes;
+      ra.geom = c->d_geom;
+      ra.nslices = c->nslices;
+      ra.nframes = n;
+      ra.rct = c->d_rct;
+      if (launch_rct_params(ra, st) < 0) return set_err(-5, "rct launch failed");
+    }
     for (int j = 0; j < maxlen; j++) {
       sa.frame_of_slot = c->d_slot_frames + size_t(j) * nsegs;
       if (timed(0, st, [&] { return launch_symbols(sa, st); }) < 0)
@@ -1725,6 +1758,27 @@ static int settle_batch(ffv1hip_ctx* c, int64_t b) {
     const int rc = run_batch(c, next.frames, next.frame_bytes, next.plane_off, next.plane_stride, next.n, nullptr);
     if (rc < 0) return rc;
   }
+  if (c->P.version > 3) {
+    // v4: the reference re-codes a range-coded slice as PCM (slice_coding_mode
+    // 1, ffv1enc.c:1207-1217) when a line starts with less than 35 * w bytes
+    // left in its buffer (:282-286; Golomb-Rice: 4 * w, and the frame
+    // fails); the buffers are a packet of 16384 + 12 * w * h bytes, all of
+    // it for slice 0, 1 / slice_count each for the others (:1281-1282,
+    // 1317-1322).  A slice that ends within that margin might have taken
+    // that path, which is not coded here: an error, never other bytes.
+    const ffv1hip_ctx::LastBatch& L = c->hist[b & 1];
+    std::vector<int64_t> sb(size_t(L.n) * c->nslices);
+    HIP_TRY(hipMemcpy(sb.data(), c->d_slice_bytes, sb.size() * sizeof(int64_t), hipMemcpyDeviceToHost));
+    const int64_t pkt = 16384 + int64_t(c->P.width) * c->P.height * 12;
+    for (size_t i = 0; i < sb.size(); i++) {
+      const int s = int(i % c->nslices);
+      const int64_t cap = s == 0 ? pkt : pkt / c->nslices;
+      if (sb[i] > cap - int64_t(c->P.ac ? 35 : 4) * c->geom[s].pw[0])
+        return set_err(-38, "version 4: slice %d of frame %lld would be coded as PCM by the reference "
+                            "(slice_coding_mode 1), which this encoder does not do", s,
+                       (long long)(L.pn0 + int64_t(i) / c->nslices));
+    }
+  }
   return 0;
 }
 
@@ -1821,7 +1875,7 @@ static int pipe_open(ffv1hip_ctx* c) {
     HIP_TRY(hipHostMalloc(&P.h_slot[k], size_t(P.slot_bytes), hipHostMallocDefault));
     HIP_TRY(hipEventCreateWithFlags(&P.slot_ev[k], hipEventDisableTiming));
   }
-  if (c->pass != 1) {
+  if (c->pass != 1 && c->P.version <= 3) {  // (v4 checks each batch's slice sizes before the next one)
     size_t free_b = 0, total_b = 0;
     HIP_TRY(hipMemGetInfo(&free_b, &total_b));
     const size_t pk_bytes = size_t(c->packet_stride) * c->max_batch;
@@ -2353,6 +2407,8 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
     return fail(set_err(-38, "GPU decoder: unsupported parameter set"));
   if (p.transparency)  // the oracle decoder reads these streams (tests/test_alpha.py)
     return fail(set_err(-38, "GPU decoder: alpha planes are not decoded on the GPU"));
+  if (p.version > 3)  // likewise (tests/test_v4.py)
+    return fail(set_err(-38, "GPU decoder: version 4 is not decoded on the GPU"));
   // The stream's extradata must be the one these parameters produce
   // (read_extradata, ffv1dec.c:509-631, would derive the same parameters);
   // versions 0 and 1 have none, their header is in band.

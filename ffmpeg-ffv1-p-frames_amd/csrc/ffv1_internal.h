@@ -15,7 +15,10 @@ namespace ffv1hip {
 // the v3 slice header (ffv1enc.c:1031-1062).  Every op names one of kOpSets
 // private 32-byte state vectors (all 128 at slice start) and which
 // transition table it adapts with.
-enum OpKind : int16_t { kOpSymU = 0, kOpSymS = 1, kOpBit = 2 };
+// kOpSymRct: an unsigned symbol whose value is the frame's slice RCT
+// coefficient (value 0: slice_rct_by_coef, 1: slice_rct_ry_coef; v4 slice
+// header, ffv1enc.c:1058-1059), chosen on the device per (frame, slice)
+enum OpKind : int16_t { kOpSymU = 0, kOpSymS = 1, kOpBit = 2, kOpSymRct = 3 };
 struct Op {
   int16_t kind;
   uint8_t set;
@@ -83,6 +86,20 @@ struct SymbolArgs {
   uint32_t* cbits;            // with rec: [slot][frame_chunks][kChunkWords]
   int64_t frame_chunks;
   int p_lo, p_hi;             // planes of this launch (p_hi 0: all); with rec, outputs by batch frame
+  const int2* rct;            // v4: [batch frame][slice] {by, ry} RCT coefficients, else null (1, 1)
+};
+
+// v4's choose_rct_params (ffv1enc.c:1064-1144) for every (frame, slice) of
+// a batch: the 15 candidate sums of one slice, then its coefficients.
+struct RctArgs {
+  const uint8_t* frames;
+  int64_t frame_bytes;
+  int64_t plane_off[3];
+  int plane_stride[3];
+  int sample_bytes;           // 4: one B, G, R, X word per pixel; 2: three u16 planes read as b, g, r
+  const SliceGeom* geom;
+  int nslices, nframes;
+  int2* rct;                  // [frame][slice] {by, ry}
 };
 
 // Walk record of one sample (frame-parallel mode), written by ffv1_symbols.
@@ -172,6 +189,7 @@ struct CodeArgs {
   int nplanes;                // coded planes (1 gray, 2 YA8, 3, 4 with alpha)
   int pset[kMaxPlanes];       // plane context set of each coded plane
   int pcount;                 // plane contexts (plane_count: 2, 3 with alpha)
+  const int2* rct;            // v4: [batch frame][slice] RCT coefficients for the slice header ops
   int nframes;                // decision-stream mode: frames of the batch
   DecisionStream ds;
   const uint8_t* init;        // chained range coder: 2-pass initial states [contexts][32], or null
@@ -297,6 +315,7 @@ int launch_conceal(const DecodeArgs& a, void* stream);
 int64_t decode_lds_bytes(const DecodeArgs& a, bool global_states);
 
 int launch_symbols(const SymbolArgs& a, void* stream);
+int launch_rct_params(const RctArgs& a, void* stream);
 int launch_code(const CodeArgs& a, void* stream);
 int launch_layout(const int* dcount, int nstreams, int64_t* dbase, int64_t* total, StreamSegs* segs,
                   int* seg_totals, int* wmap, void* stream);

@@ -143,7 +143,7 @@ __device__ __forceinline__ int wave_next(int x) { return __builtin_amdgcn_update
 // RGB32: one u32 per pixel (B, G, R, X / A bytes); gbrp: three u16 planes
 // read in AVFrame data[] order as b, g, r.
 template <int SB>
-__device__ __forceinline__ int rct_sample(const SymbolArgs& a, const uint8_t* fr, int p, int x, int y) {
+__device__ __forceinline__ int rct_sample(const SymbolArgs& a, const uint8_t* fr, int p, int x, int y, int2 co) {
   int b, g, r;
   if constexpr (SB == 4) {
     const uint32_t v = reinterpret_cast<const uint32_t*>(fr + a.plane_off[0] + (int64_t)y * a.plane_stride[0])[x];
@@ -158,7 +158,7 @@ __device__ __forceinline__ int rct_sample(const SymbolArgs& a, const uint8_t* fr
   }
   b -= g;
   r -= g;
-  g += (b + r) >> 2;
+  g += (b * co.x + r * co.y) >> 2;  // v4: the slice's coefficients (ffv1enc.c:450), else 1, 1
   return p == 0 ? g : (p == 1 ? b : r) + a.rct_offset;
 }
 
@@ -194,11 +194,12 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   // issued back to back and waited for once
   const int sh = a.packed_at_lsb ? 0 : a.msb_shift;
   const uint8_t* const fr = a.frames + (int64_t)f * a.frame_bytes;
+  const int2 co = RGB && a.rct ? a.rct[(int64_t)f * a.nslices + slice] : make_int2(1, 1);
   auto load = [&](int x, int y) -> int {
     if constexpr (SB == 4) {
-      return rct_sample<4>(a, fr, p, px + x, py + y);
+      return rct_sample<4>(a, fr, p, px + x, py + y, co);
     } else {
-      if constexpr (SB == 2 && RGB) return rct_sample<2>(a, fr, p, px + x, py + y);
+      if constexpr (SB == 2 && RGB) return rct_sample<2>(a, fr, p, px + x, py + y, co);
       const uint8_t* r = base + (int64_t)(py + y) * stride;
       if constexpr (SB == 1) return r[(px + x) * step];
       else return (int16_t)(reinterpret_cast<const uint16_t*>(r)[px + x] >> sh);
@@ -651,7 +652,7 @@ constexpr int kOpsetBytes = kOpSets * 32;
 template <class SinkT>
 __device__ __forceinline__ void run_header_ops(const CodeArgs& a, Lane& L, SinkT& S, uint8_t* os, int key,
                                                int slice, bool live, const uint8_t* dtab,
-                                               const uint8_t* ftab, int osb, int flush_at) {
+                                               const uint8_t* ftab, int osb, int flush_at, int f) {
   for (int i = 0; i < osb; i++) os[i] = 128;
   const int sel = key * a.nslices + slice;
   const int n = live ? a.nops[sel] : 0;
@@ -661,10 +662,15 @@ __device__ __forceinline__ void run_header_ops(const CodeArgs& a, Lane& L, SinkT
       const Op op = ops[q];
       const uint8_t* t = op.tab ? ftab : dtab;
       uint8_t* st = os + op.set * 32;
+      int v = op.value;
+      if (op.kind == kOpSymRct) {  // v4: the frame's slice RCT coefficient
+        const int2 co = a.rct[(int64_t)f * a.nslices + slice];
+        v = op.value ? co.y : co.x;
+      }
       if (op.kind == kOpBit)
-        put_lds(L, st, op.value, t);
+        put_lds(L, st, v, t);
       else
-        symbol_lds(L, st, op.value, op.kind == kOpSymS, t);
+        symbol_lds(L, st, v, op.kind == kOpSymS, t);
     }
     flush_if(L, S, flush_at);
   }
@@ -743,7 +749,8 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
   uint8_t* const out = a.slice_out + ((int64_t)(live ? f : 0) * a.nslices + slice) * a.slice_stride;
   Sink S = make_sink(out, live ? a.slice_cap : 0);  // idle lanes write nothing
 
-  run_header_ops(a, L, S, opsets + lane * kOpsetBytes, key, slice, live, dtab, ftab, kOpsetBytes, kHeaderFlushAt);
+  run_header_ops(a, L, S, opsets + lane * kOpsetBytes, key, slice, live, dtab, ftab, kOpsetBytes, kHeaderFlushAt,
+                 live ? f : 0);
 
   const SliceGeom& g = a.geom[slice];
   const int64_t nsym = live ? g.nsym : 0;
@@ -1999,7 +2006,7 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
   uint8_t* const out = a.slice_out + ((int64_t)(live ? f : 0) * a.nslices + slice) * a.slice_stride;
   Sink S = make_sink(out, live ? a.slice_cap : 0);  // idle lanes write nothing
   run_header_ops(a, L, S, opsets + lane * kOpsetBytes, key, slice, live, tabs, tabs + 512, kOpsetBytes,
-                 kHeaderFlushAt);
+                 kHeaderFlushAt, live ? f : 0);
   const int64_t ac_bytes = terminate(L, S, a.version > 2, kRing);
   if (!live) return;
 
@@ -2241,7 +2248,77 @@ __global__ __launch_bounds__(kAsmThreads) void ffv1_assemble_packets(AssembleArg
   if (s == a.nslices - 1 && t == 0) a.packet_size[f] = off + body + (a.ec ? 4 : 0);
 }
 
+// ---------------------------------------------------------------------------
+// choose_rct_params (ffv1enc.c:1064-1144), one block per (slice, frame).  A
+// pixel's contribution to the 15 sums needs its row's left neighbour and
+// the same two pixels one row up: ag = g - g(x-1) (0 left of the slice),
+// bg = ag - ag(x, y-1) with the row-up value as the reference keeps it in
+// its int16 sample buffer; likewise b, r; br -= bg, bb -= bg; sum i adds
+// |bg + ((br * c0 + bb * c1) >> 2)|.  The sums wrap like the reference's
+// ints (mod 2^32 in any order), compared as int; the first minimum wins.
+constexpr int kRctThreads = 256;
+__constant__ int kRctCoef[15][2] = {{0, 0}, {1, 1}, {2, 2}, {0, 2}, {2, 0}, {4, 0}, {0, 4}, {0, 3},
+                                    {3, 0}, {3, 1}, {1, 3}, {1, 2}, {2, 1}, {0, 1}, {1, 0}};
+
+__device__ __forceinline__ int3 rct_bgr(const RctArgs& a, const uint8_t* fr, int x, int y) {
+  if (a.sample_bytes == 4) {
+    const uint32_t v = reinterpret_cast<const uint32_t*>(fr + a.plane_off[0] + (int64_t)y * a.plane_stride[0])[x];
+    return make_int3(v & 0xFF, (v >> 8) & 0xFF, (v >> 16) & 0xFF);
+  }
+  return make_int3(reinterpret_cast<const uint16_t*>(fr + a.plane_off[0] + (int64_t)y * a.plane_stride[0])[x],
+                   reinterpret_cast<const uint16_t*>(fr + a.plane_off[1] + (int64_t)y * a.plane_stride[1])[x],
+                   reinterpret_cast<const uint16_t*>(fr + a.plane_off[2] + (int64_t)y * a.plane_stride[2])[x]);
+}
+
+__global__ __launch_bounds__(kRctThreads) void ffv1_rct_params(RctArgs a) {
+  __shared__ uint32_t part[15][kRctThreads];
+  const int slice = blockIdx.x, f = blockIdx.y;
+  const SliceGeom& g = a.geom[slice];
+  const uint8_t* const fr = a.frames + (int64_t)f * a.frame_bytes;
+  const int w = g.pw[0], h = g.ph[0], x0 = g.px[0], y0 = g.py[0];
+  uint32_t st[15];
+#pragma unroll
+  for (int i = 0; i < 15; i++) st[i] = 0u;
+  const int64_t n = (int64_t)(w - 1) * (h - 1);  // pixels with x, y >= 1
+  for (int64_t k = threadIdx.x; k < n; k += kRctThreads) {
+    const int x = 1 + (int)(k % (w - 1)), y = 1 + (int)(k / (w - 1));
+    const int3 c = rct_bgr(a, fr, x0 + x, y0 + y), l = rct_bgr(a, fr, x0 + x - 1, y0 + y);
+    const int3 u = rct_bgr(a, fr, x0 + x, y0 + y - 1), ul = rct_bgr(a, fr, x0 + x - 1, y0 + y - 1);
+    const int bg = (c.y - l.y) - (int)(int16_t)(u.y - ul.y);
+    int bb = (c.x - l.x) - (int)(int16_t)(u.x - ul.x);
+    int br = (c.z - l.z) - (int)(int16_t)(u.z - ul.z);
+    br -= bg;
+    bb -= bg;
+#pragma unroll
+    for (int i = 0; i < 15; i++) {
+      const int v = bg + ((br * kRctCoef[i][0] + bb * kRctCoef[i][1]) >> 2);
+      st[i] += (uint32_t)(v < 0 ? -v : v);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 15; i++) part[i][threadIdx.x] = st[i];
+  __syncthreads();
+  for (int s = kRctThreads / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s)
+      for (int i = 0; i < 15; i++) part[i][threadIdx.x] += part[i][threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    int best = 0;
+    for (int i = 1; i < 15; i++)
+      if ((int)part[i][0] < (int)part[best][0]) best = i;
+    a.rct[(int64_t)f * a.nslices + slice] = make_int2(kRctCoef[best][1], kRctCoef[best][0]);
+  }
+}
+
 }  // namespace
+
+int launch_rct_params(const RctArgs& a, void* stream) {
+  if (a.nframes <= 0) return 0;
+  hipLaunchKernelGGL(ffv1_rct_params, dim3(a.nslices, a.nframes), dim3(kRctThreads), 0,
+                     reinterpret_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int launch_symbols(const SymbolArgs& a, void* stream) {
   const int np = a.p_hi > a.p_lo ? a.p_hi - a.p_lo : a.nplanes - a.p_lo;

@@ -27,7 +27,7 @@ class Options(ctypes.Structure):
                 ("slices", ctypes.c_int), ("level", ctypes.c_int), ("coder", ctypes.c_int),
                 ("context", ctypes.c_int), ("gop_size", ctypes.c_int),
                 ("bits_per_raw_sample", ctypes.c_int), ("slicecrc", ctypes.c_int),
-                ("allow_large_grid", ctypes.c_int), ("pass_", ctypes.c_int)]
+                ("allow_large_grid", ctypes.c_int), ("pass_", ctypes.c_int), ("experimental", ctypes.c_int)]
 
 
 class Params(ctypes.Structure):
@@ -178,12 +178,13 @@ class FFV1Error(RuntimeError):
 def configure(width: int, height: int, pix_fmt: str, slices: int = 0, level: int = -1,
               coder: int = -1, context: int = 0, gop_size: int = 12,
               bits_per_raw_sample: int = 0, slicecrc: int = -1,
-              allow_large_grid: bool = False, pass_: int = 0) -> Params:
+              allow_large_grid: bool = False, pass_: int = 0, experimental: bool = False) -> Params:
     """encode_init's option -> bitstream-parameter derivation (ffv1enc.c:669-1029);
-    pass_ 1 / 2 are AV_CODEC_FLAG_PASS1 / PASS2."""
+    pass_ 1 / 2 are AV_CODEC_FLAG_PASS1 / PASS2; experimental is -strict
+    experimental (version 4 at level 4, ffv1enc.c:703-706)."""
     L = load_library()
     o = Options(width, height, pix_fmt.encode(), slices, level, coder, context, gop_size,
-                bits_per_raw_sample, slicecrc, int(allow_large_grid), pass_)
+                bits_per_raw_sample, slicecrc, int(allow_large_grid), pass_, int(experimental))
     p = Params()
     rc = L.ffv1hip_configure(ctypes.byref(p), ctypes.byref(o))
     if rc < 0:

@@ -46,6 +46,11 @@ typedef struct ffv1hip_options {
                                  refuses (ffv1enc.c:988-1000); used for 8K  */
     int pass;                 /* 1 / 2: AV_CODEC_FLAG_PASS1 / PASS2 (version
                                  >= 2, ffv1enc.c:680-682); see ffv1hip_set_pass */
+    int experimental;         /* -strict experimental: admits version 4
+                                 (level 4, ffv1enc.c:703-706) for the RGB
+                                 formats and >8-bit 4:4:4 YCbCr, the formats
+                                 whose choose_rct_params reads stay inside
+                                 the frame (:1064-1144, 1163-1164)          */
 } ffv1hip_options;
 
 /* Effective bitstream parameters (what encode_init derives). */
@@ -57,7 +62,8 @@ typedef struct ffv1hip_params {
     int packed_at_lsb;        /* u16 samples LSB-aligned (yuv*p9/p10, gbrp) */
     int sample_bytes;         /* 1 or 2 bytes per stored sample; 4: bgr0,
                                  one packed B,G,R,X plane                   */
-    int version;              /* 0, 1 or 3                                  */
+    int version;              /* 0, 1, 3 or 4 (experimental: per-slice RCT
+                                 coefficients in the slice header)          */
     int ac;                   /* 0 Golomb-Rice, 1 range default, 2 range custom */
     int ec;                   /* slice CRC-32 trailers                      */
     int context_model;        /* 0: 666 contexts, 1: 7563                   */

@@ -575,6 +575,15 @@ int ffv1o_configure2(ffv1o_config *cfg, int width, int height,
                      int context, int gop_size, int bits_per_raw_sample,
                      int slicecrc, int pass)
 {
+    return ffv1o_configure3(cfg, width, height, pix_fmt, slices, level, coder, context, gop_size,
+                            bits_per_raw_sample, slicecrc, pass, 0);
+}
+
+int ffv1o_configure3(ffv1o_config *cfg, int width, int height,
+                     const char *pix_fmt, int slices, int level, int coder,
+                     int context, int gop_size, int bits_per_raw_sample,
+                     int slicecrc, int pass, int experimental)
+{
     const pixfmt_info *pf = NULL;
     for (size_t i = 0; i < sizeof(PIXFMTS) / sizeof(PIXFMTS[0]); i++)
         if (!strcmp(PIXFMTS[i].name, pix_fmt))
@@ -605,8 +614,12 @@ int ffv1o_configure2(ffv1o_config *cfg, int width, int height,
     int ec = slicecrc;
     if (ec < 0)
         ec = version >= 3;
-    if (version == 2 || version > 3) /* needs -strict experimental (:703) */
+    /* versions 2 and 4 need -strict experimental (:703-706); version 2's
+     * in-band slice layout (write_header, :523-541) is not restated */
+    if ((version == 2 || version > 3) && !experimental)
         return AVERR_INVALIDDATA;
+    if (version == 2)
+        return AVERR_ENOSYS;
 
     /* coder, ffv1enc.c:708-718 (coder -1 keeps the private default 0) */
     int ac = 0;
@@ -675,8 +688,14 @@ int ffv1o_configure2(ffv1o_config *cfg, int width, int height,
     cfg->context_model = context;
     cfg->num_h_slices = 1;
     cfg->num_v_slices = 1;
-
-    /* slice grid search, ffv1enc.c:988-1000 */
+    /* v4 runs choose_rct_params on every slice (ffv1enc.c:1163-1164), which
+     * reads plane 0 as 32-bit B, G, R words at 8 bit and planes 0-2 as u16
+     * at the LUMA position otherwise: inside the frame only for the RGB
+     * formats and 4:4:4 YCbCr above 8 bits (gray has no planes 1, 2;
+     * subsampled chroma and 8-bit YCbCr are read past their end) */
+    if (version > 3 && !cfg->colorspace &&
+        !(cfg->chroma_planes && !cfg->chroma_h_shift && !cfg->chroma_v_shift && cfg->sample_bytes == 2))
+        return AVERR_ENOSYS;
     if (version > 1) {
         int nv = (width > 352 || height > 288 || !slices) ? 2 : 1;
         for (; nv < 9; nv++)
@@ -706,6 +725,7 @@ typedef struct slice_ctx {
     int64_t cap;
     int64_t bytes;
     int error;
+    int pcm;            /* the last frame coded this slice as PCM (v4) */
 } slice_ctx;
 
 struct ffv1o_enc {
@@ -719,6 +739,10 @@ struct ffv1o_enc {
     slice_ctx *sl;
     int64_t picture_number;
     int plane_count;    /* 2 + transparency (ffv1enc.c:720, 890-891) */
+    /* the slice being coded: encode_line's buffer check failed (ffv1enc.c:
+     * 283-292), slice_coding_mode (1 = PCM, :294-304, 1207-1217) and the
+     * RCT coefficients (v4: choose_rct_params, :1064-1144; else 1, 1) */
+    int line_err, pcm, rct_by, rct_ry;
     int16_t *scratch;   /* one slice plane of samples */
     /* 2-pass (ffv1enc.c:898-986, 1236-1277) */
     int pass1;
@@ -773,10 +797,13 @@ ffv1o_enc *ffv1o_enc_new(const ffv1o_config *cfg)
         slice_rects(cfg, i, &s->x0, &s->y0, &s->w, &s->h);
         if ((int64_t)s->w * s->h > maxw)
             maxw = (int64_t)s->w * s->h;
-        /* the reference's slice buffer: pkt->size / slice_count of a packet
-         * of AV_INPUT_BUFFER_MIN_SIZE + w*h*140 bytes (ffv1enc.c:1232-1233,
-         * 1317-1322); malloc'd pages are only touched as far as used */
-        s->cap = (16384 + (int64_t)cfg->width * cfg->height * 140) / e->nslices;
+        /* the reference's slice buffers in a packet of AV_INPUT_BUFFER_MIN_SIZE
+         * + w*h*140 bytes (v4: w*h*12), ffv1enc.c:1232-1233, 1281-1282: slice
+         * 0 codes on with the packet's coder (the whole packet), slice i in
+         * pkt->size / slice_count bytes (:1317-1322); malloc'd pages are only
+         * touched as far as used */
+        const int64_t pkt = 16384 + (int64_t)cfg->width * cfg->height * (cfg->version > 3 ? 12 : 140);
+        s->cap = i == 0 ? pkt : pkt / e->nslices;
         s->buf = malloc(s->cap);
         for (int p = 0; p < e->plane_count; p++) {
             s->ps[p].rac = malloc((size_t)e->contexts * 32);
@@ -1143,7 +1170,9 @@ static void put_v01_header(const ffv1o_enc *e, rc_enc *c)
 }
 
 /* encode_slice_header (ffv1enc.c:1031-1062) */
-static void put_slice_header(const ffv1o_enc *e, const slice_ctx *s, rc_enc *c)
+static void clear_slice_states(ffv1o_enc *e, slice_ctx *s);
+
+static void put_slice_header(ffv1o_enc *e, slice_ctx *s, rc_enc *c)
 {
     const ffv1o_config *cfg = &e->cfg;
     uint8_t st[32];
@@ -1158,6 +1187,16 @@ static void put_slice_header(const ffv1o_enc *e, const slice_ctx *s, rc_enc *c)
     rc_put_symbol(c, st, 3, 0); /* progressive picture structure */
     rc_put_symbol(c, st, cfg->sar_num, 0);
     rc_put_symbol(c, st, cfg->sar_den, 0);
+    if (cfg->version > 3) { /* ffv1enc.c:1052-1061 */
+        rc_put(c, &st[0], e->pcm);
+        if (e->pcm)
+            clear_slice_states(e, s);
+        rc_put_symbol(c, st, e->pcm, 0);
+        if (!e->pcm) {
+            rc_put_symbol(c, st, e->rct_by, 0);
+            rc_put_symbol(c, st, e->rct_ry, 0);
+        }
+    }
 }
 
 /* Load one slice plane into int16 storage, as encode_plane does
@@ -1267,6 +1306,20 @@ static void code_row_rac(ffv1o_enc *e, rc_enc *c, plane_state *ps,
                          const int16_t *P, int w, int y)
 {
     int model1 = e->cfg.context_model;
+    if (c->end - c->ptr < (int64_t)w * 35) { /* ffv1enc.c:282-286 */
+        e->line_err = 1;
+        return;
+    }
+    if (e->pcm) { /* slice_coding_mode 1: every bit on a fresh state 128 (:294-304) */
+        for (int x = 0; x < w; x++) {
+            int v = P[(int64_t)y * w + x];
+            for (int i = e->coded_bits - 1; i >= 0; i--) {
+                uint8_t st = 128;
+                rc_put(c, &st, (v >> i) & 1);
+            }
+        }
+        return;
+    }
     for (int x = 0; x < w; x++) {
         taps t;
         int ctx, diff;
@@ -1288,6 +1341,10 @@ static void code_row_golomb(ffv1o_enc *e, bitw *b, plane_state *ps,
     int bits = e->coded_bits;
     int run_index = *run_index_io;
     int run_count = 0, run_mode = 0;
+    if (b->end - b->base - (b->nbits >> 3) < (int64_t)w * 4) { /* ffv1enc.c:287-291 */
+        e->line_err = 1;
+        return;
+    }
     for (int x = 0; x < w; x++) {
         taps t;
         int ctx, diff;
@@ -1332,7 +1389,7 @@ static void code_plane(ffv1o_enc *e, void *coder, int golomb, plane_state *ps,
                        const int16_t *P, int w, int h)
 {
     int run_index = 0;
-    for (int y = 0; y < h; y++) {
+    for (int y = 0; y < h && !e->line_err; y++) {
         if (golomb)
             code_row_golomb(e, (bitw *)coder, ps, P, w, y, &run_index);
         else
@@ -1345,7 +1402,7 @@ static void code_plane(ffv1o_enc *e, void *coder, int golomb, plane_state *ps,
  * one packed plane (B, G, R, X bytes); gbrp is three u16 planes whose first
  * is read as "b", second as "g", third as "r", as the reference does. */
 static void rct_sample(const ffv1o_config *cfg, const uint8_t *const planes[4],
-                       const int strides[4], int x, int y, int out[4])
+                       const int strides[4], int x, int y, int by, int ry, int pcm, int out[4])
 {
     int b, g, r;
     int bits = cfg->bits_per_raw_sample;
@@ -1364,12 +1421,88 @@ static void rct_sample(const ffv1o_config *cfg, const uint8_t *const planes[4],
         g = q1[0] | (q1[1] << 8);
         r = q2[0] | (q2[1] << 8);
     }
+    if (pcm) { /* slice_coding_mode 1: no transform (ffv1enc.c:447) */
+        out[0] = g;
+        out[1] = b;
+        out[2] = r;
+        return;
+    }
     b -= g;
     r -= g;
-    g += (b + r) >> 2;
+    g += (b * by + r * ry) >> 2;
     out[0] = g;
     out[1] = b + (1 << bits);
     out[2] = r + (1 << bits);
+}
+
+/* encode_line's "bits" (ffv1enc.c:393-405, 464-467): 8 or the raw depth
+ * for YCbCr; RGB one more (9 at 8 bit) for the transformed samples, the raw
+ * depth in PCM slices */
+static int coded_bits_of(const ffv1o_config *cfg, int pcm)
+{
+    int bits = cfg->bits_per_raw_sample <= 8 ? 8 : cfg->bits_per_raw_sample;
+    if (cfg->colorspace && !pcm)
+        return bits + 1;
+    return bits;
+}
+
+/* choose_rct_params (ffv1enc.c:1064-1144): the RCT luma coefficients whose
+ * gradient-predicted G' residual is smallest over the slice.  Read as the
+ * reference reads: 8-bit: one 32-bit B, G, R, X word per pixel of plane 0;
+ * else three u16 planes as b, g, r at the slice's luma position.  The row's
+ * differences are kept in int16 (sample_buffer) and the 15 sums in int,
+ * both as the reference's arithmetic wraps. */
+static void choose_rct(ffv1o_enc *e, const slice_ctx *s, const uint8_t *const planes[4],
+                       const int strides[4])
+{
+    static const int coef[15][2] = {{0, 0}, {1, 1}, {2, 2}, {0, 2}, {2, 0}, {4, 0}, {0, 4}, {0, 3},
+                                    {3, 0}, {3, 1}, {1, 3}, {1, 2}, {2, 1}, {0, 1}, {1, 0}};
+    uint32_t stat[15] = {0};
+    const int lbd = e->cfg.bits_per_raw_sample <= 8;
+    int16_t *S = e->scratch; /* [3][w] */
+    const int w = s->w;
+    for (int y = 0; y < s->h; y++) {
+        int lastr = 0, lastg = 0, lastb = 0;
+        for (int x = 0; x < w; x++) {
+            int b, g, r;
+            const int X = s->x0 + x, Y = s->y0 + y;
+            if (lbd) {
+                const uint8_t *px = planes[0] + (int64_t)Y * strides[0] + 4 * (int64_t)X;
+                b = px[0];
+                g = px[1];
+                r = px[2];
+            } else {
+                const uint8_t *q0 = planes[0] + (int64_t)Y * strides[0] + 2 * (int64_t)X;
+                const uint8_t *q1 = planes[1] + (int64_t)Y * strides[1] + 2 * (int64_t)X;
+                const uint8_t *q2 = planes[2] + (int64_t)Y * strides[2] + 2 * (int64_t)X;
+                b = q0[0] | (q0[1] << 8);
+                g = q1[0] | (q1[1] << 8);
+                r = q2[0] | (q2[1] << 8);
+            }
+            int ar = r - lastr, ag = g - lastg, ab = b - lastb;
+            if (x && y) {
+                int bg = ag - S[x], bb = ab - S[w + x], br = ar - S[2 * w + x];
+                br -= bg;
+                bb -= bg;
+                for (int i = 0; i < 15; i++) {
+                    int v = bg + ((br * coef[i][0] + bb * coef[i][1]) >> 2);
+                    stat[i] += (uint32_t)(v < 0 ? -v : v);
+                }
+            }
+            S[x] = (int16_t)ag;
+            S[w + x] = (int16_t)ab;
+            S[2 * w + x] = (int16_t)ar;
+            lastr = r;
+            lastg = g;
+            lastb = b;
+        }
+    }
+    int best = 0;
+    for (int i = 1; i < 15; i++)
+        if ((int32_t)stat[i] < (int32_t)stat[best])
+            best = i;
+    e->rct_by = coef[best][1];
+    e->rct_ry = coef[best][0];
 }
 
 /* encode_rgb_frame (ffv1enc.c:413-473): the lines of G', B', R' (and A
@@ -1385,13 +1518,13 @@ static void code_rgb_slice(ffv1o_enc *e, slice_ctx *s, const uint8_t *const plan
     for (int y = 0; y < s->h; y++)
         for (int x = 0; x < s->w; x++) {
             int v[4];
-            rct_sample(&e->cfg, planes, strides, s->x0 + x, s->y0 + y, v);
+            rct_sample(&e->cfg, planes, strides, s->x0 + x, s->y0 + y, e->rct_by, e->rct_ry, e->pcm, v);
             for (int p = 0; p < np; p++)
                 P[p][(int64_t)y * s->w + x] = (int16_t)v[p];
         }
     int run_index = 0;
-    for (int y = 0; y < s->h; y++)
-        for (int p = 0; p < np; p++) {
+    for (int y = 0; y < s->h && !e->line_err; y++)
+        for (int p = 0; p < np && !e->line_err; p++) {
             plane_state *ps = &s->ps[(p + 1) / 2];
             if (golomb)
                 code_row_golomb(e, (bitw *)coder, ps, P[p], s->w, y, &run_index);
@@ -1400,7 +1533,7 @@ static void code_rgb_slice(ffv1o_enc *e, slice_ctx *s, const uint8_t *const plan
         }
 }
 
-static void reset_slice_states(ffv1o_enc *e, slice_ctx *s)
+static void clear_slice_states(ffv1o_enc *e, slice_ctx *s)
 {
     const uint8_t *is = e->init_states[e->cfg.context_model];
     for (int p = 0; p < e->plane_count; p++) {
@@ -1484,8 +1617,19 @@ int64_t ffv1o_enc_frame(ffv1o_enc *e, const uint8_t *const planes[4],
                 put_v01_header(e, &c);
             c.t = &e->frame_tab;
         }
+        /* encode_slice (ffv1enc.c:1146-1220): v4 picks the slice's RCT
+         * coefficients; a range-coded v4 slice that does not fit its buffer
+         * is coded again as PCM from the coder state it started with */
+        e->pcm = 0;
+        e->rct_by = e->rct_ry = 1;
+        if (cfg->version > 3)
+            choose_rct(e, s, planes, strides);
+        const rc_enc c_bak = c;
+    retry:
+        e->line_err = 0;
+        e->coded_bits = coded_bits_of(cfg, e->pcm);
         if (key)
-            reset_slice_states(e, s);
+            clear_slice_states(e, s);
         if (cfg->version > 2)
             put_slice_header(e, s, &c);
 
@@ -1501,13 +1645,19 @@ int64_t ffv1o_enc_frame(ffv1o_enc *e, const uint8_t *const planes[4],
             bw_init(&b, s->buf + ac_bytes, s->cap - ac_bytes);
             code_slice_planes(e, s, planes, strides, &b, 1);
             s->bytes = ac_bytes + bw_bytes(&b);
-            s->error = b.overflow || c.overflow;
+            s->error = b.overflow || c.overflow || e->line_err;
         } else {
             code_slice_planes(e, s, planes, strides, &c, 0);
+            if (e->line_err && cfg->version > 3 && !e->pcm) {
+                e->pcm = 1;
+                c = c_bak;
+                goto retry;
+            }
             uint8_t st = 129;
             rc_put(&c, &st, 0);
             s->bytes = rc_finish(&c);
-            s->error = c.overflow;
+            s->error = c.overflow || e->line_err;
+            s->pcm = e->pcm;
         }
         if (s->error)
             return AVERR_INVALIDDATA;
@@ -1573,6 +1723,13 @@ int ffv1o_enc_set_states(ffv1o_enc *e, const uint8_t *buf, int64_t size,
     return 0;
 }
 
+int ffv1o_enc_last_slice_pcm(const ffv1o_enc *e, int *pcm, int n)
+{
+    for (int i = 0; i < n && i < e->nslices; i++)
+        pcm[i] = e->sl[i].pcm;
+    return e->nslices;
+}
+
 int ffv1o_enc_last_slice_bytes(const ffv1o_enc *e, int *bytes, int n)
 {
     for (int i = 0; i < n && i < e->nslices; i++)
@@ -1623,6 +1780,7 @@ int64_t ffv1o_slice_symbols(const ffv1o_config *cfg,
 
 typedef struct dslice {
     int x0, y0, w, h;
+    int pcm, rct_by, rct_ry; /* v4 slice header (ffv1dec.c:344-356); else 0, 1, 1 */
     plane_state ps[3];
     int damaged; /* slice_damaged: set by a CRC / header / end mismatch, cleared by read_header */
 } dslice;
@@ -1631,6 +1789,7 @@ struct ffv1o_dec {
     ffv1o_config cfg;
     int version, micro_version, ac, ec, bits, chroma_planes, hs, vs, colorspace;
     int transparency, plane_count; /* ffv1dec.c:558-559, 693-695 */
+    int cur_pcm;                   /* the slice being decoded is PCM */
     int num_h, num_v;
     int16_t qsets[2][5][256];
     int ctx_count[2];
@@ -1871,6 +2030,19 @@ static void decode_row(void *coder, int golomb, plane_state *ps, const int16_t q
     *run_index_io = run_index;
 }
 
+/* decode_line's PCM branch (ffv1dec.c:111-120): every bit on a fresh state 128 */
+static void decode_row_pcm(rc_dec *c, int16_t *P, int w, int y, int bits)
+{
+    for (int x = 0; x < w; x++) {
+        int v = 0;
+        for (int i = 0; i < bits; i++) {
+            uint8_t st = 128;
+            v += v + rc_get(c, &st);
+        }
+        P[(int64_t)y * w + x] = (int16_t)v;
+    }
+}
+
 /* decode_plane (ffv1dec.c:200-224): reconstruct into P, then store with
  * the pixel format's alignment. */
 static void decode_plane_any(ffv1o_dec *d, void *coder, int golomb,
@@ -1882,7 +2054,10 @@ static void decode_plane_any(ffv1o_dec *d, void *coder, int golomb,
     int16_t *P = d->scratch;
     int run_index = 0;
     for (int y = 0; y < h; y++)
-        decode_row(coder, golomb, ps, qt, model1, P, w, y, bits, &run_index);
+        if (d->cur_pcm)
+            decode_row_pcm((rc_dec *)coder, P, w, y, bits);
+        else
+            decode_row(coder, golomb, ps, qt, model1, P, w, y, bits, &run_index);
     for (int y = 0; y < h; y++) {
         uint8_t *row = dst + (int64_t)(y0 + y) * stride;
         for (int x = 0; x < w; x++) {
@@ -1906,7 +2081,7 @@ static void decode_rgb_slice(ffv1o_dec *d, void *coder, int golomb, dslice *s,
                              uint8_t *const planes[4], const int strides[4])
 {
     int lbd = d->bits <= 8;
-    int bits = lbd ? 9 : d->bits + 1;
+    int bits = (lbd ? 8 : d->bits) + !s->pcm; /* ffv1dec.c:252-255 */
     int offset = 1 << (lbd ? 8 : d->bits);
     int64_t n = (int64_t)s->w * s->h;
     int16_t *P[4] = {d->scratch, d->scratch + n, d->scratch + 2 * n, d->scratch + 3 * n};
@@ -1914,15 +2089,22 @@ static void decode_rgb_slice(ffv1o_dec *d, void *coder, int golomb, dslice *s,
     int run_index = 0;
     for (int y = 0; y < s->h; y++)
         for (int p = 0; p < np; p++)
-            decode_row(coder, golomb, &s->ps[(p + 1) / 2], qt, model1, P[p], s->w, y, bits,
-                       &run_index);
+            if (s->pcm)
+                decode_row_pcm((rc_dec *)coder, P[p], s->w, y, bits);
+            else
+                decode_row(coder, golomb, &s->ps[(p + 1) / 2], qt, model1, P[p], s->w, y, bits,
+                           &run_index);
     for (int y = 0; y < s->h; y++)
         for (int x = 0; x < s->w; x++) {
             int64_t i = (int64_t)y * s->w + x;
-            int g = P[0][i], b = P[1][i] - offset, r = P[2][i] - offset;
-            g -= (b + r) >> 2;
-            b += g;
-            r += g;
+            int g = P[0][i], b = P[1][i], r = P[2][i];
+            if (!s->pcm) { /* ffv1dec.c:263-269 */
+                b -= offset;
+                r -= offset;
+                g -= (b * s->rct_by + r * s->rct_ry) >> 2;
+                b += g;
+                r += g;
+            }
             int X = s->x0 + x, Y = s->y0 + y;
             if (lbd) { /* one 32-bit store of b + (g << 8) + (r << 16) + (a << 24): carries cross bytes */
                 uint8_t *px = planes[0] + (int64_t)Y * strides[0] + 4 * (int64_t)X;
@@ -2027,6 +2209,9 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
             rc_dec_init(&c, pkt + starts[i], lens[i], &d->frame_tab);
         }
         c.t = &d->frame_tab;
+        int reset = 0;
+        s->pcm = 0;
+        s->rct_by = s->rct_ry = 1;
         const int16_t(*qt)[256] = (const int16_t(*)[256])d->qt;
         /* get_context takes the LL / TT terms when the table has them
          * (ffv1.h:161-176): context model 1's in-band v0/v1 tables */
@@ -2061,11 +2246,27 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
             (void)rc_get_symbol(&c, st, 0); /* picture structure */
             (void)rc_get_symbol(&c, st, 0);
             (void)rc_get_symbol(&c, st, 0);
+            s->pcm = 0;
+            s->rct_by = s->rct_ry = 1;
+            reset = 0;
+            if (d->version > 3) { /* ffv1dec.c:344-356 */
+                reset = rc_get(&c, &st[0]);
+                s->pcm = rc_get_symbol(&c, st, 0);
+                if (s->pcm != 1) {
+                    s->rct_by = rc_get_symbol(&c, st, 0);
+                    s->rct_ry = rc_get_symbol(&c, st, 0);
+                    if ((uint64_t)(uint32_t)s->rct_by + (uint64_t)(uint32_t)s->rct_ry > 4) {
+                        s->x0 = s->y0 = s->w = s->h = 0;
+                        s->damaged = 1;
+                        continue;
+                    }
+                }
+            }
             qt = (const int16_t(*)[256])d->qsets[qi];
             model1 = qi;
             contexts = d->ctx_count[qi];
         }
-        if (key)
+        if (key || reset) /* ffv1dec.c:414-415 */
             for (int pp = 0; pp < d->plane_count; pp++) {
                 if (d->version > 2 && d->init_states[model1])
                     memcpy(s->ps[pp].rac, d->init_states[model1], (size_t)contexts * 32);
@@ -2091,6 +2292,7 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
             b.nbits = blen * 8;
             coder = &b;
         }
+        d->cur_pcm = s->pcm;
         if (d->colorspace) {
             decode_rgb_slice(d, coder, golomb, s, qt, model1, planes, strides);
         } else if (d->chroma_planes || !d->transparency) { /* ffv1dec.c:437-449 */

@@ -44,7 +44,7 @@ typedef struct ffv1o_config {
     int bits_per_raw_sample;  /* 8..16                                         */
     int packed_at_lsb;        /* 1: u16 samples hold the value in the LSBs     */
     int sample_bytes;         /* 1 (8-bit formats) or 2                        */
-    int version;              /* 0, 1, 2 or 3                                  */
+    int version;              /* 0, 1, 3 or 4 (experimental)                   */
     int ac;                   /* 0 Golomb-Rice, 1 range default, 2 range custom */
     int ec;                   /* slice CRCs                                    */
     int context_model;        /* 0 (666 contexts) or 1 (7563)                  */
@@ -79,6 +79,15 @@ int ffv1o_configure2(ffv1o_config *cfg, int width, int height,
                      int context, int gop_size, int bits_per_raw_sample,
                      int slicecrc, int pass);
 
+/* As ffv1o_configure2; experimental = -strict experimental, which admits
+ * version 4 (level 4, ffv1enc.c:703-706): micro_version 2, per-slice RCT
+ * coefficients and slice_coding_mode in the slice header, the PCM re-code
+ * of a slice that does not fit its buffer.  Version 2 is not restated. */
+int ffv1o_configure3(ffv1o_config *cfg, int width, int height,
+                     const char *pix_fmt, int slices, int level, int coder,
+                     int context, int gop_size, int bits_per_raw_sample,
+                     int slicecrc, int pass, int experimental);
+
 typedef struct ffv1o_enc ffv1o_enc;
 
 ffv1o_enc *ffv1o_enc_new(const ffv1o_config *cfg);
@@ -101,6 +110,8 @@ int64_t    ffv1o_enc_get_states(const ffv1o_enc *e, uint8_t *buf, int64_t cap);
 int        ffv1o_enc_set_states(ffv1o_enc *e, const uint8_t *buf, int64_t size,
                                 int64_t picture_number);
 int        ffv1o_enc_last_slice_bytes(const ffv1o_enc *e, int *bytes, int n);
+/* Per slice: 1 when the last frame coded it as PCM (v4 slice_coding_mode). */
+int        ffv1o_enc_last_slice_pcm(const ffv1o_enc *e, int *pcm, int n);
 
 /* Symbols of one slice in coding order: (context << 16) | (uint16)diff, the
  * context already made non-negative and diff folded (ffv1enc.c:306-317).

@@ -55,6 +55,7 @@ def lib():
         L.ffv1o_enc_frame.argtypes = [ctypes.c_void_p, P(u8p), P(ctypes.c_int), u8p, ctypes.c_int64, P(ctypes.c_int)]
         L.ffv1o_enc_frame.restype = ctypes.c_int64
         L.ffv1o_enc_last_slice_bytes.argtypes = [ctypes.c_void_p, P(ctypes.c_int), ctypes.c_int]
+        L.ffv1o_enc_last_slice_pcm.argtypes = [ctypes.c_void_p, P(ctypes.c_int), ctypes.c_int]
         L.ffv1o_enc_get_states.argtypes = [ctypes.c_void_p, P(ctypes.c_uint8), ctypes.c_int64]
         L.ffv1o_enc_get_states.restype = ctypes.c_int64
         L.ffv1o_enc_set_states.argtypes = [ctypes.c_void_p, P(ctypes.c_uint8), ctypes.c_int64,
@@ -70,6 +71,9 @@ def lib():
         L.ffv1o_configure2.argtypes = [P(Config), ctypes.c_int, ctypes.c_int, ctypes.c_char_p] + \
             [ctypes.c_int] * 8
         L.ffv1o_configure2.restype = ctypes.c_int
+        L.ffv1o_configure3.argtypes = [P(Config), ctypes.c_int, ctypes.c_int, ctypes.c_char_p] + \
+            [ctypes.c_int] * 9
+        L.ffv1o_configure3.restype = ctypes.c_int
         L.ffv1o_enc_new2.argtypes = [P(Config), ctypes.c_int, ctypes.c_char_p]
         L.ffv1o_enc_new2.restype = ctypes.c_void_p
         L.ffv1o_enc_stats_out.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64]
@@ -85,13 +89,14 @@ def _u8p(a: np.ndarray):
 
 
 def configure(width, height, pix_fmt, slices=0, level=-1, coder=-1, context=0,
-              gop_size=12, bits_per_raw_sample=0, slicecrc=-1, pass_=0) -> Config:
+              gop_size=12, bits_per_raw_sample=0, slicecrc=-1, pass_=0, experimental=False) -> Config:
     """encode_init's parameter derivation (ffv1enc.c:669-1029); pass_ 1 / 2
-    are AV_CODEC_FLAG_PASS1 / PASS2."""
+    are AV_CODEC_FLAG_PASS1 / PASS2; experimental = -strict experimental
+    (version 4 at level 4, ffv1enc.c:703-706)."""
     cfg = Config()
-    rc = lib().ffv1o_configure2(ctypes.byref(cfg), width, height, pix_fmt.encode(), slices,
+    rc = lib().ffv1o_configure3(ctypes.byref(cfg), width, height, pix_fmt.encode(), slices,
                                 level, coder, context, gop_size, bits_per_raw_sample, slicecrc,
-                                pass_)
+                                pass_, int(experimental))
     if rc < 0:
         raise ValueError(f"ffv1o_configure rejected {pix_fmt} {width}x{height} slices={slices}: {rc}")
     return cfg
@@ -190,6 +195,13 @@ class Encoder:
         n = self.cfg.num_h_slices * self.cfg.num_v_slices
         arr = (ctypes.c_int * n)()
         lib().ffv1o_enc_last_slice_bytes(self._h, arr, n)
+        return list(arr)
+
+    def last_slice_pcm(self):
+        """Per slice: the last frame coded it as PCM (v4 slice_coding_mode 1)."""
+        n = self.cfg.num_h_slices * self.cfg.num_v_slices
+        arr = (ctypes.c_int * n)()
+        lib().ffv1o_enc_last_slice_pcm(self._h, arr, n)
         return list(arr)
 
 

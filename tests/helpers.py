@@ -37,6 +37,7 @@ class Stream:
     depth: int = 8                 # widening depth for videogen sources
     chroma444: bool = False
     allow_large_grid: bool = False
+    experimental: bool = False     # -strict experimental (version 4)
     seed: int = 1
     # False where the reference itself leaves samples uncoded: odd slice x
     # offsets with chroma subsampling (cx = x >> hs, ffv1enc.c:1186-1188)
@@ -57,7 +58,8 @@ class Stream:
         return oracle.configure(self.width, self.height, self.pix_fmt, slices=self.slices,
                                 level=self.level, coder=self.coder, context=self.context,
                                 gop_size=self.gop_size,
-                                bits_per_raw_sample=self.bits_per_raw_sample)
+                                bits_per_raw_sample=self.bits_per_raw_sample,
+                                experimental=self.experimental)
 
     def frames(self):
         if self.source == "videogen":

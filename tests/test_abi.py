@@ -172,3 +172,22 @@ def test_host_planes_are_checked_before_the_copy():
     check_planes(q, [np.zeros((32, 256), np.uint8)])
     with pytest.raises(ValueError):
         check_planes(q, [np.zeros((32, 64), np.uint8)])
+
+
+@pytest.mark.parametrize("fmt,slices,coder", [("bgr0", 4, 1), ("bgra", 0, 0), ("gbrp12", 6, -2),
+                                              ("yuv444p10", 4, 1), ("yuva444p16", 0, 1)])
+def test_configure_v4_matches_oracle(fmt, slices, coder):
+    """-strict experimental admits level 4 (ffv1enc.c:703-706); the same
+    formats are refused on both sides without it and for 8-bit / subsampled
+    YCbCr (choose_rct_params reads outside the frame there)."""
+    from ffv1hip import configure, FFV1Error
+    ref = oracle.configure(352, 288, fmt, slices=slices, level=4, coder=coder, experimental=True).as_dict()
+    got = configure(352, 288, fmt, slices=slices, level=4, coder=coder, experimental=True).as_dict()
+    assert got["version"] == 4
+    for f in FIELDS:
+        assert got[f] == ref[f], f
+    with pytest.raises(FFV1Error):
+        configure(352, 288, fmt, slices=slices, level=4, coder=coder)
+    for bad in ("yuv420p10", "yuv444p", "gray16"):
+        with pytest.raises(FFV1Error):
+            configure(352, 288, bad, level=4, experimental=True)

@@ -22,7 +22,7 @@ def hip_params(s: Stream):
     return configure(s.width, s.height, s.pix_fmt, slices=s.slices, level=s.level, coder=s.coder,
                      context=s.context, gop_size=s.gop_size,
                      bits_per_raw_sample=s.bits_per_raw_sample,
-                     allow_large_grid=s.allow_large_grid)
+                     allow_large_grid=s.allow_large_grid, experimental=s.experimental)
 
 
 def hip_encode(s: Stream, frames, batch):

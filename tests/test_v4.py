@@ -1,0 +1,131 @@
+"""FFV1 version 4 (`-strict experimental`, level 4; ffv1enc.c:703-706):
+micro_version 2 in the extradata (:566-570), per-slice RCT luma
+coefficients from choose_rct_params (:1064-1144) used by the colour
+transform (:450) and written in the slice header with slice_coding_mode
+(:1052-1061), and the PCM re-code of a range-coded slice that runs out of
+its buffer (:282-286, 294-304, 1207-1217; buffers :1281-1282, 1317-1322).
+The decoder side is ffv1dec.c:344-356, 111-120, 252-269, 414-415.
+
+Parity unpinned: the reference's FATE set has no version-4 vector, so the
+oracle's restatement is checked by its own lossless round trip, and the HIP
+encoder byte-for-byte against the oracle.  Version 4 is admitted where the
+reference's choose_rct_params reads stay inside the frame: the RGB formats
+and >8-bit 4:4:4 YCbCr (8-bit YCbCr is read as 32-bit RGB words, subsampled
+chroma at luma positions, gray through null planes 1 and 2).
+"""
+import numpy as np
+import pytest
+
+from helpers import Stream, oracle, oracle_encode
+
+V4_STREAMS = [
+    Stream("v4_bgr0_range", 96, 64, "bgr0", 5, level=4, slices=4, coder=1, gop_size=3, source="random",
+           experimental=True, seed=11),
+    Stream("v4_bgra_golomb", 64, 48, "bgra", 4, level=4, slices=4, coder=0, gop_size=2, source="random",
+           experimental=True, seed=12),
+    Stream("v4_gbrp10_ctx1", 80, 48, "gbrp10", 4, level=4, slices=6, coder=1, context=1, gop_size=4,
+           source="random", experimental=True, seed=13),
+    Stream("v4_gbrp14_default_tab", 64, 40, "gbrp14", 3, level=4, slices=4, coder=-2, gop_size=2,
+           source="random", experimental=True, seed=14),
+    Stream("v4_yuv444p10", 64, 48, "yuv444p10", 4, level=4, slices=4, coder=1, gop_size=2, source="random",
+           experimental=True, seed=15),
+    Stream("v4_yuva444p16_ctx1", 48, 32, "yuva444p16", 3, level=4, slices=4, coder=1, context=1, gop_size=3,
+           source="random", experimental=True, seed=16),
+]
+IDS = [s.name for s in V4_STREAMS]
+
+
+def _lossless(cfg, ex, pkts, frames):
+    dec = oracle.Decoder(cfg, ex)
+    for (pk, key), fr in zip(pkts, frames):
+        planes, k = dec.decode(pk)
+        assert k == key
+        for a, b in zip(planes, fr):
+            if cfg.colorspace and cfg.sample_bytes == 4 and not cfg.transparency:
+                a, b = a.reshape(a.shape[0], -1, 4)[..., :3], b.reshape(b.shape[0], -1, 4)[..., :3]
+            np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("stream", V4_STREAMS, ids=IDS)
+def test_oracle_v4_roundtrip(stream):
+    frames = list(stream.frames())
+    cfg, ex, pkts = oracle_encode(stream, frames)
+    assert cfg.version == 4
+    _lossless(cfg, ex, pkts, frames)
+
+
+def test_v4_needs_experimental_and_a_readable_format():
+    with pytest.raises(ValueError):  # AVERROR_INVALIDDATA without -strict experimental
+        oracle.configure(64, 48, "bgr0", level=4)
+    for fmt in ("yuv420p10", "yuv444p", "gray16", "ya8", "yuva420p10"):
+        with pytest.raises(ValueError):
+            oracle.configure(64, 48, fmt, level=4, experimental=True)
+    assert oracle.configure(64, 48, "yuv444p16", level=4, experimental=True).version == 4
+
+
+def test_v4_rct_coefficients_follow_the_content():
+    """A slice whose R carries G's detail and B is flat picks a coefficient
+    pair other than (1, 1); the stream still decodes losslessly, and differs
+    from the same frame coded at version 3 beyond the header."""
+    W, H = 64, 32
+    rng = np.random.default_rng(3)
+    g = rng.integers(0, 200, size=(H, W))
+    px = np.zeros((H, W, 4), np.uint8)
+    px[..., 1] = g
+    px[..., 2] = np.clip(g + rng.integers(0, 2, size=(H, W)), 0, 255)
+    px[..., 0] = 17
+    frame = [np.ascontiguousarray(px.reshape(H, 4 * W))]
+    cfg4 = oracle.configure(W, H, "bgr0", level=4, slices=4, coder=1, experimental=True)
+    enc = oracle.Encoder(cfg4)
+    pk4 = enc.encode(frame)
+    _lossless(cfg4, enc.extradata(), [pk4], [frame])
+    cfg3 = oracle.configure(W, H, "bgr0", level=3, slices=4, coder=1)
+    pk3 = oracle.Encoder(cfg3).encode(frame)
+    assert len(pk4[0]) < len(pk3[0])  # the better transform codes smaller
+
+
+def test_v4_pcm_fallback():
+    """Slices two rows high in a 370-400 wide gbrp14 frame of noise run out
+    of their 1/6 of the 12-bytes-per-pixel packet partway (the 35 * w check)
+    and are coded again as PCM; slice 0 owns the whole packet and never
+    does.  The PCM stream decodes losslessly."""
+    rng = np.random.default_rng(1)
+    cfg = oracle.configure(376, 4, "gbrp14", level=4, slices=6, coder=1, gop_size=2, experimental=True)
+    frames = [[np.ascontiguousarray(rng.integers(0, 1 << 14, size=s).astype(np.uint16))
+               for s in oracle.plane_shapes(cfg)] for _ in range(3)]
+    enc = oracle.Encoder(cfg)
+    pkts, modes = [], []
+    for f in frames:
+        pkts.append(enc.encode(f))
+        modes.append(enc.last_slice_pcm())
+    assert all(m == [0, 1, 1, 1, 1, 1] for m in modes)
+    _lossless(cfg, enc.extradata(), pkts, frames)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stream", V4_STREAMS, ids=IDS)
+def test_hip_v4_matches_oracle(stream):
+    """HIP (RCT coefficients chosen on the device per frame and slice, the
+    slice header taking them) against the oracle, batch of 3."""
+    from test_gpu_parity import hip_encode
+    frames = list(stream.frames())
+    _, ex_ref, ref = oracle_encode(stream, frames)
+    ex, got = hip_encode(stream, frames, batch=3)
+    assert ex == ex_ref
+    for i, (g, r) in enumerate(zip(got, ref)):
+        assert g == r, f"frame {i}"
+
+
+@pytest.mark.gpu
+def test_hip_v4_refuses_the_pcm_path():
+    """Where the reference would re-code slices as PCM the HIP encoder
+    returns an error instead of other bytes."""
+    from ffv1hip import FFV1Error, HipEncoder, configure
+    rng = np.random.default_rng(1)
+    p = configure(376, 4, "gbrp14", slices=6, level=4, coder=1, gop_size=2, experimental=True)
+    frames = [[np.ascontiguousarray(rng.integers(0, 1 << 14, size=s).astype(np.uint16))
+               for s in p.plane_shapes()] for _ in range(2)]
+    enc = HipEncoder(p, 0, 2)
+    with pytest.raises(FFV1Error):
+        enc.encode(frames)
+    enc.close()
