@@ -480,6 +480,7 @@ struct ffv1hip_ctx {
     bool overlap = false;  // two frame sets and two packet sets: batch k+1 stages while batch k codes
     std::unique_ptr<CopyPool> pool;
     hipStream_t xfer = nullptr;
+    hipStream_t d2h = nullptr;  // ffv1hip_encode: packets out beside the next batch's frames in
     static constexpr int kSlots = 6;
     int64_t slot_bytes = 0;
     uint8_t* h_slot[kSlots]{};
@@ -1574,16 +1575,18 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       HIP_TRY(hipMemcpyAsync(h.data(), d_dbg, h.size() * 8, hipMemcpyDeviceToHost, st));
       HIP_TRY(hipStreamSynchronize(st));
       HIP_TRY(hipFree(d_dbg));
-      double all[2] = {0, 0}, loop[2] = {0, 0}, steps[2] = {0, 0};
+      double all[2] = {0, 0}, loop[2] = {0, 0}, steps[2] = {0, 0}, rt[2] = {0, 0};
       for (int b = 0; b < nblk; b++) {  // luma chains are the first half of the grid
         const int gi = b >= nblk / 2;
         all[gi] += double(h[4 * b]);
         loop[gi] += double(h[4 * b + 1]);
         steps[gi] += double(h[4 * b + 2]);
+        rt[gi] += double(h[4 * b + 3]);
       }
       for (int g = 0; g < 2; g++)
-        std::fprintf(stderr, "walkdbg grp %d: blocks %d, memtime per block %.3g, loop share %.3f, memtime/step %.1f\n", g,
-                     nblk / 2, all[g] / (nblk / 2), loop[g] / all[g], loop[g] / steps[g]);
+        std::fprintf(stderr, "walkdbg grp %d: blocks %d, memtime per block %.3g, loop share %.3f, memtime/step %.1f, "
+                     "shader clock %.0f MHz, %.1f ns/step\n", g, nblk / 2, all[g] / (nblk / 2), loop[g] / all[g],
+                     loop[g] / steps[g], all[g] / (rt[g] / 100.0), loop[g] / steps[g] / (all[g] / (rt[g] / 100.0)) * 1e3);
     }
     // the coder stream continues once this batch's walk is done; the walk of
     // the next batch (on st) then overlaps this batch's coding
@@ -1865,6 +1868,7 @@ static int pipe_open(ffv1hip_ctx* c) {
                    double(fset) / 1e9);
   }
   HIP_TRY(hipStreamCreateWithFlags(&P.xfer, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&P.d2h, hipStreamNonBlocking));
   int nt = int(std::thread::hardware_concurrency());
   if (const char* e = std::getenv("OMP_NUM_THREADS"))  // the host's CPU share where it is set
     if (std::atoi(e) > 0) nt = std::min(nt, std::atoi(e));
@@ -1907,6 +1911,7 @@ static void pipe_close(ffv1hip_ctx* c) {
   for (uint8_t* h : P.h_pk)
     if (h) (void)hipHostFree(h);
   if (P.xfer) (void)hipStreamDestroy(P.xfer);
+  if (P.d2h) (void)hipStreamDestroy(P.d2h);
   for (void* q : {(void*)c->d_frames2, (void*)c->d_packets2, (void*)c->d_packet_size2})
     if (q) (void)hipFree(q);
 }
@@ -1972,40 +1977,49 @@ static int launch_staged(ffv1hip_ctx* c, int set, int n) {
   return run_batch(c, set ? c->d_frames2 : c->d_frames, c->frame_bytes, off, pst, n, c->pipe.xfer);
 }
 
-// Batch b's packets (its slice budget settled first) into the pinned buffer
-// of its packet set: sizes, offsets and the buffer out.
-static int collect(ffv1hip_ctx* c, int64_t b, std::vector<int64_t>& sz, std::vector<int64_t>& off,
-                   const uint8_t** data) {
-  int rc = settle_batch(c, b);
-  if (rc < 0) return rc;
+// A settled batch's packets (n of them, packet set pk) into the pinned
+// buffer of that set, on `st`: sizes, offsets and the buffer out.  Only
+// reads the context's buffers, so the copy-out thread of ffv1hip_encode
+// runs it beside the main thread's staging.
+static int copy_packets(ffv1hip_ctx* c, int n, int pk, hipStream_t st, std::vector<int64_t>& sz,
+                        std::vector<int64_t>& off, const uint8_t** data) {
   ffv1hip_ctx::HostPipe& P = c->pipe;
-  const ffv1hip_ctx::LastBatch& L = c->hist[b & 1];
-  const int n = L.n;
   sz.resize(n);
   off.resize(n);
-  HIP_TRY(hipEventSynchronize(c->hist_done[b & 1]));
-  HIP_TRY(hipMemcpy(sz.data(), c->psize(L.pk), sizeof(int64_t) * n, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpyAsync(sz.data(), c->psize(pk), sizeof(int64_t) * n, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
   int64_t total = 0;
   for (int i = 0; i < n; i++) {
     off[i] = total;
     total += sz[i];
   }
-  if (total > P.h_pk_cap[L.pk]) {
-    if (P.h_pk[L.pk]) HIP_TRY(hipHostFree(P.h_pk[L.pk]));
-    P.h_pk[L.pk] = nullptr;
-    P.h_pk_cap[L.pk] = 0;
+  if (total > P.h_pk_cap[pk]) {
+    if (P.h_pk[pk]) HIP_TRY(hipHostFree(P.h_pk[pk]));
+    P.h_pk[pk] = nullptr;
+    P.h_pk_cap[pk] = 0;
     const int64_t cap = (total + total / 4 + (int64_t(1) << 20)) & ~int64_t(4095);
-    HIP_TRY(hipHostMalloc(&P.h_pk[L.pk], size_t(cap), hipHostMallocDefault));
-    P.h_pk_cap[L.pk] = cap;
+    HIP_TRY(hipHostMalloc(&P.h_pk[pk], size_t(cap), hipHostMallocDefault));
+    P.h_pk_cap[pk] = cap;
   }
-  uint8_t* const h = P.h_pk[L.pk];
-  const uint8_t* const d = c->pkts(L.pk);
+  uint8_t* const h = P.h_pk[pk];
+  const uint8_t* const d = c->pkts(pk);
   for (int i = 0; i < n; i++)
     if (sz[i]) HIP_TRY(hipMemcpyAsync(h + off[i], d + int64_t(i) * c->packet_stride, size_t(sz[i]),
-                                      hipMemcpyDeviceToHost, P.xfer));
-  HIP_TRY(hipStreamSynchronize(P.xfer));
+                                      hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
   *data = h;
   return 0;
+}
+
+// Batch b's packets (its slice budget settled first) into the pinned buffer
+// of its packet set.
+static int collect(ffv1hip_ctx* c, int64_t b, std::vector<int64_t>& sz, std::vector<int64_t>& off,
+                   const uint8_t** data) {
+  int rc = settle_batch(c, b);
+  if (rc < 0) return rc;
+  HIP_TRY(hipEventSynchronize(c->hist_done[b & 1]));
+  const ffv1hip_ctx::LastBatch& L = c->hist[b & 1];
+  return copy_packets(c, L.n, L.pk, c->pipe.xfer, sz, off, data);
 }
 
 int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides, int n_frames,
@@ -2018,46 +2032,79 @@ int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides
   if (rc < 0) return rc;
   ffv1hip_ctx::HostPipe& P = c->pipe;
   int64_t used = 0;
-  // batch b's packets out, frames base.. of this call
-  auto finish = [&](int64_t b, int base) -> int {
+  // A settled batch's packets out, frames base.. of this call: sizes and
+  // packets over PCIe on the d2h stream, then into `out`.  With two sets it
+  // runs on a thread of its own while this one stages the next batch (the
+  // two PCIe directions at once); the threads go in batch order.
+  struct Out {
+    std::thread th;
+    int rc = 0;
+    std::string err;
+  } ot;
+  auto copy_out = [&, c](int n, int pk, std::vector<int> keys, int base) {
     std::vector<int64_t> sz, off;
     const uint8_t* h = nullptr;
-    int r = collect(c, b, sz, off, &h);
-    if (r < 0) return r;
-    int64_t total = 0;
-    for (int64_t v : sz) total += v;
-    if (out) {
-      if (used + total > out_cap) return set_err(-22, "output buffer too small");
-      pool_copy2d(*P.pool, out + used, total, h, total, total, 1);
+    int r = copy_packets(c, n, pk, P.d2h, sz, off, &h);
+    if (r >= 0) {
+      int64_t total = 0;
+      for (int64_t v : sz) total += v;
+      if (out && used + total > out_cap) {
+        r = set_err(-22, "output buffer too small");
+      } else {
+        if (out) std::memcpy(out + used, h, size_t(total));
+        for (int i = 0; i < n; i++) {
+          if (sizes) sizes[base + i] = sz[i];
+          if (key_flags) key_flags[base + i] = keys[i];
+        }
+        used += total;
+      }
     }
-    const std::vector<int>& keys = c->hist[b & 1].keys;
-    for (size_t i = 0; i < sz.size(); i++) {
-      if (sizes) sizes[base + i] = sz[i];
-      if (key_flags) key_flags[base + i] = keys[i];
+    if (r < 0) {
+      ot.rc = r;
+      ot.err = g_err;
     }
-    used += total;
+  };
+  auto join_out = [&]() -> int {
+    if (ot.th.joinable()) ot.th.join();
+    if (ot.rc < 0) return set_err(ot.rc, "%s", ot.err.c_str());
     return 0;
+  };
+  auto finish = [&](int64_t b, int base, bool async) -> int {
+    int r = settle_batch(c, b);
+    if (r < 0) return r;
+    HIP_TRY(hipEventSynchronize(c->hist_done[b & 1]));
+    const ffv1hip_ctx::LastBatch& L = c->hist[b & 1];
+    if ((r = join_out()) < 0) return r;
+    if (async)
+      ot.th = std::thread(copy_out, L.n, L.pk, L.keys, base);
+    else
+      copy_out(L.n, L.pk, L.keys, base);
+    return ot.rc < 0 ? set_err(ot.rc, "%s", ot.err.c_str()) : 0;
   };
   int64_t prev = -1;
   int prev_base = 0;
   const int fstep = input_planes(c->P) == 4 ? FFV1HIP_PLANES_YUVA : FFV1HIP_PLANES;  // plane pointers per frame
   for (int j = 0, base = 0; base < n_frames; j++, base += c->max_batch) {
     const int n = std::min(c->max_batch, n_frames - base);
-    // set j % 2 was last read by batch j - 2, collected in iteration j - 1
+    // set j % 2 was last read by batch j - 2, settled in iteration j - 1
     const int set = P.overlap ? (j & 1) : 0;
-    for (int i = 0; i < n; i++)
-      if ((rc = stage_frame(c, set, i, planes + fstep * (base + i), strides + fstep * (base + i))) < 0) return rc;
-    if ((rc = launch_staged(c, set, n)) < 0) return rc;
-    if (!P.overlap) {
-      if ((rc = finish(c->nsub - 1, base)) < 0) return rc;
-      continue;
+    for (int i = 0; i < n && rc >= 0; i++)
+      rc = stage_frame(c, set, i, planes + fstep * (base + i), strides + fstep * (base + i));
+    // batch j's packets go where batch j - 2's were: those are out first
+    if (rc >= 0) rc = join_out();
+    if (rc >= 0) rc = launch_staged(c, set, n);
+    if (rc >= 0 && !P.overlap) rc = finish(c->nsub - 1, base, false);
+    if (rc >= 0 && P.overlap && prev >= 0) rc = finish(prev, prev_base, true);
+    if (rc < 0) {
+      (void)join_out();
+      return rc;
     }
-    if (prev >= 0 && (rc = finish(prev, prev_base)) < 0) return rc;
     prev = c->nsub - 1;
     prev_base = base;
   }
-  if (prev >= 0 && (rc = finish(prev, prev_base)) < 0) return rc;
-  return 0;
+  if (P.overlap && prev >= 0) rc = finish(prev, prev_base, false);
+  const int jr = join_out();
+  return rc < 0 ? rc : jr;
 }
 
 int ffv1hip_encode2_delay(ffv1hip_ctx* c) {

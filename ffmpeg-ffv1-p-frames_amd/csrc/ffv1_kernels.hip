@@ -938,7 +938,9 @@ __device__ __forceinline__ StreamRef stream_of(const CodeArgs& a, int64_t c) {
 }
 
 constexpr int kRangeThreads = kWave;
+template <bool FAT>
 __global__ __launch_bounds__(kRangeThreads) void ffv1_range(CodeArgs a) {
+  if constexpr (FAT) asm volatile("" ::: "v255", "a255");  // a SIMD to itself (see ffv1_walk)
   const StreamRef sr = stream_of(a, (int64_t)blockIdx.x * kRangeThreads + threadIdx.x);
   const int key = sr.live ? a.keyflags[sr.f] : 0;
   const HdrState h = a.hdr[key * a.nslices + sr.slice];
@@ -1470,7 +1472,12 @@ __device__ __forceinline__ uint4 pick(bool c, uint4 a, uint4 b) {
 }
 
 
+// FAT: the wave takes the whole register file of its SIMD (256 VGPRs + 256
+// AGPRs), so no other wave is placed on that SIMD: the coder's waves go to
+// the SIMDs the walk leaves free instead of sharing a walk wave's issue.
+template <bool FAT>
 __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
+  if constexpr (FAT) asm volatile("" ::: "v255", "a255");
   __shared__ __attribute__((aligned(16))) uint8_t fixed[kLdsFixed];
   extern __shared__ __attribute__((aligned(16))) uint8_t tbl[];  // [2][contexts + 1 dummy row][32]
   const int64_t half = a.state_bytes / 2;  // one plane group's [contexts][32]
@@ -1576,6 +1583,7 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   }
   uint64_t t_loop = 0, n_steps = 0;
   const uint64_t t_all = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+  const uint64_t rt_all = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz: the wave's shader clock
   for (int j = 0; j < seg.nframes; j++) {
     const int f = seg.first_frame + j;
     const int64_t sid = (int64_t)f * a.nslices + (live ? sl : 0);
@@ -1724,6 +1732,7 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
     a.dbg[item * 4 + 0] = __builtin_amdgcn_s_memtime() - t_all;
     a.dbg[item * 4 + 1] = t_loop;
     a.dbg[item * 4 + 2] = n_steps;
+    a.dbg[item * 4 + 3] = __builtin_amdgcn_s_memrealtime() - rt_all;
   }
 }
 
@@ -2348,7 +2357,12 @@ int launch_code(const CodeArgs& a, void* stream) {
 int launch_range(const CodeArgs& a, void* stream) {
   const int64_t streams = (int64_t)a.nframes * a.nslices;
   dim3 grid((unsigned)((streams + kRangeThreads - 1) / kRangeThreads)), block(kRangeThreads);
-  hipLaunchKernelGGL(ffv1_range, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
+  // FFV1HIP_RANGE_FAT=1 (measurement hook): each wave owns its SIMD
+  static const bool fat = std::getenv("FFV1HIP_RANGE_FAT") && std::atoi(std::getenv("FFV1HIP_RANGE_FAT"));
+  if (fat)
+    hipLaunchKernelGGL((ffv1_range<true>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
+  else
+    hipLaunchKernelGGL((ffv1_range<false>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2379,7 +2393,14 @@ int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first, int count
   if (count < 0) count = b.nitems - first;
   if (first < 0 || count <= 0 || first + count > b.nitems) return count == 0 ? 0 : -1;
   b.item0 = first;
-  hipLaunchKernelGGL(ffv1_walk, dim3((unsigned)count), dim3(kWalkThreads), dyn, reinterpret_cast<hipStream_t>(stream), b);
+  // FFV1HIP_WALK_FAT=1 (measurement hook): each wave owns its SIMD
+  static const bool fat = std::getenv("FFV1HIP_WALK_FAT") && std::atoi(std::getenv("FFV1HIP_WALK_FAT"));
+  if (fat)
+    hipLaunchKernelGGL((ffv1_walk<true>), dim3((unsigned)count), dim3(kWalkThreads), dyn,
+                       reinterpret_cast<hipStream_t>(stream), b);
+  else
+    hipLaunchKernelGGL((ffv1_walk<false>), dim3((unsigned)count), dim3(kWalkThreads), dyn,
+                       reinterpret_cast<hipStream_t>(stream), b);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2389,7 +2410,7 @@ int walk_items(int nsegs, int nslices) { return nsegs * ((nslices + 1) / 2) * 2;
 int walk_resident(const WalkArgs& a) {
   const size_t dyn = (size_t)(2 * (a.state_bytes / 2 + 32));
   int per_cu = 0, dev = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ffv1_walk, kWalkThreads, dyn) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ffv1_walk<false>, kWalkThreads, dyn) != hipSuccess ||
       hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
     (void)hipGetLastError();
     return 0;

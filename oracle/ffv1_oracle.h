@@ -19,7 +19,7 @@
  *   - slice CRC                  libavutil/crc.c:310-380 (AV_CRC_32_IEEE)
  *   - decoder (round trips)      libavcodec/ffv1dec.c:42-474, 638-1021
  *
- * Pinning: see oracle/README.md and tests/golden/ -- the restatement is
+ * Pinning: see DESIGN.md ("Oracle and parity") and tests/golden/ -- the restatement is
  * checked against the known-answer MD5s recorded from the reference encoder
  *  and against the reference FATE goldens.
  */
