@@ -465,6 +465,7 @@ def main():
             "decode_selfcheck": decode,
         }
         print(json.dumps(res), flush=True)
+    enc.close()
     if dist:
         dist.destroy_process_group()
     if (vs_oracle and not vs_oracle["equal"]) or bitexact is False:

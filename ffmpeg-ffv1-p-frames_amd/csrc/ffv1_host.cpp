@@ -10,6 +10,7 @@
 #include <cstring>
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -104,6 +105,10 @@ class CopyPool {
   int pending_ = 0;
   bool stop_ = false;
 };
+
+double wall_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 // rows of wb bytes from src (pitch sp) to dst (pitch dp), split over the pool
 void pool_copy2d(CopyPool& pool, uint8_t* dst, int64_t dp, const uint8_t* src, int64_t sp, int64_t wb, int64_t rows) {
@@ -407,6 +412,7 @@ struct ffv1hip_ctx {
   hipEvent_t entry[2] = {nullptr, nullptr};  // set k's batch: the launch stream's work so far
   hipEvent_t walk_a = nullptr;               // the first part of the last batch's walk is done
   bool walk_a_valid = false;
+  std::vector<uint32_t> cu_walk, cu_side;  // FFV1HIP_RESERVE_CUS: CU masks of the walk's and the side streams
   SliceGeom* d_geom = nullptr;
   int* d_slot_frames = nullptr;  // [j][slot]
   int* d_status = nullptr;       // [set][4]: [0] slices over budget, [1] most bytes one needed
@@ -445,6 +451,14 @@ struct ffv1hip_ctx {
     std::vector<int> keys;
   } hist[2];
   hipEvent_t hist_done[2] = {nullptr, nullptr};  // batch slot k's last kernel
+  // FFV1HIP_WALKTRACE=1 (measurement hook): every walk wave's start and end
+  // (s_memrealtime, 100 MHz) for up to kTraceBatches batches, kept on the
+  // device and summarised at ffv1hip_destroy: dispatch spread and duration
+  // of each launch part
+  static constexpr int kTraceBatches = 64;
+  uint64_t* d_trace = nullptr;
+  int trace_items = 0, trace_n = 0;
+  std::vector<int> trace_first;  // per traced batch: part A's waves (0: one launch)
   int64_t nsub = 0;                              // batches submitted
   // packet slots: set 0 always; a second set (two_pk) for the host-frame
   // path, so that batch k's packets are copied out while batch k+1 codes
@@ -490,6 +504,14 @@ struct ffv1hip_ctx {
     int64_t fill = 0;
     uint8_t* h_pk[2]{};  // pinned packets of a collected batch, per packet set
     int64_t h_pk_cap[2]{};
+    uint8_t* d_compact[2]{};  // the same, back to back in HBM (one D2H copy)
+    int64_t d_compact_cap[2]{};
+    // FFV1HIP_HOSTDBG=1 (measurement hook): where ffv1hip_encode's host time
+    // goes, seconds: waiting for a staging slot, copying into slots, issuing
+    // their DMA, waiting for the copy-out thread, settling a batch, and in
+    // the copy-out: packets over PCIe, into the caller's buffer
+    bool dbg = false;
+    double t_slot = 0, t_copy = 0, t_dma = 0, t_join = 0, t_settle = 0, t_d2h = 0, t_out = 0;
   } pipe;
   uint8_t* d_frames2 = nullptr;
   // encode2 with the pipe: the set being filled and the launched batches
@@ -822,7 +844,53 @@ static int upload_hdr(ffv1hip_ctx* c) {
 
 static void pipe_close(ffv1hip_ctx* c);
 
+// FFV1HIP_WALKTRACE: per traced batch and launch part, when its waves
+// started (spread from the batch's first), how long they ran, when the
+// last ended (ms).
+static void dump_walk_trace(ffv1hip_ctx* c) {
+  if (!c->d_trace || !c->trace_n) return;
+  std::vector<uint64_t> t(size_t(2) * c->trace_items * c->trace_n);
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(t.data(), c->d_trace, t.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return;
+  uint64_t prev_end = 0;
+  for (int b = 0; b < c->trace_n; b++) {
+    const uint64_t* w = t.data() + size_t(2) * c->trace_items * b;
+    int n = 0;
+    while (n < c->trace_items && w[2 * n]) n++;
+    if (!n) continue;
+    uint64_t t0 = ~0ull;
+    for (int i = 0; i < n; i++) t0 = std::min(t0, w[2 * i]);
+    const int first = c->trace_first[b] ? c->trace_first[b] : n;
+    for (int part = 0; part < 2; part++) {
+      const int lo = part ? first : 0, hi = part ? n : first;
+      if (lo >= hi) continue;
+      uint64_t s0 = ~0ull, s1 = 0, e1 = 0;
+      double dur = 0, dmax = 0;
+      for (int i = lo; i < hi; i++) {
+        s0 = std::min(s0, w[2 * i]);
+        s1 = std::max(s1, w[2 * i]);
+        e1 = std::max(e1, w[2 * i + 1]);
+        const double d = double(w[2 * i + 1] - w[2 * i]) / 1e5;
+        dur += d;
+        dmax = std::max(dmax, d);
+      }
+      std::fprintf(stderr, "walktrace batch %d part %c: %d waves, start %.2f..%.2f ms, run mean %.2f max %.2f ms, "
+                           "end %.2f ms%s\n", b, part ? 'B' : 'A', hi - lo, double(s0 - t0) / 1e5,
+                   double(s1 - t0) / 1e5, dur / (hi - lo), dmax, double(e1 - t0) / 1e5,
+                   part == 0 && prev_end ? "" : "");
+    }
+    if (prev_end)
+      std::fprintf(stderr, "walktrace batch %d: starts %.2f ms after batch %d's last wave ended\n", b,
+                   (double(t0) - double(prev_end)) / 1e5, b - 1);
+    prev_end = 0;
+    for (int i = 0; i < n; i++) prev_end = std::max(prev_end, w[2 * i + 1]);
+  }
+}
+
 static void free_device(ffv1hip_ctx* c) {
+  dump_walk_trace(c);
+  if (c->d_trace) (void)hipFree(c->d_trace);
   pipe_close(c);
   void* ptrs[] = {c->d_frames, c->d_qt, c->d_tabs, c->d_ops, c->d_nops, c->d_segs, c->d_keys,
                   c->d_slice_out, c->d_slice_bytes, c->d_packets, c->d_packet_size, c->d_persist[0],
@@ -938,7 +1006,29 @@ static int alloc_device(ffv1hip_ctx* c) {
                      (long long)fit);
     }
   }
-  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  // FFV1HIP_RESERVE_CUS=R: R CUs, spread over the chip (every ncu / R-th),
+  // run the next batch's symbols, layout and bits (bits_stream), the other
+  // CUs the states walk (stream); the coder's stream may use all.  The walk
+  // then never shares a CU's LDS with the symbols kernel, and the symbols of
+  // batch k+1 run beside the whole walk of batch k.
+  {
+    static const int reserve = std::getenv("FFV1HIP_RESERVE_CUS") ? std::atoi(std::getenv("FFV1HIP_RESERVE_CUS")) : 0;
+    int ncu = 0;
+    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
+    if (reserve > 0 && reserve < ncu) {
+      c->cu_walk.assign((ncu + 31) / 32, 0u);
+      c->cu_side.assign((ncu + 31) / 32, 0u);
+      const int every = std::max(1, ncu / reserve);
+      for (int i = 0; i < ncu; i++) {
+        const bool side = i % every == every - 1 && i / every < reserve;
+        (side ? c->cu_side : c->cu_walk)[i / 32] |= 1u << (i % 32);
+      }
+    }
+  }
+  if (!c->cu_walk.empty())
+    HIP_TRY(hipExtStreamCreateWithCUMask(&c->stream, uint32_t(c->cu_walk.size() * 32), c->cu_walk.data()));
+  else
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   for (hipEvent_t& e : c->hist_done) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_TRY(hipMalloc(&c->d_qt, sizeof(c->qt)));
   HIP_TRY(hipMemcpy(c->d_qt, c->qt, sizeof(c->qt), hipMemcpyHostToDevice));
@@ -988,7 +1078,10 @@ static int alloc_device(ffv1hip_ctx* c) {
       HIP_TRY(hipMemcpy(c->d_ident, ident.data(), sizeof(int) * size_t(nb), hipMemcpyHostToDevice));
     }
     HIP_TRY(hipStreamCreateWithFlags(&c->code_stream, hipStreamNonBlocking));
-    HIP_TRY(hipStreamCreateWithFlags(&c->bits_stream, hipStreamNonBlocking));
+    if (!c->cu_side.empty())
+      HIP_TRY(hipExtStreamCreateWithCUMask(&c->bits_stream, uint32_t(c->cu_side.size() * 32), c->cu_side.data()));
+    else
+      HIP_TRY(hipStreamCreateWithFlags(&c->bits_stream, hipStreamNonBlocking));
     for (hipEvent_t& e : c->laid) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->bitsed) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->walked) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1341,7 +1434,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     // FFV1HIP_SYM_DELAY_US)
     HIP_TRY(hipStreamWaitEvent(sst, c->walked[fb], 0));
     HIP_TRY(hipStreamWaitEvent(sst, c->coded3[t3], 0));
-    if (c->walk_a_valid) {
+    if (c->walk_a_valid && c->cu_side.empty()) {
       HIP_TRY(hipStreamWaitEvent(sst, c->walk_a, 0));
       static const int delay_us =
           std::getenv("FFV1HIP_SYM_DELAY_US") ? std::atoi(std::getenv("FFV1HIP_SYM_DELAY_US")) : 1000;
@@ -1528,6 +1621,16 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     static const int walk_prio = std::getenv("FFV1HIP_WALK_PRIO") ? std::atoi(std::getenv("FFV1HIP_WALK_PRIO")) : 2;
     wa.prio = walk_prio;
     wa.init = c->d_init;
+    static const bool walktrace = std::getenv("FFV1HIP_WALKTRACE") && std::atoi(std::getenv("FFV1HIP_WALKTRACE"));
+    if (walktrace && c->trace_n < ffv1hip_ctx::kTraceBatches) {
+      const int items = walk_items(nsegs, c->nslices);
+      if (!c->d_trace) {
+        c->trace_items = walk_items(c->max_slots, c->nslices);
+        HIP_TRY(hipMalloc(&c->d_trace, sizeof(uint64_t) * 2 * c->trace_items * ffv1hip_ctx::kTraceBatches));
+        HIP_TRY(hipMemset(c->d_trace, 0, sizeof(uint64_t) * 2 * c->trace_items * ffv1hip_ctx::kTraceBatches));
+      }
+      if (items <= c->trace_items) wa.trace = c->d_trace + size_t(2) * c->trace_items * c->trace_n;
+    }
     // FFV1HIP_WALKDBG=1 (measurement hook): per-block cycle split to stderr
     static const bool walkdbg = std::getenv("FFV1HIP_WALKDBG") && std::atoi(std::getenv("FFV1HIP_WALKDBG"));
     uint64_t* d_dbg = nullptr;
@@ -1543,7 +1646,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     const int nitems = walk_items(nsegs, c->nslices);
     // FFV1HIP_WALK_PART_A (test hook, read per batch): the first part's waves
     const char* pa = std::getenv("FFV1HIP_WALK_PART_A");
-    const int first = sst != st && split_env ? (pa ? std::atoi(pa) : walk_resident(wa)) : 0;
+    const int first = sst != st && split_env && c->cu_side.empty() ? (pa ? std::atoi(pa) : walk_resident(wa)) : 0;
     // ... and only when the second part leaves room on the CUs for the
     // symbols beside it (c3: 576 of 768 slots; c5's 768 of 768 ran slower)
     // (FFV1HIP_SPLIT_MAX: that share in percent, default 80)
@@ -1557,6 +1660,10 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
         }) < 0)
       return set_err(-5, "walk launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (!two_parts) HIP_TRY(hipEventRecord(c->walk_a, st));
+    if (wa.trace) {
+      c->trace_first.push_back(two_parts ? first : 0);
+      c->trace_n++;
+    }
     c->walk_a_valid = sst != st;
     StatsArgs sta{};
     if (c->pass == 1) {  // slot counts from the records, before the next batch's symbols rewrite them
@@ -1874,6 +1981,7 @@ static int pipe_open(ffv1hip_ctx* c) {
     if (std::atoi(e) > 0) nt = std::min(nt, std::atoi(e));
   if (const char* e = std::getenv("FFV1HIP_COPY_THREADS")) nt = std::atoi(e);
   P.pool = std::make_unique<CopyPool>(std::max(1, std::min(nt, 16)));
+  P.dbg = std::getenv("FFV1HIP_HOSTDBG") && std::atoi(std::getenv("FFV1HIP_HOSTDBG"));
   P.slot_bytes = std::max<int64_t>(int64_t(32) << 20, int64_t(c->P.width) * 4);
   for (int k = 0; k < ffv1hip_ctx::HostPipe::kSlots; k++) {
     HIP_TRY(hipHostMalloc(&P.h_slot[k], size_t(P.slot_bytes), hipHostMallocDefault));
@@ -1910,6 +2018,8 @@ static void pipe_close(ffv1hip_ctx* c) {
   }
   for (uint8_t* h : P.h_pk)
     if (h) (void)hipHostFree(h);
+  for (uint8_t* d : P.d_compact)
+    if (d) (void)hipFree(d);
   if (P.xfer) (void)hipStreamDestroy(P.xfer);
   if (P.d2h) (void)hipStreamDestroy(P.d2h);
   for (void* q : {(void*)c->d_frames2, (void*)c->d_packets2, (void*)c->d_packet_size2})
@@ -1939,14 +2049,23 @@ static int stage_rows(ffv1hip_ctx* c, uint8_t* dst, const uint8_t* src, int64_t 
       const int rc = stage_flush(c);
       if (rc < 0) return rc;
     }
+    double t0 = P.dbg ? wall_s() : 0;
     if (P.fill == 0 && P.slot_busy[P.next]) {
       HIP_TRY(hipEventSynchronize(P.slot_ev[P.next]));
       P.slot_busy[P.next] = false;
     }
     const int64_t nr = std::min(rows - r, (P.slot_bytes - P.fill) / wb);
     uint8_t* const h = P.h_slot[P.next] + P.fill;
+    double t1 = P.dbg ? wall_s() : 0;
     pool_copy2d(*P.pool, h, wb, src + r * sp, sp, wb, nr);
+    double t2 = P.dbg ? wall_s() : 0;
     HIP_TRY(hipMemcpyAsync(dst + r * wb, h, size_t(nr * wb), hipMemcpyHostToDevice, P.xfer));
+    if (P.dbg) {
+      const double t3 = wall_s();
+      P.t_slot += t1 - t0;
+      P.t_copy += t2 - t1;
+      P.t_dma += t3 - t2;
+    }
     P.fill += nr * wb;
     r += nr;
   }
@@ -2003,9 +2122,28 @@ static int copy_packets(ffv1hip_ctx* c, int n, int pk, hipStream_t st, std::vect
   }
   uint8_t* const h = P.h_pk[pk];
   const uint8_t* const d = c->pkts(pk);
-  for (int i = 0; i < n; i++)
-    if (sz[i]) HIP_TRY(hipMemcpyAsync(h + off[i], d + int64_t(i) * c->packet_stride, size_t(sz[i]),
-                                      hipMemcpyDeviceToHost, st));
+  // one D2H copy of the packets packed back to back on the device (a copy
+  // per packet runs at a few GB/s); per packet when the packed buffer does
+  // not fit
+  if (total > P.d_compact_cap[pk]) {
+    if (P.d_compact[pk]) HIP_TRY(hipFree(P.d_compact[pk]));
+    P.d_compact[pk] = nullptr;
+    P.d_compact_cap[pk] = 0;
+    const int64_t cap = (total + total / 4 + (int64_t(1) << 20)) & ~int64_t(4095);
+    if (hipMalloc(&P.d_compact[pk], size_t(cap)) == hipSuccess)
+      P.d_compact_cap[pk] = cap;
+    else
+      (void)hipGetLastError();
+  }
+  if (total <= P.d_compact_cap[pk]) {
+    if (launch_compact_packets(d, c->packet_stride, c->psize(pk), n, P.d_compact[pk], st) < 0)
+      return set_err(-5, "compact launch failed");
+    if (total) HIP_TRY(hipMemcpyAsync(h, P.d_compact[pk], size_t(total), hipMemcpyDeviceToHost, st));
+  } else {
+    for (int i = 0; i < n; i++)
+      if (sz[i]) HIP_TRY(hipMemcpyAsync(h + off[i], d + int64_t(i) * c->packet_stride, size_t(sz[i]),
+                                        hipMemcpyDeviceToHost, st));
+  }
   HIP_TRY(hipStreamSynchronize(st));
   *data = h;
   return 0;
@@ -2044,7 +2182,10 @@ int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides
   auto copy_out = [&, c](int n, int pk, std::vector<int> keys, int base) {
     std::vector<int64_t> sz, off;
     const uint8_t* h = nullptr;
+    const double t0 = wall_s();
     int r = copy_packets(c, n, pk, P.d2h, sz, off, &h);
+    const double t1 = wall_s();
+    P.t_d2h += t1 - t0;
     if (r >= 0) {
       int64_t total = 0;
       for (int64_t v : sz) total += v;
@@ -2052,6 +2193,7 @@ int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides
         r = set_err(-22, "output buffer too small");
       } else {
         if (out) std::memcpy(out + used, h, size_t(total));
+        P.t_out += wall_s() - t1;
         for (int i = 0; i < n; i++) {
           if (sizes) sizes[base + i] = sz[i];
           if (key_flags) key_flags[base + i] = keys[i];
@@ -2065,14 +2207,18 @@ int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides
     }
   };
   auto join_out = [&]() -> int {
+    const double t0 = wall_s();
     if (ot.th.joinable()) ot.th.join();
+    P.t_join += wall_s() - t0;
     if (ot.rc < 0) return set_err(ot.rc, "%s", ot.err.c_str());
     return 0;
   };
   auto finish = [&](int64_t b, int base, bool async) -> int {
+    const double t0 = wall_s();
     int r = settle_batch(c, b);
     if (r < 0) return r;
     HIP_TRY(hipEventSynchronize(c->hist_done[b & 1]));
+    P.t_settle += wall_s() - t0;
     const ffv1hip_ctx::LastBatch& L = c->hist[b & 1];
     if ((r = join_out()) < 0) return r;
     if (async)
@@ -2084,6 +2230,8 @@ int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides
   int64_t prev = -1;
   int prev_base = 0;
   const int fstep = input_planes(c->P) == 4 ? FFV1HIP_PLANES_YUVA : FFV1HIP_PLANES;  // plane pointers per frame
+  // FFV1HIP_COPYOUT_SYNC=1 (measurement hook): the copy-out on this thread
+  static const bool sync_out = std::getenv("FFV1HIP_COPYOUT_SYNC") && std::atoi(std::getenv("FFV1HIP_COPYOUT_SYNC"));
   for (int j = 0, base = 0; base < n_frames; j++, base += c->max_batch) {
     const int n = std::min(c->max_batch, n_frames - base);
     // set j % 2 was last read by batch j - 2, settled in iteration j - 1
@@ -2094,7 +2242,7 @@ int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides
     if (rc >= 0) rc = join_out();
     if (rc >= 0) rc = launch_staged(c, set, n);
     if (rc >= 0 && !P.overlap) rc = finish(c->nsub - 1, base, false);
-    if (rc >= 0 && P.overlap && prev >= 0) rc = finish(prev, prev_base, true);
+    if (rc >= 0 && P.overlap && prev >= 0) rc = finish(prev, prev_base, !sync_out);
     if (rc < 0) {
       (void)join_out();
       return rc;
@@ -2104,6 +2252,10 @@ int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides
   }
   if (P.overlap && prev >= 0) rc = finish(prev, prev_base, false);
   const int jr = join_out();
+  if (P.dbg)
+    std::fprintf(stderr, "hostdbg: %d frames, %d copy threads: slot wait %.3f s, copy in %.3f s, DMA issue %.3f s, "
+                         "copy-out wait %.3f s, settle %.3f s; copy-out: D2H %.3f s, into the buffer %.3f s\n",
+                 n_frames, P.pool->size(), P.t_slot, P.t_copy, P.t_dma, P.t_join, P.t_settle, P.t_d2h, P.t_out);
   return rc < 0 ? rc : jr;
 }
 

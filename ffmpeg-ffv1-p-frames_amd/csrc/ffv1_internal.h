@@ -239,6 +239,7 @@ struct WalkArgs {
   DecisionStream ds;
   uint8_t* scratch;           // >= 2 KiB: where idle chains write their stage
   uint64_t* dbg;              // optional [block][4] cycle counters (FFV1HIP_WALKDBG)
+  uint64_t* trace;            // optional [item][2] start / end s_memrealtime of each wave (FFV1HIP_WALKTRACE)
   int force_multi;            // measurement hook: every chunk on the checked (multi) step
   const uint8_t* init;        // 2-pass initial states [contexts][32] at keyframes, or null (all 128)
   int nitems, item0;          // set by launch_walk: all items of the batch, the launch's first
@@ -334,5 +335,7 @@ constexpr int64_t kWalkLdsMax = 64 * 1024;  // states walk: one plane group's ta
 constexpr int kStreamAlign = 64;            // decisions: every stream starts at a multiple
 int launch_code_golomb(const CodeArgs& a, void* stream);
 int launch_assemble(const AssembleArgs& a, int nframes, void* stream);
+int launch_compact_packets(const uint8_t* packets, int64_t stride, const int64_t* sizes, int n, uint8_t* out,
+                           void* stream);
 
 }  // namespace ffv1hip

@@ -1583,7 +1583,7 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   }
   uint64_t t_loop = 0, n_steps = 0;
   const uint64_t t_all = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
-  const uint64_t rt_all = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz: the wave's shader clock
+  const uint64_t rt_all = a.dbg || a.trace ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz: the wave's shader clock
   for (int j = 0; j < seg.nframes; j++) {
     const int f = seg.first_frame + j;
     const int64_t sid = (int64_t)f * a.nslices + (live ? sl : 0);
@@ -1727,6 +1727,10 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
     uint4* dst = reinterpret_cast<uint4*>(a.persist_out + (int64_t)sl * a.state_bytes + goff);
     const uint4* t4 = reinterpret_cast<const uint4*>(mytbl);
     for (int64_t i = k; i < n16; i += 32) dst[i] = t4[i];
+  }
+  if (a.trace && lane == 0) {
+    a.trace[item * 2 + 0] = rt_all;
+    a.trace[item * 2 + 1] = __builtin_amdgcn_s_memrealtime();
   }
   if (a.dbg && lane == 0) {
     a.dbg[item * 4 + 0] = __builtin_amdgcn_s_memtime() - t_all;
@@ -2464,6 +2468,42 @@ int launch_code_golomb(const CodeArgs& a, void* stream) {
   const int64_t chains = (int64_t)a.nsegs * a.nslices;
   dim3 grid((unsigned)((chains + kCodeThreads - 1) / kCodeThreads)), block(kCodeThreads);
   hipLaunchKernelGGL(ffv1_code_golomb, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+namespace {
+// The host-frame path's packets, back to back for one D2H copy: block i
+// sums the sizes before packet i and copies packet i there (16-byte loads
+// from its aligned slot, byte stores to the unaligned place).
+constexpr int kCompactThreads = 256;
+__global__ __launch_bounds__(kCompactThreads) void ffv1_compact_packets(const uint8_t* packets, int64_t stride,
+                                                                         const int64_t* sizes, int n, uint8_t* out) {
+  __shared__ int64_t part[kCompactThreads];
+  const int i = blockIdx.x;
+  int64_t s = 0;
+  for (int k = threadIdx.x; k < i; k += kCompactThreads) s += sizes[k];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = kCompactThreads / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  const int64_t off = part[0], sz = sizes[i];
+  const uint4* src = reinterpret_cast<const uint4*>(packets + (int64_t)i * stride);
+  uint8_t* dst = out + off;
+  for (int64_t k = threadIdx.x; k * 16 < sz; k += kCompactThreads) {
+    const uint4 v = src[k];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (int b = 0; b < 16 && k * 16 + b < sz; b++) dst[k * 16 + b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+  }
+}
+}  // namespace
+
+int launch_compact_packets(const uint8_t* packets, int64_t stride, const int64_t* sizes, int n, uint8_t* out,
+                           void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(ffv1_compact_packets, dim3(n), dim3(kCompactThreads), 0, reinterpret_cast<hipStream_t>(stream),
+                     packets, stride, sizes, n, out);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -30,3 +30,21 @@ with torch.cuda.stream(s2):
 torch.cuda.synchronize()
 both = 2 * n / (time.perf_counter() - t) / 1e9
 print(f"pinned H2D {h2d:.1f} GB/s, D2H {d2h:.1f} GB/s, both directions at once {both:.1f} GB/s total")
+
+# host side of the staging: pageable -> pinned copies, 1 and 16 threads
+import threading
+import numpy as np
+src = np.random.default_rng(0).integers(0, 255, size=n, dtype=np.uint8)
+dst = h.numpy()
+for nt in (1, 4, 16):
+    per = n // nt
+    def work(i):
+        dst[i * per:(i + 1) * per] = src[i * per:(i + 1) * per]
+    work(0)
+    t = time.perf_counter()
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(nt)]
+    for x in ths:
+        x.start()
+    for x in ths:
+        x.join()
+    print(f"pageable -> pinned memcpy, {nt} threads: {n / (time.perf_counter() - t) / 1e9:.1f} GB/s")
