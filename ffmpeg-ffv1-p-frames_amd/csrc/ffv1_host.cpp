@@ -360,7 +360,7 @@ struct ffv1hip_ctx {
   uint8_t* d_persist[2] = {nullptr, nullptr};
   int pcur = 0;
   uint8_t* d_tables = nullptr;   // [slot][slice][2][contexts][32]
-  uint32_t* d_sym = nullptr;     // [slot][frame_samples]; frames mode: walk records (uint4), 2 x [batch frame][frame_samples]
+  uint32_t* d_sym = nullptr;     // [slot][frame_samples]; frames mode: walk records (uint2), set 0 of [batch frame][frame_samples]
   // frames mode, two buffer sets: the walk of batch k+1 runs while batch k codes
   uint8_t* d_keys2 = nullptr;    // 3 x [batch frame] keyflags
   uint32_t* d_cbits = nullptr;   // 2 x [batch frame][frame_chunks][kChunkWords] packed decision bits
@@ -406,13 +406,19 @@ struct ffv1hip_ctx {
   // once the first part of batch k's walk is done, beside its second part,
   // instead of in front of the next walk on its stream
   bool two_rec = false;
-  uint4* d_rec2 = nullptr;       // [batch frame][frame_samples] walk records of set 1
+  uint2* d_rec2 = nullptr;       // [batch frame][frame_samples] walk records of set 1
   uint32_t* d_cbits2 = nullptr;  // chunk bits of set 1
   int* d_ident = nullptr;        // [batch frame] i: the frames mode's frame of each slot
   hipEvent_t entry[2] = {nullptr, nullptr};  // set k's batch: the launch stream's work so far
   hipEvent_t walk_a = nullptr;               // the first part of the last batch's walk is done
+  hipEvent_t walk_go = nullptr;              // everything before the last batch's walk is done (it starts)
   bool walk_a_valid = false;
   std::vector<uint32_t> cu_walk, cu_side;  // FFV1HIP_RESERVE_CUS: CU masks of the walk's and the side streams
+  // grid caps of the kernels that run beside the states walk (their blocks
+  // stride over the work): a grid of one block per item fills every SIMD's
+  // wave slots and registers, and walk waves launched meanwhile wait for CU
+  // room until those blocks retire (FFV1HIP_SYM_GRID / _BITS_GRID / _DSEG_GRID)
+  int grid_sym = 3072, grid_bits = 1024, grid_dseg = 3072;
   SliceGeom* d_geom = nullptr;
   int* d_slot_frames = nullptr;  // [j][slot]
   int* d_status = nullptr;       // [set][4]: [0] slices over budget, [1] most bytes one needed
@@ -493,6 +499,7 @@ struct ffv1hip_ctx {
     bool on = false;
     bool overlap = false;  // two frame sets and two packet sets: batch k+1 stages while batch k codes
     std::unique_ptr<CopyPool> pool;
+    std::unique_ptr<CopyPool> pool_out;  // the copy-out thread's: packets into the caller's buffer
     hipStream_t xfer = nullptr;
     hipStream_t d2h = nullptr;  // ffv1hip_encode: packets out beside the next batch's frames in
     static constexpr int kSlots = 6;
@@ -503,6 +510,10 @@ struct ffv1hip_ctx {
     int next = 0;
     int64_t fill = 0;
     uint8_t* h_pk[2]{};  // pinned packets of a collected batch, per packet set
+    int64_t* h_sizes[2]{};   // mapped pinned: a batch's packet sizes, written by a kernel
+    int64_t* hd_sizes[2]{};  // their device-side address
+    int* h_status = nullptr;  // mapped pinned: a batch's slice-budget status (settle_batch)
+    int* hd_status = nullptr;
     int64_t h_pk_cap[2]{};
     uint8_t* d_compact[2]{};  // the same, back to back in HBM (one D2H copy)
     int64_t d_compact_cap[2]{};
@@ -512,6 +523,7 @@ struct ffv1hip_ctx {
     // the copy-out: packets over PCIe, into the caller's buffer
     bool dbg = false;
     double t_slot = 0, t_copy = 0, t_dma = 0, t_join = 0, t_settle = 0, t_d2h = 0, t_out = 0;
+    double t_sizes = 0, t_compact = 0, t_dcopy = 0;  // inside the D2H (FFV1HIP_HOSTDBG)
   } pipe;
   uint8_t* d_frames2 = nullptr;
   // encode2 with the pipe: the set being filled and the launched batches
@@ -925,6 +937,7 @@ static void free_device(ffv1hip_ctx* c) {
   for (hipEvent_t& e : c->entry)
     if (e) (void)hipEventDestroy(e);
   if (c->walk_a) (void)hipEventDestroy(c->walk_a);
+  if (c->walk_go) (void)hipEventDestroy(c->walk_go);
   for (hipEvent_t& e : c->hist_done)
     if (e) (void)hipEventDestroy(e);
 }
@@ -963,7 +976,7 @@ static int64_t device_bytes(const ffv1hip_ctx* c, int64_t nb) {
   int64_t b = nb * (c->slice_stride * c->nslices + c->packet_stride);
   b += 2 * int64_t(c->pcount) * c->contexts * 32 * c->nslices;  // the P-frame carry
   if (c->frames_mode) {
-    b += nb * (16 * c->frame_samples + 4 * int64_t(kChunkWords) * c->frame_chunks);  // walk records, chunk bits
+    b += nb * (8 * c->frame_samples + 4 * int64_t(kChunkWords) * c->frame_chunks);  // walk records, chunk bits
     const int64_t dcap = decision_cap(c, nb);
     b += 2 * (dcap + dcap / 8);                                                      // two decision sets
     int64_t segs = 0, groups = 0;
@@ -1025,6 +1038,15 @@ static int alloc_device(ffv1hip_ctx* c) {
       }
     }
   }
+  {
+    auto knob = [](const char* name, int dflt) {
+      const char* e = std::getenv(name);
+      return e ? std::atoi(e) : dflt;
+    };
+    c->grid_sym = knob("FFV1HIP_SYM_GRID", c->grid_sym);
+    c->grid_bits = knob("FFV1HIP_BITS_GRID", c->grid_bits);
+    c->grid_dseg = std::max(1, knob("FFV1HIP_DSEG_GRID", c->grid_dseg));
+  }
   if (!c->cu_walk.empty())
     HIP_TRY(hipExtStreamCreateWithCUMask(&c->stream, uint32_t(c->cu_walk.size() * 32), c->cu_walk.data()));
   else
@@ -1062,7 +1084,7 @@ static int alloc_device(ffv1hip_ctx* c) {
     // double-buffered: the states walk of batch k+1 runs while batch k codes
     // the walk records and chunk bits: one set (the next batch's symbols run
     // after this batch's walk on the same stream, and wait for its bits)
-    HIP_TRY(hipMalloc(&c->d_sym, sizeof(uint4) * size_t(c->frame_samples) * nb));
+    HIP_TRY(hipMalloc(&c->d_sym, sizeof(uint2) * size_t(c->frame_samples) * nb));
     HIP_TRY(hipMalloc(&c->d_keys2, 3 * size_t(nb)));
     HIP_TRY(hipMalloc(&c->d_cbits, sizeof(uint32_t) * kChunkWords * size_t(c->frame_chunks) * nb));
     HIP_TRY(hipMalloc(&c->d_dcount, 3 * sizeof(int) * 3 * size_t(nb) * c->nslices));
@@ -1071,6 +1093,7 @@ static int alloc_device(ffv1hip_ctx* c) {
     HIP_TRY(hipHostMalloc(&c->h_dtotal, 3 * sizeof(int64_t), hipHostMallocDefault));
     for (hipEvent_t& e : c->coded3) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->walk_a, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->walk_go, hipEventDisableTiming));
     {
       std::vector<int> ident(nb);
       for (int i = 0; i < nb; i++) ident[i] = i;
@@ -1109,7 +1132,7 @@ static int alloc_device(ffv1hip_ctx* c) {
     // the second records set, only with room to spare (a later batch may
     // still grow the decision buffers); FFV1HIP_RECSETS=1 keeps one set
     const char* rs = std::getenv("FFV1HIP_RECSETS");
-    const size_t rec_bytes = sizeof(uint4) * size_t(c->frame_samples) * nb;
+    const size_t rec_bytes = sizeof(uint2) * size_t(c->frame_samples) * nb;
     const size_t cb_bytes = sizeof(uint32_t) * kChunkWords * size_t(c->frame_chunks) * nb;
     size_t free_b = 0, total_b = 0;
     HIP_TRY(hipMemGetInfo(&free_b, &total_b));
@@ -1428,18 +1451,13 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   }
   if (sst != st) {
     // what the symbols rewrite: records set fb (read by the walk of batch
-    // k-2) and metadata set t3 (read by the coder of batch k-3); and they
-    // start once the first part of the previous batch's walk is done and its
-    // second part's waves are on the CUs (a short wait kernel,
-    // FFV1HIP_SYM_DELAY_US)
+    // k-2) and metadata set t3 (read by the coder of batch k-3)
     HIP_TRY(hipStreamWaitEvent(sst, c->walked[fb], 0));
     HIP_TRY(hipStreamWaitEvent(sst, c->coded3[t3], 0));
-    if (c->walk_a_valid && c->cu_side.empty()) {
-      HIP_TRY(hipStreamWaitEvent(sst, c->walk_a, 0));
-      static const int delay_us =
-          std::getenv("FFV1HIP_SYM_DELAY_US") ? std::atoi(std::getenv("FFV1HIP_SYM_DELAY_US")) : 1000;
-      if (delay_us > 0 && launch_delay(delay_us, sst) < 0) return set_err(-5, "delay launch failed");
-    }
+    // ... and start with the previous batch's walk: their bounded grids (no
+    // LDS but a few hundred bytes per block) leave every CU the room its
+    // three walk waves need, so the walk is never held back by them
+    if (c->walk_a_valid && c->cu_side.empty()) HIP_TRY(hipStreamWaitEvent(sst, c->walk_go, 0));
   }
   // the previous batch (possibly on another stream) is done with what this
   // one rewrites first: segments, slot lists, keyflags, the persist buffer
@@ -1490,7 +1508,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   uint32_t* const d_sym = c->frames_mode ? nullptr : c->d_sym;
   // walk records / chunk bits: set fb when there are two sets
   const bool rec1 = c->frames_mode && c->two_rec && fb == 1;
-  uint4* const d_rec = c->frames_mode ? (rec1 ? c->d_rec2 : reinterpret_cast<uint4*>(c->d_sym)) : nullptr;
+  uint2* const d_rec = c->frames_mode ? (rec1 ? c->d_rec2 : reinterpret_cast<uint2*>(c->d_sym)) : nullptr;
   uint32_t* const d_cbits = rec1 ? c->d_cbits2 : c->d_cbits;
   int* const d_dcount = c->frames_mode ? c->d_dcount + size_t(t3) * 3 * c->max_batch * c->nslices : nullptr;
   int64_t* const d_dbase = c->frames_mode ? c->d_dbase + size_t(t3) * c->max_batch * c->nslices : nullptr;
@@ -1566,6 +1584,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     // one set: the previous batch's bits kernel (its own stream) has read the chunk bits
     if (sst == st) HIP_TRY(hipStreamWaitEvent(st, c->bitsed[fb ^ 1], 0));
     sa.frame_chunks = c->frame_chunks;
+    sa.max_blocks = c->grid_sym;
     if (timed(0, sst, [&] { return launch_symbols(sa, sst); }) < 0)
       return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (timed(4, sst, [&] {
@@ -1593,6 +1612,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     ba.nslices = c->nslices;
     ba.nframes = n;
     ba.ds = ds;
+    ba.max_blocks = c->grid_bits;
     // the bits run beside the walk, on their own stream (after the layout
     // and the memset with the split schedule); the coder waits for both
     hipStream_t const bst = sst != st ? sst : serial ? st : c->bits_stream;
@@ -1652,6 +1672,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     // (FFV1HIP_SPLIT_MAX: that share in percent, default 80)
     const int split_max = std::getenv("FFV1HIP_SPLIT_MAX") ? std::atoi(std::getenv("FFV1HIP_SPLIT_MAX")) : 80;
     const bool two_parts = first > 0 && first < nitems && int64_t(nitems - first) * 100 <= int64_t(first) * split_max;
+    HIP_TRY(hipEventRecord(c->walk_go, st));
     if (timed(2, st, [&] {
           if (!two_parts) return launch_walk(wa, nsegs, st);
           if (launch_walk(wa, nsegs, st, 0, first) < 0) return -1;
@@ -1711,7 +1732,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     ca.ck = c->d_ck;
     ca.segrec = c->d_segrec;
     ca.digit_cap = c->slice_stride / 4;
-    ca.dseg_blocks = int(std::min<int64_t>(c->max_groups, 16384));
+    ca.dseg_blocks = int(std::min<int64_t>(c->max_groups, c->grid_dseg));
     HIP_TRY(hipMemsetAsync(ca.status, 0, sizeof(int) * 4, cst));
     // range alone (the serial chain), every segment from its checkpoint,
     // the segments joined, then the bytes
@@ -1833,7 +1854,21 @@ static int settle_batch(ffv1hip_ctx* c, int64_t b) {
     const ffv1hip_ctx::LastBatch& L = c->hist[b & 1];
     HIP_TRY(hipEventSynchronize(c->hist_done[b & 1]));
     int status[4];
-    HIP_TRY(hipMemcpy(status, c->d_status + 4 * L.status_set, sizeof(status), hipMemcpyDeviceToHost));
+    if (c->pipe.on) {
+      // on the host-frame path a DMA copy would queue behind the next batch's
+      // frames: a kernel writes the status into mapped host memory
+      ffv1hip_ctx::HostPipe& P = c->pipe;
+      if (!P.h_status) {
+        HIP_TRY(hipHostMalloc(&P.h_status, 64, hipHostMallocMapped));
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&P.hd_status), P.h_status, 0));
+      }
+      if (launch_ints_out(c->d_status + 4 * L.status_set, 4, P.hd_status, P.d2h) < 0)
+        return set_err(-5, "status launch failed");
+      HIP_TRY(hipStreamSynchronize(P.d2h));
+      std::memcpy(status, P.h_status, sizeof(status));
+    } else {
+      HIP_TRY(hipMemcpy(status, c->d_status + 4 * L.status_set, sizeof(status), hipMemcpyDeviceToHost));
+    }
     if (!status[0]) break;
     if (attempt >= 2 || !L.valid)
       return set_err(-28, "%d slices exceeded the slice byte budget", status[0]);
@@ -1981,6 +2016,7 @@ static int pipe_open(ffv1hip_ctx* c) {
     if (std::atoi(e) > 0) nt = std::min(nt, std::atoi(e));
   if (const char* e = std::getenv("FFV1HIP_COPY_THREADS")) nt = std::atoi(e);
   P.pool = std::make_unique<CopyPool>(std::max(1, std::min(nt, 16)));
+  P.pool_out = std::make_unique<CopyPool>(std::max(1, std::min(nt / 4, 4)));
   P.dbg = std::getenv("FFV1HIP_HOSTDBG") && std::atoi(std::getenv("FFV1HIP_HOSTDBG"));
   P.slot_bytes = std::max<int64_t>(int64_t(32) << 20, int64_t(c->P.width) * 4);
   for (int k = 0; k < ffv1hip_ctx::HostPipe::kSlots; k++) {
@@ -2012,12 +2048,16 @@ static void pipe_close(ffv1hip_ctx* c) {
   ffv1hip_ctx::HostPipe& P = c->pipe;
   if (P.xfer) (void)hipStreamSynchronize(P.xfer);
   P.pool.reset();
+  P.pool_out.reset();
   for (int k = 0; k < ffv1hip_ctx::HostPipe::kSlots; k++) {
     if (P.h_slot[k]) (void)hipHostFree(P.h_slot[k]);
     if (P.slot_ev[k]) (void)hipEventDestroy(P.slot_ev[k]);
   }
   for (uint8_t* h : P.h_pk)
     if (h) (void)hipHostFree(h);
+  for (int64_t* h : P.h_sizes)
+    if (h) (void)hipHostFree(h);
+  if (P.h_status) (void)hipHostFree(P.h_status);
   for (uint8_t* d : P.d_compact)
     if (d) (void)hipFree(d);
   if (P.xfer) (void)hipStreamDestroy(P.xfer);
@@ -2105,8 +2145,15 @@ static int copy_packets(ffv1hip_ctx* c, int n, int pk, hipStream_t st, std::vect
   ffv1hip_ctx::HostPipe& P = c->pipe;
   sz.resize(n);
   off.resize(n);
-  HIP_TRY(hipMemcpyAsync(sz.data(), c->psize(pk), sizeof(int64_t) * n, hipMemcpyDeviceToHost, st));
+  const double ts0 = P.dbg ? wall_s() : 0;
+  if (!P.h_sizes[pk]) {
+    HIP_TRY(hipHostMalloc(&P.h_sizes[pk], sizeof(int64_t) * size_t(c->max_batch), hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&P.hd_sizes[pk]), P.h_sizes[pk], 0));
+  }
+  if (launch_sizes_out(c->psize(pk), n, P.hd_sizes[pk], st) < 0) return set_err(-5, "sizes launch failed");
   HIP_TRY(hipStreamSynchronize(st));
+  std::memcpy(sz.data(), P.h_sizes[pk], sizeof(int64_t) * size_t(n));
+  if (P.dbg) P.t_sizes += wall_s() - ts0;
   int64_t total = 0;
   for (int i = 0; i < n; i++) {
     off[i] = total;
@@ -2136,9 +2183,19 @@ static int copy_packets(ffv1hip_ctx* c, int n, int pk, hipStream_t st, std::vect
       (void)hipGetLastError();
   }
   if (total <= P.d_compact_cap[pk]) {
+    const double tc0 = P.dbg ? wall_s() : 0;
     if (launch_compact_packets(d, c->packet_stride, c->psize(pk), n, P.d_compact[pk], st) < 0)
       return set_err(-5, "compact launch failed");
+    if (P.dbg) {
+      HIP_TRY(hipStreamSynchronize(st));
+      P.t_compact += wall_s() - tc0;
+    }
+    const double tc1 = P.dbg ? wall_s() : 0;
     if (total) HIP_TRY(hipMemcpyAsync(h, P.d_compact[pk], size_t(total), hipMemcpyDeviceToHost, st));
+    if (P.dbg) {
+      HIP_TRY(hipStreamSynchronize(st));
+      P.t_dcopy += wall_s() - tc1;
+    }
   } else {
     for (int i = 0; i < n; i++)
       if (sz[i]) HIP_TRY(hipMemcpyAsync(h + off[i], d + int64_t(i) * c->packet_stride, size_t(sz[i]),
@@ -2157,7 +2214,7 @@ static int collect(ffv1hip_ctx* c, int64_t b, std::vector<int64_t>& sz, std::vec
   if (rc < 0) return rc;
   HIP_TRY(hipEventSynchronize(c->hist_done[b & 1]));
   const ffv1hip_ctx::LastBatch& L = c->hist[b & 1];
-  return copy_packets(c, L.n, L.pk, c->pipe.xfer, sz, off, data);
+  return copy_packets(c, L.n, L.pk, c->pipe.d2h, sz, off, data);  // not behind the frames on xfer
 }
 
 int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides, int n_frames,
@@ -2192,7 +2249,7 @@ int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides
       if (out && used + total > out_cap) {
         r = set_err(-22, "output buffer too small");
       } else {
-        if (out) std::memcpy(out + used, h, size_t(total));
+        if (out) pool_copy2d(*P.pool_out, out + used, total, h, total, total, 1);
         P.t_out += wall_s() - t1;
         for (int i = 0; i < n; i++) {
           if (sizes) sizes[base + i] = sz[i];
@@ -2254,8 +2311,10 @@ int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides
   const int jr = join_out();
   if (P.dbg)
     std::fprintf(stderr, "hostdbg: %d frames, %d copy threads: slot wait %.3f s, copy in %.3f s, DMA issue %.3f s, "
-                         "copy-out wait %.3f s, settle %.3f s; copy-out: D2H %.3f s, into the buffer %.3f s\n",
-                 n_frames, P.pool->size(), P.t_slot, P.t_copy, P.t_dma, P.t_join, P.t_settle, P.t_d2h, P.t_out);
+                         "copy-out wait %.3f s, settle %.3f s; copy-out: D2H %.3f s (sizes %.3f, compact %.3f, "
+                         "copy %.3f), into the buffer %.3f s\n",
+                 n_frames, P.pool->size(), P.t_slot, P.t_copy, P.t_dma, P.t_join, P.t_settle, P.t_d2h, P.t_sizes,
+                 P.t_compact, P.t_dcopy, P.t_out);
   return rc < 0 ? rc : jr;
 }
 

@@ -82,11 +82,13 @@ struct SymbolArgs {
   uint32_t* sym;              // [slot][frame_samples]: (row << 16) | (uint16)diff
   int64_t frame_samples;
   int* dcount;                // optional [slot][slice][3]: range-coder decisions per plane
-  uint4* rec;                 // optional, instead of sym: [slot][frame_samples] walk records
+  uint2* rec;                 // optional, instead of sym: [slot][frame_samples] walk records
   uint32_t* cbits;            // with rec: [slot][frame_chunks][kChunkWords]
   int64_t frame_chunks;
   int p_lo, p_hi;             // planes of this launch (p_hi 0: all); with rec, outputs by batch frame
   const int2* rct;            // v4: [batch frame][slice] {by, ry} RCT coefficients, else null (1, 1)
+  int max_blocks;             // grid cap (0: one block per item); the blocks stride over the items
+  int nz;                     // set by launch_symbols: plane parts per (slice, slot)
 };
 
 // v4's choose_rct_params (ffv1enc.c:1064-1144) for every (frame, slice) of
@@ -104,15 +106,16 @@ struct RctArgs {
 
 // Walk record of one sample (frame-parallel mode), written by ffv1_symbols.
 // A plane is walked in chunks of 64 consecutive samples (one per lane).
+// 8 bytes, uint2 {x, w}:
 //   x: row * 32 inside the plane group's table (bits 0..15) | (int16)diff << 16
-//   y, z: two bits per slot (slots 0..15, 16..31): 0/1 the slot's decision
-//         bit, 2 no decision, 3 several decisions (slot 10 at e >= 10, slot
-//         31 at e >= 11: the walk derives them from diff); e <= 11 only, the
-//         chunks with a larger exponent take walk_long
 //   w: D | (D + 2e) << 16, D = the symbol's first decision counted from the
 //      start of its chunk; bit 31: same row as the previous sample of the
-//      chunk
-//   bit 30: same row as the sample two back in the chunk
+//      chunk; bit 30: same row as the sample two back in the chunk; bits
+//      12..14 / 28..29: the composed rows of slots 10 / 31 at e = 10, 11
+// The walk expands a chunk's records in LDS to uint4 {x, y, z, w}, y and z
+// two bits per slot (slots 0..15, 16..31): 0/1 the slot's decision bit, 2
+// no decision, 3 several decisions (slot 10 at e >= 10, slot 31 at e >= 11);
+// e <= 11 only, the chunks with a larger exponent take walk_long.
 constexpr uint32_t kRecSame = 0x80000000u;
 constexpr uint32_t kRecSame2 = 0x40000000u;
 
@@ -208,7 +211,7 @@ struct CodeArgs {
 // Pass-1 statistics (ffv1enc.c:190-199): rc_stat[state][bit] from the
 // decision stream, rc_stat2[context][slot][bit] from the walk records.
 struct StatsArgs {
-  const uint4* rec;           // [batch frame][frame_samples]
+  const uint2* rec;           // [batch frame][frame_samples]
   int64_t frame_samples;
   const SliceGeom* geom;
   int nslices, nframes;
@@ -225,7 +228,7 @@ int launch_stats(const StatsArgs& a, bool states, void* stream);
 // decision, the state it is coded with and its bit; the coding of all
 // (frame, slice) streams then runs in parallel (launch_dcode).
 struct WalkArgs {
-  const uint4* rec;           // [batch frame][frame_samples] walk records
+  const uint2* rec;           // [batch frame][frame_samples] walk records
   const uint32_t* cbits;      // [batch frame][frame_chunks][kChunkWords]
   int64_t frame_chunks;
   int64_t frame_samples;
@@ -254,6 +257,7 @@ struct BitsArgs {
   const SliceGeom* geom;
   int nslices, nframes;
   DecisionStream ds;
+  int max_blocks;             // grid cap (0: one block per stream); the blocks stride over the streams
 };
 
 struct AssembleArgs {
@@ -337,5 +341,7 @@ int launch_code_golomb(const CodeArgs& a, void* stream);
 int launch_assemble(const AssembleArgs& a, int nframes, void* stream);
 int launch_compact_packets(const uint8_t* packets, int64_t stride, const int64_t* sizes, int n, uint8_t* out,
                            void* stream);
+int launch_sizes_out(const int64_t* sizes, int n, int64_t* host_mapped, void* stream);
+int launch_ints_out(const int* src, int n, int* host_mapped, void* stream);
 
 }  // namespace ffv1hip

@@ -167,15 +167,23 @@ __device__ __forceinline__ int rct_sample(const SymbolArgs& a, const uint8_t* fr
 // them from issuing back to back)
 template <int SB, bool RGB>
 __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
-  __shared__ int16_t qt[5 * 256];
+  // the quant tables from global memory (2.5 KB, cached): with them in LDS
+  // the kernel's blocks would take the LDS the states walk's waves need
+  // beside it (~13 KB per CU is left by three walk waves)
+  const int16_t* __restrict__ const qt = a.qt;
   __shared__ int red[kSymThreads / kWave];
   __shared__ uint32_t cstage[kSymThreads / kWave][kChunkWords];  // a wave's chunk bits
-  for (int i = threadIdx.x; i < 5 * 256; i += kSymThreads) qt[i] = a.qt[i];
-  __syncthreads();
-  // a plane of a slice is split into kSymSplit runs of whole 256-sample steps
-  const int slice = blockIdx.x, slot = blockIdx.y, p = a.p_lo + blockIdx.z / kSymSplit, part = blockIdx.z % kSymSplit;
+  // a plane of a slice is split into kSymSplit runs of whole 256-sample steps;
+  // work item vb = ((plane part) * nslots + slot) * nslices + slice, strided
+  // over a grid that may be smaller than the items (launch_symbols: a bounded
+  // grid leaves the CUs room for the states walk's waves beside it)
+  const int64_t nvb = (int64_t)a.nslices * a.nslots * a.nz;
+  for (int64_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
+  const int slice = (int)(vb % a.nslices), slot = (int)(vb / a.nslices % a.nslots);
+  const int z = (int)(vb / ((int64_t)a.nslices * a.nslots));
+  const int p = a.p_lo + z / kSymSplit, part = z % kSymSplit;
   const int f = a.frame_of_slot[slot];
-  if (f < 0 || p >= a.nplanes) return;
+  if (f < 0 || p >= a.nplanes) continue;
   // frames mode (walk records): the outputs are indexed by batch frame (a
   // launch may cover a subset of the frames)
   const int fs = a.rec ? f : slot;
@@ -211,7 +219,7 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   const int64_t span = (n + kSymSplit * kSymThreads - 1) / (kSymSplit * kSymThreads) * kSymThreads;
   const int64_t b0 = part * span, b1 = min(n, b0 + span);
   const int lane = threadIdx.x & (kWave - 1);
-  uint4* const rec = a.rec ? a.rec + (int64_t)fs * a.frame_samples + g.sym_off + g.plane_sym_off[p] : nullptr;
+  uint2* const rec = a.rec ? a.rec + (int64_t)fs * a.frame_samples + g.sym_off + g.plane_sym_off[p] : nullptr;
   // the plane's chunk headers (read once: a reload inside the loop would
   // wait for the record stores)
   uint32_t* const cbase = rec ? a.cbits + ((int64_t)fs * a.frame_chunks + g.chunk_off[p]) * kChunkWords : nullptr;
@@ -278,13 +286,11 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
       const int e = diff ? 31 - __builtin_clz(mag) : 0;
       const int prev = wave_prev(raddr);
       const int prev2 = wave_prev(prev);
-      uint32_t c0, c1;
-      slot_codes(diff, c0, c1);
       // e = 10, 11: the composed N rows of slots 10 and 31 (ffv1_walk)
       const uint32_t mrows = e >= 10 && e <= 11 ? (((e == 11 ? 3u : 6u) << 12) | (((mag >> 9) & 3u) << 28)) : 0u;
       const uint32_t w = (uint32_t)d0 | ((uint32_t)(d0 + 2 * e) << 16) | (lane > 0 && prev == raddr ? kRecSame : 0u) |
                          (lane > 1 && prev2 == raddr ? kRecSame2 : 0u) | mrows;
-      if (valid) rec[idx] = make_uint4((uint32_t)raddr | ((uint32_t)(uint16_t)diff << 16), c0, c1, w);
+      if (valid) rec[idx] = make_uint2((uint32_t)raddr | ((uint32_t)(uint16_t)diff << 16), w);
       // the chunk's decision bits, packed in coding order, and its header
       const int wv = threadIdx.x / kWave;
       uint32_t* const cs = cstage[wv];
@@ -318,6 +324,8 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
       for (int w = 0; w < kSymThreads / kWave; w++) t += red[w];
       atomicAdd(count, t);
     }
+    __syncthreads();  // red[] is reused by the next item
+  }
   }
 }
 
@@ -938,9 +946,7 @@ __device__ __forceinline__ StreamRef stream_of(const CodeArgs& a, int64_t c) {
 }
 
 constexpr int kRangeThreads = kWave;
-template <bool FAT>
 __global__ __launch_bounds__(kRangeThreads) void ffv1_range(CodeArgs a) {
-  if constexpr (FAT) asm volatile("" ::: "v255", "a255");  // a SIMD to itself (see ffv1_walk)
   const StreamRef sr = stream_of(a, (int64_t)blockIdx.x * kRangeThreads + threadIdx.x);
   const int key = sr.live ? a.keyflags[sr.f] : 0;
   const HdrState h = a.hdr[key * a.nslices + sr.slice];
@@ -1012,30 +1018,18 @@ struct DigitOut {
 };
 constexpr int kBufDword3 = 0x00020000;  // gfx9-family raw buffer (32-bit data format)
 
-#ifndef FFV1_DSEG_STORE
-#define FFV1_DSEG_STORE 0  // 0: every lane stores, out of range without a shift; 1: exec-masked; 2: LDS ring
-#endif
-constexpr int kSRing = 32, kSRingStride = kSRing + 3;
 
 // put_rac + renorm_encoder's shift (rangecoder.h:52-102): the value of low
 // before a shift is stored as the lane's next digit.
-__device__ __forceinline__ void put_dec(int& low, int& range, DigitOut& o, int s, int m, lds_u32* ring = nullptr) {
+__device__ __forceinline__ void put_dec(int& low, int& range, DigitOut& o, int s, int m) {
   const int r1 = (int)(__umul24((unsigned)range, (unsigned)s) >> 8);
   const int d = range - r1;
   low += d & m;
   const int nr = (m & r1) | (~m & d);  // m ? r1 : d, one bitwise select
   // all ones when a byte shifts out: nr < 0x100 (24+ leading zeros, see range32)
   const int sm = __builtin_amdgcn_sbfe((int)__builtin_clz((unsigned)nr), 3, 1);
-#if FFV1_DSEG_STORE == 0
   __builtin_amdgcn_raw_buffer_store_b32((uint32_t)low, o.rs, o.kb | (~sm & (int)0x80000000), 0, 0);
   o.kb += sm & 4;
-#elif FFV1_DSEG_STORE == 1
-  if (sm) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)low, o.rs, o.kb, 0, 0);
-  o.kb += sm & 4;
-#else
-  ring[o.kb] = (uint32_t)low;  // kb: the ring head here
-  o.kb += sm & 1;
-#endif
   const int shifted = (int)__builtin_amdgcn_perm(0u, (uint32_t)low, 0x0c0c000cu);  // (low & 0xFF) << 8
   low = (sm & shifted) | (~sm & low);
   range = nr << (sm & 8);
@@ -1043,12 +1037,6 @@ __device__ __forceinline__ void put_dec(int& low, int& range, DigitOut& o, int s
 
 __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
   const int lane = threadIdx.x;
-#if FFV1_DSEG_STORE == 2
-  __shared__ uint32_t sring[kDsegThreads * kSRingStride];
-  lds_u32* const ring = (lds_u32*)(sring + lane * kSRingStride);
-#else
-  lds_u32* const ring = nullptr;
-#endif
   const int ngroups = a.seg_totals[1];
   for (int w = blockIdx.x; w < ngroups; w += gridDim.x) {
     const int st = a.wmap[w];  // wave-uniform
@@ -1071,24 +1059,7 @@ __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
     DigitOut o;
     o.rs = __builtin_amdgcn_make_buffer_rsrc(a.slice_out + (int64_t)st * a.slice_stride, 0,
                                             (int)(a.digit_cap * 4), kBufDword3);
-#if FFV1_DSEG_STORE == 2
-    int gpos = (int)ck.y;  // digits flushed so far (stream-wide index of the ring's first)
-    o.kb = 0;
-    auto flush = [&]() {
-      const int nr = o.kb;
-      for (int t = 0; __ballot(t < nr); t += 4) {
-        const uint32_t d0 = ring[t], d1 = ring[t + 1], d2 = ring[t + 2], d3 = ring[t + 3];
-        if (t < nr) __builtin_amdgcn_raw_buffer_store_b32(d0, o.rs, (gpos + t) * 4, 0, 0);
-        if (t + 1 < nr) __builtin_amdgcn_raw_buffer_store_b32(d1, o.rs, (gpos + t + 1) * 4, 0, 0);
-        if (t + 2 < nr) __builtin_amdgcn_raw_buffer_store_b32(d2, o.rs, (gpos + t + 2) * 4, 0, 0);
-        if (t + 3 < nr) __builtin_amdgcn_raw_buffer_store_b32(d3, o.rs, (gpos + t + 3) * 4, 0, 0);
-      }
-      gpos += nr;
-      o.kb = 0;
-    };
-#else
     o.kb = (int)ck.y * 4;
-#endif
     const int kb0 = o.kb;
     const uint4* P = reinterpret_cast<const uint4*>(a.ds.pre + pb);
     const uint32_t* B = a.ds.bits + (pb >> 5);
@@ -1129,22 +1100,10 @@ __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
         static_for<0, 8>([&](auto jc) {
           constexpr int J = 8 * G + decltype(jc)::value;
           const uint32_t sw = state_word<J>(wa, wb);
-          put_dec(low, range, o, (int)((sw >> ((J & 3) * 8)) & 0xFFu), k.m[J & 7], ring);
-#if FFV1_DSEG_STORE == 2
-          if constexpr ((J & 15) == 15) {
-            if (__ballot(o.kb > 15)) flush();  // <= 16 shifts per 16 decisions
-          }
-#endif
+          put_dec(low, range, o, (int)((sw >> ((J & 3) * 8)) & 0xFFu), k.m[J & 7]);
         });
       });
     }
-#if FFV1_DSEG_STORE == 2
-    flush();
-    o.kb = gpos * 4;  // byte offset of the next digit, for the terminate
-    const int kb0b = (int)ck.y * 4;
-#else
-    const int kb0b = kb0;
-#endif
     if (last) {  // a 0 on state 129, then ff_rac_terminate (ffv1enc.c:1331-1334, rangecoder.c:104-116)
       {  // the trailer decision: at most one shift
         const int r1 = (int)(__umul24((unsigned)range, 129u) >> 8);
@@ -1163,8 +1122,7 @@ __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
       low = (low & 0xFF) << 8;
       o.kb += 8;
     }
-    if (act) a.segrec[ss.seg_base + s] = make_uint2((uint32_t)low, (uint32_t)((o.kb - kb0b) >> 2));
-    (void)kb0;
+    if (act) a.segrec[ss.seg_base + s] = make_uint2((uint32_t)low, (uint32_t)((o.kb - kb0) >> 2));
   }
 }
 
@@ -1463,6 +1421,19 @@ __device__ __forceinline__ void walk_multi_fill(uint8_t* fixed, const uint4* myr
 
 int64_t walk_lds_bytes_dev(int64_t state_bytes) { return kLdsFixed + 2 * (state_bytes / 2 + 32); }
 
+// The 8-byte record in HBM (ffv1_symbols) as the walk's step reads it from
+// LDS: the slot codes (y, z) follow from the residual in x (slot_codes), so
+// they are derived here once per chunk instead of being stored and read back
+// (16 -> 8 bytes per sample).
+__device__ __forceinline__ uint4 expand_rec(const uint2& r) {
+  uint32_t c0, c1;
+  slot_codes((int)(int16_t)(r.x >> 16), c0, c1);
+  return make_uint4(r.x, c0, c1, r.y);
+}
+
+// (Expanding the next chunk's records inside the step loop, in the shadow of
+// the lookups, measured slower: 114 -> 131 cycles per step.)
+
 // c ? a : b by value (b in registers, pinned there: a select between a load
 // and a local would become a load from a selected address, via scratch).
 // Pinning a instead would force a wait for its load right here.
@@ -1472,12 +1443,7 @@ __device__ __forceinline__ uint4 pick(bool c, uint4 a, uint4 b) {
 }
 
 
-// FAT: the wave takes the whole register file of its SIMD (256 VGPRs + 256
-// AGPRs), so no other wave is placed on that SIMD: the coder's waves go to
-// the SIMDs the walk leaves free instead of sharing a walk wave's issue.
-template <bool FAT>
 __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
-  if constexpr (FAT) asm volatile("" ::: "v255", "a255");
   __shared__ __attribute__((aligned(16))) uint8_t fixed[kLdsFixed];
   extern __shared__ __attribute__((aligned(16))) uint8_t tbl[];  // [2][contexts + 1 dummy row][32]
   const int64_t half = a.state_bytes / 2;  // one plane group's [contexts][32]
@@ -1592,13 +1558,13 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
     int64_t run = 0;  // decisions so far in this frame's chain
     for (int pl = p0; pl < p1; pl++) {
       const int64_t nsym = live ? (pl < 2 ? g.plane_sym_off[pl + 1] : g.nsym) - g.plane_sym_off[pl] : 0;
-      const uint4* rp = a.rec + (int64_t)f * a.frame_samples + g.sym_off + g.plane_sym_off[pl];
+      const uint2* rp = a.rec + (int64_t)f * a.frame_samples + g.sym_off + g.plane_sym_off[pl];
       const uint32_t* cp = a.cbits + ((int64_t)f * a.frame_chunks + g.chunk_off[pl]) * kChunkWords;
       const int nch = (int)((nsym + kChunk - 1) / kChunk);
       const int nchunks = max(__builtin_amdgcn_readlane(nch, 0), __builtin_amdgcn_readlane(nch, 32));
       // a chunk's inputs: 2 records per lane and the chunk header
       struct In {
-        uint4 m0, m1;
+        uint2 m0, m1;
         uint32_t hd, mlo, mhi;  // header, multi-symbol mask
       };
       // raw loads (indices past the plane read record / chunk 0 of a plane of
@@ -1620,8 +1586,8 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
         In cx = nx;
         // wait for chunk c's data NOW, while everything older is long done;
         // after the stores and loads below, vmcnt would wait for those too
-        pin(cx.m0.x); pin(cx.m0.y); pin(cx.m0.z); pin(cx.m0.w);
-        pin(cx.m1.x); pin(cx.m1.y); pin(cx.m1.z); pin(cx.m1.w);
+        pin(cx.m0.x); pin(cx.m0.y);
+        pin(cx.m1.x); pin(cx.m1.y);
         pin(cx.hd);
         pin(cx.mlo);
         pin(cx.mhi);
@@ -1637,8 +1603,8 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
                              (uint64_t)(__builtin_amdgcn_readlane(mlo, 0) | __builtin_amdgcn_readlane(mlo, 32));
         const bool mul = msk != 0 || a.force_multi;
         const int64_t pos0 = gbase + run;  // decision index of the chunk's first decision
-        myrecs[k] = pick(k < cnt, cx.m0, nullrec);
-        myrecs[k + 32] = pick(k + 32 < cnt, cx.m1, nullrec);
+        myrecs[k] = pick(k < cnt, expand_rec(cx.m0), nullrec);
+        myrecs[k + 32] = pick(k + 32 < cnt, expand_rec(cx.m1), nullrec);
         if (k < kRecSlots - kChunk) myrecs[kChunk + k] = nullrec;
         __builtin_amdgcn_wave_barrier();
 
@@ -1819,10 +1785,12 @@ __global__ __launch_bounds__(kBitsThreads) void ffv1_bits(BitsArgs a) {
   __shared__ int off[kBitsThreads];
   __shared__ int tot[kBitsThreads];
   __shared__ int wsum[kBitsWaves];
-  const int s = blockIdx.x, f = blockIdx.y;
   const int t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
+  // stream sid = frame * nslices + slice, strided over a grid that may be
+  // smaller than the streams (a bounded grid: room for the walk beside it)
+  for (int64_t sid = blockIdx.x; sid < (int64_t)a.nframes * a.nslices; sid += gridDim.x) {
+  const int s = (int)(sid % a.nslices), f = (int)(sid / a.nslices);
   const SliceGeom& g = a.geom[s];
-  const int64_t sid = (int64_t)f * a.nslices + s;
   const int* dc = a.ds.dcount + sid * 3;
   const int64_t base = a.ds.dbase[sid];
   const uint32_t* const fc = a.cbits + (int64_t)f * a.frame_chunks * kChunkWords;
@@ -1911,6 +1879,7 @@ __global__ __launch_bounds__(kBitsThreads) void ffv1_bits(BitsArgs a) {
       run += all;
       __syncthreads();
     }
+  }
   }
 }
 
@@ -2126,9 +2095,9 @@ __global__ __launch_bounds__(kStatsThreads) void ffv1_stats_slots(StatsArgs a) {
   const int slice = blockIdx.x, f = blockIdx.y, p = blockIdx.z;
   const SliceGeom& g = a.geom[slice];
   const int64_t n = (int64_t)g.pw[p] * g.ph[p];
-  const uint4* r = a.rec + (int64_t)f * a.frame_samples + g.sym_off + g.plane_sym_off[p];
+  const uint2* r = a.rec + (int64_t)f * a.frame_samples + g.sym_off + g.plane_sym_off[p];
   for (int64_t i = threadIdx.x; i < n; i += kStatsThreads) {
-    const uint4 v = r[i];
+    const uint2 v = r[i];
     const int ctx = (int)(v.x & 0xFFFFu) >> 5;
     const int diff = (int16_t)(v.x >> 16);
     const bool lds = ctx < kStatsLdsCtx;
@@ -2336,16 +2305,19 @@ int launch_rct_params(const RctArgs& a, void* stream) {
 int launch_symbols(const SymbolArgs& a, void* stream) {
   const int np = a.p_hi > a.p_lo ? a.p_hi - a.p_lo : a.nplanes - a.p_lo;
   if (np <= 0 || a.nslots <= 0) return 0;
-  dim3 grid(a.nslices, a.nslots, np * kSymSplit), block(kSymThreads);
+  SymbolArgs b = a;
+  b.nz = np * kSymSplit;
+  const int64_t items = (int64_t)a.nslices * a.nslots * b.nz;
+  dim3 grid((unsigned)(a.max_blocks > 0 ? std::min<int64_t>(items, a.max_blocks) : items)), block(kSymThreads);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (a.sample_bytes == 1 && !a.rgb)
-    hipLaunchKernelGGL((ffv1_symbols<1, false>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((ffv1_symbols<1, false>), grid, block, 0, st, b);
   else if (a.sample_bytes == 4 && a.rgb)
-    hipLaunchKernelGGL((ffv1_symbols<4, true>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((ffv1_symbols<4, true>), grid, block, 0, st, b);
   else if (a.sample_bytes == 2 && a.rgb)
-    hipLaunchKernelGGL((ffv1_symbols<2, true>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((ffv1_symbols<2, true>), grid, block, 0, st, b);
   else if (a.sample_bytes == 2)
-    hipLaunchKernelGGL((ffv1_symbols<2, false>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((ffv1_symbols<2, false>), grid, block, 0, st, b);
   else
     return -1;
   return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -2361,12 +2333,7 @@ int launch_code(const CodeArgs& a, void* stream) {
 int launch_range(const CodeArgs& a, void* stream) {
   const int64_t streams = (int64_t)a.nframes * a.nslices;
   dim3 grid((unsigned)((streams + kRangeThreads - 1) / kRangeThreads)), block(kRangeThreads);
-  // FFV1HIP_RANGE_FAT=1 (measurement hook): each wave owns its SIMD
-  static const bool fat = std::getenv("FFV1HIP_RANGE_FAT") && std::atoi(std::getenv("FFV1HIP_RANGE_FAT"));
-  if (fat)
-    hipLaunchKernelGGL((ffv1_range<true>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
-  else
-    hipLaunchKernelGGL((ffv1_range<false>), grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
+  hipLaunchKernelGGL(ffv1_range, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2387,24 +2354,13 @@ int64_t walk_lds_bytes(int64_t state_bytes) { return walk_lds_bytes_dev(state_by
 
 int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first, int count) {
   if (walk_lds_bytes_dev(a.state_bytes) > kWalkLdsMax) return -1;
-  size_t dyn = (size_t)(2 * (a.state_bytes / 2 + 32));  // the tables; the fixed part is static
-  // FFV1HIP_WALK_LDS_PAD (measurement hook): extra LDS per walk wave, to
-  // run the walk at a lower occupancy
-  static const long pad = std::getenv("FFV1HIP_WALK_LDS_PAD") ? std::atol(std::getenv("FFV1HIP_WALK_LDS_PAD")) : 0;
-  dyn += (size_t)pad;
+  const size_t dyn = (size_t)(2 * (a.state_bytes / 2 + 32));  // the tables; the fixed part is static
   WalkArgs b = a;
   b.nitems = nsegs * ((a.nslices + 1) / 2) * 2;
   if (count < 0) count = b.nitems - first;
   if (first < 0 || count <= 0 || first + count > b.nitems) return count == 0 ? 0 : -1;
   b.item0 = first;
-  // FFV1HIP_WALK_FAT=1 (measurement hook): each wave owns its SIMD
-  static const bool fat = std::getenv("FFV1HIP_WALK_FAT") && std::atoi(std::getenv("FFV1HIP_WALK_FAT"));
-  if (fat)
-    hipLaunchKernelGGL((ffv1_walk<true>), dim3((unsigned)count), dim3(kWalkThreads), dyn,
-                       reinterpret_cast<hipStream_t>(stream), b);
-  else
-    hipLaunchKernelGGL((ffv1_walk<false>), dim3((unsigned)count), dim3(kWalkThreads), dyn,
-                       reinterpret_cast<hipStream_t>(stream), b);
+  hipLaunchKernelGGL(ffv1_walk, dim3((unsigned)count), dim3(kWalkThreads), dyn, reinterpret_cast<hipStream_t>(stream), b);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2414,7 +2370,7 @@ int walk_items(int nsegs, int nslices) { return nsegs * ((nslices + 1) / 2) * 2;
 int walk_resident(const WalkArgs& a) {
   const size_t dyn = (size_t)(2 * (a.state_bytes / 2 + 32));
   int per_cu = 0, dev = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ffv1_walk<false>, kWalkThreads, dyn) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ffv1_walk, kWalkThreads, dyn) != hipSuccess ||
       hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
     (void)hipGetLastError();
     return 0;
@@ -2436,8 +2392,9 @@ int launch_delay(int us, void* stream) {
 }
 
 int launch_bits(const BitsArgs& a, void* stream) {
-  hipLaunchKernelGGL(ffv1_bits, dim3(a.nslices, a.nframes), dim3(kBitsThreads), 0, reinterpret_cast<hipStream_t>(stream),
-                     a);
+  const int64_t streams = (int64_t)a.nslices * a.nframes;
+  const int64_t grid = a.max_blocks > 0 ? std::min<int64_t>(streams, a.max_blocks) : streams;
+  hipLaunchKernelGGL(ffv1_bits, dim3((unsigned)grid), dim3(kBitsThreads), 0, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2497,7 +2454,29 @@ __global__ __launch_bounds__(kCompactThreads) void ffv1_compact_packets(const ui
     for (int b = 0; b < 16 && k * 16 + b < sz; b++) dst[k * 16 + b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
   }
 }
+// A batch's packet sizes into host memory (mapped pinned), written by the
+// kernel itself: a DMA copy of them would queue behind the next batch's
+// frames going the other way.
+__global__ __launch_bounds__(256) void ffv1_sizes_out(const int64_t* sizes, int n, int64_t* host) {
+  for (int i = threadIdx.x; i < n; i += 256) host[i] = sizes[i];
+}
+__global__ __launch_bounds__(64) void ffv1_ints_out(const int* src, int n, int* host) {
+  if ((int)threadIdx.x < n) host[threadIdx.x] = src[threadIdx.x];
+}
 }  // namespace
+
+int launch_sizes_out(const int64_t* sizes, int n, int64_t* host_mapped, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(ffv1_sizes_out, dim3(1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), sizes, n,
+                     host_mapped);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_ints_out(const int* src, int n, int* host_mapped, void* stream) {
+  if (n <= 0 || n > 64) return -1;
+  hipLaunchKernelGGL(ffv1_ints_out, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), src, n, host_mapped);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int launch_compact_packets(const uint8_t* packets, int64_t stride, const int64_t* sizes, int n, uint8_t* out,
                            void* stream) {
