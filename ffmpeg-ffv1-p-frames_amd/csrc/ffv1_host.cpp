@@ -345,6 +345,8 @@ struct ffv1hip_ctx {
   // device buffers
   uint8_t* d_frames = nullptr;
   int16_t* d_qt = nullptr;
+  int walk_rows = 0;             // frames mode: context rows per plane group in the walk's LDS
+  int16_t* d_qt_walk = nullptr;  // dense rows (kDenseRows): quant tables with weights 1, 9, 81
   uint8_t* d_tabs = nullptr;
   Op* d_ops = nullptr;
   int* d_nops = nullptr;
@@ -419,6 +421,7 @@ struct ffv1hip_ctx {
   // wave slots and registers, and walk waves launched meanwhile wait for CU
   // room until those blocks retire (FFV1HIP_SYM_GRID / _BITS_GRID / _DSEG_GRID)
   int grid_sym = 3072, grid_bits = 1024, grid_dseg = 3072;
+  int prio_range = 0, prio_dseg = 0;  // FFV1HIP_RANGE_PRIO / FFV1HIP_DSEG_PRIO (the walk's is 2)
   SliceGeom* d_geom = nullptr;
   int* d_slot_frames = nullptr;  // [j][slot]
   int* d_status = nullptr;       // [set][4]: [0] slices over budget, [1] most bytes one needed
@@ -510,9 +513,14 @@ struct ffv1hip_ctx {
     int next = 0;
     int64_t fill = 0;
     uint8_t* h_pk[2]{};  // pinned packets of a collected batch, per packet set
-    int64_t* h_sizes[2]{};   // mapped pinned: a batch's packet sizes, written by a kernel
+    // Written at the end of each batch by kernels on the coder stream, so
+    // that collecting a batch needs no GPU work but one D2H copy (a small
+    // copy or kernel issued then would queue behind the next batch's frames
+    // or kernels): mapped pinned packet sizes per packet set, the
+    // slice-budget status per status set, the packets back to back in HBM
+    int64_t* h_sizes[2]{};
     int64_t* hd_sizes[2]{};  // their device-side address
-    int* h_status = nullptr;  // mapped pinned: a batch's slice-budget status (settle_batch)
+    int* h_status = nullptr;  // [2][4]
     int* hd_status = nullptr;
     int64_t h_pk_cap[2]{};
     uint8_t* d_compact[2]{};  // the same, back to back in HBM (one D2H copy)
@@ -904,7 +912,7 @@ static void free_device(ffv1hip_ctx* c) {
   dump_walk_trace(c);
   if (c->d_trace) (void)hipFree(c->d_trace);
   pipe_close(c);
-  void* ptrs[] = {c->d_frames, c->d_qt, c->d_tabs, c->d_ops, c->d_nops, c->d_segs, c->d_keys,
+  void* ptrs[] = {c->d_frames, c->d_qt, c->d_qt_walk, c->d_tabs, c->d_ops, c->d_nops, c->d_segs, c->d_keys,
                   c->d_slice_out, c->d_slice_bytes, c->d_packets, c->d_packet_size, c->d_persist[0],
                   c->d_persist[1], c->d_tables, c->d_sym, c->d_keys2, c->d_cbits, c->d_dcount, c->d_dbase, c->d_dtotal, c->d_pre[0],
                   c->d_pre[1], c->d_bits[0], c->d_bits[1], c->d_scratch, c->d_hdr, c->d_hdr_digits, c->d_geom, c->d_slot_frames, c->d_status,
@@ -1046,6 +1054,8 @@ static int alloc_device(ffv1hip_ctx* c) {
     c->grid_sym = knob("FFV1HIP_SYM_GRID", c->grid_sym);
     c->grid_bits = knob("FFV1HIP_BITS_GRID", c->grid_bits);
     c->grid_dseg = std::max(1, knob("FFV1HIP_DSEG_GRID", c->grid_dseg));
+    c->prio_range = knob("FFV1HIP_RANGE_PRIO", c->prio_range);
+    c->prio_dseg = knob("FFV1HIP_DSEG_PRIO", c->prio_dseg);
   }
   if (!c->cu_walk.empty())
     HIP_TRY(hipExtStreamCreateWithCUMask(&c->stream, uint32_t(c->cu_walk.size() * 32), c->cu_walk.data()));
@@ -1054,6 +1064,15 @@ static int alloc_device(ffv1hip_ctx* c) {
   for (hipEvent_t& e : c->hist_done) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_TRY(hipMalloc(&c->d_qt, sizeof(c->qt)));
   HIP_TRY(hipMemcpy(c->d_qt, c->qt, sizeof(c->qt), hipMemcpyHostToDevice));
+  if (c->frames_mode && c->walk_rows != c->contexts) {
+    int16_t qd[5][256] = {};
+    const auto A = {5, 13, 27, 56};  // quant9_10bit's steps (quant_set, bits > 8)
+    quant_table(qd[0], A, 1);
+    quant_table(qd[1], A, 9);
+    quant_table(qd[2], A, 81);
+    HIP_TRY(hipMalloc(&c->d_qt_walk, sizeof(qd)));
+    HIP_TRY(hipMemcpy(c->d_qt_walk, qd, sizeof(qd), hipMemcpyHostToDevice));
+  }
   uint8_t tabs[1024];
   std::memcpy(tabs, c->dflt.to0, 256);
   std::memcpy(tabs + 256, c->dflt.to1, 256);
@@ -1261,7 +1280,12 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
   // the chained per-GOP coder (a test hook: both must give equal bytes).
   {
     const char* mode = std::getenv("FFV1HIP_CODER");
-    const int64_t lds = walk_lds_bytes(int64_t(2) * c->contexts * 32);
+    // dense rows above 8 bits with context model 0 (FFV1HIP_DENSE=0: the
+    // context numbering, a measurement hook)
+    const char* dn = std::getenv("FFV1HIP_DENSE");
+    const bool dense = p.context_model == 0 && p.bits_per_raw_sample > 8 && !(dn && std::atoi(dn) == 0);
+    c->walk_rows = dense ? kDenseRows : c->contexts;
+    const int64_t lds = walk_lds_bytes(c->walk_rows);
     // RGB interleaves the three planes' rows (encode_rgb_frame): chained
     // alpha (a third plane context) and v4 (per-frame slice header values):
     // the chained coders
@@ -1504,7 +1528,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   sa.rct_offset = 1 << p.bits_per_raw_sample;
   sa.contexts = c->contexts;
   sa.model1 = p.context_model;
-  sa.qt = c->d_qt;
+  sa.qt = c->frames_mode && c->d_qt_walk ? c->d_qt_walk : c->d_qt;
   uint32_t* const d_sym = c->frames_mode ? nullptr : c->d_sym;
   // walk records / chunk bits: set fb when there are two sets
   const bool rec1 = c->frames_mode && c->two_rec && fb == 1;
@@ -1641,6 +1665,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     static const int walk_prio = std::getenv("FFV1HIP_WALK_PRIO") ? std::atoi(std::getenv("FFV1HIP_WALK_PRIO")) : 2;
     wa.prio = walk_prio;
     wa.init = c->d_init;
+    wa.rows = c->walk_rows;
+    wa.dense = c->d_qt_walk != nullptr;
     static const bool walktrace = std::getenv("FFV1HIP_WALKTRACE") && std::atoi(std::getenv("FFV1HIP_WALKTRACE"));
     if (walktrace && c->trace_n < ffv1hip_ctx::kTraceBatches) {
       const int items = walk_items(nsegs, c->nslices);
@@ -1696,6 +1722,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       sta.ds = ds;
       sta.rc_stat = c->d_rcstat;
       sta.rc_stat2 = c->d_rcstat + 512;
+      sta.dense = c->d_qt_walk != nullptr;
       if (launch_stats(sta, false, st) < 0) return set_err(-5, "stats launch failed");
     }
     if (walkdbg) {
@@ -1733,6 +1760,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     ca.segrec = c->d_segrec;
     ca.digit_cap = c->slice_stride / 4;
     ca.dseg_blocks = int(std::min<int64_t>(c->max_groups, c->grid_dseg));
+    ca.range_prio = c->prio_range;
+    ca.dseg_prio = c->prio_dseg;
     HIP_TRY(hipMemsetAsync(ca.status, 0, sizeof(int) * 4, cst));
     // range alone (the serial chain), every segment from its checkpoint,
     // the segments joined, then the bytes
@@ -1786,6 +1815,13 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev[1], cst));
   if (timed(3, cst, [&] { return launch_assemble(b, n, cst); }) < 0) return set_err(-5, "assemble launch failed");
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev[2], cst));
+  if (c->pipe.on) {  // the host-frame path then collects the batch with one D2H copy and no GPU work
+    ffv1hip_ctx::HostPipe& P = c->pipe;
+    if (launch_sizes_out(c->psize(L.pk), n, P.hd_sizes[L.pk], cst) < 0 ||
+        launch_compact_packets(c->pkts(L.pk), c->packet_stride, c->psize(L.pk), n, P.d_compact[L.pk], cst) < 0 ||
+        launch_ints_out(ca.status, 4, P.hd_status + 4 * sset, cst) < 0)
+      return set_err(-5, "collect launch failed: %s", hipGetErrorString(hipGetLastError()));
+  }
   if (c->frames_mode) {
     HIP_TRY(hipEventRecord(c->coded[fb], cst));
     HIP_TRY(hipEventRecord(c->coded3[t3], cst));
@@ -1819,6 +1855,7 @@ int ffv1hip_encode_device(ffv1hip_ctx* c, const void* d_frames, int64_t frame_by
 // back (picture number, P-frame carry, buffer sets) and encoded again with a
 // budget sized from what the slice needed.  The batch's input frames must
 // still be where the call found them.
+static int alloc_compact(ffv1hip_ctx* c);
 static int grow_slice_budget(ffv1hip_ctx* c, int64_t needed) {
   const int64_t cap = ((needed + needed / 4 + 4096) + 255) & ~int64_t(255);
   if (cap <= c->slice_cap) return set_err(-28, "slice byte budget %lld not enough", (long long)c->slice_cap);
@@ -1835,7 +1872,7 @@ static int grow_slice_budget(ffv1hip_ctx* c, int64_t needed) {
       hipMalloc(&c->d_packets, pk_bytes) != hipSuccess ||
       (c->two_pk && hipMalloc(&c->d_packets2, pk_bytes) != hipSuccess))
     return set_err(-12, "slice buffers for a %lld-byte budget", (long long)cap);
-  return 0;
+  return c->pipe.on ? alloc_compact(c) : 0;
 }
 
 // Once batch b (one of the last two submitted) is done: if a slice of it
@@ -1857,15 +1894,7 @@ static int settle_batch(ffv1hip_ctx* c, int64_t b) {
     if (c->pipe.on) {
       // on the host-frame path a DMA copy would queue behind the next batch's
       // frames: a kernel writes the status into mapped host memory
-      ffv1hip_ctx::HostPipe& P = c->pipe;
-      if (!P.h_status) {
-        HIP_TRY(hipHostMalloc(&P.h_status, 64, hipHostMallocMapped));
-        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&P.hd_status), P.h_status, 0));
-      }
-      if (launch_ints_out(c->d_status + 4 * L.status_set, 4, P.hd_status, P.d2h) < 0)
-        return set_err(-5, "status launch failed");
-      HIP_TRY(hipStreamSynchronize(P.d2h));
-      std::memcpy(status, P.h_status, sizeof(status));
+      std::memcpy(status, c->pipe.h_status + 4 * L.status_set, sizeof(status));
     } else {
       HIP_TRY(hipMemcpy(status, c->d_status + 4 * L.status_set, sizeof(status), hipMemcpyDeviceToHost));
     }
@@ -1999,6 +2028,23 @@ static void slot_layout(const ffv1hip_ctx* c, int64_t off[kMaxPlanes], int pst[k
 // spare and outside pass 1, a second frame set and a second packet set, so
 // that batch k+1's frames are copied in while batch k codes and batch k-1's
 // packets are copied out (PCIe both ways beside the kernels).
+// The packed packets of a packet set: the worst case, a full set.
+static int alloc_compact(ffv1hip_ctx* c) {
+  ffv1hip_ctx::HostPipe& P = c->pipe;
+  const int64_t cap = c->packet_stride * c->max_batch;
+  for (int k = 0; k < (c->two_pk ? 2 : 1); k++) {
+    if (P.d_compact[k]) HIP_TRY(hipFree(P.d_compact[k]));
+    P.d_compact[k] = nullptr;
+    if (hipMalloc(&P.d_compact[k], size_t(cap)) != hipSuccess) {
+      (void)hipGetLastError();
+      return set_err(-12, "packed packets of a %d-frame batch (%.1f GB) do not fit in device memory", c->max_batch,
+                     double(cap) / 1e9);
+    }
+    P.d_compact_cap[k] = cap;
+  }
+  return 0;
+}
+
 static int pipe_open(ffv1hip_ctx* c) {
   ffv1hip_ctx::HostPipe& P = c->pipe;
   if (P.on) return 0;
@@ -2040,6 +2086,14 @@ static int pipe_open(ffv1hip_ctx* c) {
       }
     }
   }
+  for (int k = 0; k < (c->two_pk ? 2 : 1); k++) {
+    HIP_TRY(hipHostMalloc(&P.h_sizes[k], sizeof(int64_t) * size_t(c->max_batch), hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&P.hd_sizes[k]), P.h_sizes[k], 0));
+  }
+  HIP_TRY(hipHostMalloc(&P.h_status, sizeof(int) * 8, hipHostMallocMapped));
+  HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&P.hd_status), P.h_status, 0));
+  const int rc = alloc_compact(c);
+  if (rc < 0) return rc;
   P.on = true;
   return 0;
 }
@@ -2146,13 +2200,7 @@ static int copy_packets(ffv1hip_ctx* c, int n, int pk, hipStream_t st, std::vect
   sz.resize(n);
   off.resize(n);
   const double ts0 = P.dbg ? wall_s() : 0;
-  if (!P.h_sizes[pk]) {
-    HIP_TRY(hipHostMalloc(&P.h_sizes[pk], sizeof(int64_t) * size_t(c->max_batch), hipHostMallocMapped));
-    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&P.hd_sizes[pk]), P.h_sizes[pk], 0));
-  }
-  if (launch_sizes_out(c->psize(pk), n, P.hd_sizes[pk], st) < 0) return set_err(-5, "sizes launch failed");
-  HIP_TRY(hipStreamSynchronize(st));
-  std::memcpy(sz.data(), P.h_sizes[pk], sizeof(int64_t) * size_t(n));
+  std::memcpy(sz.data(), P.h_sizes[pk], sizeof(int64_t) * size_t(n));  // the batch is done (hist_done)
   if (P.dbg) P.t_sizes += wall_s() - ts0;
   int64_t total = 0;
   for (int i = 0; i < n; i++) {
@@ -2168,38 +2216,13 @@ static int copy_packets(ffv1hip_ctx* c, int n, int pk, hipStream_t st, std::vect
     P.h_pk_cap[pk] = cap;
   }
   uint8_t* const h = P.h_pk[pk];
-  const uint8_t* const d = c->pkts(pk);
-  // one D2H copy of the packets packed back to back on the device (a copy
-  // per packet runs at a few GB/s); per packet when the packed buffer does
-  // not fit
-  if (total > P.d_compact_cap[pk]) {
-    if (P.d_compact[pk]) HIP_TRY(hipFree(P.d_compact[pk]));
-    P.d_compact[pk] = nullptr;
-    P.d_compact_cap[pk] = 0;
-    const int64_t cap = (total + total / 4 + (int64_t(1) << 20)) & ~int64_t(4095);
-    if (hipMalloc(&P.d_compact[pk], size_t(cap)) == hipSuccess)
-      P.d_compact_cap[pk] = cap;
-    else
-      (void)hipGetLastError();
-  }
-  if (total <= P.d_compact_cap[pk]) {
-    const double tc0 = P.dbg ? wall_s() : 0;
-    if (launch_compact_packets(d, c->packet_stride, c->psize(pk), n, P.d_compact[pk], st) < 0)
-      return set_err(-5, "compact launch failed");
-    if (P.dbg) {
-      HIP_TRY(hipStreamSynchronize(st));
-      P.t_compact += wall_s() - tc0;
-    }
-    const double tc1 = P.dbg ? wall_s() : 0;
-    if (total) HIP_TRY(hipMemcpyAsync(h, P.d_compact[pk], size_t(total), hipMemcpyDeviceToHost, st));
-    if (P.dbg) {
-      HIP_TRY(hipStreamSynchronize(st));
-      P.t_dcopy += wall_s() - tc1;
-    }
-  } else {
-    for (int i = 0; i < n; i++)
-      if (sz[i]) HIP_TRY(hipMemcpyAsync(h + off[i], d + int64_t(i) * c->packet_stride, size_t(sz[i]),
-                                        hipMemcpyDeviceToHost, st));
+  // one D2H copy of the packets the batch packed back to back (a copy per
+  // packet runs at a few GB/s)
+  const double tc1 = P.dbg ? wall_s() : 0;
+  if (total) HIP_TRY(hipMemcpyAsync(h, P.d_compact[pk], size_t(total), hipMemcpyDeviceToHost, st));
+  if (P.dbg) {
+    HIP_TRY(hipStreamSynchronize(st));
+    P.t_dcopy += wall_s() - tc1;
   }
   HIP_TRY(hipStreamSynchronize(st));
   *data = h;
@@ -2227,95 +2250,143 @@ int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides
   if (rc < 0) return rc;
   ffv1hip_ctx::HostPipe& P = c->pipe;
   int64_t used = 0;
-  // A settled batch's packets out, frames base.. of this call: sizes and
-  // packets over PCIe on the d2h stream, then into `out`.  With two sets it
-  // runs on a thread of its own while this one stages the next batch (the
-  // two PCIe directions at once); the threads go in batch order.
+  // Batch b's collector: once the batch is done on the GPU, its packets come
+  // over PCIe into the pinned buffer of its packet set (a thread of its own,
+  // started when the batch is launched, so that this thread only stages
+  // frames).  It is joined two batches later, before batch b + 2 is staged
+  // into b's frame set and launched into b's packet set; the packets then go
+  // into `out` in batch order.  A batch over the slice byte budget is left to
+  // that join: its frames are still in place for the re-encode.
   struct Out {
     std::thread th;
+    int64_t b = -1;  // the batch, -1: none
+    int base = 0, n = 0;
+    bool redo = false;
     int rc = 0;
     std::string err;
-  } ot;
-  auto copy_out = [&, c](int n, int pk, std::vector<int> keys, int base) {
-    std::vector<int64_t> sz, off;
+    std::vector<int64_t> sz;
+    std::vector<int> keys;
     const uint8_t* h = nullptr;
-    const double t0 = wall_s();
-    int r = copy_packets(c, n, pk, P.d2h, sz, off, &h);
-    const double t1 = wall_s();
-    P.t_d2h += t1 - t0;
-    if (r >= 0) {
-      int64_t total = 0;
-      for (int64_t v : sz) total += v;
-      if (out && used + total > out_cap) {
-        r = set_err(-22, "output buffer too small");
-      } else {
-        if (out) pool_copy2d(*P.pool_out, out + used, total, h, total, total, 1);
-        P.t_out += wall_s() - t1;
-        for (int i = 0; i < n; i++) {
-          if (sizes) sizes[base + i] = sz[i];
-          if (key_flags) key_flags[base + i] = keys[i];
-        }
-        used += total;
+  } ot[2];
+  auto collect_async = [&, c](Out& o, int64_t b, int base) {
+    const ffv1hip_ctx::LastBatch& L = c->hist[b & 1];
+    o.b = b;
+    o.base = base;
+    o.n = L.n;
+    o.keys = L.keys;
+    o.redo = false;
+    o.rc = 0;
+    const int pk = L.pk, sset = L.status_set;
+    hipEvent_t const ev = c->hist_done[b & 1];
+    o.th = std::thread([&o, &P, c, ev, pk, sset]() {
+      const double t0 = wall_s();
+      if (hipEventSynchronize(ev) != hipSuccess) {
+        o.rc = set_err(-5, "batch wait failed");
+        o.err = g_err;
+        return;
       }
-    }
-    if (r < 0) {
-      ot.rc = r;
-      ot.err = g_err;
-    }
+      P.t_settle += wall_s() - t0;
+      if (P.h_status[4 * sset]) {  // over the budget: settled at the join
+        o.redo = true;
+        return;
+      }
+      std::vector<int64_t> off;
+      const double t1 = wall_s();
+      const int r = copy_packets(c, o.n, pk, P.d2h, o.sz, off, &o.h);
+      P.t_d2h += wall_s() - t1;
+      if (r < 0) {
+        o.rc = r;
+        o.err = g_err;
+      }
+    });
   };
-  auto join_out = [&]() -> int {
+  // the collected packets of o's batch into `out`
+  auto deliver = [&](Out& o) -> int {
+    int64_t total = 0;
+    for (int64_t v : o.sz) total += v;
+    if (out && used + total > out_cap) return set_err(-22, "output buffer too small");
     const double t0 = wall_s();
-    if (ot.th.joinable()) ot.th.join();
-    P.t_join += wall_s() - t0;
-    if (ot.rc < 0) return set_err(ot.rc, "%s", ot.err.c_str());
+    if (out && total) pool_copy2d(*P.pool, out + used, total, o.h, total, total, 1);
+    P.t_out += wall_s() - t0;
+    for (int i = 0; i < o.n; i++) {
+      if (sizes) sizes[o.base + i] = o.sz[i];
+      if (key_flags) key_flags[o.base + i] = o.keys[i];
+    }
+    used += total;
+    o.b = -1;
     return 0;
   };
-  auto finish = [&](int64_t b, int base, bool async) -> int {
-    const double t0 = wall_s();
-    int r = settle_batch(c, b);
+  // a batch settled (re-encoded if need be) and collected on this thread
+  auto collect_sync = [&](Out& o) -> int {
+    int r = settle_batch(c, o.b);
     if (r < 0) return r;
-    HIP_TRY(hipEventSynchronize(c->hist_done[b & 1]));
-    P.t_settle += wall_s() - t0;
-    const ffv1hip_ctx::LastBatch& L = c->hist[b & 1];
-    if ((r = join_out()) < 0) return r;
-    if (async)
-      ot.th = std::thread(copy_out, L.n, L.pk, L.keys, base);
-    else
-      copy_out(L.n, L.pk, L.keys, base);
-    return ot.rc < 0 ? set_err(ot.rc, "%s", ot.err.c_str()) : 0;
+    HIP_TRY(hipEventSynchronize(c->hist_done[o.b & 1]));
+    const ffv1hip_ctx::LastBatch& L = c->hist[o.b & 1];
+    o.keys = L.keys;
+    std::vector<int64_t> off;
+    return copy_packets(c, o.n, L.pk, P.d2h, o.sz, off, &o.h);
   };
-  int64_t prev = -1;
-  int prev_base = 0;
+  auto join = [&](Out& o) -> int {
+    const double t0 = wall_s();
+    if (o.th.joinable()) o.th.join();
+    P.t_join += wall_s() - t0;
+    return o.rc < 0 ? set_err(o.rc, "%s", o.err.c_str()) : 0;
+  };
+  // batch j - 2's collector (before batch j reuses its sets); a re-encode of
+  // it also re-encodes batch j - 1, whose collector is then redone here
+  auto retire = [&](int64_t b) -> int {
+    Out& o = ot[b & 1];
+    if (o.b != b) return 0;
+    int r = join(o);
+    if (r < 0) return r;
+    if (o.redo) {
+      Out& nx = ot[(b + 1) & 1];
+      if (nx.b == b + 1) {
+        if ((r = join(nx)) < 0) return r;
+      }
+      if ((r = collect_sync(o)) < 0) return r;
+      if (nx.b == b + 1) {
+        if ((r = collect_sync(nx)) < 0) return r;
+        nx.redo = false;
+      }
+    }
+    return deliver(o);
+  };
+  auto cleanup = [&]() {
+    for (Out& o : ot)
+      if (o.th.joinable()) o.th.join();
+  };
   const int fstep = input_planes(c->P) == 4 ? FFV1HIP_PLANES_YUVA : FFV1HIP_PLANES;  // plane pointers per frame
-  // FFV1HIP_COPYOUT_SYNC=1 (measurement hook): the copy-out on this thread
-  static const bool sync_out = std::getenv("FFV1HIP_COPYOUT_SYNC") && std::atoi(std::getenv("FFV1HIP_COPYOUT_SYNC"));
   for (int j = 0, base = 0; base < n_frames; j++, base += c->max_batch) {
     const int n = std::min(c->max_batch, n_frames - base);
-    // set j % 2 was last read by batch j - 2, settled in iteration j - 1
     const int set = P.overlap ? (j & 1) : 0;
+    // batch j's frames and packets go where batch j - 2's were
+    if (P.overlap && (rc = retire(c->nsub - 2)) < 0) break;
     for (int i = 0; i < n && rc >= 0; i++)
       rc = stage_frame(c, set, i, planes + fstep * (base + i), strides + fstep * (base + i));
-    // batch j's packets go where batch j - 2's were: those are out first
-    if (rc >= 0) rc = join_out();
     if (rc >= 0) rc = launch_staged(c, set, n);
-    if (rc >= 0 && !P.overlap) rc = finish(c->nsub - 1, base, false);
-    if (rc >= 0 && P.overlap && prev >= 0) rc = finish(prev, prev_base, !sync_out);
-    if (rc < 0) {
-      (void)join_out();
-      return rc;
+    if (rc < 0) break;
+    Out& o = ot[(c->nsub - 1) & 1];
+    if (P.overlap) {
+      collect_async(o, c->nsub - 1, base);
+    } else {
+      o.b = c->nsub - 1;
+      o.base = base;
+      o.n = n;
+      if ((rc = collect_sync(o)) < 0 || (rc = deliver(o)) < 0) break;
     }
-    prev = c->nsub - 1;
-    prev_base = base;
   }
-  if (P.overlap && prev >= 0) rc = finish(prev, prev_base, false);
-  const int jr = join_out();
+  if (rc >= 0 && P.overlap) {
+    if ((rc = retire(c->nsub - 2)) >= 0) rc = retire(c->nsub - 1);
+  }
+  cleanup();
   if (P.dbg)
     std::fprintf(stderr, "hostdbg: %d frames, %d copy threads: slot wait %.3f s, copy in %.3f s, DMA issue %.3f s, "
-                         "copy-out wait %.3f s, settle %.3f s; copy-out: D2H %.3f s (sizes %.3f, compact %.3f, "
+                         "collector join wait %.3f s, batch wait (collectors) %.3f s; collectors: D2H %.3f s (sizes %.3f, "
                          "copy %.3f), into the buffer %.3f s\n",
                  n_frames, P.pool->size(), P.t_slot, P.t_copy, P.t_dma, P.t_join, P.t_settle, P.t_d2h, P.t_sizes,
-                 P.t_compact, P.t_dcopy, P.t_out);
-  return rc < 0 ? rc : jr;
+                 P.t_dcopy, P.t_out);
+  return rc;
 }
 
 int ffv1hip_encode2_delay(ffv1hip_ctx* c) {
@@ -2393,7 +2464,7 @@ int ffv1hip_encode2(ffv1hip_ctx* c, const void* const planes[4], const int strid
       if (size) *size = R.size[i];
       return set_err(-28, "packet of %lld bytes, buffer %lld", (long long)R.size[i], (long long)out_cap);
     }
-    std::memcpy(out, R.base + R.off[i], size_t(R.size[i]));
+    pool_copy2d(*c->pipe.pool_out, out, R.size[i], R.base + R.off[i], R.size[i], R.size[i], 1);
   }
   if (size) *size = R.size[i];
   if (pts_out) *pts_out = R.pts[i];

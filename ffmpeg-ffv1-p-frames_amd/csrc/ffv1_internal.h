@@ -206,6 +206,7 @@ struct CodeArgs {
   uint2* segrec;              // [segment] {local low at its end, its shifts}
   int64_t digit_cap;          // values of low a slice slot holds (slice_stride / 4)
   int dseg_blocks;            // ffv1_dseg grid
+  int range_prio, dseg_prio;  // wave priorities (s_setprio) of ffv1_range / ffv1_dseg beside the walk (2)
 };
 
 // Pass-1 statistics (ffv1enc.c:190-199): rc_stat[state][bit] from the
@@ -218,6 +219,7 @@ struct StatsArgs {
   DecisionStream ds;
   unsigned long long* rc_stat;   // [256][2]
   unsigned long long* rc_stat2;  // [contexts][32][2]
+  int dense;                     // the records address dense rows (dense_ctx)
 };
 int launch_stats(const StatsArgs& a, bool states, void* stream);
 
@@ -247,7 +249,34 @@ struct WalkArgs {
   const uint8_t* init;        // 2-pass initial states [contexts][32] at keyframes, or null (all 128)
   int nitems, item0;          // set by launch_walk: all items of the batch, the launch's first
   int prio;                   // wave priority (s_setprio)
+  int rows;                   // context rows of a plane group's table in LDS (kDenseRows when dense)
+  int dense;                  // records address dense rows (dense_row), the state tables keep contexts
 };
+
+// Above 8 bits the quantisers of context model 0 have 9 levels (ffv1enc.c:
+// 846-879, quant9_10bit), so only 365 of the 666 contexts q0 + 11 q1 + 121 q2
+// (|q| <= 4, folded) occur.  The frame-parallel path then numbers rows
+// densely, row = q0 + 9 q1 + 81 q2 (folded the same way: the sign of either
+// sum is the sign of its highest nonzero digit), so that a plane group's
+// table in the walk's LDS is 365 x 32 bytes instead of 666 x 32 and five
+// walk waves fit on a CU instead of three.  Persisted / initial states keep
+// the context numbering.
+constexpr int kDenseRows = 365;
+__host__ __device__ inline int dense_ctx(int row) {  // row -> its context
+  const int q0 = (row + 4) % 9 - 4;
+  const int r1 = (row - q0) / 9;
+  const int q1 = (r1 + 4) % 9 - 4;
+  const int q2 = (r1 - q1) / 9;
+  return q0 + 11 * q1 + 121 * q2;
+}
+__host__ __device__ inline int dense_row(int ctx) {  // context -> its row, -1 when it cannot occur
+  const int q0 = (ctx + 5) % 11 - 5;
+  const int r1 = (ctx - q0) / 11;
+  const int q1 = (r1 + 5) % 11 - 5;
+  const int q2 = (r1 - q1) / 11;
+  if (q0 < -4 || q0 > 4 || q1 < -4 || q1 > 4 || q2 < -4 || q2 > 4) return -1;
+  return q0 + 9 * q1 + 81 * q2;
+}
 
 // Kernel 2b: the decision bits, from the chunks' packed words to their place
 // in the decision stream (one block per (frame, slice) stream).
@@ -327,14 +356,14 @@ int launch_layout(const int* dcount, int nstreams, int64_t* dbase, int64_t* tota
 // items [first, first + count) of the batch's walk (count < 0: to the end)
 int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first = 0, int count = -1);
 int walk_items(int nsegs, int nslices);
-int walk_resident(const WalkArgs& a);
+int walk_resident(const WalkArgs& a);  // (uses a.rows)
 int launch_delay(int us, void* stream);
 int launch_range(const CodeArgs& a, void* stream);
 int launch_dseg(const CodeArgs& a, void* stream);
 int launch_dfix(const CodeArgs& a, void* stream);
 int launch_sink(const CodeArgs& a, void* stream);
 int launch_bits(const BitsArgs& a, void* stream);
-int64_t walk_lds_bytes(int64_t state_bytes);
+int64_t walk_lds_bytes(int rows);  // one walk wave's LDS for tables of `rows` context rows
 constexpr int64_t kWalkLdsMax = 64 * 1024;  // states walk: one plane group's table + T9 + staging in LDS
 constexpr int kStreamAlign = 64;            // decisions: every stream starts at a multiple
 int launch_code_golomb(const CodeArgs& a, void* stream);

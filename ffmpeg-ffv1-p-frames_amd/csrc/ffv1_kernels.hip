@@ -946,7 +946,17 @@ __device__ __forceinline__ StreamRef stream_of(const CodeArgs& a, int64_t c) {
 }
 
 constexpr int kRangeThreads = kWave;
+__device__ __forceinline__ void set_prio(int p) {
+  switch (p) {
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    case 3: __builtin_amdgcn_s_setprio(3); break;
+    default: break;
+  }
+}
+
 __global__ __launch_bounds__(kRangeThreads) void ffv1_range(CodeArgs a) {
+  set_prio(a.range_prio);
   const StreamRef sr = stream_of(a, (int64_t)blockIdx.x * kRangeThreads + threadIdx.x);
   const int key = sr.live ? a.keyflags[sr.f] : 0;
   const HdrState h = a.hdr[key * a.nslices + sr.slice];
@@ -1036,6 +1046,7 @@ __device__ __forceinline__ void put_dec(int& low, int& range, DigitOut& o, int s
 }
 
 __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
+  set_prio(a.dseg_prio);
   const int lane = threadIdx.x;
   const int ngroups = a.seg_totals[1];
   for (int w = blockIdx.x; w < ngroups; w += gridDim.x) {
@@ -1275,7 +1286,7 @@ constexpr int kLdsRecs = kLdsN + kT3Bytes;                    // [2][kRecSlots] 
 constexpr int kLdsPre = kLdsRecs + 2 * kRecSlots * 16;        // [2][kPreHalf] recorded states
 constexpr int kLdsFixed = kLdsPre + 2 * kPreHalf;
 
-int64_t walk_lds_bytes_dev(int64_t state_bytes);
+int64_t walk_lds_bytes_dev(int rows);
 
 // Any exponent, one symbol: lane k < 32 of a half applies all decisions of
 // slot k in order (slot 10 takes e-8 exponent decisions beyond e = 9, slot
@@ -1419,7 +1430,7 @@ __device__ __forceinline__ void walk_multi_fill(uint8_t* fixed, const uint4* myr
   }
 }
 
-int64_t walk_lds_bytes_dev(int64_t state_bytes) { return kLdsFixed + 2 * (state_bytes / 2 + 32); }
+int64_t walk_lds_bytes_dev(int rows) { return kLdsFixed + 2 * ((int64_t)rows * 32 + 32); }
 
 // The 8-byte record in HBM (ffv1_symbols) as the walk's step reads it from
 // LDS: the slot codes (y, z) follow from the residual in x (slot_codes), so
@@ -1445,9 +1456,10 @@ __device__ __forceinline__ uint4 pick(bool c, uint4 a, uint4 b) {
 
 __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t fixed[kLdsFixed];
-  extern __shared__ __attribute__((aligned(16))) uint8_t tbl[];  // [2][contexts + 1 dummy row][32]
-  const int64_t half = a.state_bytes / 2;  // one plane group's [contexts][32]
-  const int tsz = (int)half + 32;
+  extern __shared__ __attribute__((aligned(16))) uint8_t tbl[];  // [2][rows + 1 dummy row][32]
+  const int64_t half = a.state_bytes / 2;  // one plane group's [contexts][32] in the persisted states
+  const int64_t thalf = (int64_t)a.rows * 32;  // ... and its table in LDS (dense rows: 365 x 32)
+  const int tsz = (int)thalf + 32;
   const int lane = threadIdx.x;
   const int h = lane >> 5, k = lane & 31;
   for (int i = lane; i < kT3Bytes; i += kWalkThreads) {
@@ -1490,21 +1502,21 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   uint4* const myrecs = reinterpret_cast<uint4*>(fixed + kLdsRecs) + h * kRecSlots;
   uint8_t* const stage = fixed + kLdsPre + h * kPreHalf;
   uint4* const stage4 = reinterpret_cast<uint4*>(stage);
-  const int64_t n16 = half / 16;
+  const int64_t n16 = half / 16, t16 = thalf / 16;
   const int64_t goff = grp * half;
+  // where the segment's states come from: the carry, the 2-pass initial
+  // states (a keyframe), or all 128 (ff_ffv1_clear_slice_state); null: 128
+  const uint4* const src = seg.load_states && live
+                               ? reinterpret_cast<const uint4*>(a.persist_in + (int64_t)sl * a.state_bytes + goff)
+                               : reinterpret_cast<const uint4*>(a.init);
+  const uint4 v128 = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
   {
     uint4* const t4 = reinterpret_cast<uint4*>(mytbl);
-    if (seg.load_states && live) {
-      const uint4* src = reinterpret_cast<const uint4*>(a.persist_in + (int64_t)sl * a.state_bytes + goff);
-      for (int64_t i = k; i < n16; i += 32) t4[i] = src[i];
-    } else if (a.init) {  // the segment starts at a keyframe: 2-pass initial states
-      const uint4* src = reinterpret_cast<const uint4*>(a.init);
-      for (int64_t i = k; i < n16; i += 32) t4[i] = src[i];
-    } else {  // the segment starts at a keyframe (ff_ffv1_clear_slice_state)
-      const uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
-      for (int64_t i = k; i < n16; i += 32) t4[i] = v;
+    for (int64_t i = k; i < t16; i += 32) {  // table block i: row i / 2 (dense: its context's)
+      const int64_t si = a.dense ? (int64_t)dense_ctx((int)(i >> 1)) * 2 + (i & 1) : i;
+      t4[i] = src ? src[si] : v128;
     }
-    if (k < 2) t4[n16 + k] = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);  // dummy row
+    if (k < 2) t4[t16 + k] = v128;  // dummy row
   }
   __syncthreads();
 
@@ -1519,7 +1531,7 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   W.msh = k == 31 ? 28 : 12;
   W.mwd = k == 31 ? 2 : 3;
   W.mbase = k == 31 ? 4 : 0;
-  const uint4 nullrec = make_uint4((uint32_t)half, 0xAAAAAAAAu, 0xAAAAAAAAu, 0u);  // dummy row, no decisions
+  const uint4 nullrec = make_uint4((uint32_t)thalf, 0xAAAAAAAAu, 0xAAAAAAAAu, 0u);  // dummy row, no decisions
 
   // The stage of chunk c goes out at the start of chunk c+1, before its
   // loads are issued: vmcnt counts in issue order, so waiting for chunk
@@ -1692,7 +1704,14 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   if (seg.save_states && live) {
     uint4* dst = reinterpret_cast<uint4*>(a.persist_out + (int64_t)sl * a.state_bytes + goff);
     const uint4* t4 = reinterpret_cast<const uint4*>(mytbl);
-    for (int64_t i = k; i < n16; i += 32) dst[i] = t4[i];
+    if (!a.dense) {
+      for (int64_t i = k; i < n16; i += 32) dst[i] = t4[i];
+    } else {  // contexts that cannot occur keep the states the segment started from
+      for (int64_t i = k; i < n16; i += 32) {
+        const int row = dense_row((int)(i >> 1));
+        dst[i] = row >= 0 ? t4[row * 2 + (i & 1)] : (src ? src[i] : v128);
+      }
+    }
   }
   if (a.trace && lane == 0) {
     a.trace[item * 2 + 0] = rt_all;
@@ -1709,7 +1728,7 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
 // Decision-stream layout: stream (frame, slice) i starts at the sum of the
 // earlier streams' lengths: the luma chain, its pad, the chroma chain from
 // chroma_start, its pad (ffv1_internal.h, DecisionStream).
-constexpr int kLayoutThreads = 1024;
+constexpr int kLayoutThreads = 128;  // 2 KB of LDS: it runs beside the walk, which holds the rest
 __global__ __launch_bounds__(kLayoutThreads) void ffv1_layout(const int* dcount, int nstreams, int64_t* dbase,
                                                               int64_t* total, StreamSegs* segs, int* seg_totals,
                                                               int* wmap) {
@@ -2098,7 +2117,8 @@ __global__ __launch_bounds__(kStatsThreads) void ffv1_stats_slots(StatsArgs a) {
   const uint2* r = a.rec + (int64_t)f * a.frame_samples + g.sym_off + g.plane_sym_off[p];
   for (int64_t i = threadIdx.x; i < n; i += kStatsThreads) {
     const uint2 v = r[i];
-    const int ctx = (int)(v.x & 0xFFFFu) >> 5;
+    const int row = (int)(v.x & 0xFFFFu) >> 5;
+    const int ctx = a.dense ? dense_ctx(row) : row;
     const int diff = (int16_t)(v.x >> 16);
     const bool lds = ctx < kStatsLdsCtx;
     uint32_t* hl = h + ctx * 64;
@@ -2350,11 +2370,11 @@ int launch_dfix(const CodeArgs& a, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int64_t walk_lds_bytes(int64_t state_bytes) { return walk_lds_bytes_dev(state_bytes); }
+int64_t walk_lds_bytes(int rows) { return walk_lds_bytes_dev(rows); }
 
 int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first, int count) {
-  if (walk_lds_bytes_dev(a.state_bytes) > kWalkLdsMax) return -1;
-  const size_t dyn = (size_t)(2 * (a.state_bytes / 2 + 32));  // the tables; the fixed part is static
+  if (walk_lds_bytes_dev(a.rows) > kWalkLdsMax || a.rows * 32 > 0xFFFF) return -1;
+  const size_t dyn = (size_t)(2 * ((int64_t)a.rows * 32 + 32));  // the tables; the fixed part is static
   WalkArgs b = a;
   b.nitems = nsegs * ((a.nslices + 1) / 2) * 2;
   if (count < 0) count = b.nitems - first;
@@ -2368,7 +2388,7 @@ int walk_items(int nsegs, int nslices) { return nsegs * ((nslices + 1) / 2) * 2;
 
 // Walk waves one CU holds at once (LDS-bound), for launch splitting.
 int walk_resident(const WalkArgs& a) {
-  const size_t dyn = (size_t)(2 * (a.state_bytes / 2 + 32));
+  const size_t dyn = (size_t)(2 * ((int64_t)a.rows * 32 + 32));
   int per_cu = 0, dev = 0, cus = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ffv1_walk, kWalkThreads, dyn) != hipSuccess ||
       hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
