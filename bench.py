@@ -14,8 +14,8 @@ Multi-GPU: one process per GPU over ONE clip of N x gops GOPs: rank r encodes
 GOPs r, r+N, r+2N, ... (GOPs are independent: keyframes reset every context
 state, ffv1enc.c:1171-1172), no data-path collective; value = all frames of
 all ranks / max-over-ranks time.  After the timed steps the per-GOP packet
-digests are gathered on rank 0 (a digest of the first 21 GOPs that does not
-depend on N), the packets of the pinned frames are gathered from the ranks
+digests are gathered on rank 0 (a digest of the first config-default count
+of GOPs that does not depend on N), the packets of the pinned frames are gathered from the ranks
 that own them and checked against the reference's MD5, and every rank
 decodes its own packets with the GPU decoder.
 """
@@ -40,7 +40,7 @@ W, H, PIX_FMT, SLICES, GOP = 3840, 2160, "yuv420p10", 64, 12
 # lossless round trip (and c2 also by the reference's MD5 pin).
 CONFIGS = {
     "c3": dict(W=3840, H=2160, PIX_FMT="yuv420p10", SLICES=64, GOP=12, BPR=0, DEPTH=10, C444=False,
-               GRID=False, GOPS=21, PIN=("08e3975d4d0f5f2e5c82cd4037764789", 24),
+               GRID=False, GOPS=20, PIN=("08e3975d4d0f5f2e5c82cd4037764789", 24),  # 20 GOPs: 1280 walk waves, one round
                metric="Mpixels/s encoded (bit-exact) 4K yuv420p10 FFV1 P-frames",
                workload="4K 3840x2160 yuv420p10le, coder=1 (range, custom table), slices=64, keyint=12 P-frames"),
     "c2": dict(W=1920, H=1080, PIX_FMT="yuv420p", SLICES=24, GOP=1, BPR=0, DEPTH=8, C444=False,
@@ -234,10 +234,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)  # the pipelines fill and drain once per run
     ap.add_argument("--warmup", type=int, default=1)
-    # 21 GOPs = 252 frames per batch: 252 coder waves (one per frame of each
-    # slice) fit the CUs beside the states walk of the next batch
+    # c3: 20 GOPs = 240 frames per batch: 1280 walk waves, all resident at
+    # once (5 per CU with the dense context rows), one walk round per batch
     ap.add_argument("--gops", type=int, default=0,
-                    help="GOPs per rank per step (default: 21 for c3, see CONFIGS)")
+                    help="GOPs per rank per step (default: 20 for c3, see CONFIGS)")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c3",
                     help="BASELINE config: c3 (the metric's, default), c2, c4, c5")
     ap.add_argument("--data", choices=("d1", "d2"), default="d1")

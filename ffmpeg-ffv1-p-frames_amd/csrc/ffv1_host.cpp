@@ -420,8 +420,10 @@ struct ffv1hip_ctx {
   // stride over the work): a grid of one block per item fills every SIMD's
   // wave slots and registers, and walk waves launched meanwhile wait for CU
   // room until those blocks retire (FFV1HIP_SYM_GRID / _BITS_GRID / _DSEG_GRID)
-  int grid_sym = 3072, grid_bits = 1024, grid_dseg = 3072;
-  int prio_range = 0, prio_dseg = 0;  // FFV1HIP_RANGE_PRIO / FFV1HIP_DSEG_PRIO (the walk's is 2)
+  int grid_sym = 4096, grid_bits = 2048, grid_dseg = 4096;
+  // wave priorities (s_setprio): the coder's serial range pass above the rest
+  // (FFV1HIP_RANGE_PRIO / FFV1HIP_DSEG_PRIO / FFV1HIP_WALK_PRIO)
+  int prio_range = 3, prio_dseg = 0;
   SliceGeom* d_geom = nullptr;
   int* d_slot_frames = nullptr;  // [j][slot]
   int* d_status = nullptr;       // [set][4]: [0] slices over budget, [1] most bytes one needed
@@ -1662,7 +1664,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     wa.scratch = c->d_scratch;
     static const bool force_multi = std::getenv("FFV1HIP_FORCE_MULTI") && std::atoi(std::getenv("FFV1HIP_FORCE_MULTI"));
     wa.force_multi = force_multi;
-    static const int walk_prio = std::getenv("FFV1HIP_WALK_PRIO") ? std::atoi(std::getenv("FFV1HIP_WALK_PRIO")) : 2;
+    static const int walk_prio = std::getenv("FFV1HIP_WALK_PRIO") ? std::atoi(std::getenv("FFV1HIP_WALK_PRIO")) : 0;
     wa.prio = walk_prio;
     wa.init = c->d_init;
     wa.rows = c->walk_rows;

@@ -1551,14 +1551,9 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
     stage4[0] = t;
   };
 
-  // the walk is the longer of the two pipelines it overlaps with (the coder
-  // of the previous batch): it wins the VALU arbitration on a shared SIMD
-  switch (a.prio) {  // wave priority (FFV1HIP_WALK_PRIO, default 2)
-    case 0: __builtin_amdgcn_s_setprio(0); break;
-    case 1: __builtin_amdgcn_s_setprio(1); break;
-    case 3: __builtin_amdgcn_s_setprio(3); break;
-    default: __builtin_amdgcn_s_setprio(2); break;
-  }
+  // wave priority (FFV1HIP_WALK_PRIO, default 0: with the walk in one round
+  // the coder's range pass is the longer chain and runs above it)
+  set_prio(a.prio);
   uint64_t t_loop = 0, n_steps = 0;
   const uint64_t t_all = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
   const uint64_t rt_all = a.dbg || a.trace ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz: the wave's shader clock
