@@ -1075,45 +1075,45 @@ __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
     const uint4* P = reinterpret_cast<const uint4*>(a.ds.pre + pb);
     const uint32_t* B = a.ds.bits + (pb >> 5);
     const int nmax = wave_max(n);
+    // Blocks of 128 decisions: a whole 128-byte line of states and four
+    // bit words per lane, the next block's loaded while this one codes.  The
+    // 64 lanes of a wave read 64 segments 4 KB apart, so a line read 16 or
+    // 32 bytes at a time was fetched from HBM again for each part (PMC:
+    // 185 GB per launch for 34 GB of states and bits).
     const uint4 z4 = make_uint4(0, 0, 0, 0);
-    uint4 na = z4, nb = z4, ma = z4, mb = z4;
-    uint32_t nw = 0u, mw = 0u;
-    if (n > 0) {
-      na = P[0];
-      nb = P[1];
-      nw = B[0];
-    }
-    if (n > 32) {
-      ma = P[2];
-      mb = P[3];
-      mw = B[1];
-    }
-    for (int i = 0; i < nmax; i += 32) {
-      uint4 wa = na, wb = nb;
-      uint32_t bw = nw;
-      na = ma;
-      nb = mb;
-      nw = mw;
-      if (i + 64 < n) {
-        ma = P[(i >> 4) + 4];
-        mb = P[(i >> 4) + 5];
-        mw = B[(i >> 5) + 2];
-      }
-      const int rem = n - i;
-      if (rem < 32) {
-        wa = tail_mask(wa, rem);
-        wb = tail_mask(wb, rem - 16);
-        bw = rem > 0 ? bw & ((1u << rem) - 1u) : 0u;
-      }
-      static_for<0, 4>([&](auto gc) {
-        constexpr int G = decltype(gc)::value;
-        const Masks8 k = masks8<G>(bw);
-        static_for<0, 8>([&](auto jc) {
-          constexpr int J = 8 * G + decltype(jc)::value;
-          const uint32_t sw = state_word<J>(wa, wb);
-          put_dec(low, range, o, (int)((sw >> ((J & 3) * 8)) & 0xFFu), k.m[J & 7]);
+    uint4 cur[8], nxt[8];
+    uint32_t cbw[4], nbw[4];
+    auto fetch = [&](int blk, uint4* q, uint32_t* w) {
+      static_for<0, 8>([&](auto jc) { q[decltype(jc)::value] = P[blk * 8 + decltype(jc)::value]; });
+      static_for<0, 4>([&](auto jc) { w[decltype(jc)::value] = B[blk * 4 + decltype(jc)::value]; });
+    };
+    static_for<0, 8>([&](auto jc) { cur[decltype(jc)::value] = nxt[decltype(jc)::value] = z4; });
+    static_for<0, 4>([&](auto jc) { cbw[decltype(jc)::value] = nbw[decltype(jc)::value] = 0u; });
+    if (n > 0) fetch(0, cur, cbw);  // (parts are padded: reads stay inside the stream)
+    for (int i = 0; i < nmax; i += 128) {
+      if (i + 128 < n) fetch((i >> 7) + 1, nxt, nbw);
+      static_for<0, 4>([&](auto sc) {
+        constexpr int S = decltype(sc)::value;
+        uint4 wa = cur[2 * S], wb = cur[2 * S + 1];
+        uint32_t bw = cbw[S];
+        const int rem = n - (i + 32 * S);
+        if (rem < 32) {
+          wa = tail_mask(wa, rem);
+          wb = tail_mask(wb, rem - 16);
+          bw = rem > 0 ? bw & ((1u << rem) - 1u) : 0u;
+        }
+        static_for<0, 4>([&](auto gc) {
+          constexpr int G = decltype(gc)::value;
+          const Masks8 k = masks8<G>(bw);
+          static_for<0, 8>([&](auto jc) {
+            constexpr int J = 8 * G + decltype(jc)::value;
+            const uint32_t sw = state_word<J>(wa, wb);
+            put_dec(low, range, o, (int)((sw >> ((J & 3) * 8)) & 0xFFu), k.m[J & 7]);
+          });
         });
       });
+      static_for<0, 8>([&](auto jc) { cur[decltype(jc)::value] = nxt[decltype(jc)::value]; });
+      static_for<0, 4>([&](auto jc) { cbw[decltype(jc)::value] = nbw[decltype(jc)::value]; });
     }
     if (last) {  // a 0 on state 129, then ff_rac_terminate (ffv1enc.c:1331-1334, rangecoder.c:104-116)
       {  // the trailer decision: at most one shift
