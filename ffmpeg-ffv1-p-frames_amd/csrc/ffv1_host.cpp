@@ -415,7 +415,6 @@ struct ffv1hip_ctx {
   hipEvent_t walk_a = nullptr;               // the first part of the last batch's walk is done
   hipEvent_t walk_go = nullptr;              // everything before the last batch's walk is done (it starts)
   bool walk_a_valid = false;
-  std::vector<uint32_t> cu_walk, cu_side;  // FFV1HIP_RESERVE_CUS: CU masks of the walk's and the side streams
   // grid caps of the kernels that run beside the states walk (their blocks
   // stride over the work): a grid of one block per item fills every SIMD's
   // wave slots and registers, and walk waves launched meanwhile wait for CU
@@ -1029,25 +1028,6 @@ static int alloc_device(ffv1hip_ctx* c) {
                      (long long)fit);
     }
   }
-  // FFV1HIP_RESERVE_CUS=R: R CUs, spread over the chip (every ncu / R-th),
-  // run the next batch's symbols, layout and bits (bits_stream), the other
-  // CUs the states walk (stream); the coder's stream may use all.  The walk
-  // then never shares a CU's LDS with the symbols kernel, and the symbols of
-  // batch k+1 run beside the whole walk of batch k.
-  {
-    static const int reserve = std::getenv("FFV1HIP_RESERVE_CUS") ? std::atoi(std::getenv("FFV1HIP_RESERVE_CUS")) : 0;
-    int ncu = 0;
-    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
-    if (reserve > 0 && reserve < ncu) {
-      c->cu_walk.assign((ncu + 31) / 32, 0u);
-      c->cu_side.assign((ncu + 31) / 32, 0u);
-      const int every = std::max(1, ncu / reserve);
-      for (int i = 0; i < ncu; i++) {
-        const bool side = i % every == every - 1 && i / every < reserve;
-        (side ? c->cu_side : c->cu_walk)[i / 32] |= 1u << (i % 32);
-      }
-    }
-  }
   {
     auto knob = [](const char* name, int dflt) {
       const char* e = std::getenv(name);
@@ -1059,10 +1039,7 @@ static int alloc_device(ffv1hip_ctx* c) {
     c->prio_range = knob("FFV1HIP_RANGE_PRIO", c->prio_range);
     c->prio_dseg = knob("FFV1HIP_DSEG_PRIO", c->prio_dseg);
   }
-  if (!c->cu_walk.empty())
-    HIP_TRY(hipExtStreamCreateWithCUMask(&c->stream, uint32_t(c->cu_walk.size() * 32), c->cu_walk.data()));
-  else
-    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   for (hipEvent_t& e : c->hist_done) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_TRY(hipMalloc(&c->d_qt, sizeof(c->qt)));
   HIP_TRY(hipMemcpy(c->d_qt, c->qt, sizeof(c->qt), hipMemcpyHostToDevice));
@@ -1122,10 +1099,7 @@ static int alloc_device(ffv1hip_ctx* c) {
       HIP_TRY(hipMemcpy(c->d_ident, ident.data(), sizeof(int) * size_t(nb), hipMemcpyHostToDevice));
     }
     HIP_TRY(hipStreamCreateWithFlags(&c->code_stream, hipStreamNonBlocking));
-    if (!c->cu_side.empty())
-      HIP_TRY(hipExtStreamCreateWithCUMask(&c->bits_stream, uint32_t(c->cu_side.size() * 32), c->cu_side.data()));
-    else
-      HIP_TRY(hipStreamCreateWithFlags(&c->bits_stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&c->bits_stream, hipStreamNonBlocking));
     for (hipEvent_t& e : c->laid) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->bitsed) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->walked) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1483,7 +1457,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     // ... and start with the previous batch's walk: their bounded grids (no
     // LDS but a few hundred bytes per block) leave every CU the room its
     // three walk waves need, so the walk is never held back by them
-    if (c->walk_a_valid && c->cu_side.empty()) HIP_TRY(hipStreamWaitEvent(sst, c->walk_go, 0));
+    if (c->walk_a_valid) HIP_TRY(hipStreamWaitEvent(sst, c->walk_go, 0));
   }
   // the previous batch (possibly on another stream) is done with what this
   // one rewrites first: segments, slot lists, keyflags, the persist buffer
@@ -1694,12 +1668,10 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     const int nitems = walk_items(nsegs, c->nslices);
     // FFV1HIP_WALK_PART_A (test hook, read per batch): the first part's waves
     const char* pa = std::getenv("FFV1HIP_WALK_PART_A");
-    const int first = sst != st && split_env && c->cu_side.empty() ? (pa ? std::atoi(pa) : walk_resident(wa)) : 0;
-    // ... and only when the second part leaves room on the CUs for the
-    // symbols beside it (c3: 576 of 768 slots; c5's 768 of 768 ran slower)
-    // (FFV1HIP_SPLIT_MAX: that share in percent, default 80)
-    const int split_max = std::getenv("FFV1HIP_SPLIT_MAX") ? std::atoi(std::getenv("FFV1HIP_SPLIT_MAX")) : 80;
-    const bool two_parts = first > 0 && first < nitems && int64_t(nitems - first) * 100 <= int64_t(first) * split_max;
+    const int first = sst != st && split_env ? (pa ? std::atoi(pa) : walk_resident(wa)) : 0;
+    // ... and only when the second part leaves room on the CUs beside it
+    // (at most 80 % of the resident slots: c5's 100 % ran slower in round 2)
+    const bool two_parts = first > 0 && first < nitems && (pa || int64_t(nitems - first) * 100 <= int64_t(first) * 80);
     HIP_TRY(hipEventRecord(c->walk_go, st));
     if (timed(2, st, [&] {
           if (!two_parts) return launch_walk(wa, nsegs, st);

@@ -357,7 +357,6 @@ int launch_layout(const int* dcount, int nstreams, int64_t* dbase, int64_t* tota
 int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first = 0, int count = -1);
 int walk_items(int nsegs, int nslices);
 int walk_resident(const WalkArgs& a);  // (uses a.rows)
-int launch_delay(int us, void* stream);
 int launch_range(const CodeArgs& a, void* stream);
 int launch_dseg(const CodeArgs& a, void* stream);
 int launch_dfix(const CodeArgs& a, void* stream);

@@ -2393,19 +2393,6 @@ int walk_resident(const WalkArgs& a) {
   return per_cu * cus;
 }
 
-// A one-wave wait of `us` microseconds (s_memrealtime: 100 MHz), in front of
-// a kernel that should start only after the kernels that became ready with
-// it have their waves on the CUs.
-__global__ __launch_bounds__(64) void ffv1_delay(int64_t ticks) {
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) __builtin_amdgcn_s_sleep(127);
-}
-
-int launch_delay(int us, void* stream) {
-  hipLaunchKernelGGL(ffv1_delay, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), (int64_t)us * 100);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
 int launch_bits(const BitsArgs& a, void* stream) {
   const int64_t streams = (int64_t)a.nslices * a.nframes;
   const int64_t grid = a.max_blocks > 0 ? std::min<int64_t>(streams, a.max_blocks) : streams;

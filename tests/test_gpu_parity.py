@@ -85,7 +85,6 @@ def test_split_walk_matches_oracle(stream, recsets, monkeypatch):
     it): the same bytes as the oracle across batches."""
     monkeypatch.setenv("FFV1HIP_RECSETS", str(recsets))
     monkeypatch.setenv("FFV1HIP_WALK_PART_A", "3")
-    monkeypatch.setenv("FFV1HIP_SPLIT_MAX", "100000")
     frames = list(stream.frames())
     _, ex_ref, ref = oracle_encode(stream, frames)
     ex, got = hip_encode(stream, frames, batch=4)
