@@ -177,6 +177,31 @@ def test_state_forwarding_between_contexts(split):
     assert [k for _, k in head + tail] == [True] + [False] * 8
 
 
+def test_dense_rows_keep_packets_and_carried_states(monkeypatch):
+    """Above 8 bits the walk numbers the 365 reachable contexts densely
+    (ffv1_internal.h, dense_ctx / dense_row).  The packets, and the P-frame
+    carry exported mid-GOP (ffv1hip_get_slice_states, context numbering, the
+    contexts that cannot occur at their initial 128), equal those of the
+    context-numbered walk (FFV1HIP_DENSE=0) and of the chained coder."""
+    from ffv1hip import HipEncoder
+    s = Stream("dense", 320, 180, "yuv420p10", 7, slices=6, gop_size=12, source="d2", depth=10)
+    frames = list(s.frames())
+    _, _, ref = oracle_encode(s, frames)
+    states = {}
+    for mode, env in [("dense", {}), ("contexts", {"FFV1HIP_DENSE": "0"}), ("chain", {"FFV1HIP_CODER": "chain"})]:
+        for k in ("FFV1HIP_DENSE", "FFV1HIP_CODER"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        enc = HipEncoder(hip_params(s), 0, 7)
+        got = enc.encode(frames[:5])
+        states[mode] = bytes(enc.get_slice_states())
+        got += enc.encode(frames[5:])
+        enc.close()
+        assert got == ref, mode
+    assert states["dense"] == states["contexts"] == states["chain"]
+
+
 def test_batch_ending_in_one_frame_segment():
     """A batch that starts mid-GOP (its first segment loads the carried
     states) and ends with a one-frame segment (which saves them): load and
