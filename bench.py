@@ -48,11 +48,11 @@ CONFIGS = {
                metric="Mpixels/s encoded (bit-exact) 1080p yuv420p FFV1 intra",
                workload="1080p 1920x1080 yuv420p, coder=1 (range, custom table), slices=24, intra-only"),
     "c4": dict(W=3840, H=2160, PIX_FMT="yuv444p16", SLICES=64, GOP=12, BPR=12, DEPTH=16, C444=True,
-               GRID=False, GOPS=16, PIN=None,  # 16: fastest that fits (12: 5.1, 14: 5.0, 16: 5.6, 17: 4.8 Gpix/s)
+               GRID=False, GOPS=19, PIN=None,  # 19: the most that fit (20 needs 296.2 of 296.5 GB); 16: 5.5 Gpix/s
                metric="Mpixels/s encoded (lossless) 4K yuv444p12 FFV1 P-frames",
                workload="4K 3840x2160 yuv444p16le + bits_per_raw_sample=12, coder=1, slices=64, keyint=12 P-frames"),
     "c5": dict(W=7680, H=4320, PIX_FMT="yuv420p10", SLICES=256, GOP=12, BPR=0, DEPTH=10, C444=False,
-               GRID=True, GOPS=6, PIN=None,
+               GRID=True, GOPS=5, PIN=None,  # 5 GOPs = 1280 walk waves, one round (6: 12.9 vs 14.7 Gpix/s)
                metric="Mpixels/s encoded (lossless) 8K yuv420p10 FFV1 P-frames",
                workload="8K 7680x4320 yuv420p10le, coder=1, slices=256 (16x16 grid), keyint=12 P-frames"),
 }
@@ -464,7 +464,9 @@ def main():
             "cpu_baseline": cpu,
             "decode_selfcheck": decode,
         }
-        print(json.dumps(res), flush=True)
+        # on a line of its own: a process group's connection chatter on stdout
+        # (gloo) may have left a partial line
+        print("\n" + json.dumps(res), flush=True)
     enc.close()
     if dist:
         dist.destroy_process_group()
