@@ -1652,8 +1652,6 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     static const char* const wp_env = std::getenv("FFV1HIP_WALK_PRIO");
     static const char* const rp_env = std::getenv("FFV1HIP_RANGE_PRIO");
     wa.prio = wp_env ? std::atoi(wp_env) : (range_first ? 0 : 2);
-    static const char* const lb_env = std::getenv("FFV1HIP_WALK_LONG_BOOST");
-    wa.long_boost = lb_env ? std::atoi(lb_env) : 0;
     const int range_prio = rp_env ? std::atoi(rp_env) : (range_first ? 3 : 0);
     wa.init = c->d_init;
     wa.rows = c->walk_rows;

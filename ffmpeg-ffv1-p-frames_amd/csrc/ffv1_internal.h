@@ -249,7 +249,6 @@ struct WalkArgs {
   const uint8_t* init;        // 2-pass initial states [contexts][32] at keyframes, or null (all 128)
   int nitems, item0;          // set by launch_walk: all items of the batch, the launch's first
   int prio;                   // wave priority (s_setprio)
-  int long_boost;             // ... plus this for the longer plane group's waves
   int rows;                   // context rows of a plane group's table in LDS (kDenseRows when dense)
   int dense;                  // records address dense rows (dense_row), the state tables keep contexts
 };

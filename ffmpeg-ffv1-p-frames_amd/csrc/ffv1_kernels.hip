@@ -1553,9 +1553,7 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
 
   // wave priority (FFV1HIP_WALK_PRIO, default 0: with the walk in one round
   // the coder's range pass is the longer chain and runs above it)
-  // the longer plane group's waves one level up: with every chain resident
-  // the walk lasts as long as those, the shorter group has slack
-  set_prio(min(3, a.prio + (grp == (chroma_first ? 1 : 0) ? a.long_boost : 0)));
+  set_prio(a.prio);
   uint64_t t_loop = 0, n_steps = 0;
   const uint64_t t_all = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
   const uint64_t rt_all = a.dbg || a.trace ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz: the wave's shader clock
