@@ -114,10 +114,14 @@ def cpu_threads():
 def cpu_baseline(frames, threads):
     """The CPU oracle (a port of the reference encoder, oracle/) on host cores.
 
-    GOP-sharded, the strongest CPU configuration: each worker
-    thread encodes one whole GOP of the batch (1 key + 11 P frames) with its
-    own encoder; ctypes drops the GIL, so the threads run in parallel.  Plus a
-    one-thread run of one GOP.  Bounded sample: one GOP per thread.
+    `value`: GOP-sharded, the strongest CPU configuration:
+    each worker thread encodes whole GOPs (1 key + 11 P frames) with its own
+    encoder; ctypes drops the GIL, so the threads run in parallel.  When the
+    batch has fewer GOPs than threads (c5: 5 GOPs), each GOP's slices are
+    coded on threads // GOPs threads, so every core works.  Plus the
+    reference's own threading model, one job per slice on min(cores, slices)
+    threads over one GOP (`slice_threaded`, ffv1enc.c:1323), and a one-thread
+    run of one GOP.  Bounded sample: one GOP per GOP worker.
     """
     sys.path.insert(0, ROOT)
     from oracle import oracle
@@ -127,30 +131,39 @@ def cpu_baseline(frames, threads):
     else:
         cfg = oracle.configure(W, H, PIX_FMT, slices=SLICES, coder=1, gop_size=GOP,
                                bits_per_raw_sample=BPR)
+    nslices = cfg.num_h_slices * cfg.num_v_slices
     per = max(GOP, 1)
     ngops = len(frames) // per
-    threads = max(1, min(threads, ngops))
+    workers = max(1, min(threads, ngops))
+    inner = max(1, threads // workers)  # slice threads per GOP worker
 
-    def one(g):
+    def one(g, th=1):
         enc = oracle.Encoder(cfg)
         for f in frames[g * per:(g + 1) * per]:
-            enc.encode(f)
+            enc.encode(f, threads=th)
 
     t0 = time.perf_counter()
     one(0)
     single = per * W * H / (time.perf_counter() - t0) / 1e6
-    ths = [threading.Thread(target=one, args=(g,)) for g in range(threads)]
+    sl_threads = max(1, min(threads, nslices))
+    t0 = time.perf_counter()
+    one(0, sl_threads)
+    slice_mt = per * W * H / (time.perf_counter() - t0) / 1e6
+    ths = [threading.Thread(target=one, args=(g, inner)) for g in range(workers)]
     t0 = time.perf_counter()
     for t in ths:
         t.start()
     for t in ths:
         t.join()
-    multi = threads * per * W * H / (time.perf_counter() - t0) / 1e6
+    multi = workers * per * W * H / (time.perf_counter() - t0) / 1e6
     return {
-        "value": round(multi, 3), "unit": "Mpixels/s", "cores": threads, "kind": "port",
-        "sample": f"{threads} threads x 1 GOP ({per} frames) each of the same {W}x{H} {PIX_FMT} "
-                  f"clip, oracle/ffv1_oracle.c, GOP-sharded",
+        "value": round(multi, 3), "unit": "Mpixels/s", "cores": workers * inner, "kind": "port",
+        "sample": f"{workers} GOP workers x {inner} slice thread(s), 1 GOP ({per} frames) each of the same "
+                  f"{W}x{H} {PIX_FMT} clip, oracle/ffv1_oracle.c, GOP-sharded",
         "host_cpus": os.cpu_count(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+        "slice_threaded": {"value": round(slice_mt, 3), "cores": sl_threads,
+                           "sample": f"1 GOP ({per} frames), one job per slice on {sl_threads} threads "
+                                     f"(the reference's threading, ffv1enc.c:1323)"},
         "single_thread": {"value": round(single, 3), "cores": 1, "sample": f"1 GOP ({per} frames)"},
         "port_vs_reference": "the port runs at ~0.6x the reference ffmpeg single-threaded on the "
                              "same 8-core host (12 vs 20.1 Mpix/s, BASELINE.md / DESIGN.md)",
@@ -220,8 +233,8 @@ def spawn_ranks(n: int, script: str = "", argv=None) -> int:
 
 
 def load_bench_golden(name):
-    """Per-GOP oracle digests of this config's D1 clip (tests/golden/bench_gops.json,
-    tools/make_bench_golden.py), or None."""
+    """Per-GOP oracle digests of a config's clip (tests/golden/bench_gops.json,
+    tools/make_bench_golden.py; key <config> for D1, <config>_d2 for D2), or None."""
     path = os.path.join(ROOT, "tests", "golden", "bench_gops.json")
     try:
         return json.load(open(path)).get(name)
@@ -365,7 +378,7 @@ def main():
     # every timed GOP against the oracle's digest of the same GOP (the last
     # step's packets: every step re-encodes the same batch)
     vs_oracle = None
-    golden = load_bench_golden(args.config) if args.data == "d1" else None
+    golden = load_bench_golden(args.config if args.data == "d1" else f"{args.config}_d2")
     if golden:
         ref = golden["gops"]
         checked = [g for g in sorted(all_digest) if g < len(ref)]

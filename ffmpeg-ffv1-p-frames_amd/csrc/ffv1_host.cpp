@@ -106,6 +106,62 @@ class CopyPool {
   bool stop_ = false;
 };
 
+// Measurement and test hooks, all in one variable, read when a context is
+// created (so each context sees the value set at its creation, and nothing is
+// cached in function statics):
+//   FFV1HIP_DEBUG="name[=value],name[=value],..."
+// measurement: serial, walkdbg, walktrace, hostdbg; schedule (defaults are
+// the measured best): walk_prio, range_prio, dseg_prio, sym_grid, bits_grid,
+// dseg_grid, walk_split=0, copy_threads, dec_swap=0; test hooks: coder=chain,
+// dense=0, recsets=1, slice_cap, walk_part_a, force_multi.  Unknown names
+// are an error at create time, so a misspelt hook never silently measures
+// the default.
+struct Knobs {
+  std::vector<std::pair<std::string, std::string>> kv;
+  const std::string* find(const char* name) const {
+    for (const auto& e : kv)
+      if (e.first == name) return &e.second;
+    return nullptr;
+  }
+  bool has(const char* name) const { return find(name) != nullptr; }
+  // "name" alone reads as 1
+  int get(const char* name, int dflt) const {
+    const std::string* v = find(name);
+    return v ? (v->empty() ? 1 : std::atoi(v->c_str())) : dflt;
+  }
+  std::string str(const char* name) const {
+    const std::string* v = find(name);
+    return v ? *v : std::string();
+  }
+};
+
+static const char* const kKnobNames[] = {"serial",     "walkdbg",    "walktrace", "hostdbg",   "walk_prio",
+                                         "range_prio", "dseg_prio",  "sym_grid",  "bits_grid", "dseg_grid",
+                                         "walk_split", "copy_threads", "dec_swap", "coder",    "dense",
+                                         "recsets",    "slice_cap",  "walk_part_a", "force_multi"};
+
+static int parse_knobs(Knobs* k) {
+  k->kv.clear();
+  const char* e = std::getenv("FFV1HIP_DEBUG");
+  if (!e) return 0;
+  std::string all(e);
+  size_t i = 0;
+  while (i <= all.size()) {
+    size_t j = all.find(',', i);
+    if (j == std::string::npos) j = all.size();
+    std::string item = all.substr(i, j - i);
+    i = j + 1;
+    if (item.empty()) continue;
+    const size_t eq = item.find('=');
+    std::string name = item.substr(0, eq), val = eq == std::string::npos ? "" : item.substr(eq + 1);
+    bool known = false;
+    for (const char* n : kKnobNames) known |= name == n;
+    if (!known) return set_err(-22, "FFV1HIP_DEBUG: unknown hook '%s'", name.c_str());
+    k->kv.emplace_back(name, val);
+  }
+  return 0;
+}
+
 double wall_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -316,6 +372,7 @@ struct OpList {
 
 // ---------------------------------------------------------------------------
 struct ffv1hip_ctx {
+  Knobs knobs;  // FFV1HIP_DEBUG at create time
   ffv1hip_params P{};
   int device = 0;
   int max_batch = 0;
@@ -1026,16 +1083,10 @@ static int alloc_device(ffv1hip_ctx* c) {
                      (long long)fit);
     }
   }
-  {
-    auto knob = [](const char* name, int dflt) {
-      const char* e = std::getenv(name);
-      return e ? std::atoi(e) : dflt;
-    };
-    c->grid_sym = knob("FFV1HIP_SYM_GRID", c->grid_sym);
-    c->grid_bits = knob("FFV1HIP_BITS_GRID", c->grid_bits);
-    c->grid_dseg = std::max(1, knob("FFV1HIP_DSEG_GRID", c->grid_dseg));
-    c->prio_dseg = knob("FFV1HIP_DSEG_PRIO", c->prio_dseg);
-  }
+  c->grid_sym = c->knobs.get("sym_grid", c->grid_sym);
+  c->grid_bits = c->knobs.get("bits_grid", c->grid_bits);
+  c->grid_dseg = std::max(1, c->knobs.get("dseg_grid", c->grid_dseg));
+  c->prio_dseg = c->knobs.get("dseg_prio", c->prio_dseg);
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   for (hipEvent_t& e : c->hist_done) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_TRY(hipMalloc(&c->d_qt, sizeof(c->qt)));
@@ -1122,14 +1173,13 @@ static int alloc_device(ffv1hip_ctx* c) {
     for (int k = 0; k < 2; k++)
       if (grow_decisions(c, k, cap) < 0) return -5;
     // the second records set, only with room to spare (a later batch may
-    // still grow the decision buffers); FFV1HIP_RECSETS=1 keeps one set
-    const char* rs = std::getenv("FFV1HIP_RECSETS");
+    // still grow the decision buffers); the recsets=1 hook keeps one set
     const size_t rec_bytes = sizeof(uint2) * size_t(c->frame_samples) * nb;
     const size_t cb_bytes = sizeof(uint32_t) * kChunkWords * size_t(c->frame_chunks) * nb;
     size_t free_b = 0, total_b = 0;
     HIP_TRY(hipMemGetInfo(&free_b, &total_b));
     const size_t margin = (size_t(c->dcap[0]) + size_t(c->dcap[1])) / 4 + (size_t(4) << 30);
-    if (!(rs && std::atoi(rs) == 1) && free_b > rec_bytes + cb_bytes + margin) {
+    if (c->knobs.get("recsets", 2) != 1 && free_b > rec_bytes + cb_bytes + margin) {
       if (hipMalloc(&c->d_rec2, rec_bytes) == hipSuccess && hipMalloc(&c->d_cbits2, cb_bytes) == hipSuccess) {
         c->two_rec = true;
       } else {
@@ -1171,6 +1221,10 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
   if (p.num_h_slices > p.width || p.num_v_slices > p.height)
     return fail(set_err(-22, "more slices than rows/columns"));
   ffv1hip_ctx* c = new ffv1hip_ctx();
+  if (parse_knobs(&c->knobs) < 0) {
+    delete c;
+    return fail(-22);
+  }
   c->P = p;
   c->device = device;
   c->max_batch = max_batch_frames;
@@ -1237,10 +1291,10 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
   // it needed (ffv1hip_fetch), as the reference codes any slice within its
   // w*h*140-byte packet (ffv1enc.c:1232).
   c->slice_cap = ((max_nsym * (std::max(8, p.bits_per_raw_sample) + 4) / 8 + 4096) + 255) & ~int64_t(255);
-  // FFV1HIP_SLICE_CAP (test hook): a small starting budget, to exercise the
+  // slice_cap (test hook): a small starting budget, to exercise the
   // re-encode with a larger one (ffv1hip_fetch)
-  if (const char* e = std::getenv("FFV1HIP_SLICE_CAP"))
-    c->slice_cap = (std::max<int64_t>(256, std::atoll(e)) + 255) & ~int64_t(255);
+  if (c->knobs.has("slice_cap"))
+    c->slice_cap = (std::max<int64_t>(256, std::atoll(c->knobs.str("slice_cap").c_str())) + 255) & ~int64_t(255);
   c->packet_stride = ((c->slice_cap + 16) * c->nslices + 255) & ~int64_t(255);
   // frame slots (segments) per call: one per GOP touched by the batch
   c->max_slots = p.gop_size > 1 ? std::min(max_batch_frames, (max_batch_frames + p.gop_size - 2) / p.gop_size + 1)
@@ -1249,21 +1303,19 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
   for (int v : c->nops) c->max_ops = std::max(c->max_ops, v);
   // Range coder with a table that fits the states walk's LDS: walk the
   // context states per GOP, recording every decision's state, then code all
-  // (frame, slice) streams of a batch in parallel.  FFV1HIP_CODER=chain keeps
+  // (frame, slice) streams of a batch in parallel.  The coder=chain hook keeps
   // the chained per-GOP coder (a test hook: both must give equal bytes).
   {
-    const char* mode = std::getenv("FFV1HIP_CODER");
-    // dense rows above 8 bits with context model 0 (FFV1HIP_DENSE=0: the
-    // context numbering, a measurement hook)
-    const char* dn = std::getenv("FFV1HIP_DENSE");
-    const bool dense = p.context_model == 0 && p.bits_per_raw_sample > 8 && !(dn && std::atoi(dn) == 0);
+    // dense rows above 8 bits with context model 0 (dense=0: the context
+    // numbering, a test hook)
+    const bool dense = p.context_model == 0 && p.bits_per_raw_sample > 8 && c->knobs.get("dense", 1) != 0;
     c->walk_rows = dense ? kDenseRows : c->contexts;
     const int64_t lds = walk_lds_bytes(c->walk_rows);
     // RGB interleaves the three planes' rows (encode_rgb_frame): chained
     // alpha (a third plane context) and v4 (per-frame slice header values):
     // the chained coders
     c->frames_mode = p.ac && !p.colorspace && !p.transparency && p.version <= 3 && lds <= kWalkLdsMax &&
-                     !(mode && std::strcmp(mode, "chain") == 0);
+                     c->knobs.str("coder") != "chain";
     c->wmax = 2 * (p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample) + 1;
     // the decision-stream coder writes a slice's digits (2 bytes each) where
     // ffv1_sink then writes its bytes
@@ -1435,8 +1487,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   const int fb = c->buf;
   const int t3 = c->frames_mode ? c->tri : 0;
   uint8_t* const d_keys = c->frames_mode ? c->d_keys2 + size_t(t3) * c->max_batch : c->d_keys;
-  // FFV1HIP_SERIAL=1 (measurement hook): no walk/code overlap
-  static const bool serial = std::getenv("FFV1HIP_SERIAL") && std::atoi(std::getenv("FFV1HIP_SERIAL"));
+  // serial (measurement hook): no walk/code overlap
+  const bool serial = c->knobs.has("serial");
   hipStream_t const cst = c->frames_mode && !serial ? c->code_stream : st;
   // the split schedule (two records sets): symbols, layout and bits on the
   // bits stream, beside the previous batch's walk
@@ -1633,55 +1685,53 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     wa.persist_out = ca.persist_out;
     wa.ds = ds;
     wa.scratch = c->d_scratch;
-    static const bool force_multi = std::getenv("FFV1HIP_FORCE_MULTI") && std::atoi(std::getenv("FFV1HIP_FORCE_MULTI"));
-    wa.force_multi = force_multi;
+    wa.force_multi = c->knobs.has("force_multi");
     // wave priorities: the coder's serial range pass above the walk when the
     // walk is one round of chains no longer than the coder's streams (dense
     // rows, every walk wave resident, chroma chains no longer than luma's:
     // c3, c5); else the walk above the rest (c2: many rounds; c4: Cb and Cr
     // share a context set, a chroma chain is twice luma's).  Measured: c3
     // 14.1 vs 13.1 Gpix/s, c2 12.3 vs 13.3, c4 6.03 vs 6.15 (walk 0 / range 3
-    // vs walk 2 / range 0).  FFV1HIP_WALK_PRIO / FFV1HIP_RANGE_PRIO override.
+    // vs walk 2 / range 0).  The walk_prio / range_prio hooks override.
     bool range_first = false;
     {
       const SliceGeom& g0 = c->geom[0];
       const bool chroma_long = 2 * int64_t(g0.pw[1]) * g0.ph[1] > int64_t(g0.pw[0]) * g0.ph[0];
       wa.rows = c->walk_rows;
-      range_first = c->d_qt_walk && !chroma_long && walk_items(nsegs, c->nslices) <= walk_resident(wa);
+      wa.per_short = walk_per_short(g0);
+      range_first = c->d_qt_walk && !chroma_long && walk_items(nsegs, c->nslices, wa.per_short) <= walk_resident(wa);
     }
-    static const char* const wp_env = std::getenv("FFV1HIP_WALK_PRIO");
-    static const char* const rp_env = std::getenv("FFV1HIP_RANGE_PRIO");
-    wa.prio = wp_env ? std::atoi(wp_env) : (range_first ? 0 : 2);
-    const int range_prio = rp_env ? std::atoi(rp_env) : (range_first ? 3 : 0);
+    wa.prio = c->knobs.get("walk_prio", range_first ? 0 : 2);
+    const int range_prio = c->knobs.get("range_prio", range_first ? 3 : 0);
     wa.init = c->d_init;
     wa.rows = c->walk_rows;
     wa.dense = c->d_qt_walk != nullptr;
-    static const bool walktrace = std::getenv("FFV1HIP_WALKTRACE") && std::atoi(std::getenv("FFV1HIP_WALKTRACE"));
-    if (walktrace && c->trace_n < ffv1hip_ctx::kTraceBatches) {
-      const int items = walk_items(nsegs, c->nslices);
+    if (c->knobs.has("walktrace") && c->trace_n < ffv1hip_ctx::kTraceBatches) {
+      const int items = walk_items(nsegs, c->nslices, wa.per_short);
       if (!c->d_trace) {
-        c->trace_items = walk_items(c->max_slots, c->nslices);
+        c->trace_items = walk_items(c->max_slots, c->nslices, 1);
         HIP_TRY(hipMalloc(&c->d_trace, sizeof(uint64_t) * 2 * c->trace_items * ffv1hip_ctx::kTraceBatches));
         HIP_TRY(hipMemset(c->d_trace, 0, sizeof(uint64_t) * 2 * c->trace_items * ffv1hip_ctx::kTraceBatches));
       }
       if (items <= c->trace_items) wa.trace = c->d_trace + size_t(2) * c->trace_items * c->trace_n;
     }
-    // FFV1HIP_WALKDBG=1 (measurement hook): per-block cycle split to stderr
-    static const bool walkdbg = std::getenv("FFV1HIP_WALKDBG") && std::atoi(std::getenv("FFV1HIP_WALKDBG"));
+    // walkdbg (measurement hook): per-block cycle split to stderr
+    const bool walkdbg = c->knobs.has("walkdbg");
     uint64_t* d_dbg = nullptr;
-    const int nblk = nsegs * ((c->nslices + 1) / 2) * 2;
+    const int nblk = walk_items(nsegs, c->nslices, wa.per_short);
+    const int nlong = nsegs * ((c->nslices + 1) / 2);
     if (walkdbg) {
       HIP_TRY(hipMalloc(&d_dbg, sizeof(uint64_t) * 4 * nblk));
       HIP_TRY(hipMemsetAsync(d_dbg, 0, sizeof(uint64_t) * 4 * nblk, st));
       wa.dbg = d_dbg;
     }
     // split schedule: the first part is what the CUs hold at once
-    // (FFV1HIP_WALK_SPLIT=0: one launch); one timed region either way
-    static const bool split_env = !(std::getenv("FFV1HIP_WALK_SPLIT") && std::atoi(std::getenv("FFV1HIP_WALK_SPLIT")) == 0);
-    const int nitems = walk_items(nsegs, c->nslices);
-    // FFV1HIP_WALK_PART_A (test hook, read per batch): the first part's waves
-    const char* pa = std::getenv("FFV1HIP_WALK_PART_A");
-    const int first = sst != st && split_env ? (pa ? std::atoi(pa) : walk_resident(wa)) : 0;
+    // (the walk_split=0 hook: one launch); one timed region either way
+    const bool split_env = c->knobs.get("walk_split", 1) != 0;
+    const int nitems = walk_items(nsegs, c->nslices, wa.per_short);
+    // walk_part_a (test hook): the first part's waves
+    const bool pa = c->knobs.has("walk_part_a");
+    const int first = sst != st && split_env ? (pa ? c->knobs.get("walk_part_a", 0) : walk_resident(wa)) : 0;
     // ... and only when the second part leaves room on the CUs beside it
     // (at most 80 % of the resident slots: c5's 100 % ran slower in round 2)
     const bool two_parts = first > 0 && first < nitems && (pa || int64_t(nitems - first) * 100 <= int64_t(first) * 80);
@@ -1718,8 +1768,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       HIP_TRY(hipStreamSynchronize(st));
       HIP_TRY(hipFree(d_dbg));
       double all[2] = {0, 0}, loop[2] = {0, 0}, steps[2] = {0, 0}, rt[2] = {0, 0};
-      for (int b = 0; b < nblk; b++) {  // luma chains are the first half of the grid
-        const int gi = b >= nblk / 2;
+      for (int b = 0; b < nblk; b++) {  // the longer plane group's chains first
+        const int gi = b >= nlong;
         all[gi] += double(h[4 * b]);
         loop[gi] += double(h[4 * b + 1]);
         steps[gi] += double(h[4 * b + 2]);
@@ -1727,7 +1777,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       }
       for (int g = 0; g < 2; g++)
         std::fprintf(stderr, "walkdbg grp %d: blocks %d, memtime per block %.3g, loop share %.3f, memtime/step %.1f, "
-                     "shader clock %.0f MHz, %.1f ns/step\n", g, nblk / 2, all[g] / (nblk / 2), loop[g] / all[g],
+                     "shader clock %.0f MHz, %.1f ns/step\n", g, g ? nblk - nlong : nlong, all[g] / (g ? nblk - nlong : nlong), loop[g] / all[g],
                      loop[g] / steps[g], all[g] / (rt[g] / 100.0), loop[g] / steps[g] / (all[g] / (rt[g] / 100.0)) * 1e3);
     }
     // the coder stream continues once this batch's walk is done; the walk of
@@ -2032,9 +2082,21 @@ static int alloc_compact(ffv1hip_ctx* c) {
   return 0;
 }
 
-static int pipe_open(ffv1hip_ctx* c) {
+static void pipe_release(ffv1hip_ctx* c);
+
+// The second frame / packet set of the overlapped host path, freed.
+static void drop_second_set(ffv1hip_ctx* c) {
+  (void)hipGetLastError();
+  for (void** q : {(void**)&c->d_frames2, (void**)&c->d_packets2, (void**)&c->d_packet_size2}) {
+    if (*q) (void)hipFree(*q);
+    *q = nullptr;
+  }
+  c->two_pk = false;
+  c->pipe.overlap = false;
+}
+
+static int pipe_open_parts(ffv1hip_ctx* c) {
   ffv1hip_ctx::HostPipe& P = c->pipe;
-  if (P.on) return 0;
   const size_t fset = size_t(c->frame_bytes) * c->max_batch;
   if (!c->d_frames && hipMalloc(&c->d_frames, fset) != hipSuccess) {
     (void)hipGetLastError();
@@ -2047,41 +2109,60 @@ static int pipe_open(ffv1hip_ctx* c) {
   int nt = int(std::thread::hardware_concurrency());
   if (const char* e = std::getenv("OMP_NUM_THREADS"))  // the host's CPU share where it is set
     if (std::atoi(e) > 0) nt = std::min(nt, std::atoi(e));
-  if (const char* e = std::getenv("FFV1HIP_COPY_THREADS")) nt = std::atoi(e);
+  nt = c->knobs.get("copy_threads", nt);
   P.pool = std::make_unique<CopyPool>(std::max(1, std::min(nt, 16)));
   P.pool_out = std::make_unique<CopyPool>(std::max(1, std::min(nt / 4, 4)));
-  P.dbg = std::getenv("FFV1HIP_HOSTDBG") && std::atoi(std::getenv("FFV1HIP_HOSTDBG"));
+  P.dbg = c->knobs.has("hostdbg");
   P.slot_bytes = std::max<int64_t>(int64_t(32) << 20, int64_t(c->P.width) * 4);
   for (int k = 0; k < ffv1hip_ctx::HostPipe::kSlots; k++) {
     HIP_TRY(hipHostMalloc(&P.h_slot[k], size_t(P.slot_bytes), hipHostMallocDefault));
     HIP_TRY(hipEventCreateWithFlags(&P.slot_ev[k], hipEventDisableTiming));
   }
   if (c->pass != 1 && c->P.version <= 3) {  // (v4 checks each batch's slice sizes before the next one)
+    // the second set: frames, packets, their sizes, and the second packed
+    // packets buffer alloc_compact adds (with the first one, not allocated
+    // yet either), with 2 GB to spare
     size_t free_b = 0, total_b = 0;
     HIP_TRY(hipMemGetInfo(&free_b, &total_b));
     const size_t pk_bytes = size_t(c->packet_stride) * c->max_batch;
-    if (free_b > fset + pk_bytes + (size_t(2) << 30) && hipMalloc(&c->d_frames2, fset) == hipSuccess &&
+    if (free_b > fset + 3 * pk_bytes + (size_t(2) << 30) && hipMalloc(&c->d_frames2, fset) == hipSuccess &&
         hipMalloc(&c->d_packets2, pk_bytes) == hipSuccess &&
         hipMalloc(&c->d_packet_size2, sizeof(int64_t) * c->max_batch) == hipSuccess) {
       c->two_pk = true;
       P.overlap = true;
     } else {
-      (void)hipGetLastError();
-      for (void** q : {(void**)&c->d_frames2, (void**)&c->d_packets2, (void**)&c->d_packet_size2}) {
-        if (*q) (void)hipFree(*q);
-        *q = nullptr;
-      }
+      drop_second_set(c);
     }
   }
-  for (int k = 0; k < (c->two_pk ? 2 : 1); k++) {
+  for (int k = 0; k < 2; k++) {  // both packet sets' mapped sizes (the second may come into use)
     HIP_TRY(hipHostMalloc(&P.h_sizes[k], sizeof(int64_t) * size_t(c->max_batch), hipHostMallocMapped));
     HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&P.hd_sizes[k]), P.h_sizes[k], 0));
   }
   HIP_TRY(hipHostMalloc(&P.h_status, sizeof(int) * 8, hipHostMallocMapped));
   HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&P.hd_status), P.h_status, 0));
-  const int rc = alloc_compact(c);
-  if (rc < 0) return rc;
-  P.on = true;
+  int rc = alloc_compact(c);
+  if (rc < 0 && P.overlap) {  // one set then: the second one's memory goes to the packed packets
+    for (uint8_t*& d : P.d_compact) {
+      if (d) (void)hipFree(d);
+      d = nullptr;
+    }
+    drop_second_set(c);
+    rc = alloc_compact(c);
+  }
+  return rc;
+}
+
+// On first use of the host-frame path; a failure part way releases what it
+// had set up, so a later call starts from scratch.
+static int pipe_open(ffv1hip_ctx* c) {
+  if (c->pipe.on) return 0;
+  const int rc = pipe_open_parts(c);
+  if (rc < 0) {
+    const std::string err = g_err;
+    pipe_release(c);
+    return set_err(rc, "%s", err.c_str());
+  }
+  c->pipe.on = true;
   return 0;
 }
 
@@ -2105,6 +2186,18 @@ static void pipe_close(ffv1hip_ctx* c) {
   if (P.d2h) (void)hipStreamDestroy(P.d2h);
   for (void* q : {(void*)c->d_frames2, (void*)c->d_packets2, (void*)c->d_packet_size2})
     if (q) (void)hipFree(q);
+  c->d_frames2 = nullptr;
+  c->d_packets2 = nullptr;
+  c->d_packet_size2 = nullptr;
+}
+
+// pipe_close, and the pipe back to its unopened state
+static void pipe_release(ffv1hip_ctx* c) {
+  pipe_close(c);
+  c->pipe.~HostPipe();
+  new (&c->pipe) ffv1hip_ctx::HostPipe();
+  c->two_pk = false;
+  (void)hipGetLastError();
 }
 
 // The current staging slot's copies are all queued: mark it busy until they
@@ -2547,6 +2640,7 @@ int ffv1hip_set_slice_states(ffv1hip_ctx* c, const uint8_t* buf, int64_t size) {
 // decoder's own host work: the key bit and the slice chain read backwards
 // from the packet end (ffv1dec.c:931-989); the slices decode on the GPU.
 struct ffv1hip_dec {
+  Knobs knobs;
   ffv1hip_params P{};
   int device = 0;
   int nslices = 0;
@@ -2743,6 +2837,10 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
       (extradata_size && (!extradata || std::memcmp(extradata, tmp.extradata.data(), tmp.extradata.size()) != 0)))
     return fail(set_err(FFV1HIP_AVERROR_INVALIDDATA, "extradata does not match the parameters"));
   ffv1hip_dec* d = new ffv1hip_dec();
+  if (parse_knobs(&d->knobs) < 0) {
+    delete d;
+    return fail(-22);
+  }
   d->P = p;
   d->device = device;
   d->nslices = p.num_h_slices * p.num_v_slices;
@@ -2789,9 +2887,8 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
   la.row_cap = d->row_cap;
   constexpr int64_t kDecLds = 64 * 1024;
   d->global_states = decode_lds_bytes(la, false) > kDecLds;
-  // FFV1HIP_DEC_SWAP=0 (measurement hook): both plane groups in the LDS
-  const char* sw = std::getenv("FFV1HIP_DEC_SWAP");
-  d->swap = !d->global_states && p.ac && !p.colorspace && p.chroma_planes && !(sw && std::atoi(sw) == 0);
+  // dec_swap=0 (measurement hook): both plane groups in the LDS
+  d->swap = !d->global_states && p.ac && !p.colorspace && p.chroma_planes && d->knobs.get("dec_swap", 1) != 0;
   if (decode_lds_bytes(la, true) > kDecLds) {
     delete d;
     return fail(set_err(-38, "GPU decoder: slice too wide for the LDS row buffer"));

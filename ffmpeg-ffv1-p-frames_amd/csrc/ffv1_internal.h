@@ -248,6 +248,8 @@ struct WalkArgs {
   int force_multi;            // measurement hook: every chunk on the checked (multi) step
   const uint8_t* init;        // 2-pass initial states [contexts][32] at keyframes, or null (all 128)
   int nitems, item0;          // set by launch_walk: all items of the batch, the launch's first
+  int nsegs;                  // segments of the batch
+  int per_short;              // segments one wave of the shorter plane group walks, one after the other
   int prio;                   // wave priority (s_setprio)
   int rows;                   // context rows of a plane group's table in LDS (kDenseRows when dense)
   int dense;                  // records address dense rows (dense_row), the state tables keep contexts
@@ -355,7 +357,12 @@ int launch_layout(const int* dcount, int nstreams, int64_t* dbase, int64_t* tota
                   int* seg_totals, int* wmap, void* stream);
 // items [first, first + count) of the batch's walk (count < 0: to the end)
 int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first = 0, int count = -1);
-int walk_items(int nsegs, int nslices);
+// Items (waves) of a batch's walk: the longer plane group's chains first, one
+// segment per wave, then the shorter group's, per_short segments per wave one
+// after the other, so that both kinds of wave walk about as many symbols
+// (4:2:0 luma vs Cb + Cr, 4:4:4 Cb + Cr vs luma: 2).
+int walk_items(int nsegs, int nslices, int per_short);
+int walk_per_short(const SliceGeom& g);
 int walk_resident(const WalkArgs& a);  // (uses a.rows)
 int launch_range(const CodeArgs& a, void* stream);
 int launch_dseg(const CodeArgs& a, void* stream);

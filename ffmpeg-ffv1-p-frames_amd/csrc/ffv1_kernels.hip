@@ -1480,19 +1480,23 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
     fixed[kLdsN + i] = (uint8_t)v;
   }
   // the longer plane group's chains first (luma at 4:2:0, twice as long as
-  // chroma; chroma at 4:4:4, where Cb and Cr make one chain twice luma's);
-  // the shorter ones then fill the CUs as those waves finish
-  // item = (plane group, segment, slice pair): the launch may cover a part
+  // chroma; chroma at 4:4:4, where Cb and Cr make one chain twice luma's),
+  // one segment per wave; then the shorter group's, a.per_short segments per
+  // wave one after the other, so that every wave walks about as many symbols
+  // and a batch's waves all finish together
+  // item = (plane group, segment(s), slice pair): the launch may cover a part
   // of the items (launch_walk's first / count)
   const int item = (int)blockIdx.x + a.item0;
-  const int nblk = a.nitems / 2;
+  const int npairs = (a.nslices + 1) / 2;
+  const int nlong = a.nsegs * npairs;
+  const int nshort_segs = (a.nsegs + a.per_short - 1) / a.per_short;  // waves per slice pair, shorter group
   const SliceGeom& g0 = a.geom[0];
   const bool chroma_first = 2 * (int64_t)g0.pw[1] * g0.ph[1] > (int64_t)g0.pw[0] * g0.ph[0];
-  const int grp = (item >= nblk) != chroma_first;
-  const int npairs = (a.nslices + 1) / 2;
-  const int bi = item - (item >= nblk ? nblk : 0);
-  const int seg_i = bi / npairs, pair = bi % npairs;
-  const Segment seg = a.segs[seg_i];
+  const bool is_long = item < nlong;
+  const int grp = is_long == chroma_first ? 1 : 0;  // long: luma (4:2:0) or chroma (4:4:4)
+  const int bi = is_long ? item : item - nlong;
+  const int pair = bi % npairs, seg_first = bi / npairs;
+  const int seg_step = is_long ? a.nsegs : nshort_segs;  // this wave's segments: seg_first, + seg_step, ...
   const int sl = 2 * pair + h;              // this half's slice
   const bool live = sl < a.nslices;
   const SliceGeom& g = a.geom[live ? sl : 2 * pair];
@@ -1504,21 +1508,7 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   uint4* const stage4 = reinterpret_cast<uint4*>(stage);
   const int64_t n16 = half / 16, t16 = thalf / 16;
   const int64_t goff = grp * half;
-  // where the segment's states come from: the carry, the 2-pass initial
-  // states (a keyframe), or all 128 (ff_ffv1_clear_slice_state); null: 128
-  const uint4* const src = seg.load_states && live
-                               ? reinterpret_cast<const uint4*>(a.persist_in + (int64_t)sl * a.state_bytes + goff)
-                               : reinterpret_cast<const uint4*>(a.init);
   const uint4 v128 = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
-  {
-    uint4* const t4 = reinterpret_cast<uint4*>(mytbl);
-    for (int64_t i = k; i < t16; i += 32) {  // table block i: row i / 2 (dense: its context's)
-      const int64_t si = a.dense ? (int64_t)dense_ctx((int)(i >> 1)) * 2 + (i & 1) : i;
-      t4[i] = src ? src[si] : v128;
-    }
-    if (k < 2) t4[t16 + k] = v128;  // dummy row
-  }
-  __syncthreads();
 
   WalkLane W;
   W.csh = (2 * k) & 31;
@@ -1557,6 +1547,22 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   uint64_t t_loop = 0, n_steps = 0;
   const uint64_t t_all = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
   const uint64_t rt_all = a.dbg || a.trace ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz: the wave's shader clock
+  for (int seg_i = seg_first; seg_i < a.nsegs; seg_i += seg_step) {
+  const Segment seg = a.segs[seg_i];
+  // where the segment's states come from: the carry, the 2-pass initial
+  // states (a keyframe), or all 128 (ff_ffv1_clear_slice_state); null: 128
+  const uint4* const src = seg.load_states && live
+                               ? reinterpret_cast<const uint4*>(a.persist_in + (int64_t)sl * a.state_bytes + goff)
+                               : reinterpret_cast<const uint4*>(a.init);
+  {
+    uint4* const t4 = reinterpret_cast<uint4*>(mytbl);
+    for (int64_t i = k; i < t16; i += 32) {  // table block i: row i / 2 (dense: its context's)
+      const int64_t si = a.dense ? (int64_t)dense_ctx((int)(i >> 1)) * 2 + (i & 1) : i;
+      t4[i] = src ? src[si] : v128;
+    }
+    if (k < 2) t4[t16 + k] = v128;  // dummy row
+  }
+  __syncthreads();
   for (int j = 0; j < seg.nframes; j++) {
     const int f = seg.first_frame + j;
     const int64_t sid = (int64_t)f * a.nslices + (live ? sl : 0);
@@ -1696,6 +1702,8 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   }
   copy_out();
   __builtin_amdgcn_wave_barrier();
+  pdst = a.scratch;  // the next segment's first copy-out has nothing to write
+  plast = 0;
   if (seg.save_states && live) {
     uint4* dst = reinterpret_cast<uint4*>(a.persist_out + (int64_t)sl * a.state_bytes + goff);
     const uint4* t4 = reinterpret_cast<const uint4*>(mytbl);
@@ -1708,6 +1716,8 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
       }
     }
   }
+  __syncthreads();  // the table is read out before the next segment loads its own
+  }  // segments of this wave
   if (a.trace && lane == 0) {
     a.trace[item * 2 + 0] = rt_all;
     a.trace[item * 2 + 1] = __builtin_amdgcn_s_memrealtime();
@@ -2371,7 +2381,9 @@ int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first, int count
   if (walk_lds_bytes_dev(a.rows) > kWalkLdsMax || a.rows * 32 > 0xFFFF) return -1;
   const size_t dyn = (size_t)(2 * ((int64_t)a.rows * 32 + 32));  // the tables; the fixed part is static
   WalkArgs b = a;
-  b.nitems = nsegs * ((a.nslices + 1) / 2) * 2;
+  if (b.per_short < 1) b.per_short = 1;
+  b.nsegs = nsegs;
+  b.nitems = walk_items(nsegs, a.nslices, b.per_short);
   if (count < 0) count = b.nitems - first;
   if (first < 0 || count <= 0 || first + count > b.nitems) return count == 0 ? 0 : -1;
   b.item0 = first;
@@ -2379,7 +2391,18 @@ int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first, int count
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int walk_items(int nsegs, int nslices) { return nsegs * ((nslices + 1) / 2) * 2; }
+int walk_items(int nsegs, int nslices, int per_short) {
+  const int npairs = (nslices + 1) / 2;
+  return npairs * (nsegs + (nsegs + per_short - 1) / per_short);
+}
+
+int walk_per_short(const SliceGeom& g) {
+  const int64_t l = (int64_t)g.pw[0] * g.ph[0];
+  const int64_t c = (int64_t)g.pw[1] * g.ph[1] + (int64_t)g.pw[2] * g.ph[2];
+  if (l <= 0 || c <= 0) return 1;
+  const int64_t lo = std::min(l, c), hi = std::max(l, c);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(4, (hi + lo / 2) / lo));
+}
 
 // Walk waves one CU holds at once (LDS-bound), for launch splitting.
 int walk_resident(const WalkArgs& a) {

@@ -12,6 +12,7 @@
 #include "ffv1_oracle.h"
 
 #include <math.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -1593,76 +1594,164 @@ static void code_slice_planes(ffv1o_enc *e, slice_ctx *s, const uint8_t *const p
         for_each_plane(e, s, planes, strides, coder, golomb);
 }
 
+/* encode_slice (ffv1enc.c:1146-1220) of slice i into its buffer.  Slices
+ * are independent (their own coder, states and buffer), which is what the
+ * reference's per-slice jobs rely on (avctx->execute, ffv1enc.c:1323); the
+ * per-slice scratch fields of e (line_err, pcm, rct, scratch) belong to the
+ * caller's thread. */
+static int enc_slice(ffv1o_enc *e, int i, int key, const uint8_t *const planes[4],
+                     const int strides[4])
+{
+    const ffv1o_config *cfg = &e->cfg;
+    slice_ctx *s = &e->sl[i];
+    rc_enc c;
+    s->error = 0;
+    /* slice 0 continues the packet-level coder that carries the key bit
+     * (+ the v0/v1 header) coded with the default table, ffv1enc.c:1287-1315 */
+    rc_enc_init(&c, s->buf, s->cap, &e->frame_tab);
+    if (i == 0) {
+        uint8_t ks = 128;
+        c.t = &e->dflt;
+        rc_put(&c, &ks, key);
+        if (key && cfg->version < 2)
+            put_v01_header(e, &c);
+        c.t = &e->frame_tab;
+    }
+    /* v4 picks the slice's RCT coefficients; a range-coded v4 slice that
+     * does not fit its buffer is coded again as PCM from the coder state it
+     * started with */
+    e->pcm = 0;
+    e->rct_by = e->rct_ry = 1;
+    if (cfg->version > 3)
+        choose_rct(e, s, planes, strides);
+    const rc_enc c_bak = c;
+retry:
+    e->line_err = 0;
+    e->coded_bits = coded_bits_of(cfg, e->pcm);
+    if (key)
+        clear_slice_states(e, s);
+    if (cfg->version > 2)
+        put_slice_header(e, s, &c);
+
+    if (cfg->ac == 0) {
+        bitw b;
+        int64_t ac_bytes = 0;
+        if (cfg->version > 2) {
+            uint8_t st = 129;
+            rc_put(&c, &st, 0);
+        }
+        if (cfg->version > 2 || (s->x0 == 0 && s->y0 == 0))
+            ac_bytes = rc_finish(&c);
+        bw_init(&b, s->buf + ac_bytes, s->cap - ac_bytes);
+        code_slice_planes(e, s, planes, strides, &b, 1);
+        s->bytes = ac_bytes + bw_bytes(&b);
+        s->error = b.overflow || c.overflow || e->line_err;
+    } else {
+        code_slice_planes(e, s, planes, strides, &c, 0);
+        if (e->line_err && cfg->version > 3 && !e->pcm) {
+            e->pcm = 1;
+            c = c_bak;
+            goto retry;
+        }
+        uint8_t st = 129;
+        rc_put(&c, &st, 0);
+        s->bytes = rc_finish(&c);
+        s->error = c.overflow || e->line_err;
+        s->pcm = e->pcm;
+    }
+    return s->error ? AVERR_INVALIDDATA : 0;
+}
+
+/* One worker of ffv1o_enc_frame_mt: slices t, t + n, ... with a private
+ * copy of the encoder's per-slice scratch fields. */
+typedef struct slice_job {
+    ffv1o_enc w;
+    int first, step, key, rc;
+    const uint8_t *const *planes;
+    const int *strides;
+} slice_job;
+
+static void *slice_worker(void *arg)
+{
+    slice_job *j = arg;
+    for (int i = j->first; i < j->w.nslices && !j->rc; i += j->step)
+        j->rc = enc_slice(&j->w, i, j->key, j->planes, j->strides);
+    return NULL;
+}
+
+static int64_t assemble_packet(ffv1o_enc *e, uint8_t *out, int64_t cap);
+
 int64_t ffv1o_enc_frame(ffv1o_enc *e, const uint8_t *const planes[4],
                         const int strides[4], uint8_t *out, int64_t cap,
                         int *key_out)
+{
+    return ffv1o_enc_frame_mt(e, planes, strides, out, cap, key_out, 1);
+}
+
+int64_t ffv1o_enc_frame_mt(ffv1o_enc *e, const uint8_t *const planes[4],
+                           const int strides[4], uint8_t *out, int64_t cap,
+                           int *key_out, int threads)
 {
     const ffv1o_config *cfg = &e->cfg;
     int key = cfg->gop_size == 0 || e->picture_number % cfg->gop_size == 0;
     if (key)
         e->gob_count++; /* ffv1enc.c:1302 */
-
-    for (int i = 0; i < e->nslices; i++) {
-        slice_ctx *s = &e->sl[i];
-        rc_enc c;
-        s->error = 0;
-        /* slice 0 continues the packet-level coder that carries the key bit
-         * (+ the v0/v1 header) coded with the default table, ffv1enc.c:1287-1315 */
-        rc_enc_init(&c, s->buf, s->cap, &e->frame_tab);
-        if (i == 0) {
-            uint8_t ks = 128;
-            c.t = &e->dflt;
-            rc_put(&c, &ks, key);
-            if (key && cfg->version < 2)
-                put_v01_header(e, &c);
-            c.t = &e->frame_tab;
+    if (threads > e->nslices)
+        threads = e->nslices;
+    if (threads <= 1 || e->pass1) {  /* pass 1 counts into one table: serial */
+        for (int i = 0; i < e->nslices; i++) {
+            int rc = enc_slice(e, i, key, planes, strides);
+            if (rc)
+                return rc;
         }
-        /* encode_slice (ffv1enc.c:1146-1220): v4 picks the slice's RCT
-         * coefficients; a range-coded v4 slice that does not fit its buffer
-         * is coded again as PCM from the coder state it started with */
-        e->pcm = 0;
-        e->rct_by = e->rct_ry = 1;
-        if (cfg->version > 3)
-            choose_rct(e, s, planes, strides);
-        const rc_enc c_bak = c;
-    retry:
-        e->line_err = 0;
-        e->coded_bits = coded_bits_of(cfg, e->pcm);
-        if (key)
-            clear_slice_states(e, s);
-        if (cfg->version > 2)
-            put_slice_header(e, s, &c);
-
-        if (cfg->ac == 0) {
-            bitw b;
-            int64_t ac_bytes = 0;
-            if (cfg->version > 2) {
-                uint8_t st = 129;
-                rc_put(&c, &st, 0);
+    } else {
+        /* the reference's threading: one job per slice, threads =
+         * min(cores, slices) (ffv1enc.c:1323, avctx->execute) */
+        slice_job *jobs = calloc((size_t)threads, sizeof(slice_job));
+        pthread_t *th = calloc((size_t)threads, sizeof(pthread_t));
+        int64_t maxw = 0;
+        for (int i = 0; i < e->nslices; i++)
+            if ((int64_t)e->sl[i].w * e->sl[i].h > maxw)
+                maxw = (int64_t)e->sl[i].w * e->sl[i].h;
+        int rc = jobs && th ? 0 : AVERR_ENOMEM, started = 0;
+        for (int t = 0; t < threads && !rc; t++) {
+            jobs[t].w = *e;
+            jobs[t].w.scratch = malloc(4 * (size_t)maxw * sizeof(int16_t) + 16);
+            jobs[t].first = t;
+            jobs[t].step = threads;
+            jobs[t].key = key;
+            jobs[t].planes = planes;
+            jobs[t].strides = strides;
+            if (!jobs[t].w.scratch || pthread_create(&th[t], NULL, slice_worker, &jobs[t])) {
+                free(jobs[t].w.scratch);
+                rc = AVERR_ENOMEM;
+                break;
             }
-            if (cfg->version > 2 || (s->x0 == 0 && s->y0 == 0))
-                ac_bytes = rc_finish(&c);
-            bw_init(&b, s->buf + ac_bytes, s->cap - ac_bytes);
-            code_slice_planes(e, s, planes, strides, &b, 1);
-            s->bytes = ac_bytes + bw_bytes(&b);
-            s->error = b.overflow || c.overflow || e->line_err;
-        } else {
-            code_slice_planes(e, s, planes, strides, &c, 0);
-            if (e->line_err && cfg->version > 3 && !e->pcm) {
-                e->pcm = 1;
-                c = c_bak;
-                goto retry;
-            }
-            uint8_t st = 129;
-            rc_put(&c, &st, 0);
-            s->bytes = rc_finish(&c);
-            s->error = c.overflow || e->line_err;
-            s->pcm = e->pcm;
+            started++;
         }
-        if (s->error)
-            return AVERR_INVALIDDATA;
+        for (int t = 0; t < started; t++) {
+            pthread_join(th[t], NULL);
+            if (!rc)
+                rc = jobs[t].rc;
+            free(jobs[t].w.scratch);
+        }
+        free(jobs);
+        free(th);
+        if (rc)
+            return rc;
     }
+    int64_t pos = assemble_packet(e, out, cap);
+    if (pos < 0)
+        return pos;
+    e->picture_number++;
+    if (key_out)
+        *key_out = key;
+    return pos;
+}
 
+static int64_t assemble_packet(ffv1o_enc *e, uint8_t *out, int64_t cap)
+{
+    const ffv1o_config *cfg = &e->cfg;
     /* packet assembly, ffv1enc.c:1326-1354 */
     int64_t pos = 0;
     for (int i = 0; i < e->nslices; i++) {
@@ -1685,9 +1774,6 @@ int64_t ffv1o_enc_frame(ffv1o_enc *e, const uint8_t *const planes[4],
         }
         pos += n;
     }
-    e->picture_number++;
-    if (key_out)
-        *key_out = key;
     return pos;
 }
 

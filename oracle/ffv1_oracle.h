@@ -106,6 +106,11 @@ int64_t    ffv1o_enc_frame(ffv1o_enc *e, const uint8_t *const planes[4],
                            const int strides[4], uint8_t *out, int64_t cap,
                            int *key);
 /* Per-slice byte counts of the last frame (before the trailer). */
+/* ffv1o_enc_frame with the slices coded by `threads` threads (the
+ * reference's per-slice jobs; threads <= 1: serial).  Same bytes. */
+int64_t    ffv1o_enc_frame_mt(ffv1o_enc *e, const uint8_t *const planes[4],
+                              const int strides[4], uint8_t *out, int64_t cap,
+                              int *key_out, int threads);
 int64_t    ffv1o_enc_get_states(const ffv1o_enc *e, uint8_t *buf, int64_t cap);
 int        ffv1o_enc_set_states(ffv1o_enc *e, const uint8_t *buf, int64_t size,
                                 int64_t picture_number);

@@ -54,6 +54,9 @@ def lib():
         L.ffv1o_enc_extradata.restype = ctypes.c_int
         L.ffv1o_enc_frame.argtypes = [ctypes.c_void_p, P(u8p), P(ctypes.c_int), u8p, ctypes.c_int64, P(ctypes.c_int)]
         L.ffv1o_enc_frame.restype = ctypes.c_int64
+        L.ffv1o_enc_frame_mt.argtypes = [ctypes.c_void_p, P(u8p), P(ctypes.c_int), u8p, ctypes.c_int64,
+                                         P(ctypes.c_int), ctypes.c_int]
+        L.ffv1o_enc_frame_mt.restype = ctypes.c_int64
         L.ffv1o_enc_last_slice_bytes.argtypes = [ctypes.c_void_p, P(ctypes.c_int), ctypes.c_int]
         L.ffv1o_enc_last_slice_pcm.argtypes = [ctypes.c_void_p, P(ctypes.c_int), ctypes.c_int]
         L.ffv1o_enc_get_states.argtypes = [ctypes.c_void_p, P(ctypes.c_uint8), ctypes.c_int64]
@@ -164,7 +167,9 @@ class Encoder:
             raise RuntimeError(n)
         return buf[:n].tobytes()
 
-    def encode(self, planes):
+    def encode(self, planes, threads: int = 1):
+        """One frame; threads > 1 codes its slices on that many threads (the
+        reference's per-slice jobs, ffv1enc.c:1323): the same bytes."""
         for k, (rows, cols) in enumerate(plane_shapes(self.cfg)):
             a = planes[k]
             if a.shape[0] < rows or a.shape[1] < cols:
@@ -175,7 +180,7 @@ class Encoder:
             cap += p.nbytes * 20  # <= 33 decisions (bytes) per 16-bit sample
         out = np.empty(cap, np.uint8)
         key = ctypes.c_int()
-        n = lib().ffv1o_enc_frame(self._h, arr, strides, _u8p(out), cap, ctypes.byref(key))
+        n = lib().ffv1o_enc_frame_mt(self._h, arr, strides, _u8p(out), cap, ctypes.byref(key), int(threads))
         if n < 0:
             raise RuntimeError(f"ffv1o_enc_frame: {n}")
         return out[:n].tobytes(), bool(key.value)

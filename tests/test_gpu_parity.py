@@ -66,9 +66,9 @@ def test_hip_rgb_matches_oracle(stream):
 @pytest.mark.parametrize("stream", [s for s in PARITY_STREAMS if s.coder != 0][:6],
                          ids=[s.name for s in PARITY_STREAMS if s.coder != 0][:6])
 def test_chained_coder_matches_oracle(stream, monkeypatch):
-    """The per-GOP chained range coder (FFV1HIP_CODER=chain) gives the same
-    bytes as the frame-parallel default."""
-    monkeypatch.setenv("FFV1HIP_CODER", "chain")
+    """The per-GOP chained range coder (FFV1HIP_DEBUG=coder=chain) gives the
+    same bytes as the frame-parallel default."""
+    monkeypatch.setenv("FFV1HIP_DEBUG", "coder=chain")
     frames = list(stream.frames())
     _, _, ref = oracle_encode(stream, frames)
     _, got = hip_encode(stream, frames, batch=4)
@@ -83,8 +83,7 @@ def test_split_walk_matches_oracle(stream, recsets, monkeypatch):
     forced by the test hooks) and the next batch's symbols beside its second
     part (two records sets), and one records set (symbols, walk, bits beside
     it): the same bytes as the oracle across batches."""
-    monkeypatch.setenv("FFV1HIP_RECSETS", str(recsets))
-    monkeypatch.setenv("FFV1HIP_WALK_PART_A", "3")
+    monkeypatch.setenv("FFV1HIP_DEBUG", f"recsets={recsets},walk_part_a=3")
     frames = list(stream.frames())
     _, ex_ref, ref = oracle_encode(stream, frames)
     ex, got = hip_encode(stream, frames, batch=4)
@@ -182,17 +181,14 @@ def test_dense_rows_keep_packets_and_carried_states(monkeypatch):
     (ffv1_internal.h, dense_ctx / dense_row).  The packets, and the P-frame
     carry exported mid-GOP (ffv1hip_get_slice_states, context numbering, the
     contexts that cannot occur at their initial 128), equal those of the
-    context-numbered walk (FFV1HIP_DENSE=0) and of the chained coder."""
+    context-numbered walk (FFV1HIP_DEBUG=dense=0) and of the chained coder."""
     from ffv1hip import HipEncoder
     s = Stream("dense", 320, 180, "yuv420p10", 7, slices=6, gop_size=12, source="d2", depth=10)
     frames = list(s.frames())
     _, _, ref = oracle_encode(s, frames)
     states = {}
-    for mode, env in [("dense", {}), ("contexts", {"FFV1HIP_DENSE": "0"}), ("chain", {"FFV1HIP_CODER": "chain"})]:
-        for k in ("FFV1HIP_DENSE", "FFV1HIP_CODER"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
+    for mode, dbg in [("dense", ""), ("contexts", "dense=0"), ("chain", "coder=chain")]:
+        monkeypatch.setenv("FFV1HIP_DEBUG", dbg)
         enc = HipEncoder(hip_params(s), 0, 7)
         got = enc.encode(frames[:5])
         states[mode] = bytes(enc.get_slice_states())
@@ -223,9 +219,7 @@ def test_slice_budget_overflow_reencodes(coder, monkeypatch):
     """A slice over the byte budget is encoded again with a larger budget
     (the reference codes it: its buffer is ~w*h*140 bytes, ffv1enc.c:1232),
     with the P-frame carry rolled back: the stream equals the oracle's."""
-    monkeypatch.setenv("FFV1HIP_SLICE_CAP", "512")
-    if coder == "chain":
-        monkeypatch.setenv("FFV1HIP_CODER", "chain")
+    monkeypatch.setenv("FFV1HIP_DEBUG", "slice_cap=512" + (",coder=chain" if coder == "chain" else ""))
     s = PARITY_STREAMS[1]
     frames = list(s.frames())
     _, _, ref = oracle_encode(s, frames)
@@ -296,7 +290,7 @@ def test_encode2_pipelined_budget_reencode(batch, monkeypatch):
     rolls back two batches in flight; packets, pts and keys equal the
     oracle's stream."""
     from ffv1hip import AVCodecContext, FFV1Encoder
-    monkeypatch.setenv("FFV1HIP_SLICE_CAP", "512")
+    monkeypatch.setenv("FFV1HIP_DEBUG", "slice_cap=512")
     s = PARITY_STREAMS[1]
     frames = list(s.frames())
     _, ex_ref, ref = oracle_encode(s, frames)
@@ -318,7 +312,7 @@ def test_host_encode_many_batches(cap, monkeypatch):
     """ffv1hip_encode over several batches in one call (frames staged while
     the previous batch codes), with and without the budget re-encode."""
     if cap:
-        monkeypatch.setenv("FFV1HIP_SLICE_CAP", cap)
+        monkeypatch.setenv("FFV1HIP_DEBUG", f"slice_cap={cap}")
     from ffv1hip import HipEncoder
     s = PARITY_STREAMS[1]
     frames = list(s.frames())
@@ -363,7 +357,7 @@ def test_device_path_never_truncates(sync, monkeypatch):
     the reference fails a frame it cannot fit, ffv1enc.c:283-292)."""
     import torch
     from ffv1hip import HipEncoder
-    monkeypatch.setenv("FFV1HIP_SLICE_CAP", "512")
+    monkeypatch.setenv("FFV1HIP_DEBUG", "slice_cap=512")
     s = PARITY_STREAMS[1]  # 480x270 10-bit, 4 slices, gop 4
     frames = list(s.frames())[:8]
     _, _, ref = oracle_encode(s, frames)

@@ -204,3 +204,16 @@ def test_oracle_two_pass(coder):
     assert e.extradata() == ex
     with pytest.raises(ValueError):
         oracle.Encoder(cfg, 2, stats.rsplit(" ", 3)[0])
+
+
+@pytest.mark.parametrize("name", ["p10_gop4", "p10_9slices", "golomb_v3_pframes", "grid16x16", "bgr0_v3"])
+def test_slice_threaded_oracle_equals_serial(name):
+    # the per-slice-threaded oracle (the reference's threading model, the
+    # CPU baseline's slice-threaded figure) writes the same bytes
+    streams = {s.name: s for s in PARITY_STREAMS + RGB_STREAMS}
+    s = streams[name]
+    cfg = s.oracle_config()
+    frames = list(s.frames())
+    serial, threaded = oracle.Encoder(cfg), oracle.Encoder(cfg)
+    for f in frames:
+        assert threaded.encode(f, threads=3) == serial.encode(f)

@@ -35,7 +35,7 @@ B = gops * GOP
 frames = list(synth.videogen_frames(W, H, B, depth=10))
 L = load_library()
 res = {"config": "4K 3840x2160 yuv420p10le, coder=1, slices=64, keyint=12", "clip_frames": B,
-       "copy_threads": os.environ.get("FFV1HIP_COPY_THREADS") or os.environ.get("OMP_NUM_THREADS")}
+       "copy_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 def plane_ptrs(idx):

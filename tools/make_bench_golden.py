@@ -17,6 +17,7 @@ worker thread (ctypes drops the GIL).
 
     python tools/make_bench_golden.py                 # all configs, 8 ranks' worth
     python tools/make_bench_golden.py --configs c3 --ranks 1
+    python tools/make_bench_golden.py --configs c3 --data d2 --gops 40   # key c3_d2
 """
 from __future__ import annotations
 
@@ -58,12 +59,15 @@ def encode_gop(cfg, frames):
     return h.hexdigest(), n
 
 
-def run_config(name, ngops, threads):
+def run_config(name, ngops, threads, data="d1"):
     c = bench.CONFIGS[name]
     cfg = oracle_cfg(c)
     per = max(c["GOP"], 1)
     group = per  # intra configs (GOP 1): one frame per entry
-    gen = synth.videogen_frames(c["W"], c["H"], ngops * group, depth=c["DEPTH"], chroma444=c["C444"])
+    if data == "d1":
+        gen = synth.videogen_frames(c["W"], c["H"], ngops * group, depth=c["DEPTH"], chroma444=c["C444"])
+    else:  # the seeded LSB-active clip bench.py --data d2 encodes
+        gen = synth.d2_frames(c["W"], c["H"], ngops * group, depth=c["DEPTH"], chroma444=c["C444"])
     res = [None] * ngops
     t0 = time.time()
     with cf.ThreadPoolExecutor(threads) as ex:
@@ -78,7 +82,7 @@ def run_config(name, ngops, threads):
         for d in cf.as_completed(pending):
             res[pending[d]] = d.result()
     print(f"{name}: {ngops} GOPs of {group} frames in {time.time() - t0:.1f}s", flush=True)
-    return {"workload": c["workload"], "frames_per_gop": group, "data": "d1",
+    return {"workload": c["workload"], "frames_per_gop": group, "data": data,
             "gops": [{"md5": m, "bytes": b} for m, b in res]}
 
 
@@ -87,6 +91,9 @@ def main():
     ap.add_argument("--configs", default="c3,c2,c4,c5")
     ap.add_argument("--ranks", type=int, default=8, help="GOPs for this many ranks at the default batch")
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 1)
+    ap.add_argument("--data", choices=("d1", "d2"), default="d1",
+                    help="clip: d1 (videogen, key <config>) or d2 (key <config>_d2)")
+    ap.add_argument("--gops", type=int, default=0, help="GOPs per config (default: --ranks x the bench batch)")
     args = ap.parse_args()
     data = json.load(open(OUT)) if os.path.exists(OUT) else {}
     data["note"] = ("per-GOP oracle digests of bench.py's D1 clips (tools/make_bench_golden.py); "
@@ -95,7 +102,8 @@ def main():
         c = bench.CONFIGS[name]
         # intra 1080p: 2 ranks' worth of frames keeps the file small
         ranks = args.ranks if c["GOP"] > 1 else min(args.ranks, 2)
-        data[name] = run_config(name, c["GOPS"] * ranks, args.threads)
+        key = name if args.data == "d1" else f"{name}_d2"
+        data[key] = run_config(name, args.gops or c["GOPS"] * ranks, args.threads, args.data)
         with open(OUT, "w") as f:
             json.dump(data, f, indent=0)
             f.write("\n")

@@ -7,7 +7,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/pmc_$TAG
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-export FFV1HIP_SERIAL=1
+export FFV1HIP_DEBUG=serial
 BENCH="$R/bench.py --steps 1 --warmup 0 --gops ${GOPS:-2} --no-cpu-baseline"
 timeout -k 10 300 python3 $BENCH > $O/plain.json 2> $O/plain.err || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 $BENCH > $O/kt.log 2>&1 || exit 2
