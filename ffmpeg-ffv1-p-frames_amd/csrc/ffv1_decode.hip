@@ -278,6 +278,29 @@ __device__ inline void decode_row_u(RacDec& c, uint8_t* st8, const sconst_i32* s
   }
 }
 
+// decode_line's slice_coding_mode 1 (version 4 PCM, ffv1dec.c:111-120): every
+// sample's bits MSB first, each on a fresh state 128; uniform like
+// decode_row_u
+__device__ inline void decode_row_pcm_u(RacDec& c, const uint64_t* pkw, int16_t* cur, int w, int bits) {
+  for (int x = 0; x < w; x++) {
+    int v = 0;
+    for (int i = 0; i < bits; i++) {
+      const uint32_t r1 = (c.range * 128u) >> 8;
+      const uint32_t rr = c.range - r1;
+      const int bit = c.low >= rr;
+      if (bit) {
+        c.low -= rr;
+        c.range = r1;
+      } else {
+        c.range = rr;
+      }
+      if (c.range < 0x100) refill_u(c, pkw);
+      v = 2 * v + bit;
+    }
+    if (threadIdx.x == 0) cur[x] = int16_t(v);
+  }
+}
+
 // GetBitContext over a slice's Golomb bits: MSB first, zeros past the end
 // (the safe bitstream reader).
 struct BitRd {
@@ -457,6 +480,7 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
   int16_t* const qt = reinterpret_cast<int16_t*>(hdr + 64);    // [5][256]
   int16_t* const ring = qt + 5 * 256;                          // [rgb ? 3 : 1][2][row_cap]
   __shared__ int bad;
+  __shared__ int s_reset, s_pcm, s_by, s_ry;  // v4 slice header: reset, slice_coding_mode, RCT coefficients
   const uint64_t* pkw = reinterpret_cast<const uint64_t*>(a.pkts);
   for (int i = lane; i < 256; i += kDecThreads) {
     tt[i] = uint16_t(a.ftab[i] | (a.ftab[256 + i] << 8));
@@ -492,6 +516,9 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
     if (lane == 0) {
       rac_init(c, a.pkts, a.slice_start[fs], a.slice_end[fs]);
       int ok = 1, hok = 1;
+      s_reset = 0;
+      s_pcm = 0;
+      s_by = s_ry = 1;
       if (s == 0) {  // the key bit, state 128 (ffv1dec.c:927-933)
         hdr[0] = 128;
         ok &= rac_get(c, hdr, dtt, pkw) == key;
@@ -506,7 +533,7 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
           ok &= rac_get(c, hdr, dtt, pkw) == a.chroma_planes;
           ok &= rac_symbol(c, hdr, 0, dtt, pkw) == a.chroma_h_shift;
           ok &= rac_symbol(c, hdr, 0, dtt, pkw) == a.chroma_v_shift;
-          ok &= rac_get(c, hdr, dtt, pkw) == 0;  // transparency
+          ok &= rac_get(c, hdr, dtt, pkw) == a.transparency;
           for (int t = 0; t < 5 && ok; t++) ok &= skip_quant_table(c, hdr + 32, dtt, pkw);
         }
       }
@@ -523,11 +550,21 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
         const int y1 = int(int64_t(sy + sh + 1) * a.height / a.num_v);
         hok &= sx >= 0 && sy >= 0 && sw >= 0 && sh >= 0;
         hok &= x0 == g->px[0] && y0 == g->py[0] && x1 - x0 == g->pw[0] && y1 - y0 == g->ph[0];
-        for (int i = 0; i < 2 && hok; i++) hok &= rac_symbol(c, hdr, 0, tt, pkw) == a.context_model;
+        for (int i = 0; i < a.pcount && hok; i++) hok &= rac_symbol(c, hdr, 0, tt, pkw) == a.context_model;
         if (hok) {
           (void)rac_symbol(c, hdr, 0, tt, pkw);  // picture structure
           (void)rac_symbol(c, hdr, 0, tt, pkw);  // sample aspect ratio
           (void)rac_symbol(c, hdr, 0, tt, pkw);
+        }
+        if (hok && a.version > 3) {  // ffv1dec.c:344-356
+          s_reset = rac_get(c, hdr, tt, pkw);
+          s_pcm = rac_symbol(c, hdr, 0, tt, pkw);
+          if (s_pcm != 1) {
+            s_by = rac_symbol(c, hdr, 0, tt, pkw);
+            s_ry = rac_symbol(c, hdr, 0, tt, pkw);
+            hok &= unsigned(s_by) + unsigned(s_ry) <= 4u;
+          }
+          hok &= s_pcm == 0 || s_pcm == 1;  // modes this decoder codes (the reference reads only these too)
         }
       }
       if (!ok) atomicAdd(&a.status[0], 1);
@@ -537,7 +574,9 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
     __syncthreads();
     if (bad == 2) return;
     if (bad) continue;  // not decoded: no state update (ffv1dec.c:410-414)
-    if (key) {          // ff_ffv1_clear_slice_state, after the header (ffv1dec.c:418-419)
+    const bool pcm = s_pcm == 1;
+    const int rby = s_by, rry = s_ry;
+    if (key || s_reset) {  // ff_ffv1_clear_slice_state, after the header (ffv1dec.c:418-419)
       if (swap) {  // the LDS group and the other group in the global table
         const uint32_t* src = reinterpret_cast<const uint32_t*>(a.init);
         for (int64_t i = lane; i < hw; i += kDecThreads) {
@@ -547,7 +586,7 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
         }
       } else if (!GOLOMB && a.init) {  // initial states from the extradata (ffv1.c:185-189)
         const uint32_t* src = reinterpret_cast<const uint32_t*>(a.init);
-        for (int64_t i = lane; i < words; i += kDecThreads) st4[i] = src[i % (words / 2)];
+        for (int64_t i = lane; i < words; i += kDecThreads) st4[i] = src[i % (words / a.pcount)];
       } else {
         const uint32_t v0 = GOLOMB ? uint32_t(kVlcInit) : 0x80808080u;
         const uint32_t v1 = GOLOMB ? uint32_t(kVlcInit >> 32) : 0x80808080u;
@@ -570,10 +609,15 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
     if constexpr (!GOLOMB) uni_coder(c);  // lane 0's coder after the header, to every lane
     int run_index = 0;
     uint8_t* const obase = a.out + int64_t(f) * a.frame_bytes;
+    const int64_t per = a.state_bytes / a.pcount;  // one plane context's states
     if (!a.rgb) {
-      for (int p = 0; p < a.nplanes; p++) {
+      // decode_slice (ffv1dec.c:435-453): Y, Cb, Cr (plane context 1), A
+      // (plane context 2) at the luma size; YA8: Y and A (context 1) of the
+      // one packed plane, every second byte
+      const int ncoded = a.ya8 ? 2 : a.nplanes;
+      for (int p = 0; p < ncoded; p++) {
         for (int i = lane; i < 2 * a.row_cap; i += kDecThreads) ring[i] = 0;
-        const int grp = p ? 1 : 0;
+        const int grp = a.ya8 ? p : (p == 0 ? 0 : p < 3 ? 1 : 2);
         if (swap && grp != cur) {  // the other plane group's states into the LDS
           __syncthreads();
           for (int64_t i = lane; i < hw; i += kDecThreads) {
@@ -587,23 +631,32 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
         // decode_plane (ffv1dec.c:200-224): lane 0 decodes a row into LDS;
         // the wave then stores it (coalesced), so the serial loop issues no
         // global stores
-        uint8_t* pst = states + (p && !swap ? a.state_bytes / 2 : 0);
-        const int w = g->pw[p], h = g->ph[p];
-        const int64_t poff = p == 0 ? a.plane_off[0] : (p == 1 ? a.plane_off[1] : a.plane_off[2]);
-        const int pw = p == 0 ? a.plane_w[0] : (p == 1 ? a.plane_w[1] : a.plane_w[2]);
+        uint8_t* pst = states + (swap ? 0 : grp * per);
+        const int gp = a.ya8 ? 0 : p;  // geometry of the plane
+        const int w = g->pw[gp], h = g->ph[gp];
+        const int op = a.ya8 ? 0 : p;  // output plane
+        const int64_t poff = (op == 0 ? a.plane_off[0] : op == 1 ? a.plane_off[1] : op == 2 ? a.plane_off[2]
+                                                                                      : a.plane_off[3]) +
+                             (a.ya8 ? p : 0);
+        const int pw = op == 0 ? a.plane_w[0] : op == 1 ? a.plane_w[1] : op == 2 ? a.plane_w[2] : a.plane_w[3];
+        const int step = a.ya8 ? 2 : 1;
         run_index = 0;  // per plane (ffv1dec.c:204)
         for (int y = 0; y < h; y++) {
           int16_t* cur = ring + (y & 1) * a.row_cap;  // holds row y-2 until written
           const int16_t* up = ring + ((y + 1) & 1) * a.row_cap;
-          if constexpr (!GOLOMB)
-            decode_row_u(c, pst, (const sconst_i32*)(a.stab), pkw, model1, cur, up, w, bits);
-          else if (lane == 0)
+          if constexpr (!GOLOMB) {
+            if (pcm)
+              decode_row_pcm_u(c, pkw, cur, w, bits);
+            else
+              decode_row_u(c, pst, (const sconst_i32*)(a.stab), pkw, model1, cur, up, w, bits);
+          } else if (lane == 0) {
             decode_row<GOLOMB>(c, br, pst, reinterpret_cast<uint64_t*>(pst), tt, pkw, qt, model1, cur, up, w, bits,
                                run_index);
+          }
           __syncthreads();
-          const int64_t orow = int64_t(g->py[p] + y) * pw + g->px[p];
+          const int64_t orow = int64_t(g->py[gp] + y) * pw + int64_t(g->px[gp]) * step;
           if (a.sample_bytes == 1) {
-            for (int x = lane; x < w; x += kDecThreads) obase[poff + orow + x] = uint8_t(cur[x]);
+            for (int x = lane; x < w; x += kDecThreads) obase[poff + orow + int64_t(x) * step] = uint8_t(cur[x]);
           } else {
             uint16_t* o16 = reinterpret_cast<uint16_t*>(obase + poff) + orow;
             for (int x = lane; x < w; x += kDecThreads) {
@@ -617,34 +670,48 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
     } else {
       // decode_rgb_frame (ffv1dec.c:226-280): the rows of G', B', R' in
       // turn, one run index for the slice, then the inverse transform
-      for (int i = lane; i < 6 * a.row_cap; i += kDecThreads) ring[i] = 0;
+      // (p + 1) / 2: G' context 0, B' and R' 1, A 2; PCM rows (v4 slice_coding_mode 1)
+      // at the raw depth, untransformed
+      const int np = 3 + (a.transparency ? 1 : 0);
+      for (int i = lane; i < 2 * np * a.row_cap; i += kDecThreads) ring[i] = 0;
       __syncthreads();
       const int w = g->pw[0], h = g->ph[0];
+      const int pbits = a.bits_per_raw_sample <= 8 ? 8 : a.bits_per_raw_sample;
       for (int y = 0; y < h; y++) {
-        for (int p = 0; p < 3; p++) {
-          uint8_t* pst = states + (p ? a.state_bytes / 2 : 0);
+        for (int p = 0; p < np; p++) {
+          uint8_t* pst = states + ((p + 1) / 2) * per;
           int16_t* cur = ring + (2 * p + (y & 1)) * a.row_cap;
           const int16_t* up = ring + (2 * p + ((y + 1) & 1)) * a.row_cap;
-          if constexpr (!GOLOMB)
-            decode_row_u(c, pst, (const sconst_i32*)(a.stab), pkw, model1, cur, up, w, bits);
-          else if (lane == 0)
+          if constexpr (!GOLOMB) {
+            if (pcm)
+              decode_row_pcm_u(c, pkw, cur, w, pbits);
+            else
+              decode_row_u(c, pst, (const sconst_i32*)(a.stab), pkw, model1, cur, up, w, bits);
+          } else if (lane == 0) {
             decode_row<GOLOMB>(c, br, pst, reinterpret_cast<uint64_t*>(pst), tt, pkw, qt, model1, cur, up, w, bits,
                                run_index);
+          }
         }
         __syncthreads();
         const int16_t* G = ring + (y & 1) * a.row_cap;
         const int16_t* B = ring + (2 + (y & 1)) * a.row_cap;
         const int16_t* R = ring + (4 + (y & 1)) * a.row_cap;
+        const int16_t* A = ring + (6 + (y & 1)) * a.row_cap;
         const int64_t Y = g->py[0] + y;
         for (int x = lane; x < w; x += kDecThreads) {
-          int gg = G[x], bb = B[x] - a.rct_offset, rr = R[x] - a.rct_offset;
-          gg -= (bb + rr) >> 2;
-          bb += gg;
-          rr += gg;
+          int gg = G[x], bb = B[x], rr = R[x];
+          if (!pcm) {  // ffv1dec.c:258-264, with the slice's RCT coefficients (1, 1 below v4)
+            bb -= a.rct_offset;
+            rr -= a.rct_offset;
+            gg -= (bb * rby + rr * rry) >> 2;
+            bb += gg;
+            rr += gg;
+          }
           const int64_t X = g->px[0] + x;
-          if (a.sample_bytes == 4) {  // *(uint32_t *) = b + (g << 8) + (r << 16) + (a << 24), a = 0
+          if (a.sample_bytes == 4) {  // *(uint32_t *) = b + (g << 8) + (r << 16) + (a << 24)
+            const uint32_t av = a.transparency ? uint32_t(uint16_t(A[x])) : 0u;
             reinterpret_cast<uint32_t*>(obase + a.plane_off[0] + Y * a.plane_w[0] * 4)[X] =
-                uint32_t(bb) + (uint32_t(gg) << 8) + (uint32_t(rr) << 16);
+                uint32_t(bb) + (uint32_t(gg) << 8) + (uint32_t(rr) << 16) + (av << 24);
           } else {
             reinterpret_cast<uint16_t*>(obase + a.plane_off[0] + Y * a.plane_w[0] * 2)[X] = uint16_t(bb);
             reinterpret_cast<uint16_t*>(obase + a.plane_off[1] + Y * a.plane_w[1] * 2)[X] = uint16_t(gg);
@@ -684,7 +751,7 @@ __global__ void __launch_bounds__(256) ffv1_conceal(DecodeArgs a) {
   const int s = blockIdx.x;
   const SliceGeom* g = a.geom + s;
   uint8_t sticky = a.sticky[s];
-  const int np = a.rgb && a.sample_bytes == 4 ? 1 : a.nplanes;
+  const int np = (a.rgb && a.sample_bytes == 4) || a.ya8 ? 1 : a.nplanes;
   for (int f = 0; f < a.nframes; f++) {
     if (a.keyflags[f]) sticky = 0;
     const uint8_t dmg = a.damage[int64_t(f) * a.nslices + s];
@@ -693,14 +760,17 @@ __global__ void __launch_bounds__(256) ffv1_conceal(DecodeArgs a) {
     if (!sticky || (dmg & kDamageHeader) || !src) continue;
     uint8_t* dst = a.out + int64_t(f) * a.frame_bytes;
     for (int k = 0; k < np; k++) {
-      const int hs = k ? a.chroma_h_shift : 0, vs = k ? a.chroma_v_shift : 0;
+      // planes 1 and 2 are the subsampled ones; the x offset takes the
+      // component depth (> 8 bits: << 1), not the pixel size (ffv1dec.c:1006-1011)
+      const bool sub = k == 1 || k == 2;
+      const int hs = sub ? a.chroma_h_shift : 0, vs = sub ? a.chroma_v_shift : 0;
       const int bpp = a.sample_bytes;
-      const int64_t row = int64_t(k == 0 ? a.plane_w[0] : a.plane_w[k]) * bpp;
+      const int64_t row = int64_t(a.plane_w[k]) * bpp;
       const int64_t xoff = int64_t(g->px[0] >> hs) << (bpp == 2 ? 1 : 0);
-      const int64_t bytes = int64_t(-((-g->pw[0]) >> hs)) * bpp;
+      const int64_t bytes = int64_t(-((-g->pw[0]) >> hs)) * bpp * (a.ya8 ? 2 : 1);
       const int rows = -((-g->ph[0]) >> vs);
       const int64_t y0 = g->py[0] >> vs;
-      const int64_t poff = k == 0 ? a.plane_off[0] : (k == 1 ? a.plane_off[1] : a.plane_off[2]);
+      const int64_t poff = a.plane_off[k];
       for (int64_t i = threadIdx.x; i < int64_t(rows) * bytes; i += blockDim.x) {
         const int64_t y = i / bytes, x = i - y * bytes;
         const int64_t o = poff + (y0 + y) * row + xoff + x;
@@ -716,7 +786,7 @@ __global__ void __launch_bounds__(256) ffv1_conceal(DecodeArgs a) {
 
 int64_t decode_lds_bytes(const DecodeArgs& a, bool global_states) {
   const int64_t sb = global_states ? 0 : ((a.swap ? a.state_bytes / 2 : a.state_bytes) + 15) & ~int64_t(15);
-  return sb + 1024 + 64 + 5 * 256 * 2 + int64_t(a.rgb ? 6 : 2) * a.row_cap * 2;
+  return sb + 1024 + 64 + 5 * 256 * 2 + int64_t(a.rgb ? 2 * (3 + (a.transparency ? 1 : 0)) : 2) * a.row_cap * 2;
 }
 
 int launch_decode(const DecodeArgs& a, int nsegs, void* stream) {

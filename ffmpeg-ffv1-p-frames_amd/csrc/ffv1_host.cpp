@@ -137,7 +137,7 @@ struct Knobs {
 
 static const char* const kKnobNames[] = {"serial",     "walkdbg",    "walktrace", "hostdbg",   "walk_prio",
                                          "range_prio", "dseg_prio",  "sym_grid",  "bits_grid", "dseg_grid",
-                                         "walk_split", "copy_threads", "dec_swap", "coder",    "dense",
+                                         "walk_split", "copy_threads", "dec_swap", "coder",    "dense", "walk_blocks",
                                          "recsets",    "slice_cap",  "walk_part_a", "force_multi"};
 
 static int parse_knobs(Knobs* k) {
@@ -477,6 +477,7 @@ struct ffv1hip_ctx {
   // wave slots and registers, and walk waves launched meanwhile wait for CU
   // room until those blocks retire (FFV1HIP_SYM_GRID / _BITS_GRID / _DSEG_GRID)
   int grid_sym = 4096, grid_bits = 2048, grid_dseg = 4096;
+  int cus = 256;      // compute units of the device (a walk wave per SIMD: 4 per CU)
   int prio_dseg = 0;  // FFV1HIP_DSEG_PRIO (walk / range: per batch, run_batch)
   SliceGeom* d_geom = nullptr;
   int* d_slot_frames = nullptr;  // [j][slot]
@@ -593,6 +594,7 @@ struct ffv1hip_ctx {
   // encode2 with the pipe: the set being filled and the launched batches
   // whose packets are not handed out yet (batch id, pts)
   int q_set = 0;
+  int64_t last_out = -1;  // the packet the last encode2 call handed out (ready index), -1: none
   struct Launched {
     int64_t b;
     std::vector<int64_t> pts;
@@ -835,9 +837,9 @@ static void build_ops(ffv1hip_ctx* c) {
         L.sym(kSetSlice, 1, 3, false);  // progressive
         L.sym(kSetSlice, 1, p.sar_num, false);
         L.sym(kSetSlice, 1, p.sar_den, false);
-        if (p.version > 3) {  // ffv1enc.c:1052-1061: slice_coding_mode 0, the frame's RCT coefficients
-          L.bit(kSetSlice, 1, 0);
-          L.sym(kSetSlice, 1, 0, false);
+        if (p.version > 3) {  // ffv1enc.c:1052-1061: slice_coding_mode (0, or 1 for PCM), the RCT coefficients
+          L.ops.push_back(Op{int16_t(kOpBitMode), uint8_t(kSetSlice), 1, 0});
+          L.ops.push_back(Op{int16_t(kOpSymMode), uint8_t(kSetSlice), 1, 0});
           L.ops.push_back(Op{int16_t(kOpSymRct), uint8_t(kSetSlice), 1, 0});
           L.ops.push_back(Op{int16_t(kOpSymRct), uint8_t(kSetSlice), 1, 1});
         }
@@ -905,6 +907,13 @@ static void build_hdr(ffv1hip_ctx* c) {
 
 static int upload_hdr(ffv1hip_ctx* c) {
   if (!c->frames_mode) return 0;
+  // build_hdr codes every op with its host value: a device-valued op (v4's
+  // per-slice RCT coefficients) would come out wrong, so the frame-parallel
+  // mode must never see one (it admits version <= 3 only, ffv1hip_create)
+  for (size_t sel = 0; sel < c->nops.size(); sel++)
+    for (int q = 0; q < c->nops[sel]; q++)
+      if (c->ops[sel * kMaxOps + q].kind > kOpBit)
+        return set_err(-5, "internal: a device-valued header op in the frame-parallel mode");
   if (c->d_hdr) HIP_TRY(hipFree(c->d_hdr));
   if (c->d_hdr_digits) HIP_TRY(hipFree(c->d_hdr_digits));
   c->d_hdr = nullptr;
@@ -925,18 +934,33 @@ static void pipe_close(ffv1hip_ctx* c);
 // last ended (ms).
 static void dump_walk_trace(ffv1hip_ctx* c) {
   if (!c->d_trace || !c->trace_n) return;
-  std::vector<uint64_t> t(size_t(2) * c->trace_items * c->trace_n);
+  std::vector<uint64_t> t(size_t(kTraceWords) * c->trace_items * c->trace_n);
   if (hipDeviceSynchronize() != hipSuccess ||
       hipMemcpy(t.data(), c->d_trace, t.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
     return;
+  // walktrace=<path>: every wave's start, end (s_memrealtime), HW_ID and XCC_ID
+  const std::string path = c->knobs.str("walktrace");
+  if (!path.empty()) {
+    if (FILE* fp = std::fopen(path.c_str(), "w")) {
+      std::fprintf(fp, "batch,item,start,end,hw_id,xcc_id\n");
+      for (int b = 0; b < c->trace_n; b++)
+        for (int i = 0; i < c->trace_items; i++) {
+          const uint64_t* w = t.data() + size_t(kTraceWords) * (size_t(c->trace_items) * b + i);
+          if (w[0])
+            std::fprintf(fp, "%d,%d,%llu,%llu,%llu,%llu\n", b, i, (unsigned long long)w[0], (unsigned long long)w[1],
+                         (unsigned long long)w[2], (unsigned long long)w[3]);
+        }
+      std::fclose(fp);
+    }
+  }
   uint64_t prev_end = 0;
   for (int b = 0; b < c->trace_n; b++) {
-    const uint64_t* w = t.data() + size_t(2) * c->trace_items * b;
+    const uint64_t* w = t.data() + size_t(kTraceWords) * c->trace_items * b;
     int n = 0;
-    while (n < c->trace_items && w[2 * n]) n++;
+    while (n < c->trace_items && w[kTraceWords * n]) n++;
     if (!n) continue;
     uint64_t t0 = ~0ull;
-    for (int i = 0; i < n; i++) t0 = std::min(t0, w[2 * i]);
+    for (int i = 0; i < n; i++) t0 = std::min(t0, w[kTraceWords * i]);
     const int first = c->trace_first[b] ? c->trace_first[b] : n;
     for (int part = 0; part < 2; part++) {
       const int lo = part ? first : 0, hi = part ? n : first;
@@ -944,10 +968,10 @@ static void dump_walk_trace(ffv1hip_ctx* c) {
       uint64_t s0 = ~0ull, s1 = 0, e1 = 0;
       double dur = 0, dmax = 0;
       for (int i = lo; i < hi; i++) {
-        s0 = std::min(s0, w[2 * i]);
-        s1 = std::max(s1, w[2 * i]);
-        e1 = std::max(e1, w[2 * i + 1]);
-        const double d = double(w[2 * i + 1] - w[2 * i]) / 1e5;
+        s0 = std::min(s0, w[kTraceWords * i]);
+        s1 = std::max(s1, w[kTraceWords * i]);
+        e1 = std::max(e1, w[kTraceWords * i + 1]);
+        const double d = double(w[kTraceWords * i + 1] - w[kTraceWords * i]) / 1e5;
         dur += d;
         dmax = std::max(dmax, d);
       }
@@ -960,7 +984,7 @@ static void dump_walk_trace(ffv1hip_ctx* c) {
       std::fprintf(stderr, "walktrace batch %d: starts %.2f ms after batch %d's last wave ended\n", b,
                    (double(t0) - double(prev_end)) / 1e5, b - 1);
     prev_end = 0;
-    for (int i = 0; i < n; i++) prev_end = std::max(prev_end, w[2 * i + 1]);
+    for (int i = 0; i < n; i++) prev_end = std::max(prev_end, w[kTraceWords * i + 1]);
   }
 }
 
@@ -1087,6 +1111,7 @@ static int alloc_device(ffv1hip_ctx* c) {
   c->grid_bits = c->knobs.get("bits_grid", c->grid_bits);
   c->grid_dseg = std::max(1, c->knobs.get("dseg_grid", c->grid_dseg));
   c->prio_dseg = c->knobs.get("dseg_prio", c->prio_dseg);
+  HIP_TRY(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   for (hipEvent_t& e : c->hist_done) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_TRY(hipMalloc(&c->d_qt, sizeof(c->qt)));
@@ -1599,6 +1624,22 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   ca.pcount = c->pcount;
   ca.rct = c->d_rct;
   for (int k = 0; k < kMaxPlanes; k++) ca.pset[k] = sa.pset[k];
+  // v4 range coder: the reference's slice buffers (a packet of 16384 + 12 w h
+  // bytes, all of it for slice 0, 1 / slice_count each for the others,
+  // ffv1enc.c:1281-1282, 1317-1322) and the samples for the PCM re-code
+  ca.v4pcm = p.version > 3 && p.ac;
+  ca.v4_cap0 = 16384 + int64_t(p.width) * p.height * 12;
+  ca.v4_cap = ca.v4_cap0 / c->nslices;
+  ca.frames = d_frames;
+  ca.frame_bytes = frame_bytes;
+  for (int k = 0; k < kMaxPlanes; k++) {
+    ca.plane_off[k] = sa.plane_off[k];
+    ca.plane_stride[k] = sa.plane_stride[k];
+  }
+  ca.sample_bytes = p.sample_bytes;
+  ca.packed_at_lsb = p.packed_at_lsb;
+  ca.msb_shift = 16 - p.bits_per_raw_sample;
+  ca.pcm_bits = p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample;  // coded_bits without the RGB + 1
   ca.init = c->d_init;
 
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev[0], st));
@@ -1699,7 +1740,14 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       const bool chroma_long = 2 * int64_t(g0.pw[1]) * g0.ph[1] > int64_t(g0.pw[0]) * g0.ph[0];
       wa.rows = c->walk_rows;
       wa.per_short = walk_per_short(g0);
-      range_first = c->d_qt_walk && !chroma_long && walk_items(nsegs, c->nslices, wa.per_short) <= walk_resident(wa);
+      const int resident = walk_resident(wa);
+      wa.short_multi = walk_split_short(nsegs, c->nslices, wa.per_short, 4 * c->cus, resident);
+      // (the walk_blocks=0 hook, and the split-launch test hook, keep one-wave blocks)
+      wa.block_waves = c->knobs.get("walk_blocks", 1) && !c->knobs.has("walk_part_a")
+                           ? walk_block_waves(nsegs, c->nslices, wa.per_short, wa.short_multi, wa.rows, c->cus)
+                           : 1;
+      range_first = c->d_qt_walk && !chroma_long &&
+                    walk_items(nsegs, c->nslices, wa.per_short, wa.short_multi) <= resident;
     }
     wa.prio = c->knobs.get("walk_prio", range_first ? 0 : 2);
     const int range_prio = c->knobs.get("range_prio", range_first ? 3 : 0);
@@ -1707,18 +1755,18 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     wa.rows = c->walk_rows;
     wa.dense = c->d_qt_walk != nullptr;
     if (c->knobs.has("walktrace") && c->trace_n < ffv1hip_ctx::kTraceBatches) {
-      const int items = walk_items(nsegs, c->nslices, wa.per_short);
+      const int items = walk_items(nsegs, c->nslices, wa.per_short, wa.short_multi);
       if (!c->d_trace) {
-        c->trace_items = walk_items(c->max_slots, c->nslices, 1);
-        HIP_TRY(hipMalloc(&c->d_trace, sizeof(uint64_t) * 2 * c->trace_items * ffv1hip_ctx::kTraceBatches));
-        HIP_TRY(hipMemset(c->d_trace, 0, sizeof(uint64_t) * 2 * c->trace_items * ffv1hip_ctx::kTraceBatches));
+        c->trace_items = walk_items(c->max_slots, c->nslices, 1, c->max_slots);
+        HIP_TRY(hipMalloc(&c->d_trace, sizeof(uint64_t) * kTraceWords * c->trace_items * ffv1hip_ctx::kTraceBatches));
+        HIP_TRY(hipMemset(c->d_trace, 0, sizeof(uint64_t) * kTraceWords * c->trace_items * ffv1hip_ctx::kTraceBatches));
       }
-      if (items <= c->trace_items) wa.trace = c->d_trace + size_t(2) * c->trace_items * c->trace_n;
+      if (items <= c->trace_items) wa.trace = c->d_trace + size_t(kTraceWords) * c->trace_items * c->trace_n;
     }
     // walkdbg (measurement hook): per-block cycle split to stderr
     const bool walkdbg = c->knobs.has("walkdbg");
     uint64_t* d_dbg = nullptr;
-    const int nblk = walk_items(nsegs, c->nslices, wa.per_short);
+    const int nblk = walk_items(nsegs, c->nslices, wa.per_short, wa.short_multi);
     const int nlong = nsegs * ((c->nslices + 1) / 2);
     if (walkdbg) {
       HIP_TRY(hipMalloc(&d_dbg, sizeof(uint64_t) * 4 * nblk));
@@ -1728,13 +1776,14 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     // split schedule: the first part is what the CUs hold at once
     // (the walk_split=0 hook: one launch); one timed region either way
     const bool split_env = c->knobs.get("walk_split", 1) != 0;
-    const int nitems = walk_items(nsegs, c->nslices, wa.per_short);
+    const int nitems = walk_items(nsegs, c->nslices, wa.per_short, wa.short_multi);
     // walk_part_a (test hook): the first part's waves
     const bool pa = c->knobs.has("walk_part_a");
     const int first = sst != st && split_env ? (pa ? c->knobs.get("walk_part_a", 0) : walk_resident(wa)) : 0;
     // ... and only when the second part leaves room on the CUs beside it
     // (at most 80 % of the resident slots: c5's 100 % ran slower in round 2)
-    const bool two_parts = first > 0 && first < nitems && (pa || int64_t(nitems - first) * 100 <= int64_t(first) * 80);
+    const bool two_parts = wa.block_waves == 1 && first > 0 && first < nitems &&
+                           (pa || int64_t(nitems - first) * 100 <= int64_t(first) * 80);
     HIP_TRY(hipEventRecord(c->walk_go, st));
     if (timed(2, st, [&] {
           if (!two_parts) return launch_walk(wa, nsegs, st);
@@ -1923,6 +1972,7 @@ static int grow_slice_budget(ffv1hip_ctx* c, int64_t needed) {
 static int settle_batch(ffv1hip_ctx* c, int64_t b) {
   if (b < 0 || b < c->nsub - 2 || b >= c->nsub) return 0;
   bool redo_next = false;
+  bool pcm_fail = false;
   ffv1hip_ctx::LastBatch next;
   for (int attempt = 0;; attempt++) {
     const ffv1hip_ctx::LastBatch& L = c->hist[b & 1];
@@ -1935,6 +1985,7 @@ static int settle_batch(ffv1hip_ctx* c, int64_t b) {
     } else {
       HIP_TRY(hipMemcpy(status, c->d_status + 4 * L.status_set, sizeof(status), hipMemcpyDeviceToHost));
     }
+    pcm_fail = status[2] != 0;
     if (!status[0]) break;
     if (attempt >= 2 || !L.valid)
       return set_err(-28, "%d slices exceeded the slice byte budget", status[0]);
@@ -1969,27 +2020,9 @@ static int settle_batch(ffv1hip_ctx* c, int64_t b) {
     const int rc = run_batch(c, next.frames, next.frame_bytes, next.plane_off, next.plane_stride, next.n, nullptr);
     if (rc < 0) return rc;
   }
-  if (c->P.version > 3) {
-    // v4: the reference re-codes a range-coded slice as PCM (slice_coding_mode
-    // 1, ffv1enc.c:1207-1217) when a line starts with less than 35 * w bytes
-    // left in its buffer (:282-286; Golomb-Rice: 4 * w, and the frame
-    // fails); the buffers are a packet of 16384 + 12 * w * h bytes, all of
-    // it for slice 0, 1 / slice_count each for the others (:1281-1282,
-    // 1317-1322).  A slice that ends within that margin might have taken
-    // that path, which is not coded here: an error, never other bytes.
-    const ffv1hip_ctx::LastBatch& L = c->hist[b & 1];
-    std::vector<int64_t> sb(size_t(L.n) * c->nslices);
-    HIP_TRY(hipMemcpy(sb.data(), c->d_slice_bytes, sb.size() * sizeof(int64_t), hipMemcpyDeviceToHost));
-    const int64_t pkt = 16384 + int64_t(c->P.width) * c->P.height * 12;
-    for (size_t i = 0; i < sb.size(); i++) {
-      const int s = int(i % c->nslices);
-      const int64_t cap = s == 0 ? pkt : pkt / c->nslices;
-      if (sb[i] > cap - int64_t(c->P.ac ? 35 : 4) * c->geom[s].pw[0])
-        return set_err(-38, "version 4: slice %d of frame %lld would be coded as PCM by the reference "
-                            "(slice_coding_mode 1), which this encoder does not do", s,
-                       (long long)(L.pn0 + int64_t(i) / c->nslices));
-    }
-  }
+  if (pcm_fail)  // the chained coder's v4 PCM re-code did not fit either
+    return set_err(-38, "version 4: a slice overflowed its buffer even as PCM (the reference asserts there, "
+                        "ffv1enc.c:1209)");
   return 0;
 }
 
@@ -2118,7 +2151,7 @@ static int pipe_open_parts(ffv1hip_ctx* c) {
     HIP_TRY(hipHostMalloc(&P.h_slot[k], size_t(P.slot_bytes), hipHostMallocDefault));
     HIP_TRY(hipEventCreateWithFlags(&P.slot_ev[k], hipEventDisableTiming));
   }
-  if (c->pass != 1 && c->P.version <= 3) {  // (v4 checks each batch's slice sizes before the next one)
+  if (c->pass != 1) {
     // the second set: frames, packets, their sizes, and the second packed
     // packets buffer alloc_compact adds (with the first one, not allocated
     // yet either), with 2 GB to spare
@@ -2534,6 +2567,7 @@ int ffv1hip_encode2(ffv1hip_ctx* c, const void* const planes[4], const int strid
     }
     if (!c->launched.empty() && (rc = collect_ready(c)) < 0) return rc;
   }
+  c->last_out = -1;
   if (R.next >= R.size.size()) return 0;
   const size_t i = R.next;
   if (out) {
@@ -2550,8 +2584,20 @@ int ffv1hip_encode2(ffv1hip_ctx* c, const void* const planes[4], const int strid
   if (pts_out) *pts_out = R.pts[i];
   if (key) *key = R.key[i];
   *got_packet = 1;
+  c->last_out = int64_t(i);
   R.next++;
   return 0;
+}
+
+int64_t ffv1hip_encode2_last_packet(ffv1hip_ctx* c, uint8_t* out, int64_t cap) {
+  if (!c) return set_err(-22, "null ctx");
+  const ffv1hip_ctx::Ready& R = c->ready;
+  if (c->last_out < 0 || size_t(c->last_out) >= R.size.size()) return set_err(-22, "no packet handed out");
+  const size_t i = size_t(c->last_out);
+  if (R.size[i] > cap) return set_err(-28, "packet of %lld bytes, buffer %lld", (long long)R.size[i], (long long)cap);
+  if (R.size[i] && !out) return set_err(-22, "null buffer");
+  if (R.size[i]) pool_copy2d(*c->pipe.pool_out, out, R.size[i], R.base + R.off[i], R.size[i], R.size[i], 1);
+  return R.size[i];
 }
 
 int ffv1hip_set_profiling(ffv1hip_ctx* c, int enable) {
@@ -2641,16 +2687,18 @@ int ffv1hip_set_slice_states(ffv1hip_ctx* c, const uint8_t* buf, int64_t size) {
 // from the packet end (ffv1dec.c:931-989); the slices decode on the GPU.
 struct ffv1hip_dec {
   Knobs knobs;
+  int pcount = 2;  // plane contexts: 2, 3 with alpha
   ffv1hip_params P{};
   int device = 0;
   int nslices = 0;
   int contexts = 0;
   int64_t state_bytes = 0;
   int64_t frame_bytes = 0;
-  int64_t plane_off[3]{};
-  int plane_w[3]{};
-  int out_planes = 0;      // planes handed back per frame (bgr0: one packed plane)
-  int out_rows[3]{};
+  int64_t plane_off[kMaxPlanes]{};
+  int plane_w[kMaxPlanes]{};  // samples per row (bgr0 / RGB32: 4-byte pixels; YA8: 2-byte Y, A pairs)
+  int out_planes = 0;      // planes handed back per frame (bgr0, RGB32, YA8: one packed plane)
+  int out_rows[kMaxPlanes]{};
+  int in_stride = 3;       // plane pointers per frame in ffv1hip_decode's arrays (4 for YUVA)
   int row_cap = 0;
   bool global_states = false;
   bool swap = false;  // range coder, YCbCr: one plane group's states in the LDS at a time
@@ -2810,15 +2858,13 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
   };
   if (!params) return fail(set_err(-22, "invalid arguments"));
   const ffv1hip_params& p = *params;
-  if (p.version == 2 || p.version > 3 || p.num_h_slices * p.num_v_slices > 256 || p.bits_per_raw_sample < 8 ||
+  if (p.version == 2 || p.version > 4 || p.num_h_slices * p.num_v_slices > 256 || p.bits_per_raw_sample < 8 ||
       p.bits_per_raw_sample > 16 || p.width <= 0 || p.height <= 0 || p.num_h_slices <= 0 || p.num_v_slices <= 0 ||
       (p.version < 2 && p.num_h_slices * p.num_v_slices != 1) || p.context_model < 0 || p.context_model > 1 ||
       p.colorspace < 0 || p.colorspace > 1 || p.ac < 0 || p.ac > 2)
     return fail(set_err(-38, "GPU decoder: unsupported parameter set"));
-  if (p.transparency)  // the oracle decoder reads these streams (tests/test_alpha.py)
-    return fail(set_err(-38, "GPU decoder: alpha planes are not decoded on the GPU"));
-  if (p.version > 3)  // likewise (tests/test_v4.py)
-    return fail(set_err(-38, "GPU decoder: version 4 is not decoded on the GPU"));
+  if (p.version > 4)
+    return fail(set_err(-38, "GPU decoder: unsupported parameter set"));
   // The stream's extradata must be the one these parameters produce
   // (read_extradata, ffv1dec.c:509-631, would derive the same parameters);
   // versions 0 and 1 have none, their header is in band.
@@ -2845,21 +2891,29 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
   d->device = device;
   d->nslices = p.num_h_slices * p.num_v_slices;
   d->contexts = tmp.contexts;
-  d->state_bytes = int64_t(2) * d->contexts * (p.ac ? 32 : 8);
+  d->pcount = 2 + (p.transparency != 0);
+  d->state_bytes = int64_t(d->pcount) * d->contexts * (p.ac ? 32 : 8);
   const int cw = p.chroma_planes ? -((-p.width) >> p.chroma_h_shift) : 0;
   const int ch = p.chroma_planes ? -((-p.height) >> p.chroma_v_shift) : 0;
   const bool bgr0 = p.sample_bytes == 4;
-  const int64_t pb0 = int64_t(p.width) * p.height * p.sample_bytes;
+  const bool ya8 = is_ya8(p);
+  // the encoder's input layout: Y, Cb, Cr, A (YUVA); YA8 one plane of Y, A
+  // byte pairs; bgr0 / RGB32 one plane of 4-byte pixels
+  const int64_t pb0 = int64_t(p.width) * p.height * p.sample_bytes * (ya8 ? 2 : 1);
   const int64_t pb1 = bgr0 ? 0 : int64_t(cw) * ch * p.sample_bytes;
+  const bool yuva = p.transparency && !p.colorspace && p.chroma_planes;
   d->plane_off[0] = 0;
   d->plane_off[1] = pb0;
   d->plane_off[2] = pb0 + pb1;
-  d->plane_w[0] = p.width;
+  d->plane_off[3] = pb0 + 2 * pb1;
+  d->plane_w[0] = p.width * (ya8 ? 2 : 1);
   d->plane_w[1] = d->plane_w[2] = cw;
-  d->out_planes = bgr0 ? 1 : p.chroma_planes ? 3 : 1;
-  d->out_rows[0] = p.height;
+  d->plane_w[3] = p.width;
+  d->out_planes = bgr0 || ya8 ? 1 : p.chroma_planes ? 3 + (yuva ? 1 : 0) : 1;
+  d->in_stride = yuva ? FFV1HIP_PLANES_YUVA : FFV1HIP_PLANES;
+  d->out_rows[0] = d->out_rows[3] = p.height;
   d->out_rows[1] = d->out_rows[2] = ch;
-  d->frame_bytes = (pb0 + 2 * pb1 + 255) & ~int64_t(255);
+  d->frame_bytes = (pb0 + 2 * pb1 + (yuva ? int64_t(p.width) * p.height * p.sample_bytes : 0) + 255) & ~int64_t(255);
   d->geom.resize(d->nslices);
   for (int s = 0; s < d->nslices; s++) {  // ffv1.c:117-145, ffv1dec.c:361-474
     SliceGeom& g = d->geom[s];
@@ -2877,6 +2931,9 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
       g.px[k] = x0 >> p.chroma_h_shift;
       g.py[k] = y0 >> p.chroma_v_shift;
     }
+    if (yuva) {  // A at the luma rectangle
+      g.px[3] = g.px[0]; g.py[3] = g.py[0]; g.pw[3] = g.pw[0]; g.ph[3] = g.ph[0];
+    }
     d->row_cap = std::max(d->row_cap, g.pw[0]);
   }
   d->row_cap = (d->row_cap + 7) & ~7;
@@ -2884,11 +2941,13 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
   DecodeArgs la{};
   la.state_bytes = d->state_bytes;
   la.rgb = p.colorspace;
+  la.transparency = p.transparency;
   la.row_cap = d->row_cap;
   constexpr int64_t kDecLds = 64 * 1024;
   d->global_states = decode_lds_bytes(la, false) > kDecLds;
   // dec_swap=0 (measurement hook): both plane groups in the LDS
-  d->swap = !d->global_states && p.ac && !p.colorspace && p.chroma_planes && d->knobs.get("dec_swap", 1) != 0;
+  d->swap = !d->global_states && p.ac && !p.colorspace && p.chroma_planes && !p.transparency &&
+            d->knobs.get("dec_swap", 1) != 0;
   if (decode_lds_bytes(la, true) > kDecLds) {
     delete d;
     return fail(set_err(-38, "GPU decoder: slice too wide for the LDS row buffer"));
@@ -3036,7 +3095,10 @@ int ffv1hip_decode(ffv1hip_dec* d, const uint8_t* packets, const int64_t* sizes,
     a.segs = d_segs;
     a.geom = d->d_geom;
     a.nslices = ns;
-    a.nplanes = p.chroma_planes ? 3 : 1;
+    a.nplanes = p.chroma_planes ? 3 + (p.transparency && !p.colorspace ? 1 : 0) : 1;
+    a.transparency = p.transparency;
+    a.ya8 = is_ya8(p);
+    a.pcount = d->pcount;
     a.qt = d->d_qt;
     a.ftab = d->d_tabs;
     a.dtab = d->d_tabs + 512;
@@ -3047,7 +3109,7 @@ int ffv1hip_decode(ffv1hip_dec* d, const uint8_t* packets, const int64_t* sizes,
     a.tables = d_tables;
     a.out = d_out;
     a.frame_bytes = d->frame_bytes;
-    for (int k = 0; k < 3; k++) {
+    for (int k = 0; k < kMaxPlanes; k++) {
       a.plane_off[k] = d->plane_off[k];
       a.plane_w[k] = d->plane_w[k];
     }
@@ -3092,7 +3154,7 @@ int ffv1hip_decode(ffv1hip_dec* d, const uint8_t* packets, const int64_t* sizes,
     for (int f = 0; f < n_frames; f++)
       for (int k = 0; k < d->out_planes; k++) {
         const int64_t wb = int64_t(d->plane_w[k]) * p.sample_bytes;
-        HIP_TRY(hipMemcpy2DAsync(planes[3 * f + k], strides[3 * f + k],
+        HIP_TRY(hipMemcpy2DAsync(planes[d->in_stride * f + k], strides[d->in_stride * f + k],
                                  d_out + int64_t(f) * d->frame_bytes + d->plane_off[k], size_t(wb), size_t(wb),
                                  d->out_rows[k], hipMemcpyDeviceToHost, d->stream));
       }

@@ -18,7 +18,10 @@ namespace ffv1hip {
 // kOpSymRct: an unsigned symbol whose value is the frame's slice RCT
 // coefficient (value 0: slice_rct_by_coef, 1: slice_rct_ry_coef; v4 slice
 // header, ffv1enc.c:1058-1059), chosen on the device per (frame, slice)
-enum OpKind : int16_t { kOpSymU = 0, kOpSymS = 1, kOpBit = 2, kOpSymRct = 3 };
+// kOpBitMode / kOpSymMode: v4's slice_coding_mode bit and symbol
+// (ffv1enc.c:1054-1056): 0, or 1 when the slice is coded again as PCM; the
+// RCT symbols are then left out (:1057-1060).
+enum OpKind : int16_t { kOpSymU = 0, kOpSymS = 1, kOpBit = 2, kOpSymRct = 3, kOpBitMode = 4, kOpSymMode = 5 };
 struct Op {
   int16_t kind;
   uint8_t set;
@@ -193,6 +196,17 @@ struct CodeArgs {
   int pset[kMaxPlanes];       // plane context set of each coded plane
   int pcount;                 // plane contexts (plane_count: 2, 3 with alpha)
   const int2* rct;            // v4: [batch frame][slice] RCT coefficients for the slice header ops
+  // v4 range coder (chained): the reference's per-line buffer check
+  // (ffv1enc.c:282-286) against its slice buffers (:1281-1282, 1317-1322) and
+  // the PCM re-code of a slice that fails it (:1207-1217, 294-304), which
+  // reads the samples from the frames
+  int v4pcm;
+  int64_t v4_cap0, v4_cap;    // the reference's buffer bytes: slice 0 (the packet), the others
+  const uint8_t* frames;
+  int64_t frame_bytes;
+  int64_t plane_off[kMaxPlanes];
+  int plane_stride[kMaxPlanes];
+  int sample_bytes, packed_at_lsb, msb_shift, pcm_bits;
   int nframes;                // decision-stream mode: frames of the batch
   DecisionStream ds;
   const uint8_t* init;        // chained range coder: 2-pass initial states [contexts][32], or null
@@ -244,16 +258,20 @@ struct WalkArgs {
   DecisionStream ds;
   uint8_t* scratch;           // >= 2 KiB: where idle chains write their stage
   uint64_t* dbg;              // optional [block][4] cycle counters (FFV1HIP_WALKDBG)
-  uint64_t* trace;            // optional [item][2] start / end s_memrealtime of each wave (FFV1HIP_WALKTRACE)
+  uint64_t* trace;            // optional [item][kTraceWords]: start / end s_memrealtime, HW_ID, XCC_ID of each wave
   int force_multi;            // measurement hook: every chunk on the checked (multi) step
   const uint8_t* init;        // 2-pass initial states [contexts][32] at keyframes, or null (all 128)
   int nitems, item0;          // set by launch_walk: all items of the batch, the launch's first
   int nsegs;                  // segments of the batch
   int per_short;              // segments one wave of the shorter plane group walks, one after the other
+  int short_multi;            // shorter-group waves (per slice pair) that take per_short segments; the rest take one
+  int block_waves;            // 1, or 4 / 5 waves per block for a one-round batch (walk_block_waves)
   int prio;                   // wave priority (s_setprio)
   int rows;                   // context rows of a plane group's table in LDS (kDenseRows when dense)
   int dense;                  // records address dense rows (dense_row), the state tables keep contexts
 };
+
+constexpr int kTraceWords = 4;
 
 // Above 8 bits the quantisers of context model 0 have 9 levels (ffv1enc.c:
 // 846-879, quant9_10bit), so only 365 of the 666 contexts q0 + 11 q1 + 121 q2
@@ -323,8 +341,8 @@ struct DecodeArgs {
   uint8_t* tables;             // global states [seg][slice][state_bytes] when they exceed the LDS
   uint8_t* out;                // [frame] regions of frame_bytes, planes tightly packed
   int64_t frame_bytes;
-  int64_t plane_off[3];
-  int plane_w[3];
+  int64_t plane_off[kMaxPlanes];  // output planes: Y, Cb, Cr, A (YUVA); one packed plane for bgr0 / RGB32 / YA8
+  int plane_w[kMaxPlanes];
   int sample_bytes, packed_at_lsb, msb_shift, coded_bits;
   int width, height, num_h, num_v, context_model;
   int version, ac, ec, rgb, rct_offset, contexts;
@@ -338,6 +356,8 @@ struct DecodeArgs {
   int nframes;
   const uint8_t* init;         // range coder: initial states [contexts][32] from the extradata, or null
   int swap;                    // one plane group's states in the LDS, the other in `tables` (range, YCbCr)
+  int transparency, ya8;       // alpha: a third plane context (YUVA's A, RGB32's A rows); YA8: Y, A of one plane
+  int pcount;                  // plane contexts: 2, 3 with alpha
   const int32_t* stab;         // [256] frame table pairs to0 | to1 << 8, then [5][256] quant tables (scalar loads)
 };
 int launch_decode(const DecodeArgs& a, int nsegs, void* stream);
@@ -361,7 +381,9 @@ int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first = 0, int c
 // segment per wave, then the shorter group's, per_short segments per wave one
 // after the other, so that both kinds of wave walk about as many symbols
 // (4:2:0 luma vs Cb + Cr, 4:4:4 Cb + Cr vs luma: 2).
-int walk_items(int nsegs, int nslices, int per_short);
+int walk_items(int nsegs, int nslices, int per_short, int short_multi);
+int walk_split_short(int nsegs, int nslices, int per_short, int simds, int resident);
+int walk_block_waves(int nsegs, int nslices, int per_short, int short_multi, int rows, int cus);
 int walk_per_short(const SliceGeom& g);
 int walk_resident(const WalkArgs& a);  // (uses a.rows)
 int launch_range(const CodeArgs& a, void* stream);

@@ -657,16 +657,21 @@ constexpr int kOpsetBytes = kOpSets * 32;
 // Key bit / in-band v0/v1 header / v3 slice header (per-lane op program).
 // os: this lane's op-set states (osb bytes); flush_at: the ring's flush
 // threshold before each op (<= 29 digits per op).
+// Ops [q0, q1) of the lane's program; the op states reset at q0 == 0.  pcm:
+// v4's slice_coding_mode 1 (the PCM re-code): the mode ops code 1 and the RCT
+// symbols are left out (ffv1enc.c:1054-1060).
 template <class SinkT>
 __device__ __forceinline__ void run_header_ops(const CodeArgs& a, Lane& L, SinkT& S, uint8_t* os, int key,
                                                int slice, bool live, const uint8_t* dtab,
-                                               const uint8_t* ftab, int osb, int flush_at, int f) {
-  for (int i = 0; i < osb; i++) os[i] = 128;
+                                               const uint8_t* ftab, int osb, int flush_at, int f,
+                                               int q0 = 0, int q1 = kMaxOps, bool pcm = false) {
+  if (q0 == 0)
+    for (int i = 0; i < osb; i++) os[i] = 128;
   const int sel = key * a.nslices + slice;
-  const int n = live ? a.nops[sel] : 0;
+  const int n = live ? min(a.nops[sel], q1) : 0;
   const Op* ops = a.ops + (int64_t)sel * kMaxOps;
   for (int q = 0; q < a.max_ops; q++) {
-    if (q < n) {
+    if (q >= q0 && q < n) {
       const Op op = ops[q];
       const uint8_t* t = op.tab ? ftab : dtab;
       uint8_t* st = os + op.set * 32;
@@ -675,13 +680,35 @@ __device__ __forceinline__ void run_header_ops(const CodeArgs& a, Lane& L, SinkT
         const int2 co = a.rct[(int64_t)f * a.nslices + slice];
         v = op.value ? co.y : co.x;
       }
-      if (op.kind == kOpBit)
+      if (op.kind == kOpBitMode || op.kind == kOpSymMode) v = pcm ? 1 : 0;
+      if (op.kind == kOpBit || op.kind == kOpBitMode)
         put_lds(L, st, v, t);
-      else
+      else if (!(pcm && op.kind == kOpSymRct))
         symbol_lds(L, st, v, op.kind == kOpSymS, t);
     }
     flush_if(L, S, flush_at);
   }
+}
+
+// A v4 PCM sample (encode_line's slice_coding_mode 1, ffv1enc.c:294-304):
+// coded plane p of the slice at (x, y), untransformed: YCbCr the stored
+// sample; RGB (encode_rgb_frame, :419-445) g, b, r, a from the bgr0 / RGB32
+// word or the gbrp planes read in AVFrame data[] order as b, g, r.
+__device__ __forceinline__ int pcm_sample(const CodeArgs& a, const SliceGeom& g, int f, int p, int x, int y) {
+  const uint8_t* fr = a.frames + (int64_t)f * a.frame_bytes;
+  if (a.rgb) {
+    const int X = g.px[0] + x, Y = g.py[0] + y;
+    if (a.sample_bytes == 4) {
+      const uint32_t v = reinterpret_cast<const uint32_t*>(fr + a.plane_off[0] + (int64_t)Y * a.plane_stride[0])[X];
+      return p == 0 ? (int)((v >> 8) & 0xFF) : p == 1 ? (int)(v & 0xFF) : p == 2 ? (int)((v >> 16) & 0xFF)
+                                                                              : (int)(v >> 24);
+    }
+    const int src = p == 0 ? 1 : p == 1 ? 0 : 2;  // g from data[1], b from data[0], r from data[2]
+    return reinterpret_cast<const uint16_t*>(fr + a.plane_off[src] + (int64_t)Y * a.plane_stride[src])[X];
+  }
+  const uint16_t v =
+      reinterpret_cast<const uint16_t*>(fr + a.plane_off[p] + (int64_t)(g.py[p] + y) * a.plane_stride[p])[g.px[p] + x];
+  return a.packed_at_lsb ? (int)v : (int)(v >> a.msb_shift);
 }
 
 __device__ __forceinline__ void lane_init(Lane& L, uint32_t* ring) {
@@ -757,11 +784,31 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
   uint8_t* const out = a.slice_out + ((int64_t)(live ? f : 0) * a.nslices + slice) * a.slice_stride;
   Sink S = make_sink(out, live ? a.slice_cap : 0);  // idle lanes write nothing
 
-  run_header_ops(a, L, S, opsets + lane * kOpsetBytes, key, slice, live, dtab, ftab, kOpsetBytes, kHeaderFlushAt,
-                 live ? f : 0);
+  // v4: the coder as encode_slice finds it (c_bak, ffv1enc.c:1157), after
+  // slice 0's key bit: the PCM re-code restarts from there
+  const int split = a.v4pcm && slice == 0 ? 1 : 0;
+  uint8_t* const myops = opsets + lane * kOpsetBytes;
+  run_header_ops(a, L, S, myops, key, slice, live, dtab, ftab, kOpsetBytes, kHeaderFlushAt, live ? f : 0, 0,
+                 a.v4pcm ? split : kMaxOps);
+  Lane Lb = L;
+  Sink Sb = S;
+  if (a.v4pcm) {
+    flush(L, S);
+    Lb = L;
+    Sb = S;
+    run_header_ops(a, L, S, myops, key, slice, live, dtab, ftab, kOpsetBytes, kHeaderFlushAt, live ? f : 0, split);
+  }
 
   const SliceGeom& g = a.geom[slice];
   const int64_t nsym = live ? g.nsym : 0;
+  // v4: encode_line's check at every line start (ffv1enc.c:282-286): fewer
+  // than 35 * w bytes left in the slice's buffer (the bytes written so far,
+  // renorm_encoder's outstanding byte and 0xFF run not counted) fails the
+  // slice, which is then coded again as PCM.  v4 planes all have the luma
+  // width (4:4:4 or RGB), so lines start every pw[0] symbols.
+  const int lw = g.pw[0];
+  const int64_t v4_limit = (slice == 0 ? a.v4_cap0 : a.v4_cap) - 35 * (int64_t)lw;
+  bool failed = false;
   const int64_t nmax = wave_max((int)nsym);
   // g.sym_off and frame_samples are multiples of 4 (host-side padding);
   // idle lanes read group 0 of slot 0
@@ -781,7 +828,12 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
   flush_if(L, S, kFlushAt);
 
   auto sym_step = [&](int64_t ii, uint32_t sv, uint32_t sn) {
-    const bool act = ii < nsym;
+    if (a.v4pcm) {
+      const bool ls = ii < nsym && !failed && ii % lw == 0;
+      if (__ballot(ls)) flush(L, S);
+      failed = failed || (ls && S.opos + S.on > v4_limit);
+    }
+    const bool act = ii < nsym && !failed;
     const int row = act ? (int)(sv >> 16) : cur;
     const bool sw = row != cur;  // context switch: take the prefetched row
     L.r0 = sw ? PFa.x : L.r0; L.r1 = sw ? PFa.y : L.r1; L.r2 = sw ? PFa.z : L.r2; L.r3 = sw ? PFa.w : L.r3;
@@ -824,6 +876,51 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
     flush_if(L, S, kFlushAt);
     G = GN;
     GN = sp[min(gi + 2, glast)];
+  }
+
+  if (__ballot(failed)) {
+    // the PCM re-code (ffv1enc.c:1207-1217): the coder as it was before the
+    // slice header, the header with slice_coding_mode 1 (which clears the
+    // slice's context states, :1054-1055), then every sample's bits MSB
+    // first on a fresh state 128 each (:294-304), with the same per-line
+    // buffer check (the reference asserts when that fails too)
+    if (failed) {
+      L = Lb;
+      L.rp = L.ring;
+      S = Sb;
+    }
+    run_header_ops(a, L, S, myops, key, slice, failed, dtab, ftab, kOpsetBytes, kHeaderFlushAt, live ? f : 0,
+                   split, kMaxOps, true);
+    if (failed) {
+      const uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
+      const int64_t per = a.state_bytes / (16 * a.pcount);
+      for (int64_t i = 0; i < a.state_bytes / 16; i++)
+        reinterpret_cast<uint4*>(table)[i] = a.init ? reinterpret_cast<const uint4*>(a.init)[i % per] : v;
+    }
+    const int np = a.nplanes;
+    const int64_t npcm = failed ? nsym : 0;
+    bool again = false;
+    for (int64_t ii = 0; __ballot(ii < npcm); ii++) {
+      const bool act = ii < npcm;
+      const bool ls = act && ii % lw == 0;
+      if (__ballot(ls)) flush(L, S);
+      again = again || (ls && S.opos + S.on > v4_limit);
+      // symbol ii of the slice in coding order: RGB rows interleave the
+      // planes (row, plane, x), YCbCr planes follow each other
+      const int64_t line = ii / lw;
+      const int x = (int)(ii - line * lw);
+      const int p = a.rgb ? (int)(line % np) : (int)(line / g.ph[0]);
+      const int y = a.rgb ? (int)(line / np) : (int)(line % g.ph[0]);
+      const int v = act ? pcm_sample(a, g, f, p, x, y) : 0;
+      for (int i = a.pcm_bits - 1; i >= 0; i--) {
+        rac_core(L, act ? 128 : 0, (v >> i) & 1);
+        renorm(L);
+      }
+      flush_if(L, S, kRing - 20);
+    }
+    if (again) {  // the reference's av_assert0(slice_coding_mode == 0) (ffv1enc.c:1209)
+      atomicAdd(a.status + 2, 1);
+    }
   }
 
   if (live) {
@@ -908,6 +1005,10 @@ __device__ __forceinline__ Masks8 masks8(uint32_t bw) {
 // 32 decisions on `range` alone; shifts counts the renormalisations (x 8).  A
 // state-0 decision of bit 0 (the zeroed tail of a stream) leaves range as
 // it is: r1 = 0, range - r1 = range.
+// (Measured slower: put_rac's two outcomes as one multiply-add, P = range *
+// (bit ? s : 256 - s) + (bit ? 0 : 255), renormalised by a compare on P: a
+// three-deep chain per decision instead of seven, but more instructions, and
+// the pass is issue-bound: 72 vs 63 ms alone at 21 GOPs.)
 __device__ __forceinline__ void range32(int& range, int& shifts, const uint4& wa, const uint4& wb, uint32_t bw) {
   static_for<0, 4>([&](auto gc) {
     constexpr int G = decltype(gc)::value;
@@ -1281,10 +1382,11 @@ static_assert(kCopyBlocks * 32 * 16 <= kChainPad, "the copy-out stays inside the
 
 // LDS image of the walk: a fixed part (static, so every offset below is an
 // instruction immediate) and the two state tables (dynamic).
-constexpr int kLdsN = 0;                                      // u8 [3][256]: a slot's next state
-constexpr int kLdsRecs = kLdsN + kT3Bytes;                    // [2][kRecSlots] records
-constexpr int kLdsPre = kLdsRecs + 2 * kRecSlots * 16;        // [2][kPreHalf] recorded states
-constexpr int kLdsFixed = kLdsPre + 2 * kPreHalf;
+constexpr int kLdsN = 0;                                      // u8 [8][256]: a slot's next state (the block's)
+constexpr int kLdsRecs = kLdsN + kT3Bytes;                    // wave 0: [2][kRecSlots] records
+constexpr int kLdsPre = kLdsRecs + 2 * kRecSlots * 16;        // wave 0: [2][kPreHalf] recorded states
+constexpr int kStageBytes = 2 * kRecSlots * 16 + 2 * kPreHalf;  // one wave's records and recorded states
+constexpr int kLdsFixed = kLdsN + kT3Bytes + kStageBytes;     // a one-wave block
 
 int64_t walk_lds_bytes_dev(int rows);
 
@@ -1431,6 +1533,10 @@ __device__ __forceinline__ void walk_multi_fill(uint8_t* fixed, const uint4* myr
 }
 
 int64_t walk_lds_bytes_dev(int rows) { return kLdsFixed + 2 * ((int64_t)rows * 32 + 32); }
+// a block of `waves` walk waves: one N table, each wave its stage and two tables
+int64_t walk_block_lds_dev(int rows, int waves) {
+  return kT3Bytes + (int64_t)waves * (kStageBytes + 2 * ((int64_t)rows * 32 + 32));
+}
 
 // The 8-byte record in HBM (ffv1_symbols) as the walk's step reads it from
 // LDS: the slot codes (y, z) follow from the residual in x (slot_codes), so
@@ -1454,15 +1560,24 @@ __device__ __forceinline__ uint4 pick(bool c, uint4 a, uint4 b) {
 }
 
 
-__global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t fixed[kLdsFixed];
-  extern __shared__ __attribute__((aligned(16))) uint8_t tbl[];  // [2][rows + 1 dummy row][32]
+// WAVES = 1: one wave per block, items in grid order (a batch of several
+// rounds).  WAVES = 4 or 5: one round, a block per CU whose waves 0-3 take a
+// long or multi-segment item each and land on the CU's four SIMDs (a
+// workgroup's waves go to them in turn), and wave 4 a one-segment item,
+// which shares wave 0's SIMD as the younger wave (the arbiter favours the
+// older): a wave of full length never shares its SIMD with another walk wave.
+template <int WAVES>
+__global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t fixed[kT3Bytes + WAVES * kStageBytes];
+  extern __shared__ __attribute__((aligned(16))) uint8_t tbl[];  // [wave][2][rows + 1 dummy row][32]
   const int64_t half = a.state_bytes / 2;  // one plane group's [contexts][32] in the persisted states
   const int64_t thalf = (int64_t)a.rows * 32;  // ... and its table in LDS (dense rows: 365 x 32)
   const int tsz = (int)thalf + 32;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wv = WAVES > 1 ? (int)(threadIdx.x >> 6) : 0;
+  const int wo = wv * kStageBytes;  // this wave's stage, from wave 0's
   const int h = lane >> 5, k = lane & 31;
-  for (int i = lane; i < kT3Bytes; i += kWalkThreads) {
+  for (int i = threadIdx.x; i < kT3Bytes; i += kWalkThreads * WAVES) {
     const int row = i >> 8, st = i & 255;
     const uint8_t* const t0 = a.ftab;
     const uint8_t* const t1 = a.ftab + 256;
@@ -1479,32 +1594,53 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
     }
     fixed[kLdsN + i] = (uint8_t)v;
   }
+  __syncthreads();  // the block's N table (the only barrier: the waves run independent chains)
   // the longer plane group's chains first (luma at 4:2:0, twice as long as
   // chroma; chroma at 4:4:4, where Cb and Cr make one chain twice luma's),
-  // one segment per wave; then the shorter group's, a.per_short segments per
-  // wave one after the other, so that every wave walks about as many symbols
-  // and a batch's waves all finish together
+  // one segment per wave; then the shorter group's: a.short_multi waves (per
+  // slice pair) of a.per_short consecutive segments each, so that they walk
+  // about as many symbols as a long wave, and the segments left one per wave
+  // at the end of the launch, where they land on SIMDs that already hold a
+  // walk wave and so run slower, on half the work (walk_split_short)
   // item = (plane group, segment(s), slice pair): the launch may cover a part
   // of the items (launch_walk's first / count)
-  const int item = (int)blockIdx.x + a.item0;
   const int npairs = (a.nslices + 1) / 2;
   const int nlong = a.nsegs * npairs;
-  const int nshort_segs = (a.nsegs + a.per_short - 1) / a.per_short;  // waves per slice pair, shorter group
+  const int covered = min(a.nsegs, a.short_multi * a.per_short);  // segments the multi waves take
+  const int nmulti = a.short_multi * npairs;
+  int item;
+  if constexpr (WAVES == 1) {
+    item = (int)blockIdx.x + a.item0;
+  } else {
+    const int nfull = nlong + nmulti;
+    item = wv < 4 ? 4 * (int)blockIdx.x + wv : nfull + (int)blockIdx.x;
+    if (wv < 4 ? item >= nfull : item >= a.nitems) return;  // (after the block's only barrier)
+  }
   const SliceGeom& g0 = a.geom[0];
   const bool chroma_first = 2 * (int64_t)g0.pw[1] * g0.ph[1] > (int64_t)g0.pw[0] * g0.ph[0];
   const bool is_long = item < nlong;
   const int grp = is_long == chroma_first ? 1 : 0;  // long: luma (4:2:0) or chroma (4:4:4)
-  const int bi = is_long ? item : item - nlong;
-  const int pair = bi % npairs, seg_first = bi / npairs;
-  const int seg_step = is_long ? a.nsegs : nshort_segs;  // this wave's segments: seg_first, + seg_step, ...
+  const int bi = is_long ? item : (item - nlong < nmulti ? item - nlong : item - nlong - nmulti);
+  const int pair = bi % npairs, j = bi / npairs;
+  int seg_begin, seg_end;  // this wave's segments
+  if (is_long) {
+    seg_begin = j;
+    seg_end = j + 1;
+  } else if (item - nlong < nmulti) {
+    seg_begin = min(j * a.per_short, covered);
+    seg_end = min(seg_begin + a.per_short, covered);
+  } else {
+    seg_begin = covered + j;
+    seg_end = seg_begin + 1;
+  }
   const int sl = 2 * pair + h;              // this half's slice
   const bool live = sl < a.nslices;
   const SliceGeom& g = a.geom[live ? sl : 2 * pair];
   const int p0 = grp ? 1 : 0, p1 = grp ? 3 : 1;  // planes of this group's chain
   if (grp && g.plane_sym_off[1] >= g.nsym) return;  // no chroma (uniform: geometry of a frame)
-  uint8_t* const mytbl = tbl + h * tsz;
-  uint4* const myrecs = reinterpret_cast<uint4*>(fixed + kLdsRecs) + h * kRecSlots;
-  uint8_t* const stage = fixed + kLdsPre + h * kPreHalf;
+  uint8_t* const mytbl = tbl + (2 * wv + h) * tsz;
+  uint4* const myrecs = reinterpret_cast<uint4*>(fixed + kLdsRecs + wo) + h * kRecSlots;
+  uint8_t* const stage = fixed + kLdsPre + wo + h * kPreHalf;
   uint4* const stage4 = reinterpret_cast<uint4*>(stage);
   const int64_t n16 = half / 16, t16 = thalf / 16;
   const int64_t goff = grp * half;
@@ -1516,8 +1652,8 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   const bool isU = k <= 10;                // zero flag / exponent slots: decision D + k
   W.hsh = isU ? 0 : 16;                    // else from D + 2e: sign +2, mantissa 22+i: +1-i
   const int kslot = isU ? k : (k <= 21 ? 2 : 23 - k);
-  W.kk = h * tsz + k;
-  W.dummy = h * kPreHalf + kPreData + k;
+  W.kk = (2 * wv + h) * tsz + k;
+  W.dummy = wo + h * kPreHalf + kPreData + k;
   W.msh = k == 31 ? 28 : 12;
   W.mwd = k == 31 ? 2 : 3;
   W.mbase = k == 31 ? 4 : 0;
@@ -1547,7 +1683,7 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
   uint64_t t_loop = 0, n_steps = 0;
   const uint64_t t_all = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
   const uint64_t rt_all = a.dbg || a.trace ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz: the wave's shader clock
-  for (int seg_i = seg_first; seg_i < a.nsegs; seg_i += seg_step) {
+  for (int seg_i = seg_begin; seg_i < seg_end && seg_i < a.nsegs; seg_i++) {
   const Segment seg = a.segs[seg_i];
   // where the segment's states come from: the carry, the 2-pass initial
   // states (a keyframe), or all 128 (ff_ffv1_clear_slice_state); null: 128
@@ -1562,7 +1698,7 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
     }
     if (k < 2) t4[t16 + k] = v128;  // dummy row
   }
-  __syncthreads();
+  __builtin_amdgcn_wave_barrier();  // (a wave's LDS operations run in order)
   for (int j = 0; j < seg.nframes; j++) {
     const int f = seg.first_frame + j;
     const int64_t sid = (int64_t)f * a.nslices + (live ? sl : 0);
@@ -1656,7 +1792,7 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
         }
 
         const int align = (int)(pos0 & 15);  // stage byte i <-> HBM byte pos0 - align + i
-        const int kc = kslot + h * kPreHalf + align;
+        const int kc = kslot + wo + h * kPreHalf + align;
         StepIn d0 = derive(myrecs[0], W, kc), d1 = derive(myrecs[1], W, kc);
         uint4 rn = myrecs[2];
         uint32_t l0 = tbl[d0.addr], l1 = tbl[d1.addr];
@@ -1685,7 +1821,7 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
             rn = r3;
           });
           const uint64_t hm = c < nch ? ((uint64_t)cx.mhi << 32) | cx.mlo : 0ull;  // this half's chain
-          walk_multi_fill(fixed, myrecs, hm, k, h * kPreHalf + align, W.dummy);
+          walk_multi_fill(fixed, myrecs, hm, k, wo + h * kPreHalf + align, W.dummy);
         }
         tbl[addr_prev] = (uint8_t)e1;  // the chunk's last symbol
         if (a.dbg) {
@@ -1716,11 +1852,13 @@ __global__ __launch_bounds__(kWalkThreads) void ffv1_walk(WalkArgs a) {
       }
     }
   }
-  __syncthreads();  // the table is read out before the next segment loads its own
+  __builtin_amdgcn_wave_barrier();  // the table is read out before the next segment loads its own
   }  // segments of this wave
   if (a.trace && lane == 0) {
-    a.trace[item * 2 + 0] = rt_all;
-    a.trace[item * 2 + 1] = __builtin_amdgcn_s_memrealtime();
+    a.trace[item * kTraceWords + 0] = rt_all;
+    a.trace[item * kTraceWords + 1] = __builtin_amdgcn_s_memrealtime();
+    a.trace[item * kTraceWords + 2] = __builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_REG_HW_ID
+    a.trace[item * kTraceWords + 3] = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
   }
   if (a.dbg && lane == 0) {
     a.dbg[item * 4 + 0] = __builtin_amdgcn_s_memtime() - t_all;
@@ -2379,21 +2517,65 @@ int64_t walk_lds_bytes(int rows) { return walk_lds_bytes_dev(rows); }
 
 int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first, int count) {
   if (walk_lds_bytes_dev(a.rows) > kWalkLdsMax || a.rows * 32 > 0xFFFF) return -1;
-  const size_t dyn = (size_t)(2 * ((int64_t)a.rows * 32 + 32));  // the tables; the fixed part is static
   WalkArgs b = a;
   if (b.per_short < 1) b.per_short = 1;
   b.nsegs = nsegs;
-  b.nitems = walk_items(nsegs, a.nslices, b.per_short);
+  b.short_multi = std::max(0, std::min(b.short_multi, (nsegs + b.per_short - 1) / b.per_short));
+  b.nitems = walk_items(nsegs, a.nslices, b.per_short, b.short_multi);
+  const size_t tables = (size_t)(2 * ((int64_t)a.rows * 32 + 32));  // one wave's; the fixed part is static
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (a.block_waves > 1) {  // one round: a block per CU (walk_block_waves)
+    const int npairs = (a.nslices + 1) / 2;
+    const int nfull = npairs * (nsegs + b.short_multi);
+    const int nsingle = b.nitems - nfull;
+    const int blocks = std::max((nfull + 3) / 4, nsingle);
+    b.item0 = 0;
+    if (a.block_waves == 5)
+      hipLaunchKernelGGL(ffv1_walk<5>, dim3((unsigned)blocks), dim3(kWalkThreads * 5), 5 * tables, st, b);
+    else
+      hipLaunchKernelGGL(ffv1_walk<4>, dim3((unsigned)blocks), dim3(kWalkThreads * 4), 4 * tables, st, b);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   if (count < 0) count = b.nitems - first;
   if (first < 0 || count <= 0 || first + count > b.nitems) return count == 0 ? 0 : -1;
   b.item0 = first;
-  hipLaunchKernelGGL(ffv1_walk, dim3((unsigned)count), dim3(kWalkThreads), dyn, reinterpret_cast<hipStream_t>(stream), b);
+  hipLaunchKernelGGL(ffv1_walk<1>, dim3((unsigned)count), dim3(kWalkThreads), tables, st, b);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int walk_items(int nsegs, int nslices, int per_short) {
+// Block shape of a batch's walk: 4 or 5 waves per block when the batch is
+// one round with every full-length wave alone on a SIMD (at most 4 per CU
+// of them, at most one one-segment wave per CU) and the block's LDS fits a
+// CU; else 1 (waves placed by the dispatcher, several rounds).
+int walk_block_waves(int nsegs, int nslices, int per_short, int short_multi, int rows, int cus) {
   const int npairs = (nslices + 1) / 2;
-  return npairs * (nsegs + (nsegs + per_short - 1) / per_short);
+  const int nfull = npairs * (nsegs + short_multi);
+  const int nsingle = walk_items(nsegs, nslices, per_short, short_multi) - nfull;
+  if (nfull > 4 * cus || nsingle > cus) return 1;
+  const int w = nsingle > 0 ? 5 : 4;
+  return walk_block_lds_dev(rows, w) <= 160 * 1024 ? w : 1;
+}
+
+int walk_items(int nsegs, int nslices, int per_short, int short_multi) {
+  const int npairs = (nslices + 1) / 2;
+  const int covered = std::min(nsegs, short_multi * per_short);
+  return npairs * (nsegs + short_multi + (nsegs - covered));
+}
+
+// How many of the shorter group's waves take per_short segments: all of them
+// when the long waves and those fit one per SIMD (4 per CU); else as many as
+// still fit one per SIMD beside the long ones, the segments left going one
+// per wave onto SIMDs that already hold a walk wave (where they run ~1.4x
+// slower, on half the work), provided every wave is then resident at once
+// (`resident`).  Otherwise all of them (the walk takes more than one round
+// anyway).
+int walk_split_short(int nsegs, int nslices, int per_short, int simds, int resident) {
+  const int npairs = (nslices + 1) / 2;
+  const int all = (nsegs + per_short - 1) / per_short;
+  if (per_short < 2 || npairs * (nsegs + all) <= simds) return all;
+  for (int m = all; m >= 0; m--)
+    if (npairs * (nsegs + m) <= simds && walk_items(nsegs, nslices, per_short, m) <= resident) return m;
+  return all;
 }
 
 int walk_per_short(const SliceGeom& g) {
@@ -2408,7 +2590,7 @@ int walk_per_short(const SliceGeom& g) {
 int walk_resident(const WalkArgs& a) {
   const size_t dyn = (size_t)(2 * ((int64_t)a.rows * 32 + 32));
   int per_cu = 0, dev = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ffv1_walk, kWalkThreads, dyn) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ffv1_walk<1>, kWalkThreads, dyn) != hipSuccess ||
       hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
     (void)hipGetLastError();
     return 0;

@@ -74,7 +74,8 @@ EXPORTED_SYMBOLS = (
     "ffv1hip_abi_version", "ffv1hip_set_profiling", "ffv1hip_last_kernel_ms",
     "ffv1hip_last_kernel_stats", "ffv1hip_synchronize",
     "ffv1hip_dec_create", "ffv1hip_dec_destroy", "ffv1hip_decode", "ffv1hip_dec_reset",
-    "ffv1hip_set_picture_number", "ffv1hip_encode2", "ffv1hip_encode2_delay", "ffv1hip_dec_damaged_slices",
+    "ffv1hip_set_picture_number", "ffv1hip_encode2", "ffv1hip_encode2_delay", "ffv1hip_encode2_last_packet",
+    "ffv1hip_dec_damaged_slices",
     "ffv1hip_set_pass", "ffv1hip_stats_out",
 )
 
@@ -122,6 +123,8 @@ def load_library():
     L.ffv1hip_encode2.restype = ctypes.c_int
     L.ffv1hip_encode2_delay.argtypes = [vp]
     L.ffv1hip_encode2_delay.restype = ctypes.c_int
+    L.ffv1hip_encode2_last_packet.argtypes = [vp, u8p, i64]
+    L.ffv1hip_encode2_last_packet.restype = i64
     L.ffv1hip_set_pass.argtypes = [vp, ctypes.c_int, ctypes.c_char_p]
     L.ffv1hip_set_pass.restype = ctypes.c_int
     L.ffv1hip_stats_out.argtypes = [vp, ctypes.c_char_p, i64]
@@ -486,7 +489,6 @@ class FFV1Encoder:
             self._enc.set_pass(pass_, avctx.stats_in)
         avctx.extradata = self._enc.extradata()
         avctx.delay = self._enc.encode2_delay()
-        self._out = np.empty(self._enc.max_packet_size(), np.uint8)
         return 0
 
     def encode2(self, frame: Optional[Sequence[np.ndarray]], pts: Optional[int] = None) -> Optional[AVPacket]:
@@ -509,21 +511,22 @@ class FFV1Encoder:
             self._frames_in += 1
         size, pts_out = ctypes.c_int64(), ctypes.c_int64()
         key, got = ctypes.c_int(), ctypes.c_int()
+        # the shim flow (include/ffv1hip.h): the packet handed out without a
+        # copy, then copied into a buffer of exactly its size (ff_alloc_packet2)
         rc = L.ffv1hip_encode2(self._enc._h, ptrs if frame is not None else None,
-                               strides if frame is not None else None, pts or 0, _u8p(self._out),
-                               self._out.size, ctypes.byref(size), ctypes.byref(pts_out),
-                               ctypes.byref(key), ctypes.byref(got))
-        if rc == -28:  # the packet outgrew the buffer (a budget re-encode): the frame was taken
-            self._out = np.empty(max(size.value, self._enc.max_packet_size()), np.uint8)
-            rc = L.ffv1hip_encode2(self._enc._h, None, None, 0, _u8p(self._out), self._out.size,
-                                   ctypes.byref(size), ctypes.byref(pts_out), ctypes.byref(key), ctypes.byref(got))
+                               strides if frame is not None else None, pts or 0, None, 0,
+                               ctypes.byref(size), ctypes.byref(pts_out), ctypes.byref(key), ctypes.byref(got))
         if rc < 0:
             raise FFV1Error(rc, "ffv1hip_encode2")
         if not got.value:
             if frame is None and self._pass == 1:  # the flush: stats_out (ffv1enc.c:1236-1277)
                 self.avctx.stats_out = self._enc.stats_out()
             return None
-        return AVPacket(self._out[:size.value].tobytes(), pts_out.value, pts_out.value, bool(key.value))
+        out = np.empty(max(1, size.value), np.uint8)
+        n = L.ffv1hip_encode2_last_packet(self._enc._h, _u8p(out), out.size)
+        if n < 0:
+            raise FFV1Error(int(n), "ffv1hip_encode2_last_packet")
+        return AVPacket(out[:n].tobytes(), pts_out.value, pts_out.value, bool(key.value))
 
     def close(self) -> int:
         if self._enc is not None:
@@ -534,7 +537,8 @@ class FFV1Encoder:
 
 class HipDecoder:
     """Owner of one ``ffv1hip_dec``: ff_ffv1_decoder's decode_frame on the GPU
-    (ffv1dec.c:896-1005) for version-3 range-coded streams, context model 0.
+    (ffv1dec.c:896-1005) for every stream the encoder writes (versions 0, 1,
+    3 and 4, range or Golomb-Rice, context model 0 / 1, YCbCr / RGB, alpha).
     Context states carry across :meth:`decode` calls like the encoder's."""
 
     def __init__(self, params: Params, extradata: bytes, device: int = 0):
@@ -575,13 +579,14 @@ class HipDecoder:
         dt = np.uint8 if self.params.sample_bytes in (1, 4) else np.uint16
         shapes = self.params.plane_shapes()
         frames = [[np.zeros(shp, dt) for shp in shapes] for _ in range(n)]
-        ptrs = (ctypes.c_void_p * (3 * n))()
-        strides = (ctypes.c_int * (3 * n))()
+        npf = self.params.planes_per_frame
+        ptrs = (ctypes.c_void_p * (npf * n))()
+        strides = (ctypes.c_int * (npf * n))()
         for i, fr in enumerate(frames):
-            for k in range(3):
+            for k in range(npf):
                 a = fr[min(k, len(fr) - 1)]
-                ptrs[3 * i + k] = a.ctypes.data
-                strides[3 * i + k] = a.strides[0]
+                ptrs[npf * i + k] = a.ctypes.data
+                strides[npf * i + k] = a.strides[0]
         keys = (ctypes.c_int * n)()
         rc = L.ffv1hip_decode(self._h, _u8p(buf), sizes, n, ptrs, strides, keys)
         if rc < 0:

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define FFV1HIP_ABI_VERSION 5
+#define FFV1HIP_ABI_VERSION 6
 #define FFV1HIP_AVERROR_INVALIDDATA (-1094995529)
 
 /* AVCodecContext fields + codec private options that encode_init reads
@@ -145,16 +145,27 @@ int ffv1hip_encode(ffv1hip_ctx *ctx, const void *const *planes,
  * buffers (a few host threads copy into them, DMA on a transfer stream of
  * the context) and packets come back through a pinned buffer.  A returned
  * packet has pts = dts = its frame's pts and the key flag
- * (ffv1enc.c:1365-1370).  out should hold ffv1hip_max_packet_size bytes,
- * which grows after a slice byte budget re-encode: a packet larger than
- * out_cap makes the call return -ENOSPC with *size = the packet's size,
- * having taken the frame; a call with planes = NULL and a large enough
- * buffer then hands the packet out.  *got_packet = 1 when a packet was
- * written. */
+ * (ffv1enc.c:1365-1370).  *got_packet = 1 when a packet was handed out.
+ * With out == NULL the packet is handed out without a copy (size, pts and
+ * key set) and ffv1hip_encode2_last_packet copies it: the flow for a
+ * libavcodec shim, which allocates the AVPacket with the size it was given
+ * (ff_alloc_packet2) and so never sees a packet larger than its buffer.
+ * With a buffer, out should hold ffv1hip_max_packet_size bytes, which grows
+ * after a slice byte budget re-encode: a packet larger than out_cap makes
+ * the call return -ENOSPC with *size = the packet's size, having taken the
+ * frame, and the packet stays pending: the next call, with a frame or with
+ * planes == NULL, hands it out first (so planes == NULL is a flush only once
+ * no packet is pending). */
 int ffv1hip_encode2(ffv1hip_ctx *ctx, const void *const planes[4],
                     const int strides[4], int64_t pts, uint8_t *out,
                     int64_t out_cap, int64_t *size, int64_t *pts_out,
                     int *key, int *got_packet);
+
+/* The packet the last ffv1hip_encode2 call handed out, copied into out
+ * (cap bytes).  Returns its size, -ENOSPC (nothing copied) when cap is
+ * smaller, -EINVAL when that call handed out no packet.  Valid until the
+ * next ffv1hip_encode2 call. */
+int64_t ffv1hip_encode2_last_packet(ffv1hip_ctx *ctx, uint8_t *out, int64_t cap);
 
 /* The encoder's delay in frames (avctx->delay): 2 * max_batch_frames - 1
  * when two batches fit in HBM side by side (one codes while the next
@@ -247,8 +258,9 @@ int ffv1hip_last_kernel_stats(ffv1hip_ctx *ctx, ffv1hip_kernel_stats *out);
 
 /* Decoder: the AVCodec callbacks of ff_ffv1_decoder (ffv1dec.c decode_init
  * :1007, decode_frame :896-1030, decode_end) for the streams this library
- * encodes: versions 0, 1 and 3, range coder (default or custom table) or
- * Golomb-Rice, context model 0 or 1, YCbCr or RGB.  ffv1hip_dec_create takes
+ * encodes: versions 0, 1, 3 and 4 (per-slice RCT coefficients, PCM slices),
+ * range coder (default or custom table) or Golomb-Rice, context model 0 or
+ * 1, YCbCr or RGB, with alpha (YUVA, YA8, RGB32).  ffv1hip_dec_create takes
  * the stream's parameters and its extradata, which must be the one those
  * parameters produce (what read_extradata, ffv1dec.c:509-631, would parse;
  * none below version 2, whose in-band keyframe header must agree with the
@@ -260,8 +272,9 @@ ffv1hip_dec *ffv1hip_dec_create(const ffv1hip_params *params,
                                 int device, int *err);
 void ffv1hip_dec_destroy(ffv1hip_dec *dec);
 /* decode_frame over a batch: packets back to back in HOST memory (sizes[i]
- * bytes each); plane p of frame i goes to planes[3*i + p] with row stride
- * strides[3*i + p] (the encoder's input layout).  The key bit and the slice
+ * bytes each); plane p of frame i goes to planes[np*i + p] with row stride
+ * strides[np*i + p] (the encoder's input layout; np = FFV1HIP_PLANES_YUVA
+ * for the YUVA formats, else FFV1HIP_PLANES).  The key bit and the slice
  * chain (3-byte sizes, CRC-32 when ec) are read on the host as in
  * ffv1dec.c:931-989; every (GOP segment, slice) chain decodes on the GPU.
  * Context states carry across calls like the encoder's.  key_flags may be

@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), f"{n} declared in include/ffv1hip.h but not exported"
     assert set(names) == set(EXPORTED_SYMBOLS)
-    assert lib.ffv1hip_abi_version() == 5
+    assert lib.ffv1hip_abi_version() == 6
 
 
 FIELDS = ["width", "height", "chroma_planes", "chroma_h_shift", "chroma_v_shift",

@@ -113,12 +113,51 @@ def test_hip_alpha_encode2_and_states():
     assert head + tail == ref
 
 
+def gpu_decode_vs_oracle(params, cfg, ex, pkts, frames=None, pad_byte=False):
+    """The GPU decoder's samples equal the oracle decoder's (and the input,
+    when frames are given) for every packet; with pad_byte (bgr0) the
+    input's unused fourth byte comes back 0."""
+    from ffv1hip import HipDecoder
+    odec = oracle.Decoder(cfg, ex)
+    hdec = HipDecoder(params, ex, 0)
+    got = hdec.decode([p for p, _ in pkts])
+    hdec.close()
+    for i, ((p, key), (planes, k)) in enumerate(zip(pkts, got)):
+        ref, rk = odec.decode(p)
+        assert k == key == rk, f"frame {i}: key flag"
+        assert len(planes) == len(ref)
+        for a, b in zip(planes, ref):
+            np.testing.assert_array_equal(a, b, err_msg=f"frame {i}")
+        if frames is not None:
+            for a, b in zip(planes, frames[i]):
+                if pad_byte:
+                    b = b.copy()
+                    b[:, 3::4] = 0
+                np.testing.assert_array_equal(a, b, err_msg=f"frame {i}: not lossless")
+
+
 @pytest.mark.gpu
-def test_gpu_decoder_refuses_alpha():
-    from ffv1hip import FFV1Error, HipDecoder, HipEncoder
+@pytest.mark.parametrize("stream", ALPHA_STREAMS, ids=IDS)
+def test_gpu_decoder_alpha_matches_oracle_decoder(stream):
+    """ffv1_decode_slices on alpha streams (ffv1dec.c:437-453: YUVA's A
+    plane with plane context 2, YA8's Y and A of one packed plane, RGB32's A
+    row): the oracle decoder's samples, which are the input (lossless)."""
     from test_gpu_parity import hip_params
-    s = ALPHA_STREAMS[0]
-    enc = HipEncoder(hip_params(s), 0, 2)
-    with pytest.raises(FFV1Error):
-        HipDecoder(enc.params, enc.extradata(), 0)
-    enc.close()
+    frames = list(stream.frames())
+    cfg, ex, pkts = oracle_encode(stream, frames)
+    gpu_decode_vs_oracle(hip_params(stream), cfg, ex, pkts, frames)
+
+
+@pytest.mark.gpu
+def test_gpu_decoder_alpha_conceals_damaged_slices():
+    """A flipped byte in a YUVA slice: CRC failure, decoded on, then
+    concealed from the previous picture, all four planes, as the oracle."""
+    from helpers import corrupt_slice
+    from test_gpu_parity import hip_params
+    s = Stream("yuva420p_ec", 96, 64, "yuva420p", 5, slices=4, coder=1, gop_size=5, source="random", seed=21)
+    frames = list(s.frames())
+    cfg, ex, pkts = oracle_encode(s, frames)
+    assert cfg.ec
+    n = cfg.num_h_slices * cfg.num_v_slices
+    pkts = [(corrupt_slice(p, True, n, 1) if i == 2 else p, k) for i, (p, k) in enumerate(pkts)]
+    gpu_decode_vs_oracle(hip_params(s), cfg, ex, pkts)

@@ -3,7 +3,8 @@ micro_version 2 in the extradata (:566-570), per-slice RCT luma
 coefficients from choose_rct_params (:1064-1144) used by the colour
 transform (:450) and written in the slice header with slice_coding_mode
 (:1052-1061), and the PCM re-code of a range-coded slice that runs out of
-its buffer (:282-286, 294-304, 1207-1217; buffers :1281-1282, 1317-1322).
+its buffer (:282-286, 294-304, 1207-1217; buffers :1281-1282, 1317-1322),
+on the GPU too.
 The decoder side is ffv1dec.c:344-356, 111-120, 252-269, 414-415.
 
 Parity unpinned: the reference's FATE set has no version-4 vector, so the
@@ -116,16 +117,96 @@ def test_hip_v4_matches_oracle(stream):
         assert g == r, f"frame {i}"
 
 
+def _pcm_frames(pix_fmt, w, h, slices, mixed, n=5, seed=1):
+    """Noise frames whose thin slices fail the 35 * w buffer check; with
+    `mixed`, every other frame is a smooth ramp that codes normally, so the
+    P-frame carry after a PCM slice (its states cleared by the PCM slice
+    header, ffv1enc.c:1054-1055) is exercised."""
+    cfg = oracle.configure(w, h, pix_fmt, level=4, slices=slices, coder=1, gop_size=3, experimental=True)
+    rng = np.random.default_rng(seed)
+    hi = 1 << (16 if cfg.sample_bytes == 2 and not cfg.packed_at_lsb else cfg.bits_per_raw_sample)
+    frames = []
+    for t in range(n):
+        fr = []
+        for s in oracle.plane_shapes(cfg):
+            if mixed and t % 2:
+                yy, xx = np.mgrid[0:s[0], 0:s[1]]
+                a = (xx * 7 + yy * 3 + t) % hi
+            else:
+                a = rng.integers(0, hi, size=s)
+            fr.append(np.ascontiguousarray(a.astype(np.uint16)))
+        frames.append(fr)
+    return cfg, frames
+
+
+PCM_CASES = [("gbrp14", 376, 4, 6, False), ("yuv444p16", 376, 4, 6, False), ("gbrp14", 376, 12, 12, True),
+             ("yuv444p16", 376, 12, 12, True)]
+
+
+@pytest.mark.parametrize("case", PCM_CASES, ids=[f"{c[0]}_{c[1]}x{c[2]}_s{c[3]}{'_mixed' if c[4] else ''}"
+                                                  for c in PCM_CASES])
+def test_oracle_v4_pcm_cases_code_pcm_and_roundtrip(case):
+    cfg, frames = _pcm_frames(*case, n=5)
+    enc = oracle.Encoder(cfg)
+    pkts, modes = [], []
+    for f in frames:
+        pkts.append(enc.encode(f))
+        modes.append(enc.last_slice_pcm())
+    assert any(any(m) for m in modes)
+    _lossless(cfg, enc.extradata(), pkts, frames)
+
+
 @pytest.mark.gpu
-def test_hip_v4_refuses_the_pcm_path():
-    """Where the reference would re-code slices as PCM the HIP encoder
-    returns an error instead of other bytes."""
-    from ffv1hip import FFV1Error, HipEncoder, configure
-    rng = np.random.default_rng(1)
-    p = configure(376, 4, "gbrp14", slices=6, level=4, coder=1, gop_size=2, experimental=True)
-    frames = [[np.ascontiguousarray(rng.integers(0, 1 << 14, size=s).astype(np.uint16))
-               for s in p.plane_shapes()] for _ in range(2)]
-    enc = HipEncoder(p, 0, 2)
-    with pytest.raises(FFV1Error):
-        enc.encode(frames)
-    enc.close()
+@pytest.mark.parametrize("case", PCM_CASES, ids=[f"{c[0]}_{c[1]}x{c[2]}_s{c[3]}{'_mixed' if c[4] else ''}"
+                                                  for c in PCM_CASES])
+def test_hip_v4_pcm_matches_oracle(case):
+    """Where the reference re-codes slices as PCM (the per-line 35 * w check,
+    ffv1enc.c:282-286, 1207-1217), the chained HIP coder does the same on the
+    device: the packets equal the oracle's (parity unpinned: no reference
+    vector for version 4)."""
+    from ffv1hip import HipEncoder, configure
+    pix_fmt, w, h, slices, mixed = case
+    cfg, frames = _pcm_frames(*case, n=5)
+    enc = oracle.Encoder(cfg)
+    ref = [enc.encode(f) for f in frames]
+    p = configure(w, h, pix_fmt, slices=slices, level=4, coder=1, gop_size=3, experimental=True)
+    henc = HipEncoder(p, 0, 2)
+    got = henc.encode(frames)
+    henc.close()
+    for i, (g, r) in enumerate(zip(got, ref)):
+        assert g == r, f"frame {i}"
+
+
+def _v4_params(s):
+    from ffv1hip import configure
+    return configure(s.width, s.height, s.pix_fmt, slices=s.slices, level=4, coder=s.coder, context=s.context,
+                     gop_size=s.gop_size, experimental=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stream", V4_STREAMS, ids=IDS)
+def test_gpu_decoder_v4_matches_oracle_decoder(stream):
+    """ffv1_decode_slices on version 4 (ffv1dec.c:344-356 the slice header's
+    reset bit, slice_coding_mode and RCT coefficients, 252-269 the RCT with
+    them): the oracle decoder's samples, losslessly the input."""
+    from test_alpha import gpu_decode_vs_oracle
+    frames = list(stream.frames())
+    cfg, ex, pkts = oracle_encode(stream, frames)
+    gpu_decode_vs_oracle(_v4_params(stream), cfg, ex, pkts, frames, pad_byte=stream.pix_fmt == "bgr0")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", PCM_CASES, ids=[f"{c[0]}_{c[1]}x{c[2]}_s{c[3]}{'_mixed' if c[4] else ''}"
+                                                  for c in PCM_CASES])
+def test_gpu_decoder_v4_pcm_slices(case):
+    """PCM slices (ffv1dec.c:111-120, every bit on a fresh state 128, no
+    RCT) and the states cleared after them (the reset bit): the oracle
+    decoder's samples, losslessly the input."""
+    from ffv1hip import configure
+    from test_alpha import gpu_decode_vs_oracle
+    pix_fmt, w, h, slices, mixed = case
+    cfg, frames = _pcm_frames(*case, n=5)
+    enc = oracle.Encoder(cfg)
+    pkts = [enc.encode(f) for f in frames]
+    p = configure(w, h, pix_fmt, slices=slices, level=4, coder=1, gop_size=3, experimental=True)
+    gpu_decode_vs_oracle(p, cfg, enc.extradata(), pkts, frames)
