@@ -2,6 +2,10 @@
 """Builds the in-tree native libraries of the MI355X FFV1 encoder.
 
   lib/libffv1hip.so    HIP kernels (gfx950) + the C-ABI of include/ffv1hip.h
+  lib/libffv1hip_check.so  the same with the device bounds checks (-DFFV1HIP_BOUNDS:
+                       the walk's and the coder's writes checked against their
+                       extents, ffv1_internal.h Bounds); select it with
+                       FFV1HIP_LIB (ffv1hip/_paths.py)
   lib/libffv1synth.so  synthetic input clips (host C)
 
 Everything is built in-tree so the .so files travel with the repo snapshot to
@@ -49,9 +53,11 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def build_hip(force=False, extra=()):
+def build_hip(force=False, extra=(), check=False):
     os.makedirs(LIB, exist_ok=True)
-    out = os.path.join(LIB, "libffv1hip.so")
+    out = os.path.join(LIB, "libffv1hip_check.so" if check else "libffv1hip.so")
+    if check:
+        extra = ("-DFFV1HIP_BOUNDS", *extra)
     srcs = [os.path.join(CSRC, "ffv1_kernels.hip"), os.path.join(CSRC, "ffv1_decode.hip"),
             os.path.join(CSRC, "ffv1_host.cpp"), os.path.join(CSRC, "ffv1_twopass.cpp")]
     deps = srcs + [os.path.join(CSRC, "ffv1_internal.h"), os.path.join(INCLUDE, "ffv1hip.h")]
@@ -61,11 +67,15 @@ def build_hip(force=False, extra=()):
     return out
 
 
-def build_all(force=False):
-    return build_synth(force), build_hip(force)
+def build_all(force=False, check=True):
+    # the release and the checked library compile side by side (~70 s each)
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(2) as ex:
+        jobs = [ex.submit(build_hip, force)] + ([ex.submit(build_hip, force, (), True)] if check else [])
+        return [build_synth(force)] + [j.result() for j in jobs]
 
 
 if __name__ == "__main__":
     force = "--force" in sys.argv
-    for p in build_all(force):
+    for p in build_all(force, check="--no-check" not in sys.argv):
         print(p)

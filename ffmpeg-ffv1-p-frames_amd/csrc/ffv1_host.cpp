@@ -138,7 +138,7 @@ struct Knobs {
 static const char* const kKnobNames[] = {"serial",     "walkdbg",    "walktrace", "hostdbg",   "walk_prio",
                                          "range_prio", "dseg_prio",  "sym_grid",  "bits_grid", "dseg_grid",
                                          "walk_split", "copy_threads", "dec_swap", "coder",    "dense", "walk_blocks",
-                                         "recsets",    "slice_cap",  "walk_part_a", "force_multi"};
+                                         "recsets",    "slice_cap",  "walk_part_a", "force_multi", "bounds_shrink"};
 
 static int parse_knobs(Knobs* k) {
   k->kv.clear();
@@ -432,6 +432,7 @@ struct ffv1hip_ctx {
   int64_t* h_dtotal = nullptr;   // pinned readback of d_dtotal
   uint8_t* d_pre[2] = {nullptr, nullptr};    // [decision] state before the decision
   uint8_t* d_scratch = nullptr;               // where idle walk chains write their stage
+  uint32_t* d_bounds = nullptr;               // debug build: the first out-of-bounds write's site (sticky)
   uint32_t* d_bits[2] = {nullptr, nullptr};  // [decision / 32] decision bits
   // the three-pass coder (ffv1_range / ffv1_dseg / ffv1_dfix): the header's
   // digits per (key, slice), the per-stream segment layout (three sets, with
@@ -606,6 +607,7 @@ extern "C" {
 
 const char* ffv1hip_last_error(void) { return g_err; }
 int ffv1hip_abi_version(void) { return FFV1HIP_ABI_VERSION; }
+int ffv1hip_debug_checks(void) { return kBoundsCheck ? 1 : 0; }
 
 int ffv1hip_configure(ffv1hip_params* out, const ffv1hip_options* o) {
   if (!out || !o || !o->pix_fmt || o->width <= 0 || o->height <= 0)
@@ -997,7 +999,7 @@ static void free_device(ffv1hip_ctx* c) {
                   c->d_persist[1], c->d_tables, c->d_sym, c->d_keys2, c->d_cbits, c->d_dcount, c->d_dbase, c->d_dtotal, c->d_pre[0],
                   c->d_pre[1], c->d_bits[0], c->d_bits[1], c->d_scratch, c->d_hdr, c->d_hdr_digits, c->d_geom, c->d_slot_frames, c->d_status,
                   c->d_rec2, c->d_cbits2, c->d_ident, c->d_segs_info, c->d_seg_totals, c->d_wmap, c->d_ck,
-                  c->d_segrec, c->d_rct};
+                  c->d_segrec, c->d_rct, c->d_bounds};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_dtotal) (void)hipHostFree(c->h_dtotal);
@@ -1178,6 +1180,10 @@ static int alloc_device(ffv1hip_ctx* c) {
     for (hipEvent_t& e : c->walked) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->coded) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_TRY(hipMalloc(&c->d_scratch, 4096));
+    if (kBoundsCheck) {
+      HIP_TRY(hipMalloc(&c->d_bounds, sizeof(uint32_t)));
+      HIP_TRY(hipMemset(c->d_bounds, 0, sizeof(uint32_t)));
+    }
     // the coder's segments: at most wmax decisions per sample
     c->max_segs = 0;
     c->max_groups = 0;
@@ -1726,6 +1732,15 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     wa.persist_out = ca.persist_out;
     wa.ds = ds;
     wa.scratch = c->d_scratch;
+    if (kBoundsCheck) {
+      // (the bounds_shrink hook: a smaller decision buffer than the real
+      // one, so that the checks must fire; the test of the debug build)
+      ca.bnd.err = c->d_bounds;
+      ca.bnd.pre_bytes = c->dcap[fb] >> c->knobs.get("bounds_shrink", 0);
+      ca.bnd.out_bytes = c->slice_stride * c->nslices * c->max_batch;
+      ca.bnd.persist_bytes = ca.state_bytes * c->nslices;
+      wa.bnd = ca.bnd;
+    }
     wa.force_multi = c->knobs.has("force_multi");
     // wave priorities: the coder's serial range pass above the walk when the
     // walk is one round of chains no longer than the coder's streams (dense
@@ -1969,6 +1984,19 @@ static int grow_slice_budget(ffv1hip_ctx* c, int64_t needed) {
 // ffv1enc.c:283-292; its buffer is large enough for any slice, :1232).
 // Every batch reports into its own status set, cleared when the batch
 // starts; the last two batches' sets are intact.
+static const char* bounds_site(uint32_t s) {
+  switch (s) {
+    case kBndWalkStage: return "ffv1_walk (a chunk's recorded states)";
+    case kBndWalkLong: return "ffv1_walk (a long chunk's recorded states)";
+    case kBndWalkStates: return "ffv1_walk (the carried states)";
+    case kBndDsegSlot: return "ffv1_dseg (a stream's digits)";
+    case kBndDsegRead: return "ffv1_dseg (a segment's states, read)";
+    case kBndDfixSlot: return "ffv1_dfix (a stream's digits)";
+    case kBndSinkSlot: return "ffv1_sink (a stream's bytes)";
+    default: return "an unknown site";
+  }
+}
+
 static int settle_batch(ffv1hip_ctx* c, int64_t b) {
   if (b < 0 || b < c->nsub - 2 || b >= c->nsub) return 0;
   bool redo_next = false;
@@ -1977,6 +2005,11 @@ static int settle_batch(ffv1hip_ctx* c, int64_t b) {
   for (int attempt = 0;; attempt++) {
     const ffv1hip_ctx::LastBatch& L = c->hist[b & 1];
     HIP_TRY(hipEventSynchronize(c->hist_done[b & 1]));
+    if (kBoundsCheck && c->d_bounds) {
+      uint32_t site = 0;
+      HIP_TRY(hipMemcpy(&site, c->d_bounds, sizeof(site), hipMemcpyDeviceToHost));
+      if (site) return set_err(-14, "device bounds check: %s wrote outside its extent (debug build)", bounds_site(site));
+    }
     int status[4];
     if (c->pipe.on) {
       // on the host-frame path a DMA copy would queue behind the next batch's

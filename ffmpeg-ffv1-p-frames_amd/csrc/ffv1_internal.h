@@ -142,6 +142,34 @@ struct DecisionStream {
   uint32_t* bits;
 };
 
+// Debug build (build.py --check: -DFFV1HIP_BOUNDS, lib/libffv1hip_check.so):
+// the walk's, dseg's, dfix's and sink's writes are checked against the
+// extents they own (a walk chain: its own chain and pad in pre, never a
+// neighbour's; a coder stream: its slice slot); a write outside is dropped
+// and the first offending site is recorded in *err, which the host turns
+// into an error at the batch's settle (ffv1hip_debug_checks reports the
+// build).  The release build compiles every check away.
+#ifdef FFV1HIP_BOUNDS
+constexpr bool kBoundsCheck = true;
+#else
+constexpr bool kBoundsCheck = false;
+#endif
+enum BoundsSite : uint32_t {
+  kBndWalkStage = 1,   // ffv1_walk: a chunk's stage copied out to pre
+  kBndWalkLong = 2,    // ffv1_walk: a walk_long chunk's states
+  kBndWalkStates = 3,  // ffv1_walk: the carry it leaves in persist_out
+  kBndDsegSlot = 4,    // ffv1_dseg: a stream's digits (its slice slot)
+  kBndDsegRead = 5,    // ffv1_dseg: a segment's states and bits (its chain)
+  kBndDfixSlot = 6,    // ffv1_dfix: a stream's joined digits
+  kBndSinkSlot = 7,    // ffv1_sink: a stream's bytes
+};
+struct Bounds {
+  uint32_t* err;           // first failing site (0: none); null in the release build
+  int64_t pre_bytes;       // DecisionStream.pre
+  int64_t out_bytes;       // slice_out
+  int64_t persist_bytes;   // persist_out
+};
+
 // The decision-stream range coder runs in three passes (ffv1_kernels.hip):
 // ffv1_range walks `range` alone per (frame, slice) stream and leaves a
 // checkpoint every kSeg decisions, ffv1_dseg codes every segment from its
@@ -221,6 +249,7 @@ struct CodeArgs {
   int64_t digit_cap;          // values of low a slice slot holds (slice_stride / 4)
   int dseg_blocks;            // ffv1_dseg grid
   int range_prio, dseg_prio;  // wave priorities (s_setprio) of ffv1_range / ffv1_dseg beside the walk (2)
+  Bounds bnd;                 // debug build: the extents of the writes
 };
 
 // Pass-1 statistics (ffv1enc.c:190-199): rc_stat[state][bit] from the
@@ -269,6 +298,7 @@ struct WalkArgs {
   int prio;                   // wave priority (s_setprio)
   int rows;                   // context rows of a plane group's table in LDS (kDenseRows when dense)
   int dense;                  // records address dense rows (dense_row), the state tables keep contexts
+  Bounds bnd;                 // debug build: the extents of the writes
 };
 
 constexpr int kTraceWords = 4;

@@ -346,6 +346,18 @@ constexpr int kHeaderFlushAt = kRing - 30;  // per header op (host-checked |valu
 // exec-masked block behind a branch, which costs more than the lookups.
 __device__ __forceinline__ void pin(uint32_t& v) { asm volatile("" : "+v"(v)); }
 
+// Debug build: is [p, p + n) inside [base, base + bytes)?  If not, the first
+// failing site is recorded and the caller drops the write (ffv1_internal.h,
+// Bounds).  The release build folds every call to true.
+__device__ __forceinline__ bool bounds_ok(const Bounds& b, const void* p, int64_t n, const void* base,
+                                          int64_t bytes, uint32_t site) {
+  if constexpr (!kBoundsCheck) return true;
+  const int64_t o = (int64_t)(reinterpret_cast<const uint8_t*>(p) - reinterpret_cast<const uint8_t*>(base));
+  if (o >= 0 && n >= 0 && o + n <= bytes) return true;
+  if (b.err) atomicCAS(b.err, 0u, site);
+  return false;
+}
+
 // LDS-typed pointer (address space 3): ring arithmetic stays 32-bit LDS
 // addressing, with no generic-pointer conversions on the per-decision path
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
@@ -1160,9 +1172,10 @@ __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
     const int sp = part ? s - ss.s_luma : s;
     const int npart = part ? dc[1] + dc[2] : dc[0];
     const int off = sp * kSeg;
-    const int n = act ? min(kSeg, npart - off) : 0;
+    int n = act ? min(kSeg, npart - off) : 0;
     const bool last = act && s == ss.s_all - 1;
-    const int64_t pb = a.ds.dbase[st] + (part ? chroma_start(dc[0]) : 0) + off;  // multiple of 64
+    const int64_t cb = a.ds.dbase[st] + (part ? chroma_start(dc[0]) : 0);  // the chain's first decision
+    const int64_t pb = cb + off;  // multiple of 64
     const uint2 ck = act ? a.ck[ss.seg_base + s] : make_uint2(0x100u, 0u);
     int range = (int)ck.x, low = 0;
     // the segment's digits: stream-wide shift index ck.y; stores past the
@@ -1173,6 +1186,17 @@ __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
                                             (int)(a.digit_cap * 4), kBufDword3);
     o.kb = (int)ck.y * 4;
     const int kb0 = o.kb;
+    if constexpr (kBoundsCheck) {
+      if (act && !bounds_ok(a.bnd, a.slice_out + (int64_t)st * a.slice_stride, a.digit_cap * 4, a.slice_out,
+                            a.bnd.out_bytes, kBndDsegSlot))
+        o.rs = __builtin_amdgcn_make_buffer_rsrc(a.slice_out, 0, 0, kBufDword3);  // every store dropped
+      // the blocks it reads: inside its chain and pad (the chain's extent as the layout made it)
+      const int64_t clen = part ? (npart + 63) / 64 * 64 + kChainPad : chroma_start(dc[0]);
+      const int64_t rb = (int64_t)(n + 127) / 128 * 128;
+      if (act && (!bounds_ok(a.bnd, a.ds.pre + pb, rb, a.ds.pre + cb, clen, kBndDsegRead) ||
+                  !bounds_ok(a.bnd, a.ds.pre + pb, rb, a.ds.pre, a.bnd.pre_bytes, kBndDsegRead)))
+        n = 0;
+    }
     const uint4* P = reinterpret_cast<const uint4*>(a.ds.pre + pb);
     const uint32_t* B = a.ds.bits + (pb >> 5);
     const int nmax = wave_max(n);
@@ -1254,6 +1278,9 @@ __global__ __launch_bounds__(kFixThreads) void ffv1_dfix(CodeArgs a) {
   const StreamSegs ss = a.segs_info[st];
   uint32_t* const out = reinterpret_cast<uint32_t*>(a.slice_out + st * a.slice_stride);
   const int64_t cap = a.digit_cap;
+  if (!bounds_ok(a.bnd, out, 4 * max(cap, (int64_t)h.ndig), a.slice_out, a.bnd.out_bytes, kBndDfixSlot) ||
+      !bounds_ok(a.bnd, out, 4 * (int64_t)h.ndig, out, 4 * cap, kBndDfixSlot))
+    return;
   for (int k = 0; k < h.ndig; k++) out[k] = a.hdr_digits[h.off + k];
   int L = h.low;
   int64_t total = h.ndig;
@@ -1307,6 +1334,9 @@ __global__ __launch_bounds__(kSinkThreads) void ffv1_sink(CodeArgs a) {
   const uint32_t* const din = reinterpret_cast<const uint32_t*>(out);  // values of low at the shifts
   const int n = (int)a.slice_bytes[st];  // digits
   const int cap = (int)a.slice_cap;
+  if (!bounds_ok(a.bnd, out, cap, a.slice_out, a.bnd.out_bytes, kBndSinkSlot) ||
+      !bounds_ok(a.bnd, out, cap, out, a.slice_stride, kBndSinkSlot))
+    return;
   int pend = -1;       // the last non-run digit so far: its byte and its run's wait for a carry
   uint32_t pqv = 0u;   // its qv
   uint32_t nx = lane < n ? din[lane] : 0u;
@@ -1704,6 +1734,14 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
     const int64_t sid = (int64_t)f * a.nslices + (live ? sl : 0);
     const int* dc = a.ds.dcount + sid * 3;
     const int64_t gbase = live ? a.ds.dbase[sid] + (grp ? chroma_start(dc[0]) : 0) : 0;  // chain start
+    // debug build: the chain's extent, its pad included (the layout's)
+    const int64_t gend = !kBoundsCheck || !live ? 0
+                         : grp ? gbase + ((int64_t)dc[1] + dc[2] + 63) / 64 * 64 + kChainPad
+                               : a.ds.dbase[sid] + chroma_start(dc[0]);
+    auto in_chain = [&](int64_t off, int64_t n, uint32_t site) {
+      return bounds_ok(a.bnd, a.ds.pre + off, n, a.ds.pre + gbase, gend - gbase, site) &&
+             bounds_ok(a.bnd, a.ds.pre + off, n, a.ds.pre, a.bnd.pre_bytes, site);
+    };
     int64_t run = 0;  // decisions so far in this frame's chain
     for (int pl = p0; pl < p1; pl++) {
       const int64_t nsym = live ? (pl < 2 ? g.plane_sym_off[pl + 1] : g.nsym) - g.plane_sym_off[pl] : 0;
@@ -1759,6 +1797,7 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
 
         if (lng) {  // e >= 12 somewhere: one symbol at a time, recorded straight to HBM
           const int cmax = max(__builtin_amdgcn_readlane(cnt, 0), __builtin_amdgcn_readlane(cnt, 32));
+          const bool lok = !kBoundsCheck || !live || in_chain(pos0, (int64_t)total + 16, kBndWalkLong);
           // the next symbol's row is read before this symbol's write (a symbol
           // on its predecessor's row takes the state from the register), so a
           // symbol waits on its transition lookups only
@@ -1767,7 +1806,7 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
           for (int t = 0; t < cmax; t++) {
             const uint4 rn = myrecs[t + 1];
             const int stn = mytbl[(int)(rn.x & 0xFFFFu) + k];
-            if (t < cnt) {
+            if (t < cnt && lok) {
               st = walk_long(st, fixed + kLdsN, (int)(int16_t)(r.x >> 16), k,
                              a.ds.pre + pos0 + (int)(r.w & 0xFFFu));
               mytbl[(int)(r.x & 0xFFFFu) + k] = (uint8_t)st;
@@ -1830,6 +1869,9 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
           n_steps += kChunk;
         }
         pdst = live ? a.ds.pre + (pos0 & ~(int64_t)15) : a.scratch;
+        if constexpr (kBoundsCheck) {
+          if (live && !in_chain(pos0 & ~(int64_t)15, kCopyBlocks * 32 * 16, kBndWalkStage)) pdst = a.scratch;
+        }
         plast = (align + total) >> 4;
         __builtin_amdgcn_wave_barrier();
         run += total;
@@ -1840,7 +1882,9 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
   __builtin_amdgcn_wave_barrier();
   pdst = a.scratch;  // the next segment's first copy-out has nothing to write
   plast = 0;
-  if (seg.save_states && live) {
+  if (seg.save_states && live &&
+      bounds_ok(a.bnd, a.persist_out + (int64_t)sl * a.state_bytes + goff, n16 * 16, a.persist_out,
+                a.bnd.persist_bytes, kBndWalkStates)) {
     uint4* dst = reinterpret_cast<uint4*>(a.persist_out + (int64_t)sl * a.state_bytes + goff);
     const uint4* t4 = reinterpret_cast<const uint4*>(mytbl);
     if (!a.dense) {

@@ -11,6 +11,7 @@
  *   -EINVAL (-22) bad argument      -ENOSYS (-38) unsupported parameters
  *   -ENOMEM (-12) allocation        -ENOSPC (-28) slice byte budget exceeded
  *   -EIO     (-5) HIP runtime error (message via ffv1hip_last_error)
+ *   -EFAULT (-14) debug build only: a kernel's write fell outside its buffer
  * plus FFV1HIP_AVERROR_INVALIDDATA for the reference's InvalidData cases.
  */
 #ifndef FFV1HIP_H
@@ -298,6 +299,11 @@ void ffv1hip_dec_reset(ffv1hip_dec *dec);
 /* Last error message (thread-local) and the ABI version. */
 const char *ffv1hip_last_error(void);
 int ffv1hip_abi_version(void);
+/* 1 for the debug build (lib/libffv1hip_check.so, build.py --check): the
+ * walk's and the coder's device writes are bounds-checked, and an encode
+ * call whose batch wrote outside a buffer fails with -EFAULT naming the
+ * kernel; 0 for the release build. */
+int ffv1hip_debug_checks(void);
 
 #ifdef __cplusplus
 }
