@@ -14,6 +14,7 @@
 #include <condition_variable>
 #include <deque>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -595,6 +596,15 @@ struct ffv1hip_ctx {
   // encode2 with the pipe: the set being filled and the launched batches
   // whose packets are not handed out yet (batch id, pts)
   int q_set = 0;
+  // caller-pinned host ranges (ffv1hip_host_register): begin -> {bytes,
+  // pinned here}; frames inside one go to HBM straight from the caller
+  struct HostRange {
+    int64_t bytes;
+    bool owned;
+  };
+  std::map<uintptr_t, HostRange> host_ranges;
+  bool direct_pending = false;  // a direct copy was queued on the transfer stream
+  hipEvent_t direct_ev = nullptr;
   int64_t last_out = -1;  // the packet the last encode2 call handed out (ready index), -1: none
   struct Launched {
     int64_t b;
@@ -1365,7 +1375,10 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
 void ffv1hip_destroy(ffv1hip_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  free_device(c);
+  free_device(c);  // (the transfer stream drained)
+  for (const auto& r : c->host_ranges)
+    if (r.second.owned) (void)hipHostUnregister(reinterpret_cast<void*>(r.first));
+  if (c->direct_ev) (void)hipEventDestroy(c->direct_ev);
   delete c;
 }
 
@@ -2282,8 +2295,28 @@ static int stage_flush(ffv1hip_ctx* c) {
 // rows at dst: piece by piece, copied into a pinned slot by the pool and
 // sent with one async copy on the transfer stream; a slot is reused once
 // its copies are done.
+static bool host_registered(const ffv1hip_ctx* c, const void* p, int64_t n) {
+  if (c->host_ranges.empty()) return false;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  auto it = c->host_ranges.upper_bound(a);
+  if (it == c->host_ranges.begin()) return false;
+  --it;
+  return a + uintptr_t(n) <= it->first + uintptr_t(it->second.bytes);
+}
+
 static int stage_rows(ffv1hip_ctx* c, uint8_t* dst, const uint8_t* src, int64_t sp, int64_t wb, int64_t rows) {
   ffv1hip_ctx::HostPipe& P = c->pipe;
+  if (rows > 0 && host_registered(c, src, (rows - 1) * sp + wb)) {  // caller-pinned: one DMA from it
+    const double t0 = P.dbg ? wall_s() : 0;
+    if (sp == wb)
+      HIP_TRY(hipMemcpyAsync(dst, src, size_t(rows * wb), hipMemcpyHostToDevice, P.xfer));
+    else
+      HIP_TRY(hipMemcpy2DAsync(dst, size_t(wb), src, size_t(sp), size_t(wb), size_t(rows), hipMemcpyHostToDevice,
+                               P.xfer));
+    if (P.dbg) P.t_dma += wall_s() - t0;
+    c->direct_pending = true;
+    return 0;
+  }
   for (int64_t r = 0; r < rows;) {
     if (P.fill + wb > P.slot_bytes) {
       const int rc = stage_flush(c);
@@ -2583,6 +2616,12 @@ int ffv1hip_encode2(ffv1hip_ctx* c, const void* const planes[4], const int strid
     // the frame is copied into the next batch slot (the caller keeps
     // ownership: it may reuse the buffer once the call returns)
     if ((rc = stage_frame(c, c->q_set, int64_t(c->q_pts.size()), planes, strides)) < 0) return rc;
+    if (c->direct_pending) {  // straight from the caller's pinned memory: done before the call returns
+      if (!c->direct_ev) HIP_TRY(hipEventCreateWithFlags(&c->direct_ev, hipEventDisableTiming));
+      HIP_TRY(hipEventRecord(c->direct_ev, c->pipe.xfer));
+      HIP_TRY(hipEventSynchronize(c->direct_ev));
+      c->direct_pending = false;
+    }
     c->q_pts.push_back(pts);
     if (int(c->q_pts.size()) == c->max_batch) {
       if ((rc = launch_staged(c, c->q_set, c->max_batch)) < 0) return rc;
@@ -2631,6 +2670,38 @@ int64_t ffv1hip_encode2_last_packet(ffv1hip_ctx* c, uint8_t* out, int64_t cap) {
   if (R.size[i] && !out) return set_err(-22, "null buffer");
   if (R.size[i]) pool_copy2d(*c->pipe.pool_out, out, R.size[i], R.base + R.off[i], R.size[i], R.size[i], 1);
   return R.size[i];
+}
+
+int ffv1hip_host_register(ffv1hip_ctx* c, void* ptr, int64_t bytes) {
+  if (!c || !ptr || bytes <= 0) return set_err(-22, "null or empty range");
+  const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
+  auto it = c->host_ranges.lower_bound(a);
+  if ((it != c->host_ranges.end() && it->first < a + uintptr_t(bytes)) ||
+      (it != c->host_ranges.begin() && std::prev(it)->first + uintptr_t(std::prev(it)->second.bytes) > a))
+    return set_err(-22, "the range overlaps a registered one");
+  HIP_TRY(hipSetDevice(c->device));
+  bool owned = true;
+  const hipError_t e = hipHostRegister(ptr, size_t(bytes), hipHostRegisterDefault);
+  if (e == hipErrorHostMemoryAlreadyRegistered) {
+    owned = false;  // pinned by the process itself: left so on unregister
+  } else if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(-12, "hipHostRegister of %lld bytes: %s", (long long)bytes, hipGetErrorString(e));
+  }
+  (void)hipGetLastError();
+  c->host_ranges[a] = ffv1hip_ctx::HostRange{bytes, owned};
+  return 0;
+}
+
+int ffv1hip_host_unregister(ffv1hip_ctx* c, void* ptr) {
+  if (!c) return set_err(-22, "null ctx");
+  auto it = c->host_ranges.find(reinterpret_cast<uintptr_t>(ptr));
+  if (it == c->host_ranges.end()) return set_err(-22, "no range registered at %p", ptr);
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->pipe.xfer) HIP_TRY(hipStreamSynchronize(c->pipe.xfer));  // no copy from it is in flight
+  if (it->second.owned) HIP_TRY(hipHostUnregister(ptr));
+  c->host_ranges.erase(it);
+  return 0;
 }
 
 int ffv1hip_set_profiling(ffv1hip_ctx* c, int enable) {

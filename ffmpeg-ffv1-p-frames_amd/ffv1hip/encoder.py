@@ -71,7 +71,7 @@ EXPORTED_SYMBOLS = (
     "ffv1hip_max_packet_size", "ffv1hip_encode", "ffv1hip_encode_device", "ffv1hip_fetch",
     "ffv1hip_device_packets", "ffv1hip_picture_number", "ffv1hip_reset",
     "ffv1hip_get_slice_states", "ffv1hip_set_slice_states", "ffv1hip_last_error",
-    "ffv1hip_abi_version", "ffv1hip_debug_checks", "ffv1hip_set_profiling", "ffv1hip_last_kernel_ms",
+    "ffv1hip_abi_version", "ffv1hip_debug_checks", "ffv1hip_host_register", "ffv1hip_host_unregister", "ffv1hip_set_profiling", "ffv1hip_last_kernel_ms",
     "ffv1hip_last_kernel_stats", "ffv1hip_synchronize",
     "ffv1hip_dec_create", "ffv1hip_dec_destroy", "ffv1hip_decode", "ffv1hip_dec_reset",
     "ffv1hip_set_picture_number", "ffv1hip_encode2", "ffv1hip_encode2_delay", "ffv1hip_encode2_last_packet",
@@ -167,6 +167,10 @@ def load_library():
     L.ffv1hip_dec_damaged_slices.restype = ctypes.c_int
     L.ffv1hip_abi_version.argtypes = []
     L.ffv1hip_abi_version.restype = ctypes.c_int
+    L.ffv1hip_host_register.argtypes = [vp, vp, i64]
+    L.ffv1hip_host_register.restype = ctypes.c_int
+    L.ffv1hip_host_unregister.argtypes = [vp, vp]
+    L.ffv1hip_host_unregister.restype = ctypes.c_int
     L.ffv1hip_debug_checks.argtypes = []
     L.ffv1hip_debug_checks.restype = ctypes.c_int
     _lib = L
@@ -233,6 +237,18 @@ class HipEncoder:
             self._h = None
 
     __del__ = close
+
+    def register_host(self, arr: np.ndarray):
+        """Page-lock a (C-contiguous) array the caller keeps alive, so that
+        frames in it go to HBM straight from it (ffv1hip_host_register)."""
+        rc = load_library().ffv1hip_host_register(self._h, arr.ctypes.data, arr.nbytes)
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_host_register")
+
+    def unregister_host(self, arr: np.ndarray):
+        rc = load_library().ffv1hip_host_unregister(self._h, arr.ctypes.data)
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_host_unregister")
 
     def set_pass(self, pass_: int, stats_in: Optional[str] = None):
         """2-pass mode, before the first frame (ffv1hip_set_pass)."""

@@ -168,6 +168,22 @@ int ffv1hip_encode2(ffv1hip_ctx *ctx, const void *const planes[4],
  * next ffv1hip_encode2 call. */
 int64_t ffv1hip_encode2_last_packet(ffv1hip_ctx *ctx, uint8_t *out, int64_t cap);
 
+/* Caller-pinned host memory for the host-frame paths: [ptr, ptr + bytes)
+ * is page-locked (hipHostRegister) until ffv1hip_host_unregister or
+ * ffv1hip_destroy, and a plane of ffv1hip_encode / ffv1hip_encode2 that lies
+ * inside a registered range goes to HBM by DMA straight from it, without
+ * the staging copy (ffv1hip_encode2 still returns only once the frame's
+ * copy is done, so the caller may reuse the buffer as before).  For an
+ * application's frame pool, whose buffers outlive the encoder calls: the
+ * range must stay allocated while registered.  A range the process already
+ * pinned itself is accepted and left pinned on unregister.  Returns 0,
+ * -EINVAL (null, empty, or overlapping a registered range) or -ENOMEM (the
+ * pages cannot be locked). */
+int ffv1hip_host_register(ffv1hip_ctx *ctx, void *ptr, int64_t bytes);
+/* Forget the range registered at ptr (its pages unlocked).  -EINVAL when
+ * none starts there. */
+int ffv1hip_host_unregister(ffv1hip_ctx *ctx, void *ptr);
+
 /* The encoder's delay in frames (avctx->delay): 2 * max_batch_frames - 1
  * when two batches fit in HBM side by side (one codes while the next
  * queues), else max_batch_frames - 1.  Allocates the host-frame path's

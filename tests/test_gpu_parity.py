@@ -323,6 +323,69 @@ def test_host_encode_many_batches(cap, monkeypatch):
     assert got == ref
 
 
+def _pool_views(pool, shapes_dtypes, nframes):
+    """Frames as views into one flat uint8 buffer (a caller's frame pool)."""
+    out, off = [], 0
+    for _ in range(nframes):
+        f = []
+        for shp, dt in shapes_dtypes:
+            nb = int(np.prod(shp)) * np.dtype(dt).itemsize
+            f.append(pool[off:off + nb].view(dt).reshape(shp))
+            off += nb
+        out.append(f)
+    return out
+
+
+@pytest.mark.parametrize("cap", [None, "512"])
+def test_registered_host_frames(cap, monkeypatch):
+    """Frames in caller-pinned memory (ffv1hip_host_register) go to HBM by DMA
+    straight from it: ffv1hip_encode over several batches from a registered
+    pool, and ffv1hip_encode2 from ONE registered buffer the caller rewrites
+    after every call (the frame's copy is done when the call returns), with
+    and without the budget re-encode, which reads the batch's frames again:
+    the oracle's packets."""
+    if cap:
+        monkeypatch.setenv("FFV1HIP_DEBUG", f"slice_cap={cap}")
+    from ffv1hip import AVCodecContext, FFV1Encoder, HipEncoder
+    s = PARITY_STREAMS[1]
+    frames = list(s.frames())
+    _, _, ref = oracle_encode(s, frames)
+    sd = [(p.shape, p.dtype) for p in frames[0]]
+    fbytes = sum(p.nbytes for p in frames[0])
+    pool = np.empty(fbytes * len(frames), np.uint8)
+    views = _pool_views(pool, sd, len(frames))
+    for v, f in zip(views, frames):
+        for a, b in zip(v, f):
+            a[...] = b
+    enc = HipEncoder(hip_params(s), 0, 3)
+    enc.register_host(pool)
+    assert enc.encode(views) == ref
+    enc.unregister_host(pool)
+    with pytest.raises(Exception, match="no range registered"):
+        enc.unregister_host(pool)
+    enc.close()
+
+    avctx = AVCodecContext(s.width, s.height, s.pix_fmt, gop_size=s.gop_size, slices=s.slices, coder=s.coder)
+    e2 = FFV1Encoder(batch=3)
+    assert e2.init(avctx) == 0
+    buf = np.empty(fbytes, np.uint8)
+    e2._enc.register_host(buf)
+    (one,) = _pool_views(buf, sd, 1)
+    pkts = []
+    for i, f in enumerate(frames):
+        for a, b in zip(one, f):
+            a[...] = b
+        pk = e2.encode2(one, pts=i)
+        for a in one:  # the caller reuses the buffer at once
+            a[...] = 0
+        if pk is not None:
+            pkts.append(pk)
+    while (pk := e2.encode2(None)) is not None:
+        pkts.append(pk)
+    assert e2.close() == 0
+    assert [(p.data, p.key) for p in pkts] == ref
+
+
 def _d2h(ptr, nbytes):
     """Device bytes at `ptr` through the HIP runtime the library links."""
     import ctypes
