@@ -32,7 +32,7 @@ from helpers import Stream
 assert load_library().ffv1hip_debug_checks() == 1
 from test_gpu_parity import hip_params
 for s in [Stream("c420", 352, 288, "yuv420p10", 6, slices=4, level=3, coder=1, gop_size=3, source="random"),
-          Stream("c444", 176, 144, "yuv444p", 5, slices=6, level=3, coder=1, gop_size=5)]:
+          Stream("c444", 176, 144, "yuv444p", 5, slices=6, level=3, coder=1, gop_size=5, chroma444=True)]:
     frames = list(s.frames())
     try:
         enc = HipEncoder(hip_params(s), 0, len(frames))
