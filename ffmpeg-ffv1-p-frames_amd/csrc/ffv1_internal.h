@@ -124,17 +124,25 @@ constexpr uint32_t kRecSame2 = 0x40000000u;
 
 // Decision stream of one batch (frame-parallel mode).  Every (frame, slice)
 // stream's binary decisions, in coding order, start at decision index
-// dbase[frame][slice] (a multiple of 64): the luma chain's dcount[0]
+// dbase[frame][slice] (a multiple of kStreamAlign): the luma chain's dcount[0]
 // decisions, then, from chroma_start(dcount[0]), the chroma chain's (Cb then
 // Cr).  Each chain is followed by kChainPad unused decisions: the states
 // walk writes a chunk's recorded bytes in whole 16-byte blocks, and the
 // blocks past a chain's last decision land there.  Decision d has the
 // adaptive state it is coded with in pre[d] and its value in bit d of
 // bits[] (bit d & 31 of word d >> 5).
+// Chains start at multiples of kStreamAlign = 512 decisions, so that every
+// coder segment's decision bits start on a 64-byte boundary (ffv1_dseg reads
+// them 64 bytes per lane at a time).
 constexpr int kChainPad = 2048;
-__host__ __device__ inline int64_t chroma_start(int64_t dc0) { return ((dc0 + 63) & ~int64_t(63)) + kChainPad; }
+constexpr int kStreamAlign = 512;
+// a chain of n decisions and its pad, rounded to the alignment
+__host__ __device__ inline int64_t chain_extent(int64_t n) {
+  return (n + kStreamAlign - 1) / kStreamAlign * kStreamAlign + kChainPad;
+}
+__host__ __device__ inline int64_t chroma_start(int64_t dc0) { return chain_extent(dc0); }
 // decisions a stream takes beyond its own (alignment and the two pads)
-constexpr int64_t kStreamSlack = 2 * kChainPad + 2 * 64;
+constexpr int64_t kStreamSlack = 2 * kChainPad + 2 * kStreamAlign;
 struct DecisionStream {
   const int* dcount;          // [frame][slice][3] decisions per plane
   const int64_t* dbase;       // [frame][slice]
@@ -423,7 +431,6 @@ int launch_sink(const CodeArgs& a, void* stream);
 int launch_bits(const BitsArgs& a, void* stream);
 int64_t walk_lds_bytes(int rows);  // one walk wave's LDS for tables of `rows` context rows
 constexpr int64_t kWalkLdsMax = 64 * 1024;  // states walk: one plane group's table + T9 + staging in LDS
-constexpr int kStreamAlign = 64;            // decisions: every stream starts at a multiple
 int launch_code_golomb(const CodeArgs& a, void* stream);
 int launch_assemble(const AssembleArgs& a, int nframes, void* stream);
 int launch_compact_packets(const uint8_t* packets, int64_t stride, const int64_t* sizes, int n, uint8_t* out,

@@ -1191,32 +1191,43 @@ __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
                             a.bnd.out_bytes, kBndDsegSlot))
         o.rs = __builtin_amdgcn_make_buffer_rsrc(a.slice_out, 0, 0, kBufDword3);  // every store dropped
       // the blocks it reads: inside its chain and pad (the chain's extent as the layout made it)
-      const int64_t clen = part ? (npart + 63) / 64 * 64 + kChainPad : chroma_start(dc[0]);
+      const int64_t clen = chain_extent(npart);
       const int64_t rb = (int64_t)(n + 127) / 128 * 128;
       if (act && (!bounds_ok(a.bnd, a.ds.pre + pb, rb, a.ds.pre + cb, clen, kBndDsegRead) ||
                   !bounds_ok(a.bnd, a.ds.pre + pb, rb, a.ds.pre, a.bnd.pre_bytes, kBndDsegRead)))
         n = 0;
     }
     const uint4* P = reinterpret_cast<const uint4*>(a.ds.pre + pb);
-    const uint32_t* B = a.ds.bits + (pb >> 5);
+    const uint4* B4 = reinterpret_cast<const uint4*>(a.ds.bits + (pb >> 5));  // 64-byte aligned (kStreamAlign)
     const int nmax = wave_max(n);
-    // Blocks of 128 decisions: a whole 128-byte line of states and four
-    // bit words per lane, the next block's loaded while this one codes.  The
-    // 64 lanes of a wave read 64 segments 4 KB apart, so a line read 16 or
-    // 32 bytes at a time was fetched from HBM again for each part (PMC:
-    // 185 GB per launch for 34 GB of states and bits).
+    // Blocks of 128 decisions: a whole 128-byte line of states per lane, the
+    // next block's loaded while this one codes, and the decision bits of
+    // four blocks (64 bytes) at a time, the next four's loaded a group
+    // ahead.  The 64 lanes of a wave read 64 segments 4 KB apart, so a line
+    // read a part at a time is fetched from HBM again for each part: states
+    // 16-32 bytes at a time took 185 GB per launch for 34 GB of states and
+    // bits, then whole state lines with 16 bytes of bits per block 71 GB.
     const uint4 z4 = make_uint4(0, 0, 0, 0);
     uint4 cur[8], nxt[8];
-    uint32_t cbw[4], nbw[4];
-    auto fetch = [&](int blk, uint4* q, uint32_t* w) {
+    uint4 bg[4], nbg[4];  // bits: this group of four blocks, the next group
+    auto fetch = [&](int blk, uint4* q) {
       static_for<0, 8>([&](auto jc) { q[decltype(jc)::value] = P[blk * 8 + decltype(jc)::value]; });
-      static_for<0, 4>([&](auto jc) { w[decltype(jc)::value] = B[blk * 4 + decltype(jc)::value]; });
     };
     static_for<0, 8>([&](auto jc) { cur[decltype(jc)::value] = nxt[decltype(jc)::value] = z4; });
-    static_for<0, 4>([&](auto jc) { cbw[decltype(jc)::value] = nbw[decltype(jc)::value] = 0u; });
-    if (n > 0) fetch(0, cur, cbw);  // (parts are padded: reads stay inside the stream)
+    static_for<0, 4>([&](auto jc) { bg[decltype(jc)::value] = nbg[decltype(jc)::value] = z4; });
+    if (n > 0) {  // (chains are padded to 512 decisions and more: reads stay inside the stream)
+      fetch(0, cur);
+      static_for<0, 4>([&](auto jc) { nbg[decltype(jc)::value] = B4[decltype(jc)::value]; });
+    }
     for (int i = 0; i < nmax; i += 128) {
-      if (i + 128 < n) fetch((i >> 7) + 1, nxt, nbw);
+      const int q = (i >> 7) & 3;  // wave-uniform
+      if (q == 0) {
+        static_for<0, 4>([&](auto jc) { bg[decltype(jc)::value] = nbg[decltype(jc)::value]; });
+        if (i + 512 < n) static_for<0, 4>([&](auto jc) { nbg[decltype(jc)::value] = B4[(i >> 7) + 4 + decltype(jc)::value]; });
+      }
+      if (i + 128 < n) fetch((i >> 7) + 1, nxt);
+      const uint4 b4 = q == 0 ? bg[0] : q == 1 ? bg[1] : q == 2 ? bg[2] : bg[3];
+      const uint32_t cbw[4] = {b4.x, b4.y, b4.z, b4.w};
       static_for<0, 4>([&](auto sc) {
         constexpr int S = decltype(sc)::value;
         uint4 wa = cur[2 * S], wb = cur[2 * S + 1];
@@ -1238,7 +1249,6 @@ __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
         });
       });
       static_for<0, 8>([&](auto jc) { cur[decltype(jc)::value] = nxt[decltype(jc)::value]; });
-      static_for<0, 4>([&](auto jc) { cbw[decltype(jc)::value] = nbw[decltype(jc)::value]; });
     }
     if (last) {  // a 0 on state 129, then ff_rac_terminate (ffv1enc.c:1331-1334, rangecoder.c:104-116)
       {  // the trailer decision: at most one shift
@@ -1735,9 +1745,7 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
     const int* dc = a.ds.dcount + sid * 3;
     const int64_t gbase = live ? a.ds.dbase[sid] + (grp ? chroma_start(dc[0]) : 0) : 0;  // chain start
     // debug build: the chain's extent, its pad included (the layout's)
-    const int64_t gend = !kBoundsCheck || !live ? 0
-                         : grp ? gbase + ((int64_t)dc[1] + dc[2] + 63) / 64 * 64 + kChainPad
-                               : a.ds.dbase[sid] + chroma_start(dc[0]);
+    const int64_t gend = !kBoundsCheck || !live ? 0 : gbase + chain_extent(grp ? (int64_t)dc[1] + dc[2] : dc[0]);
     auto in_chain = [&](int64_t off, int64_t n, uint32_t site) {
       return bounds_ok(a.bnd, a.ds.pre + off, n, a.ds.pre + gbase, gend - gbase, site) &&
              bounds_ok(a.bnd, a.ds.pre + off, n, a.ds.pre, a.bnd.pre_bytes, site);
@@ -1926,7 +1934,7 @@ __global__ __launch_bounds__(kLayoutThreads) void ffv1_layout(const int* dcount,
   const int lo = min(t * per, nstreams), hi = min(lo + per, nstreams);
   auto len = [&](int i) -> int64_t {
     const int64_t n = (int64_t)dcount[3 * i + 1] + dcount[3 * i + 2];
-    return chroma_start(dcount[3 * i]) + ((n + kStreamAlign - 1) / kStreamAlign * kStreamAlign) + kChainPad;
+    return chroma_start(dcount[3 * i]) + chain_extent(n);
   };
   // the coder's segments: the luma chain's, then the chroma chain's (at
   // least one segment, which carries the terminate)
