@@ -471,6 +471,7 @@ struct ffv1hip_ctx {
   uint32_t* d_cbits2 = nullptr;  // chunk bits of set 1
   int* d_ident = nullptr;        // [batch frame] i: the frames mode's frame of each slot
   hipEvent_t entry[2] = {nullptr, nullptr};  // set k's batch: the launch stream's work so far
+  hipEvent_t xchg_ev = nullptr;               // ffv1hip_set_slice_states_device: the caller's stream so far
   hipEvent_t walk_a = nullptr;               // the first part of the last batch's walk is done
   hipEvent_t walk_go = nullptr;              // everything before the last batch's walk is done (it starts)
   bool walk_a_valid = false;
@@ -1379,6 +1380,7 @@ void ffv1hip_destroy(ffv1hip_ctx* c) {
   for (const auto& r : c->host_ranges)
     if (r.second.owned) (void)hipHostUnregister(reinterpret_cast<void*>(r.first));
   if (c->direct_ev) (void)hipEventDestroy(c->direct_ev);
+  if (c->xchg_ev) (void)hipEventDestroy(c->xchg_ev);
   delete c;
 }
 
@@ -2777,6 +2779,42 @@ int ffv1hip_set_slice_states(ffv1hip_ctx* c, const uint8_t* buf, int64_t size) {
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(c->d_persist[c->pcur], buf, n, hipMemcpyHostToDevice));
+  c->have_states = true;
+  return 0;
+}
+
+int64_t ffv1hip_get_slice_states_device(ffv1hip_ctx* c, void* d_buf, int64_t cap, void* stream) {
+  if (!c) return set_err(-22, "null ctx");
+  const int64_t n = int64_t(c->pcount) * c->contexts * 32 * c->nslices;
+  if (!d_buf) return n;
+  if (cap < n) return set_err(-22, "buffer too small");
+  HIP_TRY(hipSetDevice(c->device));
+  // the carry is complete once the batch is settled (a slice over the
+  // budget re-encodes it); the copy then waits for the batch on the device
+  const int rc = settle_batch(c, c->nsub - 1);
+  if (rc < 0) return rc;
+  hipStream_t const s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+  if (c->dep_valid) HIP_TRY(hipStreamWaitEvent(s, c->done_ev, 0));
+  HIP_TRY(hipMemcpyAsync(d_buf, c->d_persist[c->pcur], size_t(n), hipMemcpyDeviceToDevice, s));
+  return n;
+}
+
+int ffv1hip_set_slice_states_device(ffv1hip_ctx* c, const void* d_buf, int64_t size, void* stream) {
+  if (!c || !d_buf) return set_err(-22, "null argument");
+  const int64_t n = int64_t(c->pcount) * c->contexts * 32 * c->nslices;
+  if (size != n) return set_err(-22, "state blob is %lld bytes, expected %lld", (long long)size, (long long)n);
+  HIP_TRY(hipSetDevice(c->device));
+  if (stream) {  // what the caller queued (the receive) first
+    if (!c->xchg_ev) HIP_TRY(hipEventCreateWithFlags(&c->xchg_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(c->xchg_ev, reinterpret_cast<hipStream_t>(stream)));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->xchg_ev, 0));
+  }
+  if (c->dep_valid) HIP_TRY(hipStreamWaitEvent(c->stream, c->done_ev, 0));  // the last batch is done with the carry
+  HIP_TRY(hipMemcpyAsync(c->d_persist[c->pcur], d_buf, size_t(n), hipMemcpyDeviceToDevice, c->stream));
+  // the next batch (its walk or chained coder, and its coder stream) starts after the copy
+  HIP_TRY(hipEventRecord(c->dep_ev, c->stream));
+  HIP_TRY(hipEventRecord(c->done_ev, c->stream));
+  c->dep_valid = true;
   c->have_states = true;
   return 0;
 }

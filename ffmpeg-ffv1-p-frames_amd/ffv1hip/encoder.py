@@ -71,7 +71,8 @@ EXPORTED_SYMBOLS = (
     "ffv1hip_max_packet_size", "ffv1hip_encode", "ffv1hip_encode_device", "ffv1hip_fetch",
     "ffv1hip_device_packets", "ffv1hip_picture_number", "ffv1hip_reset",
     "ffv1hip_get_slice_states", "ffv1hip_set_slice_states", "ffv1hip_last_error",
-    "ffv1hip_abi_version", "ffv1hip_debug_checks", "ffv1hip_host_register", "ffv1hip_host_unregister", "ffv1hip_set_profiling", "ffv1hip_last_kernel_ms",
+    "ffv1hip_abi_version", "ffv1hip_debug_checks", "ffv1hip_host_register", "ffv1hip_host_unregister",
+    "ffv1hip_get_slice_states_device", "ffv1hip_set_slice_states_device", "ffv1hip_set_profiling", "ffv1hip_last_kernel_ms",
     "ffv1hip_last_kernel_stats", "ffv1hip_synchronize",
     "ffv1hip_dec_create", "ffv1hip_dec_destroy", "ffv1hip_decode", "ffv1hip_dec_reset",
     "ffv1hip_set_picture_number", "ffv1hip_encode2", "ffv1hip_encode2_delay", "ffv1hip_encode2_last_packet",
@@ -167,6 +168,10 @@ def load_library():
     L.ffv1hip_dec_damaged_slices.restype = ctypes.c_int
     L.ffv1hip_abi_version.argtypes = []
     L.ffv1hip_abi_version.restype = ctypes.c_int
+    L.ffv1hip_get_slice_states_device.argtypes = [vp, vp, i64, vp]
+    L.ffv1hip_get_slice_states_device.restype = i64
+    L.ffv1hip_set_slice_states_device.argtypes = [vp, vp, i64, vp]
+    L.ffv1hip_set_slice_states_device.restype = ctypes.c_int
     L.ffv1hip_host_register.argtypes = [vp, vp, i64]
     L.ffv1hip_host_register.restype = ctypes.c_int
     L.ffv1hip_host_unregister.argtypes = [vp, vp]
@@ -384,6 +389,39 @@ class HipEncoder:
         rc = L.ffv1hip_set_slice_states(self._h, _u8p(buf), buf.size)
         if rc < 0:
             raise FFV1Error(rc, "ffv1hip_set_slice_states")
+        rc = L.ffv1hip_set_picture_number(self._h, picture_number)
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_set_picture_number")
+
+    def state_bytes(self) -> int:
+        n = load_library().ffv1hip_get_slice_states(self._h, None, 0)
+        if n < 0:
+            raise FFV1Error(n, "ffv1hip_get_slice_states")
+        return n
+
+    def get_slice_states_device(self, out):
+        """The carry into `out`, a uint8 torch tensor on this encoder's GPU,
+        queued on torch's current stream (ffv1hip_get_slice_states_device):
+        no host copy, ready for an RCCL send."""
+        import torch
+        assert out.is_cuda and out.dtype == torch.uint8 and out.is_contiguous()
+        st = torch.cuda.current_stream(out.device).cuda_stream
+        n = load_library().ffv1hip_get_slice_states_device(self._h, out.data_ptr(), out.numel(), st)
+        if n < 0:
+            raise FFV1Error(n, "ffv1hip_get_slice_states_device")
+        return out
+
+    def set_slice_states_device(self, buf, picture_number: int):
+        """Continue another encoder's stream at `picture_number` from states in
+        a device tensor (received over RCCL), ordered after torch's current
+        stream (ffv1hip_set_slice_states_device)."""
+        import torch
+        assert buf.is_cuda and buf.dtype == torch.uint8 and buf.is_contiguous()
+        L = load_library()
+        st = torch.cuda.current_stream(buf.device).cuda_stream
+        rc = L.ffv1hip_set_slice_states_device(self._h, buf.data_ptr(), buf.numel(), st)
+        if rc < 0:
+            raise FFV1Error(rc, "ffv1hip_set_slice_states_device")
         rc = L.ffv1hip_set_picture_number(self._h, picture_number)
         if rc < 0:
             raise FFV1Error(rc, "ffv1hip_set_picture_number")

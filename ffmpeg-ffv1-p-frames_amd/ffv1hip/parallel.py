@@ -83,7 +83,7 @@ def _is_key(i: int, gop: int) -> bool:
 def encode_exchanged(encoder_factory: Callable[[], object], frames: Callable[[int], Sequence],
                      n_frames: int, gop: int, dist, rank: int, world: int,
                      to_tensor: Callable, from_tensor: Callable,
-                     state_bytes: int) -> Dict[int, Tuple[bytes, bool]]:
+                     state_bytes: int, device=None) -> Dict[int, Tuple[bytes, bool]]:
     """Encode this rank's contiguous range.
 
     The part of the range from its first keyframe on (the body) is
@@ -93,7 +93,10 @@ def encode_exchanged(encoder_factory: Callable[[], object], frames: Callable[[in
     a second encoder placed at the right picture number.  Encoders need
     ``encode``, ``get_slice_states`` and ``set_slice_states(buf, pn)``;
     ``to_tensor``/``from_tensor`` move a state blob to and from the
-    communication device."""
+    communication device.  With ``device`` (a torch GPU device; RCCL) the
+    blob never leaves HBM: the encoder's ``get_slice_states_device`` /
+    ``set_slice_states_device`` copy it device to device, and the send and
+    receive move the device tensor itself."""
     if n_frames < world:
         raise ValueError("the exchange step needs at least one frame per rank")
     ranges = contiguous_ranges(n_frames, world)
@@ -102,28 +105,38 @@ def encode_exchanged(encoder_factory: Callable[[], object], frames: Callable[[in
     first_key = next((i for i in range(lo, hi) if _is_key(i, gop)), hi)
     send_next = rank + 1 < world and not _is_key(ranges[rank + 1][0], gop)
 
-    def send(states):
-        dist.send(to_tensor(states), dst=rank + 1)
+    def send(enc):
+        if device is not None:
+            import torch
+            buf = torch.empty(state_bytes, dtype=torch.uint8, device=device)
+            dist.send(enc.get_slice_states_device(buf), dst=rank + 1)
+        else:
+            dist.send(to_tensor(enc.get_slice_states()), dst=rank + 1)
 
-    last_states = None
     if first_key < hi:  # body: independent of the other ranks
         enc = encoder_factory()
         for i, p in zip(range(first_key, hi), enc.encode([frames(i) for i in range(first_key, hi)])):
             out[i] = p
-        last_states = enc.get_slice_states()
         if send_next:
-            send(last_states)
+            send(enc)
         _close(enc)  # one encoder's device buffers at a time
         enc = None
     if lo < first_key:  # head: continue rank-1's chain
-        buf = to_tensor(np.zeros(state_bytes, np.uint8))
+        if device is not None:
+            import torch
+            buf = torch.empty(state_bytes, dtype=torch.uint8, device=device)
+        else:
+            buf = to_tensor(np.zeros(state_bytes, np.uint8))
         dist.recv(buf, src=rank - 1)
         enc = encoder_factory()
-        enc.set_slice_states(from_tensor(buf), lo)
+        if device is not None:
+            enc.set_slice_states_device(buf, lo)
+        else:
+            enc.set_slice_states(from_tensor(buf), lo)
         for i, p in zip(range(lo, first_key), enc.encode([frames(i) for i in range(lo, first_key)])):
             out[i] = p
         if first_key == hi and send_next:  # no keyframe in the range: pass the chain on
-            send(enc.get_slice_states())
+            send(enc)
         _close(enc)
     return out
 

@@ -55,6 +55,12 @@ class _Enc:
     def set_slice_states(self, buf, pn):
         self.e.set_slice_states(buf, pn)
 
+    def get_slice_states_device(self, out):
+        return self.e.get_slice_states_device(out)
+
+    def set_slice_states_device(self, buf, pn):
+        self.e.set_slice_states_device(buf, pn)
+
     def close(self):
         self.e.close()
 
@@ -110,3 +116,52 @@ def test_hip_multiprocess_stream_matches_reference_pin(mode, world):
     assert all(p.exitcode == 0 for p in procs)
     assert keys == [i % GOP == 0 for i in range(N)]
     assert digest == _pin()["stream_md5"]
+
+
+class _DeviceMailbox:
+    """dist.send / dist.recv between ranks run one after the other in this
+    process: the device tensor itself is handed over, as RCCL moves it from
+    one GPU's HBM to the next (the single-GPU box cannot run two RCCL ranks
+    on one device)."""
+
+    def __init__(self):
+        self.rank = 0
+        self.box = {}
+
+    def send(self, t, dst):
+        assert t.is_cuda
+        self.box[(self.rank, dst)] = t.clone()
+
+    def recv(self, t, src):
+        assert t.is_cuda
+        t.copy_(self.box.pop((src, self.rank)))
+
+
+def test_exchange_step_device_resident_states():
+    """encode_exchanged with device=cuda:0: the slice states go encoder ->
+    device tensor -> (send/recv) -> encoder without a host copy
+    (ffv1hip_get/set_slice_states_device); three ranks in turn reproduce the
+    reference's config-3 MD5, and the device snapshot equals the host one."""
+    import numpy as np
+    import torch
+    from ffv1hip import parallel, synth
+    frames = list(synth.videogen_frames(W, H, N, depth=10))
+    e = _Enc()
+    state_bytes = e.e.state_bytes()
+    e.encode(frames[:7])
+    dev = torch.empty(state_bytes, dtype=torch.uint8, device="cuda:0")
+    e.get_slice_states_device(dev)
+    assert np.array_equal(dev.cpu().numpy(), e.get_slice_states())
+    e.close()
+    mb = _DeviceMailbox()
+    local = {}
+    for rank in range(3):
+        mb.rank = rank
+        local.update(parallel.encode_exchanged(_Enc, lambda i: frames[i], N, GOP, mb, rank, 3,
+                                               to_tensor=None, from_tensor=None, state_bytes=state_bytes,
+                                               device=torch.device("cuda:0")))
+    assert not mb.box
+    h = hashlib.md5()
+    for i in range(N):
+        h.update(local[i][0])
+    assert h.hexdigest() == _pin()["stream_md5"]
