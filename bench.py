@@ -40,7 +40,7 @@ W, H, PIX_FMT, SLICES, GOP = 3840, 2160, "yuv420p10", 64, 12
 # lossless round trip (and c2 also by the reference's MD5 pin).
 CONFIGS = {
     "c3": dict(W=3840, H=2160, PIX_FMT="yuv420p10", SLICES=64, GOP=12, BPR=0, DEPTH=10, C444=False,
-               GRID=False, GOPS=20, PIN=("08e3975d4d0f5f2e5c82cd4037764789", 24),  # 20 GOPs: 1280 walk waves, one round
+               GRID=False, GOPS=24, PIN=("08e3975d4d0f5f2e5c82cd4037764789", 24),  # 24 GOPs: 1280 walk waves in 5-wave blocks, one round
                metric="Mpixels/s encoded (bit-exact) 4K yuv420p10 FFV1 P-frames",
                workload="4K 3840x2160 yuv420p10le, coder=1 (range, custom table), slices=64, keyint=12 P-frames"),
     "c2": dict(W=1920, H=1080, PIX_FMT="yuv420p", SLICES=24, GOP=1, BPR=0, DEPTH=8, C444=False,
