@@ -52,7 +52,7 @@ CONFIGS = {
                metric="Mpixels/s encoded (lossless) 4K yuv444p12 FFV1 P-frames",
                workload="4K 3840x2160 yuv444p16le + bits_per_raw_sample=12, coder=1, slices=64, keyint=12 P-frames"),
     "c5": dict(W=7680, H=4320, PIX_FMT="yuv420p10", SLICES=256, GOP=12, BPR=0, DEPTH=10, C444=False,
-               GRID=True, GOPS=5, PIN=None,  # 5 GOPs = 1280 walk waves, one round (6: 12.9 vs 14.7 Gpix/s)
+               GRID=True, GOPS=6, PIN=None,  # 6 GOPs: 1280 walk waves in 5-wave blocks, one round (5: 14.1 vs 15.5 Gpix/s)
                metric="Mpixels/s encoded (lossless) 8K yuv420p10 FFV1 P-frames",
                workload="8K 7680x4320 yuv420p10le, coder=1, slices=256 (16x16 grid), keyint=12 P-frames"),
 }
@@ -117,7 +117,7 @@ def cpu_baseline(frames, threads):
     `value`: GOP-sharded, the strongest CPU configuration:
     each worker thread encodes whole GOPs (1 key + 11 P frames) with its own
     encoder; ctypes drops the GIL, so the threads run in parallel.  When the
-    batch has fewer GOPs than threads (c5: 5 GOPs), each GOP's slices are
+    batch has fewer GOPs than threads (c5: 6 GOPs), each GOP's slices are
     coded on threads // GOPs threads, so every core works.  Plus the
     reference's own threading model, one job per slice on min(cores, slices)
     threads over one GOP (`slice_threaded`, ffv1enc.c:1323), and a one-thread
@@ -135,7 +135,9 @@ def cpu_baseline(frames, threads):
     per = max(GOP, 1)
     ngops = len(frames) // per
     workers = max(1, min(threads, ngops))
-    inner = max(1, threads // workers)  # slice threads per GOP worker
+    # slice threads per GOP worker: the cores shared out, the first
+    # threads % workers workers one more (c5: 6 GOPs on 16 cores = 4 x 3 + 2 x 2)
+    inner = [max(1, threads // workers + (1 if g < threads % workers else 0)) for g in range(workers)]
 
     def one(g, th=1):
         enc = oracle.Encoder(cfg)
@@ -149,7 +151,7 @@ def cpu_baseline(frames, threads):
     t0 = time.perf_counter()
     one(0, sl_threads)
     slice_mt = per * W * H / (time.perf_counter() - t0) / 1e6
-    ths = [threading.Thread(target=one, args=(g, inner)) for g in range(workers)]
+    ths = [threading.Thread(target=one, args=(g, inner[g])) for g in range(workers)]
     t0 = time.perf_counter()
     for t in ths:
         t.start()
@@ -157,8 +159,9 @@ def cpu_baseline(frames, threads):
         t.join()
     multi = workers * per * W * H / (time.perf_counter() - t0) / 1e6
     return {
-        "value": round(multi, 3), "unit": "Mpixels/s", "cores": workers * inner, "kind": "port",
-        "sample": f"{workers} GOP workers x {inner} slice thread(s), 1 GOP ({per} frames) each of the same "
+        "value": round(multi, 3), "unit": "Mpixels/s", "cores": sum(inner), "kind": "port",
+        "sample": f"{workers} GOP workers with {'/'.join(map(str, sorted(set(inner), reverse=True)))} slice "
+                  f"thread(s) each ({sum(inner)} in all), 1 GOP ({per} frames) each of the same "
                   f"{W}x{H} {PIX_FMT} clip, oracle/ffv1_oracle.c, GOP-sharded",
         "host_cpus": os.cpu_count(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
         "slice_threaded": {"value": round(slice_mt, 3), "cores": sl_threads,
