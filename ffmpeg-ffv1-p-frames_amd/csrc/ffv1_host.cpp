@@ -139,7 +139,7 @@ struct Knobs {
 static const char* const kKnobNames[] = {"serial",     "walkdbg",    "walktrace", "hostdbg",   "walk_prio",
                                          "range_prio", "dseg_prio",  "sym_grid",  "bits_grid", "dseg_grid",
                                          "walk_split", "copy_threads", "dec_swap", "coder",    "dense", "walk_blocks",
-                                         "recsets",    "slice_cap",  "walk_part_a", "force_multi", "bounds_shrink", "one_coder"};
+                                         "recsets",    "slice_cap",  "walk_part_a", "force_multi", "bounds_shrink"};
 
 static int parse_knobs(Knobs* k) {
   k->kv.clear();
@@ -448,19 +448,17 @@ struct ffv1hip_ctx {
   int* d_wmap = nullptr;              // 3 x [64-segment group]
   int64_t max_groups = 0;             // 64-segment groups a batch can have
   int64_t max_segs = 0;               // segments a batch can have
-  uint2* d_ck = nullptr;      // [2 sets][segment]: range of batch k+1 writes one while dseg of batch k reads the other
+  uint2* d_ck = nullptr;
   uint2* d_segrec = nullptr;
   int64_t dcap[2] = {0, 0};      // decisions d_pre/d_bits hold
   int buf = 0;                   // buffer set of the next batch
-  hipStream_t code_stream = nullptr;  // ffv1_dseg .. assembly, behind the range pass
-  hipStream_t range_stream = nullptr;  // ffv1_range, behind the states walk
+  hipStream_t code_stream = nullptr;  // ffv1_range .. assembly, behind the states walk
   hipEvent_t walked[2] = {nullptr, nullptr};
   hipStream_t bits_stream = nullptr;  // ffv1_bits, beside the states walk
   hipEvent_t laid[2] = {nullptr, nullptr};    // set k's stream layout and zeroed bits are ready
   hipEvent_t bitsed[2] = {nullptr, nullptr};  // set k's decision bits are in place
   hipEvent_t coded[2] = {nullptr, nullptr};  // the coder of the batch that last used set k is done
   hipEvent_t pre_read[2] = {nullptr, nullptr};  // ... has read its decision stream (range, dseg): set k is free
-  hipEvent_t ranged[2] = {nullptr, nullptr};    // the range pass of the batch using set k is done
   int tri = 0;                                // metadata set of the next batch
   hipEvent_t coded3[3] = {nullptr, nullptr, nullptr};  // the coder of the batch that last used metadata set k
   // Split schedule (a second set of walk records and chunk bits, when HBM
@@ -1027,7 +1025,6 @@ static void free_device(ffv1hip_ctx* c) {
   if (c->done_ev) (void)hipEventDestroy(c->done_ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->code_stream) (void)hipStreamDestroy(c->code_stream);
-  if (c->range_stream) (void)hipStreamDestroy(c->range_stream);
   if (c->bits_stream) (void)hipStreamDestroy(c->bits_stream);
   for (hipEvent_t& e : c->walked)
     if (e) (void)hipEventDestroy(e);
@@ -1038,8 +1035,6 @@ static void free_device(ffv1hip_ctx* c) {
   for (hipEvent_t& e : c->coded)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t& e : c->pre_read)
-    if (e) (void)hipEventDestroy(e);
-  for (hipEvent_t& e : c->ranged)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t& e : c->coded3)
     if (e) (void)hipEventDestroy(e);
@@ -1096,7 +1091,7 @@ static int64_t device_bytes(const ffv1hip_ctx* c, int64_t nb) {
       segs += n;
       groups += (n + 63) / 64;
     }
-    b += nb * (4 * 8 * segs + 3 * 4 * groups);  // checkpoints and segment records (two sets), group maps
+    b += nb * (2 * 8 * segs + 3 * 4 * groups);  // checkpoints, segment records, group maps
   } else {
     const int64_t slots = c->max_slots;
     b += slots * (4 * c->frame_samples + int64_t(c->pcount) * c->contexts * 32 * c->nslices);
@@ -1193,14 +1188,12 @@ static int alloc_device(ffv1hip_ctx* c) {
       HIP_TRY(hipMemcpy(c->d_ident, ident.data(), sizeof(int) * size_t(nb), hipMemcpyHostToDevice));
     }
     HIP_TRY(hipStreamCreateWithFlags(&c->code_stream, hipStreamNonBlocking));
-    HIP_TRY(hipStreamCreateWithFlags(&c->range_stream, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&c->bits_stream, hipStreamNonBlocking));
     for (hipEvent_t& e : c->laid) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->bitsed) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->walked) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->coded) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->pre_read) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    for (hipEvent_t& e : c->ranged) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_TRY(hipMalloc(&c->d_scratch, 4096));
     if (kBoundsCheck) {
       HIP_TRY(hipMalloc(&c->d_bounds, sizeof(uint32_t)));
@@ -1219,8 +1212,8 @@ static int alloc_device(ffv1hip_ctx* c) {
     HIP_TRY(hipMalloc(&c->d_segs_info, 3 * sizeof(StreamSegs) * size_t(nb) * c->nslices));
     HIP_TRY(hipMalloc(&c->d_seg_totals, 3 * 2 * sizeof(int)));
     HIP_TRY(hipMalloc(&c->d_wmap, 3 * sizeof(int) * size_t(c->max_groups)));
-    HIP_TRY(hipMalloc(&c->d_ck, 2 * sizeof(uint2) * size_t(c->max_segs)));
-    HIP_TRY(hipMalloc(&c->d_segrec, 2 * sizeof(uint2) * size_t(c->max_segs)));
+    HIP_TRY(hipMalloc(&c->d_ck, sizeof(uint2) * size_t(c->max_segs)));
+    HIP_TRY(hipMalloc(&c->d_segrec, sizeof(uint2) * size_t(c->max_segs)));
     if (upload_hdr(c) < 0) return -5;
     const int64_t cap = decision_cap(c, nb);
     for (int k = 0; k < 2; k++)
@@ -1873,17 +1866,15 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
                      "shader clock %.0f MHz, %.1f ns/step\n", g, g ? nblk - nlong : nlong, all[g] / (g ? nblk - nlong : nlong), loop[g] / all[g],
                      loop[g] / steps[g], all[g] / (rt[g] / 100.0), loop[g] / steps[g] / (all[g] / (rt[g] / 100.0)) * 1e3);
     }
-    // the range stream continues once this batch's walk is done; the walk of
-    // the next batch (on st) then overlaps this batch's coding.  The range
-    // pass (a serial chain per stream, ~64 ms alone at c3) has a stream of
-    // its own, so that it runs beside the previous batch's dseg .. assembly
-    // on the coder stream: the coder's kernels then take two of the walk's
-    // periods instead of one (the one_coder hook: both on one stream)
-    hipStream_t const rst = cst != st && !c->knobs.has("one_coder") ? c->range_stream : cst;
+    // the coder stream continues once this batch's walk is done; the walk of
+    // the next batch (on st) then overlaps this batch's coding.  (Measured:
+    // the range pass on a stream of its own, beside the previous batch's
+    // dseg .. assembly, 11.0 Gpix/s against 17.6: with GPU_MAX_HW_QUEUES = 4
+    // a fifth stream shares a hardware queue and serialises; 15.9 with 8.)
     HIP_TRY(hipEventRecord(c->walked[fb], st));
-    HIP_TRY(hipStreamWaitEvent(rst, c->walked[fb], 0));
-    HIP_TRY(hipStreamWaitEvent(rst, c->bitsed[fb], 0));
-    if (c->pass == 1 && launch_stats(sta, true, rst) < 0) return set_err(-5, "stats launch failed");
+    HIP_TRY(hipStreamWaitEvent(cst, c->walked[fb], 0));
+    HIP_TRY(hipStreamWaitEvent(cst, c->bitsed[fb], 0));
+    if (c->pass == 1 && launch_stats(sta, true, cst) < 0) return set_err(-5, "stats launch failed");
     ca.nframes = n;
     ca.ds = ds;
     ca.hdr = c->d_hdr;
@@ -1891,21 +1882,17 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     ca.segs_info = d_segs;
     ca.seg_totals = d_segtot;
     ca.wmap = d_wmap;
-    ca.ck = c->d_ck + size_t(fb) * c->max_segs;  // (set fb: dseg of batch k-1 may still read the other)
-    ca.segrec = c->d_segrec + size_t(fb) * c->max_segs;
+    ca.ck = c->d_ck;
+    ca.segrec = c->d_segrec;
     ca.digit_cap = c->slice_stride / 4;
     ca.dseg_blocks = int(std::min<int64_t>(c->max_groups, c->grid_dseg));
     ca.range_prio = range_prio;
     ca.dseg_prio = c->prio_dseg;
-    HIP_TRY(hipMemsetAsync(ca.status, 0, sizeof(int) * 4, rst));
+    HIP_TRY(hipMemsetAsync(ca.status, 0, sizeof(int) * 4, cst));
     // range alone (the serial chain), every segment from its checkpoint,
     // the segments joined, then the bytes
-    if (timed(1, rst, [&] { return launch_range(ca, rst); }) < 0)
+    if (timed(1, cst, [&] { return launch_range(ca, cst); }) < 0)
       return set_err(-5, "range launch failed: %s", hipGetErrorString(hipGetLastError()));
-    if (rst != cst) {
-      HIP_TRY(hipEventRecord(c->ranged[fb], rst));
-      HIP_TRY(hipStreamWaitEvent(cst, c->ranged[fb], 0));
-    }
     if (timed(7, cst, [&] { return launch_dseg(ca, cst); }) < 0)
       return set_err(-5, "dseg launch failed: %s", hipGetErrorString(hipGetLastError()));
     HIP_TRY(hipEventRecord(c->pre_read[fb], cst));
@@ -2127,7 +2114,6 @@ int ffv1hip_synchronize(ffv1hip_ctx* c) {
   HIP_TRY(hipSetDevice(c->device));
   if (c->dep_valid) HIP_TRY(hipEventSynchronize(c->done_ev));  // also a caller-given launch stream
   HIP_TRY(hipStreamSynchronize(c->stream));
-  if (c->range_stream) HIP_TRY(hipStreamSynchronize(c->range_stream));
   if (c->code_stream) HIP_TRY(hipStreamSynchronize(c->code_stream));
   if (c->bits_stream) HIP_TRY(hipStreamSynchronize(c->bits_stream));
   return settle_batch(c, c->nsub - 1);
