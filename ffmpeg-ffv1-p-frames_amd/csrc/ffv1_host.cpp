@@ -565,13 +565,6 @@ struct ffv1hip_ctx {
     std::unique_ptr<CopyPool> pool;
     std::unique_ptr<CopyPool> pool_out;  // the copy-out thread's: packets into the caller's buffer
     hipStream_t xfer = nullptr;
-    // a second transfer stream for the copies straight from caller-pinned
-    // memory: planes alternate between the two, so that two DMA engines
-    // run at once (one moves ~26 GB/s); joined into xfer before a launch
-    hipStream_t xfer2 = nullptr;
-    hipEvent_t xfer2_ev = nullptr;
-    bool xfer2_used = false;
-    unsigned rr = 0;
     hipStream_t d2h = nullptr;  // ffv1hip_encode: packets out beside the next batch's frames in
     static constexpr int kSlots = 6;
     int64_t slot_bytes = 0;
@@ -2204,8 +2197,6 @@ static int pipe_open_parts(ffv1hip_ctx* c) {
                    double(fset) / 1e9);
   }
   HIP_TRY(hipStreamCreateWithFlags(&P.xfer, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&P.xfer2, hipStreamNonBlocking));
-  HIP_TRY(hipEventCreateWithFlags(&P.xfer2_ev, hipEventDisableTiming));
   HIP_TRY(hipStreamCreateWithFlags(&P.d2h, hipStreamNonBlocking));
   int nt = int(std::thread::hardware_concurrency());
   if (const char* e = std::getenv("OMP_NUM_THREADS"))  // the host's CPU share where it is set
@@ -2270,7 +2261,6 @@ static int pipe_open(ffv1hip_ctx* c) {
 static void pipe_close(ffv1hip_ctx* c) {
   ffv1hip_ctx::HostPipe& P = c->pipe;
   if (P.xfer) (void)hipStreamSynchronize(P.xfer);
-  if (P.xfer2) (void)hipStreamSynchronize(P.xfer2);
   P.pool.reset();
   P.pool_out.reset();
   for (int k = 0; k < ffv1hip_ctx::HostPipe::kSlots; k++) {
@@ -2285,8 +2275,6 @@ static void pipe_close(ffv1hip_ctx* c) {
   for (uint8_t* d : P.d_compact)
     if (d) (void)hipFree(d);
   if (P.xfer) (void)hipStreamDestroy(P.xfer);
-  if (P.xfer2) (void)hipStreamDestroy(P.xfer2);
-  if (P.xfer2_ev) (void)hipEventDestroy(P.xfer2_ev);
   if (P.d2h) (void)hipStreamDestroy(P.d2h);
   for (void* q : {(void*)c->d_frames2, (void*)c->d_packets2, (void*)c->d_packet_size2})
     if (q) (void)hipFree(q);
@@ -2333,13 +2321,11 @@ static int stage_rows(ffv1hip_ctx* c, uint8_t* dst, const uint8_t* src, int64_t 
   ffv1hip_ctx::HostPipe& P = c->pipe;
   if (rows > 0 && host_registered(c, src, (rows - 1) * sp + wb)) {  // caller-pinned: one DMA from it
     const double t0 = P.dbg ? wall_s() : 0;
-    const bool second = (P.rr++ & 1) != 0;
-    hipStream_t const xs = second ? P.xfer2 : P.xfer;
-    P.xfer2_used |= second;
     if (sp == wb)
-      HIP_TRY(hipMemcpyAsync(dst, src, size_t(rows * wb), hipMemcpyHostToDevice, xs));
+      HIP_TRY(hipMemcpyAsync(dst, src, size_t(rows * wb), hipMemcpyHostToDevice, P.xfer));
     else
-      HIP_TRY(hipMemcpy2DAsync(dst, size_t(wb), src, size_t(sp), size_t(wb), size_t(rows), hipMemcpyHostToDevice, xs));
+      HIP_TRY(hipMemcpy2DAsync(dst, size_t(wb), src, size_t(sp), size_t(wb), size_t(rows), hipMemcpyHostToDevice,
+                               P.xfer));
     if (P.dbg) P.t_dma += wall_s() - t0;
     c->direct_pending = true;
     return 0;
@@ -2387,21 +2373,9 @@ static int stage_frame(ffv1hip_ctx* c, int set, int64_t slot, const void* const*
 }
 
 // Batch `set`'s queued frames (staged) as one batch.
-// The second transfer stream's copies so far, ordered before what comes
-// next on the first (the batch launch, a wait on the frame's copies).
-static int join_xfer2(ffv1hip_ctx* c) {
-  ffv1hip_ctx::HostPipe& P = c->pipe;
-  if (!P.xfer2_used) return 0;
-  HIP_TRY(hipEventRecord(P.xfer2_ev, P.xfer2));
-  HIP_TRY(hipStreamWaitEvent(P.xfer, P.xfer2_ev, 0));
-  P.xfer2_used = false;
-  return 0;
-}
-
 static int launch_staged(ffv1hip_ctx* c, int set, int n) {
   int rc = stage_flush(c);
   if (rc < 0) return rc;
-  if ((rc = join_xfer2(c)) < 0) return rc;
   int64_t off[kMaxPlanes];
   int pst[kMaxPlanes], rows[kMaxPlanes], np;
   slot_layout(c, off, pst, rows, &np);
@@ -2657,7 +2631,6 @@ int ffv1hip_encode2(ffv1hip_ctx* c, const void* const planes[4], const int strid
     if ((rc = stage_frame(c, c->q_set, int64_t(c->q_pts.size()), planes, strides)) < 0) return rc;
     if (c->direct_pending) {  // straight from the caller's pinned memory: done before the call returns
       if (!c->direct_ev) HIP_TRY(hipEventCreateWithFlags(&c->direct_ev, hipEventDisableTiming));
-      if ((rc = join_xfer2(c)) < 0) return rc;
       HIP_TRY(hipEventRecord(c->direct_ev, c->pipe.xfer));
       HIP_TRY(hipEventSynchronize(c->direct_ev));
       c->direct_pending = false;
@@ -2739,7 +2712,6 @@ int ffv1hip_host_unregister(ffv1hip_ctx* c, void* ptr) {
   if (it == c->host_ranges.end()) return set_err(-22, "no range registered at %p", ptr);
   HIP_TRY(hipSetDevice(c->device));
   if (c->pipe.xfer) HIP_TRY(hipStreamSynchronize(c->pipe.xfer));  // no copy from it is in flight
-  if (c->pipe.xfer2) HIP_TRY(hipStreamSynchronize(c->pipe.xfer2));
   if (it->second.owned) HIP_TRY(hipHostUnregister(ptr));
   c->host_ranges.erase(it);
   return 0;

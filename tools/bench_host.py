@@ -22,12 +22,6 @@ import os
 import sys
 import time
 
-# the host-frame path runs five streams of the context besides the caller's
-# (walk, symbols, coder, two transfer streams, packets out): with the HIP
-# runtime's default of 4 hardware queues two of them would share one and
-# serialise (the host-frame path); set before HIP starts
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
-
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
