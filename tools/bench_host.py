@@ -22,6 +22,14 @@ import os
 import sys
 import time
 
+# the host-frame path runs four streams of the context besides the caller's
+# (walk, symbols, coder, transfer, packets out: five): with the HIP
+# runtime's default of 4 hardware queues two of them share one and
+# serialise (encode2 batch 48: 2,823 vs 3,097 Mpix/s with 8); set before HIP
+# starts.  (A second transfer stream measured no faster: the H2D DMA moves
+# ~26 GB/s either way.)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
