@@ -956,13 +956,14 @@ static void dump_walk_trace(ffv1hip_ctx* c) {
   const std::string path = c->knobs.str("walktrace");
   if (!path.empty()) {
     if (FILE* fp = std::fopen(path.c_str(), "w")) {
-      std::fprintf(fp, "batch,item,start,end,hw_id,xcc_id\n");
+      std::fprintf(fp, "batch,item,start,end,hw_id,xcc_id,loop_cycles,steps,wave_cycles\n");
       for (int b = 0; b < c->trace_n; b++)
         for (int i = 0; i < c->trace_items; i++) {
           const uint64_t* w = t.data() + size_t(kTraceWords) * (size_t(c->trace_items) * b + i);
           if (w[0])
-            std::fprintf(fp, "%d,%d,%llu,%llu,%llu,%llu\n", b, i, (unsigned long long)w[0], (unsigned long long)w[1],
-                         (unsigned long long)w[2], (unsigned long long)w[3]);
+            std::fprintf(fp, "%d,%d,%llu,%llu,%llu,%llu,%llu,%llu,%llu\n", b, i, (unsigned long long)w[0],
+                         (unsigned long long)w[1], (unsigned long long)w[2], (unsigned long long)w[3],
+                         (unsigned long long)w[4], (unsigned long long)w[5], (unsigned long long)w[6]);
         }
       std::fclose(fp);
     }

@@ -295,7 +295,8 @@ struct WalkArgs {
   DecisionStream ds;
   uint8_t* scratch;           // >= 2 KiB: where idle chains write their stage
   uint64_t* dbg;              // optional [block][4] cycle counters (FFV1HIP_WALKDBG)
-  uint64_t* trace;            // optional [item][kTraceWords]: start / end s_memrealtime, HW_ID, XCC_ID of each wave
+  uint64_t* trace;            // optional [item][kTraceWords]: start / end s_memrealtime, HW_ID, XCC_ID, step-loop
+                              // cycles, steps, the wave's cycles
   int force_multi;            // measurement hook: every chunk on the checked (multi) step
   const uint8_t* init;        // 2-pass initial states [contexts][32] at keyframes, or null (all 128)
   int nitems, item0;          // set by launch_walk: all items of the batch, the launch's first
@@ -309,7 +310,7 @@ struct WalkArgs {
   Bounds bnd;                 // debug build: the extents of the writes
 };
 
-constexpr int kTraceWords = 4;
+constexpr int kTraceWords = 8;
 
 // Above 8 bits the quantisers of context model 0 have 9 levels (ffv1enc.c:
 // 846-879, quant9_10bit), so only 365 of the 666 contexts q0 + 11 q1 + 121 q2

@@ -1721,7 +1721,7 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
   // the coder's range pass is the longer chain and runs above it)
   set_prio(a.prio);
   uint64_t t_loop = 0, n_steps = 0;
-  const uint64_t t_all = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+  const uint64_t t_all = a.dbg || a.trace ? __builtin_amdgcn_s_memtime() : 0;
   const uint64_t rt_all = a.dbg || a.trace ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz: the wave's shader clock
   for (int seg_i = seg_begin; seg_i < seg_end && seg_i < a.nsegs; seg_i++) {
   const Segment seg = a.segs[seg_i];
@@ -1845,7 +1845,7 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
         uint32_t l0 = tbl[d0.addr], l1 = tbl[d1.addr];
         uint32_t e1 = 0u, e2 = 0u, st = 0u;
         int addr_prev = (int)((stage + kPreData + k) - tbl);  // no T-1 yet: the dummy byte
-        const uint64_t t0 = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+        const uint64_t t0 = a.dbg || a.trace ? __builtin_amdgcn_s_memtime() : 0;
         if (!mul) {
           static_for<0, kChunk>([&](auto tc) {
             constexpr int T = decltype(tc)::value;
@@ -1873,6 +1873,9 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
         tbl[addr_prev] = (uint8_t)e1;  // the chunk's last symbol
         if (a.dbg) {
           __builtin_amdgcn_s_waitcnt(0);
+          t_loop += __builtin_amdgcn_s_memtime() - t0;
+          n_steps += kChunk;
+        } else if (a.trace) {  // the step loop's issue time (no wait: the schedule is not disturbed)
           t_loop += __builtin_amdgcn_s_memtime() - t0;
           n_steps += kChunk;
         }
@@ -1911,6 +1914,9 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
     a.trace[item * kTraceWords + 1] = __builtin_amdgcn_s_memrealtime();
     a.trace[item * kTraceWords + 2] = __builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_REG_HW_ID
     a.trace[item * kTraceWords + 3] = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
+    a.trace[item * kTraceWords + 4] = t_loop;                                        // step loops, shader cycles
+    a.trace[item * kTraceWords + 5] = n_steps;
+    a.trace[item * kTraceWords + 6] = __builtin_amdgcn_s_memtime() - t_all;          // the wave, shader cycles
   }
   if (a.dbg && lane == 0) {
     a.dbg[item * 4 + 0] = __builtin_amdgcn_s_memtime() - t_all;
