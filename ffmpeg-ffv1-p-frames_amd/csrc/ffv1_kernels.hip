@@ -307,9 +307,17 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
         const uint64_t mm = __ballot(valid && (diff >= 1024 || diff <= -1024) && diff < 4096 && diff > -4096);
         if (lane == 0) cs[0] = (uint32_t)total | (lng ? kChunkLong : 0u) | (mm ? kChunkMulti : 0u);
         if (lane < 2) cs[kChunkWords - 2 + lane] = (uint32_t)(mm >> (32 * lane));
+        // out: the header, the words the decisions fill and the two after
+        // them (ffv1_bits reads a chunk's words up to the one its last
+        // decision lands in at its stream offset, which may be one more),
+        // and the mask words; the rest of the 70 stay unwritten (zero words:
+        // ~3 of every 4 written before, 10 GB a c3 step)
         uint32_t* const dst = cbase + ((base + wv * kWave) / kWave) * kChunkWords;
-        dst[lane] = cs[lane];
-        if (lane < kChunkWords - kWave) dst[kWave + lane] = cs[kWave + lane];
+        const int last = min(kChunkWords - 3, (total >> 5) + 2);
+        if (lane <= last) dst[lane] = cs[lane];
+        if (kWave + lane <= last || kWave + lane >= kChunkWords - 2) {
+          if (lane < kChunkWords - kWave) dst[kWave + lane] = cs[kWave + lane];
+        }
       }
     } else if (valid) {
       out[RGB ? ((int64_t)y * a.nplanes + p) * pw + x : idx] = ((uint32_t)(row0 + ctx) << 16) | (uint16_t)diff;
