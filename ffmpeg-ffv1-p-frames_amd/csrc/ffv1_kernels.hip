@@ -1497,12 +1497,21 @@ struct StepIn {
   bool same2;     // same row as the previous symbol or the one two back (same decides first)
 };
 
+template <bool MULTI = false>
 __device__ __forceinline__ StepIn derive(const uint4& r, const WalkLane& W, int kc) {
   StepIn d;
-  d.code = __builtin_amdgcn_ubfe((r.y & W.mlo) | (r.z & ~W.mlo), W.csh, 2);  // bitwise: a select
-                                                                              // of members would go to scratch
+  const uint32_t sel = (r.y & W.mlo) | (r.z & ~W.mlo);  // bitwise: a select of members would go to scratch
+  d.code = __builtin_amdgcn_ubfe(sel, W.csh, 2);
   const int pos = (int)__builtin_amdgcn_ubfe(r.w, W.hsh, 12) + kc;
-  d.pos = d.code == 2u ? W.dummy : pos;
+  if constexpr (MULTI) {
+    d.pos = d.code == 2u ? W.dummy : pos;
+  } else {
+    // codes 0..2 only: bit 1 of the code, sign-extended, is the "no
+    // decision" mask, and a bitwise insert takes the dummy byte (no compare,
+    // so no VCC write and the wait states a select of it would need)
+    const int nd = __builtin_amdgcn_sbfe((int)sel, W.csh + 1, 1);
+    d.pos = (nd & W.dummy) | (~nd & pos);
+  }
   d.addr = (int)(r.x & 0xFFFFu) + W.kk;
   d.same = (int)r.w < 0;  // kRecSame
   d.same2 = r.w >= kRecSame2;  // bit 31 or 30: one compare, no mask (same wins in walk_step)
@@ -1513,7 +1522,7 @@ __device__ __forceinline__ StepIn derive(const uint4& r, const WalkLane& W, int 
 // becomes the slot's composed N row, kept in the record (ffv1_symbols), so
 // the state chain stays one lookup per symbol.
 __device__ __forceinline__ StepIn derive_m(const uint4& r, const WalkLane& W, int kc) {
-  StepIn d = derive(r, W, kc);
+  StepIn d = derive<true>(r, W, kc);
   const uint32_t rowm = __builtin_amdgcn_ubfe(r.w, W.msh, W.mwd) + W.mbase;
   d.code = d.code == 3u ? rowm : d.code;
   return d;
