@@ -1157,13 +1157,15 @@ __device__ __forceinline__ void put_dec(int& low, int& range, DigitOut& o, int s
   const int d = range - r1;
   low += d & m;
   const int nr = (m & r1) | (~m & d);  // m ? r1 : d, one bitwise select
-  // all ones when a byte shifts out: nr < 0x100 (24+ leading zeros, see range32)
-  const int sm = __builtin_amdgcn_sbfe((int)__builtin_clz((unsigned)nr), 3, 1);
-  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)low, o.rs, o.kb | (~sm & (int)0x80000000), 0, 0);
-  o.kb += sm & 4;
-  const int shifted = (int)__builtin_amdgcn_perm(0u, (uint32_t)low, 0x0c0c000cu);  // (low & 0xFF) << 8
-  low = (sm & shifted) | (~sm & low);
-  range = nr << (sm & 8);
+  // a byte shifts out (nr < 0x100): one compare, whose VCC the selects
+  // below read.  (A mask from the leading-zero count, as in range32, made
+  // the compiler rebuild the same VCC for the low select and cost three
+  // more VALU per decision: 17 vs 14.)
+  const bool sh = nr < 0x100;
+  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)low, o.rs, sh ? o.kb : (int)0x80000000, 0, 0);
+  o.kb += sh ? 4 : 0;
+  low = sh ? (int)__builtin_amdgcn_perm(0u, (uint32_t)low, 0x0c0c000cu) : low;  // (low & 0xFF) << 8
+  range = sh ? nr << 8 : nr;
 }
 
 __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
