@@ -1715,10 +1715,15 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     if (need > c->dcap[fb]) {
       HIP_TRY(hipMemcpyAsync(c->h_dtotal + t3, c->d_dtotal + t3, sizeof(int64_t), hipMemcpyDeviceToHost, sst));
       HIP_TRY(hipStreamSynchronize(sst));
-      HIP_TRY(hipEventSynchronize(c->coded[fb]));  // set fb's previous coder is done
       need = c->h_dtotal[t3];
-      if (need > c->dcap[fb] && grow_decisions(c, fb, need + need / 8) < 0)
-        return set_err(-12, "decision buffers for %lld decisions: %s", (long long)need, g_err);
+      if (need > c->dcap[fb]) {
+        // set fb's previous coder must be done before its buffers go (only
+        // then: waiting for it on every batch held this batch's walk behind
+        // the previous batch's packet assembly)
+        HIP_TRY(hipEventSynchronize(c->coded[fb]));
+        if (grow_decisions(c, fb, need + need / 8) < 0)
+          return set_err(-12, "decision buffers for %lld decisions: %s", (long long)need, g_err);
+      }
     }
     HIP_TRY(hipEventRecord(c->laid[fb], sst));  // the records and the stream layout: the walk may start
     if (sst != st) HIP_TRY(hipStreamWaitEvent(sst, c->pre_read[fb], 0));  // d_bits[fb]: range / dseg of batch k-2
