@@ -139,7 +139,7 @@ struct Knobs {
 static const char* const kKnobNames[] = {"serial",     "walkdbg",    "walktrace", "hostdbg",   "walk_prio",
                                          "range_prio", "dseg_prio",  "sym_grid",  "bits_grid", "dseg_grid",
                                          "walk_split", "copy_threads", "dec_swap", "coder",    "dense", "walk_blocks",
-                                         "recsets",    "slice_cap",  "walk_part_a", "force_multi", "bounds_shrink"};
+                                         "recsets",    "slice_cap",  "walk_part_a", "force_multi", "bounds_shrink", "range_split"};
 
 static int parse_knobs(Knobs* k) {
   k->kv.clear();
@@ -450,6 +450,7 @@ struct ffv1hip_ctx {
   int64_t max_segs = 0;               // segments a batch can have
   uint2* d_ck = nullptr;
   uint2* d_segrec = nullptr;
+  int2* d_rstate = nullptr;  // [stream] the range pass's {range, shifts} at the luma / chroma boundary
   int64_t dcap[2] = {0, 0};      // decisions d_pre/d_bits hold
   int buf = 0;                   // buffer set of the next batch
   hipStream_t code_stream = nullptr;  // ffv1_range .. assembly, behind the states walk
@@ -1012,7 +1013,7 @@ static void free_device(ffv1hip_ctx* c) {
                   c->d_persist[1], c->d_tables, c->d_sym, c->d_keys2, c->d_cbits, c->d_dcount, c->d_dbase, c->d_dtotal, c->d_pre[0],
                   c->d_pre[1], c->d_bits[0], c->d_bits[1], c->d_scratch, c->d_hdr, c->d_hdr_digits, c->d_geom, c->d_slot_frames, c->d_status,
                   c->d_rec2, c->d_cbits2, c->d_ident, c->d_segs_info, c->d_seg_totals, c->d_wmap, c->d_ck,
-                  c->d_segrec, c->d_rct, c->d_bounds};
+                  c->d_segrec, c->d_rct, c->d_bounds, c->d_rstate};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_dtotal) (void)hipHostFree(c->h_dtotal);
@@ -1215,6 +1216,7 @@ static int alloc_device(ffv1hip_ctx* c) {
     HIP_TRY(hipMalloc(&c->d_wmap, 3 * sizeof(int) * size_t(c->max_groups)));
     HIP_TRY(hipMalloc(&c->d_ck, sizeof(uint2) * size_t(c->max_segs)));
     HIP_TRY(hipMalloc(&c->d_segrec, sizeof(uint2) * size_t(c->max_segs)));
+    HIP_TRY(hipMalloc(&c->d_rstate, sizeof(int2) * size_t(nb) * c->nslices));
     if (upload_hdr(c) < 0) return -5;
     const int64_t cap = decision_cap(c, nb);
     for (int k = 0; k < 2; k++)
@@ -1896,9 +1898,23 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     ca.dseg_prio = c->prio_dseg;
     HIP_TRY(hipMemsetAsync(ca.status, 0, sizeof(int) * 4, cst));
     // range alone (the serial chain), every segment from its checkpoint,
-    // the segments joined, then the bytes
+    // the segments joined, then the bytes.  Split at the luma / chroma
+    // boundary (the range_split=0 hook: not), the luma segments' dseg runs
+    // beside the chroma chains' range pass in one launch, so the coder
+    // stream is range(luma) + max(range(chroma), dseg(luma)) + dseg(chroma)
+    // instead of range + dseg.  (Timing: the fused launch counts as dseg.)
+    ca.rstate = c->d_rstate;
+    const bool rsplit = c->knobs.get("range_split", 1) != 0;
+    ca.range_pass = rsplit ? 1 : 0;
+    ca.dseg_part = -1;
     if (timed(1, cst, [&] { return launch_range(ca, cst); }) < 0)
       return set_err(-5, "range launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (rsplit) {
+      ca.range_pass = 2;
+      if (timed(7, cst, [&] { return launch_range_dseg(ca, cst); }) < 0)
+        return set_err(-5, "range / dseg launch failed: %s", hipGetErrorString(hipGetLastError()));
+      ca.dseg_part = 1;
+    }
     if (timed(7, cst, [&] { return launch_dseg(ca, cst); }) < 0)
       return set_err(-5, "dseg launch failed: %s", hipGetErrorString(hipGetLastError()));
     HIP_TRY(hipEventRecord(c->pre_read[fb], cst));

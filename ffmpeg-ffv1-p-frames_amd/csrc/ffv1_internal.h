@@ -258,6 +258,11 @@ struct CodeArgs {
   int dseg_blocks;            // ffv1_dseg grid
   int range_prio, dseg_prio;  // wave priorities (s_setprio) of ffv1_range / ffv1_dseg beside the walk (2)
   Bounds bnd;                 // debug build: the extents of the writes
+  // the range pass split at the luma / chroma boundary (launch_range_dseg)
+  int2* rstate;               // [stream] {range, shifts} after the luma chain
+  int range_pass;             // 0 whole streams, 1 the luma chains, 2 the chroma chains
+  int dseg_part;              // ffv1_dseg: -1 every segment, 0 the luma chains', 1 the chroma chains'
+  int range_blocks;           // set by launch_range_dseg
 };
 
 // Pass-1 statistics (ffv1enc.c:190-199): rc_stat[state][bit] from the
@@ -427,6 +432,7 @@ int walk_per_short(const SliceGeom& g);
 int walk_resident(const WalkArgs& a);  // (uses a.rows)
 int launch_range(const CodeArgs& a, void* stream);
 int launch_dseg(const CodeArgs& a, void* stream);
+int launch_range_dseg(const CodeArgs& a, void* stream);
 int launch_dfix(const CodeArgs& a, void* stream);
 int launch_sink(const CodeArgs& a, void* stream);
 int launch_bits(const BitsArgs& a, void* stream);

@@ -1076,17 +1076,25 @@ __device__ __forceinline__ void set_prio(int p) {
   }
 }
 
-__global__ __launch_bounds__(kRangeThreads) void ffv1_range(CodeArgs a) {
-  set_prio(a.range_prio);
-  const StreamRef sr = stream_of(a, (int64_t)blockIdx.x * kRangeThreads + threadIdx.x);
+// The range pass over stream lane c: the luma chain's decisions, then the
+// chroma chain's at their own start.  pass 0: both; 1: the luma chain, its
+// final {range, shifts} kept in rstate; 2: the chroma chain from there (the
+// coder's dseg of the luma segments runs beside it, ffv1_range_dseg).
+__device__ __forceinline__ void range_pass(const CodeArgs& a, int64_t c, int pass) {
+  const StreamRef sr = stream_of(a, c);
   const int key = sr.live ? a.keyflags[sr.f] : 0;
   const HdrState h = a.hdr[key * a.nslices + sr.slice];
   const int* dc = a.ds.dcount + sr.st * 3;
   const int64_t base = sr.live ? a.ds.dbase[sr.st] : 0;  // a multiple of kStreamAlign
-  uint2* ck = a.ck + (sr.live ? a.segs_info[sr.st].seg_base : 0);
+  const StreamSegs ss = sr.live ? a.segs_info[sr.st] : StreamSegs{0, 0, 0, 0};
+  uint2* ck = a.ck + ss.seg_base + (pass == 2 ? ss.s_luma : 0);
   int range = h.range, shifts = h.ndig << 3;  // renormalisation shifts x 8
-  // the luma chain's decisions, then the chroma chain's at their own start
-  for (int part = 0; part < 2; part++) {
+  if (pass == 2 && sr.live) {
+    const int2 r = a.rstate[sr.st];
+    range = r.x;
+    shifts = r.y;
+  }
+  for (int part = pass == 2 ? 1 : 0; part < (pass == 1 ? 1 : 2); part++) {
     const int n = sr.live ? (part ? dc[1] + dc[2] : dc[0]) : 0;
     const int64_t pb = base + (part && sr.live ? chroma_start(dc[0]) : 0);  // multiple of 64
     const uint4* P = reinterpret_cast<const uint4*>(a.ds.pre + pb);
@@ -1128,6 +1136,12 @@ __global__ __launch_bounds__(kRangeThreads) void ffv1_range(CodeArgs a) {
       range32(range, shifts, wa, wb, bw);
     }
   }
+  if (pass == 1 && sr.live) a.rstate[sr.st] = make_int2(range, shifts);
+}
+
+__global__ __launch_bounds__(kRangeThreads) void ffv1_range(CodeArgs a) {
+  set_prio(a.range_prio);
+  range_pass(a, (int64_t)blockIdx.x * kRangeThreads + threadIdx.x, a.range_pass);
 }
 
 // ffv1_dseg: one wave per 64 consecutive segments of a stream, one lane per
@@ -1168,17 +1182,19 @@ __device__ __forceinline__ void put_dec(int& low, int& range, DigitOut& o, int s
   range = sh ? nr << 8 : nr;
 }
 
-__global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
-  set_prio(a.dseg_prio);
+// The segments of waves vb, vb + vgrid, ... (part: -1 all, 0 the luma
+// chain's, 1 the chroma chain's; the other lanes idle).
+__device__ __forceinline__ void dseg_body(const CodeArgs& a, int vb, int vgrid, int only_part) {
   const int lane = threadIdx.x;
   const int ngroups = a.seg_totals[1];
-  for (int w = blockIdx.x; w < ngroups; w += gridDim.x) {
+  for (int w = vb; w < ngroups; w += vgrid) {
     const int st = a.wmap[w];  // wave-uniform
     const StreamSegs ss = a.segs_info[st];
     const int s = (w - ss.wave_base) * kDsegThreads + lane;  // this lane's segment of the stream
-    const bool act = s < ss.s_all;
+    const int part = s >= ss.s_luma ? 1 : 0;
+    const bool act = s < ss.s_all && (only_part < 0 || part == only_part);
+    if (__ballot(act) == 0) continue;  // (wave-uniform) none of this group's segments in the part
     const int* dc = a.ds.dcount + (int64_t)st * 3;
-    const int part = act && s >= ss.s_luma ? 1 : 0;
     const int sp = part ? s - ss.s_luma : s;
     const int npart = part ? dc[1] + dc[2] : dc[0];
     const int off = sp * kSeg;
@@ -1279,6 +1295,27 @@ __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
       o.kb += 8;
     }
     if (act) a.segrec[ss.seg_base + s] = make_uint2((uint32_t)low, (uint32_t)((o.kb - kb0) >> 2));
+  }
+}
+
+__global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
+  set_prio(a.dseg_prio);
+  dseg_body(a, blockIdx.x, gridDim.x, a.dseg_part);
+}
+
+// The chroma chains' range pass and the luma segments' dseg in one launch:
+// blocks [0, range_blocks) continue every stream's range from its luma end
+// (rstate), the rest code the luma segments, whose checkpoints the first
+// range pass left.  The two roles share no data and never wait for each
+// other; on one stream, so no fifth hardware queue (an extra stream for the
+// same overlap serialised).
+__global__ __launch_bounds__(kRangeThreads) void ffv1_range_dseg(CodeArgs a) {
+  if ((int)blockIdx.x < a.range_blocks) {
+    set_prio(a.range_prio);
+    range_pass(a, (int64_t)blockIdx.x * kRangeThreads + threadIdx.x, 2);
+  } else {
+    set_prio(a.dseg_prio);
+    dseg_body(a, (int)blockIdx.x - a.range_blocks, (int)gridDim.x - a.range_blocks, 0);
   }
 }
 
@@ -2580,6 +2617,16 @@ int launch_range(const CodeArgs& a, void* stream) {
 int launch_dseg(const CodeArgs& a, void* stream) {
   hipLaunchKernelGGL(ffv1_dseg, dim3((unsigned)a.dseg_blocks), dim3(kDsegThreads), 0,
                      reinterpret_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_range_dseg(const CodeArgs& a, void* stream) {
+  static_assert(kRangeThreads == kDsegThreads, "one block size for both roles");
+  const int64_t streams = (int64_t)a.nframes * a.nslices;
+  CodeArgs b = a;
+  b.range_blocks = (int)((streams + kRangeThreads - 1) / kRangeThreads);
+  hipLaunchKernelGGL(ffv1_range_dseg, dim3((unsigned)(b.range_blocks + a.dseg_blocks)), dim3(kRangeThreads), 0,
+                     reinterpret_cast<hipStream_t>(stream), b);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
