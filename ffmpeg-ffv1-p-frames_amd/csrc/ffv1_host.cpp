@@ -139,7 +139,7 @@ struct Knobs {
 static const char* const kKnobNames[] = {"serial",     "walkdbg",    "walktrace", "hostdbg",   "walk_prio",
                                          "range_prio", "dseg_prio",  "sym_grid",  "bits_grid", "dseg_grid",
                                          "walk_split", "copy_threads", "dec_swap", "coder",    "dense", "walk_blocks",
-                                         "recsets",    "slice_cap",  "walk_part_a", "force_multi", "bounds_shrink", "range_split"};
+                                         "recsets",    "slice_cap",  "walk_part_a", "force_multi", "bounds_shrink", "range_split", "rd_grid"};
 
 static int parse_knobs(Knobs* k) {
   k->kv.clear();
@@ -1911,7 +1911,9 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       return set_err(-5, "range launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (rsplit) {
       ca.range_pass = 2;
-      if (timed(7, cst, [&] { return launch_range_dseg(ca, cst); }) < 0)
+      CodeArgs cf = ca;  // the fused launch's dseg grid (rd_grid hook)
+      cf.dseg_blocks = std::max(1, std::min(ca.dseg_blocks, c->knobs.get("rd_grid", ca.dseg_blocks)));
+      if (timed(7, cst, [&] { return launch_range_dseg(cf, cst); }) < 0)
         return set_err(-5, "range / dseg launch failed: %s", hipGetErrorString(hipGetLastError()));
       ca.dseg_part = 1;
     }

@@ -1096,44 +1096,56 @@ __device__ __forceinline__ void range_pass(const CodeArgs& a, int64_t c, int pas
   }
   for (int part = pass == 2 ? 1 : 0; part < (pass == 1 ? 1 : 2); part++) {
     const int n = sr.live ? (part ? dc[1] + dc[2] : dc[0]) : 0;
-    const int64_t pb = base + (part && sr.live ? chroma_start(dc[0]) : 0);  // multiple of 64
+    const int64_t pb = base + (part && sr.live ? chroma_start(dc[0]) : 0);  // multiple of 512
     const uint4* P = reinterpret_cast<const uint4*>(a.ds.pre + pb);
     const uint32_t* B = a.ds.bits + (pb >> 5);
     const int nmax = wave_max(n);
-    // blocks of 32 decisions (32 state bytes + one bits word), loaded two
-    // blocks ahead (parts are padded to 64 decisions: reads stay inside)
+    // groups of four 32-decision blocks (32 state bytes + one bits word
+    // each), the next group's loads issued while this one codes: 128-256
+    // decisions ahead, enough to cover the memory latency with dseg's
+    // streams beside it (chains are padded: reads stay inside the stream)
     const uint4 z4 = make_uint4(0, 0, 0, 0);
-    uint4 na = z4, nb = z4, ma = z4, mb = z4;
-    uint32_t nw = 0u, mw = 0u;
-    if (n > 0) {
-      na = P[0];
-      nb = P[1];
-      nw = B[0];
-    }
-    if (n > 32) {
-      ma = P[2];
-      mb = P[3];
-      mw = B[1];
-    }
-    for (int i = 0; i < nmax; i += 32) {
-      if ((i & (kSeg - 1)) == 0 && i < n) *ck++ = make_uint2((uint32_t)range, (uint32_t)shifts >> 3);
-      uint4 wa = na, wb = nb;
-      uint32_t bw = nw;
-      na = ma;
-      nb = mb;
-      nw = mw;
-      if (i + 64 < n) {
-        ma = P[(i >> 4) + 4];
-        mb = P[(i >> 4) + 5];
-        mw = B[(i >> 5) + 2];
-      }
-      const int rem = n - i;
-      if (rem < 32) {
-        wa = tail_mask(wa, rem);
-        wb = tail_mask(wb, rem - 16);
-        bw = rem > 0 ? bw & ((1u << rem) - 1u) : 0u;
-      }
-      range32(range, shifts, wa, wb, bw);
+    uint4 ca4[4], cb4[4], na4[4], nb4[4];
+    uint32_t cw4[4], nw4[4];
+    auto fetch = [&](int g, uint4* A, uint4* Bq, uint32_t* Wq) {
+      static_for<0, 4>([&](auto jc) {
+        constexpr int J = decltype(jc)::value;
+        const int blk = g * 4 + J;
+        A[J] = P[2 * blk];
+        Bq[J] = P[2 * blk + 1];
+        Wq[J] = B[blk];
+      });
+    };
+    static_for<0, 4>([&](auto jc) {
+      constexpr int J = decltype(jc)::value;
+      ca4[J] = cb4[J] = na4[J] = nb4[J] = z4;
+      cw4[J] = nw4[J] = 0u;
+    });
+    if (n > 0) fetch(0, ca4, cb4, cw4);
+    for (int i = 0; i < nmax; i += 128) {
+      if (i + 128 < n) fetch((i >> 7) + 1, na4, nb4, nw4);
+      static_for<0, 4>([&](auto jc) {
+        constexpr int J = decltype(jc)::value;
+        const int ii = i + 32 * J;
+        if (ii < nmax) {  // wave-uniform
+          if ((ii & (kSeg - 1)) == 0 && ii < n) *ck++ = make_uint2((uint32_t)range, (uint32_t)shifts >> 3);
+          uint4 wa = ca4[J], wb = cb4[J];
+          uint32_t bw = cw4[J];
+          const int rem = n - ii;
+          if (rem < 32) {
+            wa = tail_mask(wa, rem);
+            wb = tail_mask(wb, rem - 16);
+            bw = rem > 0 ? bw & ((1u << rem) - 1u) : 0u;
+          }
+          range32(range, shifts, wa, wb, bw);
+        }
+      });
+      static_for<0, 4>([&](auto jc) {
+        constexpr int J = decltype(jc)::value;
+        ca4[J] = na4[J];
+        cb4[J] = nb4[J];
+        cw4[J] = nw4[J];
+      });
     }
   }
   if (pass == 1 && sr.live) a.rstate[sr.st] = make_int2(range, shifts);
