@@ -1080,6 +1080,7 @@ __device__ __forceinline__ void set_prio(int p) {
 // chroma chain's at their own start.  pass 0: both; 1: the luma chain, its
 // final {range, shifts} kept in rstate; 2: the chroma chain from there (the
 // coder's dseg of the luma segments runs beside it, ffv1_range_dseg).
+template <int AHEAD>
 __device__ __forceinline__ void range_pass(const CodeArgs& a, int64_t c, int pass) {
   const StreamRef sr = stream_of(a, c);
   const int key = sr.live ? a.keyflags[sr.f] : 0;
@@ -1104,9 +1105,11 @@ __device__ __forceinline__ void range_pass(const CodeArgs& a, int64_t c, int pas
     // each), the next group's loads issued while this one codes: 128-256
     // decisions ahead, enough to cover the memory latency with dseg's
     // streams beside it (chains are padded: reads stay inside the stream)
+    // (AHEAD = 2: the next two groups, 256-384 decisions ahead, where the
+    // registers are there: the range pass alone, one wave per SIMD)
     const uint4 z4 = make_uint4(0, 0, 0, 0);
-    uint4 ca4[4], cb4[4], na4[4], nb4[4];
-    uint32_t cw4[4], nw4[4];
+    uint4 ca4[4], cb4[4], na4[4], nb4[4], ma4[4], mb4[4];
+    uint32_t cw4[4], nw4[4], mw4[4];
     auto fetch = [&](int g, uint4* A, uint4* Bq, uint32_t* Wq) {
       static_for<0, 4>([&](auto jc) {
         constexpr int J = decltype(jc)::value;
@@ -1118,12 +1121,17 @@ __device__ __forceinline__ void range_pass(const CodeArgs& a, int64_t c, int pas
     };
     static_for<0, 4>([&](auto jc) {
       constexpr int J = decltype(jc)::value;
-      ca4[J] = cb4[J] = na4[J] = nb4[J] = z4;
-      cw4[J] = nw4[J] = 0u;
+      ca4[J] = cb4[J] = na4[J] = nb4[J] = ma4[J] = mb4[J] = z4;
+      cw4[J] = nw4[J] = mw4[J] = 0u;
     });
     if (n > 0) fetch(0, ca4, cb4, cw4);
+    if (AHEAD > 1 && n > 128) fetch(1, na4, nb4, nw4);
     for (int i = 0; i < nmax; i += 128) {
-      if (i + 128 < n) fetch((i >> 7) + 1, na4, nb4, nw4);
+      if (AHEAD > 1) {
+        if (i + 256 < n) fetch((i >> 7) + 2, ma4, mb4, mw4);
+      } else {
+        if (i + 128 < n) fetch((i >> 7) + 1, na4, nb4, nw4);
+      }
       static_for<0, 4>([&](auto jc) {
         constexpr int J = decltype(jc)::value;
         const int ii = i + 32 * J;
@@ -1145,6 +1153,11 @@ __device__ __forceinline__ void range_pass(const CodeArgs& a, int64_t c, int pas
         ca4[J] = na4[J];
         cb4[J] = nb4[J];
         cw4[J] = nw4[J];
+        if (AHEAD > 1) {
+          na4[J] = ma4[J];
+          nb4[J] = mb4[J];
+          nw4[J] = mw4[J];
+        }
       });
     }
   }
@@ -1153,7 +1166,7 @@ __device__ __forceinline__ void range_pass(const CodeArgs& a, int64_t c, int pas
 
 __global__ __launch_bounds__(kRangeThreads) void ffv1_range(CodeArgs a) {
   set_prio(a.range_prio);
-  range_pass(a, (int64_t)blockIdx.x * kRangeThreads + threadIdx.x, a.range_pass);
+  range_pass<2>(a, (int64_t)blockIdx.x * kRangeThreads + threadIdx.x, a.range_pass);
 }
 
 // ffv1_dseg: one wave per 64 consecutive segments of a stream, one lane per
@@ -1324,7 +1337,7 @@ __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
 __global__ __launch_bounds__(kRangeThreads) void ffv1_range_dseg(CodeArgs a) {
   if ((int)blockIdx.x < a.range_blocks) {
     set_prio(a.range_prio);
-    range_pass(a, (int64_t)blockIdx.x * kRangeThreads + threadIdx.x, 2);
+    range_pass<2>(a, (int64_t)blockIdx.x * kRangeThreads + threadIdx.x, 2);
   } else {
     set_prio(a.dseg_prio);
     dseg_body(a, (int)blockIdx.x - a.range_blocks, (int)gridDim.x - a.range_blocks, 0);
