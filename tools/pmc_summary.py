@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def short(name):
     for k in ("ffv1_decode_slices", "ffv1_code_golomb", "ffv1_dcode", "ffv1_code", "ffv1_walk", "ffv1_bits", "ffv1_layout", "ffv1_symbols",
-              "ffv1_sink", "ffv1_assemble_packets", "ffv1_range", "ffv1_dseg", "ffv1_dfix", "ffv1_compact_packets",
+              "ffv1_sink", "ffv1_assemble_packets", "ffv1_range_dseg", "ffv1_range", "ffv1_dseg", "ffv1_dfix", "ffv1_compact_packets",
               "ffv1_sizes_out", "ffv1_ints_out", "ffv1_delay"):
         if k in name:
             return k
@@ -50,6 +50,7 @@ def main(tag, frames_per_launch, config, out_name="pmc_traffic_rNN.json"):
         stats[short(r["Name"])] = float(r["AverageNs"]) / 1e6
         calls[short(r["Name"])] = int(r["Calls"])
     # launches per step: the split schedule launches the walk in two parts
+    # (the range pass: one launch of ffv1_range and one of ffv1_range_dseg)
     per_step = calls.get("ffv1_range", calls.get("ffv1_dcode", 0))
     for k, v in kernels.items():
         n = max(1, round(calls.get(k, per_step) / per_step)) if per_step else 1
