@@ -75,6 +75,23 @@ def test_chained_coder_matches_oracle(stream, monkeypatch):
     assert got == ref
 
 
+@pytest.mark.parametrize("debug", ["range_split=0", "walk_blocks=0", "serial", "range_split=0,serial"])
+def test_schedule_variants_match_oracle(debug, monkeypatch):
+    """The coder's range pass whole or split at the luma / chroma boundary
+    (ffv1_range_dseg), the walk in 5-wave or one-wave blocks, overlapped or
+    one kernel at a time: the same bytes, at a batch (two GOPs of 4:2:0
+    10-bit and a 4:4:4 stream, whose chroma chains are the long ones) that
+    puts every chain in one round."""
+    monkeypatch.setenv("FFV1HIP_DEBUG", debug)
+    for s in [Stream("sched420", 352, 288, "yuv420p10", 8, slices=4, coder=1, gop_size=4, depth=10),
+              Stream("sched444", 176, 144, "yuv444p16", 6, slices=4, coder=1, gop_size=3,
+                     bits_per_raw_sample=12, depth=16, chroma444=True)]:
+        frames = list(s.frames())
+        _, _, ref = oracle_encode(s, frames)
+        _, got = hip_encode(s, frames, batch=len(frames))
+        assert got == ref, (debug, s.name)
+
+
 @pytest.mark.parametrize("recsets", [2, 1])
 @pytest.mark.parametrize("stream", [s for s in PARITY_STREAMS if s.coder != 0 and s.gop_size != 1][:4],
                          ids=[s.name for s in PARITY_STREAMS if s.coder != 0 and s.gop_size != 1][:4])
