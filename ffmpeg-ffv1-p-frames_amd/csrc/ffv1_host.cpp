@@ -114,7 +114,8 @@ class CopyPool {
 // measurement: serial, walkdbg, walktrace, hostdbg; schedule (defaults are
 // the measured best): walk_prio, range_prio, dseg_prio, sym_grid, bits_grid,
 // dseg_grid, walk_split=0, copy_threads, dec_swap=0; test hooks: coder=chain,
-// dense=0, recsets=1, slice_cap, walk_part_a, force_multi.  Unknown names
+// dense=0, recsets=1, slice_cap, walk_part_a, force_multi, dsets=eager|lazy,
+// rec2_drop=set.  Unknown names
 // are an error at create time, so a misspelt hook never silently measures
 // the default.
 struct Knobs {
@@ -139,7 +140,8 @@ struct Knobs {
 static const char* const kKnobNames[] = {"serial",     "walkdbg",    "walktrace", "hostdbg",   "walk_prio",
                                          "range_prio", "dseg_prio",  "sym_grid",  "bits_grid", "dseg_grid",
                                          "walk_split", "copy_threads", "dec_swap", "coder",    "dense", "walk_blocks",
-                                         "recsets",    "slice_cap",  "walk_part_a", "force_multi", "bounds_shrink", "range_split", "rd_grid"};
+                                         "recsets",    "slice_cap",  "walk_part_a", "force_multi", "bounds_shrink", "range_split", "rd_grid",
+                                         "dsets", "rec2_drop"};
 
 static int parse_knobs(Knobs* k) {
   k->kv.clear();
@@ -471,6 +473,11 @@ struct ffv1hip_ctx {
   bool two_rec = false;
   uint2* d_rec2 = nullptr;       // [batch frame][frame_samples] walk records of set 1
   uint32_t* d_cbits2 = nullptr;  // chunk bits of set 1
+  // the decision sets of a large batch are sized from the first batches'
+  // decisions (lazy), and the second records set is taken from what they
+  // leave (rec2_pending until the first batch has sized set 0)
+  bool lazy_sets = false;
+  bool rec2_pending = false;
   int* d_ident = nullptr;        // [batch frame] i: the frames mode's frame of each slot
   hipEvent_t entry[2] = {nullptr, nullptr};  // set k's batch: the launch stream's work so far
   hipEvent_t xchg_ev = nullptr;               // ffv1hip_set_slice_states_device: the caller's stream so far
@@ -1101,6 +1108,79 @@ static int64_t device_bytes(const ffv1hip_ctx* c, int64_t nb) {
   return b;
 }
 
+// The second set of walk records and chunk bits, only with room to spare:
+// set 1 before its first batch counts as large as set 0, and a later batch
+// may still grow the sets by an eighth (plus 2 GB for the runtime).  Beyond
+// that, ensure_decisions gives the second set back.
+static int alloc_rec2(ffv1hip_ctx* c) {
+  if (!c->rec2_pending) return 0;
+  c->rec2_pending = false;
+  const int nb = c->max_batch;
+  const size_t rec_bytes = sizeof(uint2) * size_t(c->frame_samples) * nb;
+  const size_t cb_bytes = sizeof(uint32_t) * kChunkWords * size_t(c->frame_chunks) * nb;
+  size_t free_b = 0, total_b = 0;
+  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  const size_t d0 = size_t(c->dcap[0]), d1 = c->dcap[1] ? size_t(c->dcap[1]) : d0;
+  const size_t unsized = c->dcap[1] ? 0 : d1 + d1 / 8;  // set 1, still to come
+  const size_t margin = unsized + (d0 + d1) / 8 + (size_t(2) << 30);
+  if (free_b > rec_bytes + cb_bytes + margin) {
+    if (hipMalloc(&c->d_rec2, rec_bytes) == hipSuccess && hipMalloc(&c->d_cbits2, cb_bytes) == hipSuccess) {
+      c->two_rec = true;
+    } else {
+      (void)hipGetLastError();
+      if (c->d_rec2) (void)hipFree(c->d_rec2);
+      c->d_rec2 = nullptr;
+    }
+  }
+  if (c->knobs.has("hostdbg"))
+    std::fprintf(stderr, "hostdbg: decision sets %.2f / %.2f GB, %.2f GB free, second records set (%.2f GB + "
+                         "margin %.2f GB): %s\n", double(c->dcap[0]) / 1e9, double(c->dcap[1]) / 1e9,
+                 double(free_b) / 1e9, double(rec_bytes + cb_bytes) / 1e9, double(margin) / 1e9,
+                 c->two_rec ? "yes" : "no");
+  return 0;
+}
+
+// Decision set fb for `need` decisions (a batch's, read back after its
+// layout).  When HBM does not hold the larger set beside two records sets,
+// the records set this batch does not use is given back (after every stream
+// of the context has drained) and the context goes on with one set: the one
+// holding this batch's records becomes set 0.  *rec / *cbits: this batch's.
+static int ensure_decisions(ffv1hip_ctx* c, int fb, int64_t need, uint2** rec, uint32_t** cbits) {
+  const int64_t want = need + need / 8;
+  // rec2_drop=k (test hook): as if set fb = k did not fit beside two records sets
+  const bool drop_hook = c->two_rec && c->knobs.has("rec2_drop") && c->knobs.get("rec2_drop", 0) == fb;
+  if (!drop_hook) {
+    if (grow_decisions(c, fb, want) == 0) {
+      if (c->rec2_pending) return alloc_rec2(c);
+      return 0;
+    }
+    (void)hipGetLastError();
+    if (!c->two_rec) return -1;
+  }
+  if (c->knobs.has("hostdbg"))
+    std::fprintf(stderr, "hostdbg: decision set %d to %.2f GB: the second records set goes\n", fb, double(want) / 1e9);
+  // every stream of the context drained: nothing reads either records set
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipStreamSynchronize(c->code_stream));
+  HIP_TRY(hipStreamSynchronize(c->bits_stream));
+  uint2* const set0 = reinterpret_cast<uint2*>(c->d_sym);
+  if (*rec == c->d_rec2) {  // this batch's records are in set 1: keep those
+    HIP_TRY(hipFree(set0));
+    HIP_TRY(hipFree(c->d_cbits));
+    c->d_sym = reinterpret_cast<uint32_t*>(c->d_rec2);
+    c->d_cbits = c->d_cbits2;
+  } else {
+    HIP_TRY(hipFree(c->d_rec2));
+    HIP_TRY(hipFree(c->d_cbits2));
+  }
+  c->d_rec2 = nullptr;
+  c->d_cbits2 = nullptr;
+  c->two_rec = false;
+  *rec = reinterpret_cast<uint2*>(c->d_sym);
+  *cbits = c->d_cbits;
+  return grow_decisions(c, fb, want);
+}
+
 static int alloc_device(ffv1hip_ctx* c) {
   HIP_TRY(hipSetDevice(c->device));
   const int nb = c->max_batch;
@@ -1218,25 +1298,21 @@ static int alloc_device(ffv1hip_ctx* c) {
     HIP_TRY(hipMalloc(&c->d_segrec, sizeof(uint2) * size_t(c->max_segs)));
     HIP_TRY(hipMalloc(&c->d_rstate, sizeof(int2) * size_t(nb) * c->nslices));
     if (upload_hdr(c) < 0) return -5;
+    // Decision sets: a batch whose worst case is small gets it now; a large
+    // one (the guess of decision_cap) is sized from what its first batches
+    // need (ensure_decisions), and the second records set then takes the
+    // room real content leaves (4:4:4 12-bit at 19 GOPs: ~3 decisions per
+    // sample against the guess of 12, so both records sets fit beside them)
     const int64_t cap = decision_cap(c, nb);
-    for (int k = 0; k < 2; k++)
-      if (grow_decisions(c, k, cap) < 0) return -5;
-    // the second records set, only with room to spare (a later batch may
-    // still grow the decision buffers); the recsets=1 hook keeps one set
-    const size_t rec_bytes = sizeof(uint2) * size_t(c->frame_samples) * nb;
-    const size_t cb_bytes = sizeof(uint32_t) * kChunkWords * size_t(c->frame_chunks) * nb;
-    size_t free_b = 0, total_b = 0;
-    HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-    const size_t margin = (size_t(c->dcap[0]) + size_t(c->dcap[1])) / 4 + (size_t(4) << 30);
-    if (c->knobs.get("recsets", 2) != 1 && free_b > rec_bytes + cb_bytes + margin) {
-      if (hipMalloc(&c->d_rec2, rec_bytes) == hipSuccess && hipMalloc(&c->d_cbits2, cb_bytes) == hipSuccess) {
-        c->two_rec = true;
-      } else {
-        (void)hipGetLastError();
-        if (c->d_rec2) (void)hipFree(c->d_rec2);
-        c->d_rec2 = nullptr;
-      }
-    }
+    const int64_t worst = int64_t(nb) * c->frame_samples * c->wmax + int64_t(nb) * c->nslices * kStreamSlack;
+    const std::string ds = c->knobs.str("dsets");
+    c->lazy_sets = ds == "lazy" || (cap < worst && ds != "eager");
+    if (!c->lazy_sets)
+      for (int k = 0; k < 2; k++)
+        if (grow_decisions(c, k, cap) < 0) return -5;
+    // the recsets=1 hook keeps one set
+    c->rec2_pending = c->knobs.get("recsets", 2) != 1;
+    if (!c->lazy_sets && alloc_rec2(c) < 0) return -5;
   } else {
     const size_t chains = (size_t(c->max_slots) * c->nslices + 63) & ~size_t(63);
     HIP_TRY(hipMalloc(&c->d_tables, state_bytes * chains));
@@ -1613,8 +1689,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   uint32_t* const d_sym = c->frames_mode ? nullptr : c->d_sym;
   // walk records / chunk bits: set fb when there are two sets
   const bool rec1 = c->frames_mode && c->two_rec && fb == 1;
-  uint2* const d_rec = c->frames_mode ? (rec1 ? c->d_rec2 : reinterpret_cast<uint2*>(c->d_sym)) : nullptr;
-  uint32_t* const d_cbits = rec1 ? c->d_cbits2 : c->d_cbits;
+  uint2* d_rec = c->frames_mode ? (rec1 ? c->d_rec2 : reinterpret_cast<uint2*>(c->d_sym)) : nullptr;
+  uint32_t* d_cbits = rec1 ? c->d_cbits2 : c->d_cbits;
   int* const d_dcount = c->frames_mode ? c->d_dcount + size_t(t3) * 3 * c->max_batch * c->nslices : nullptr;
   int64_t* const d_dbase = c->frames_mode ? c->d_dbase + size_t(t3) * c->max_batch * c->nslices : nullptr;
   StreamSegs* const d_segs = c->frames_mode ? c->d_segs_info + size_t(t3) * c->max_batch * c->nslices : nullptr;
@@ -1723,8 +1799,10 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
         // then: waiting for it on every batch held this batch's walk behind
         // the previous batch's packet assembly)
         HIP_TRY(hipEventSynchronize(c->coded[fb]));
-        if (grow_decisions(c, fb, need + need / 8) < 0)
+        if (ensure_decisions(c, fb, need, &d_rec, &d_cbits) < 0)
           return set_err(-12, "decision buffers for %lld decisions: %s", (long long)need, g_err);
+        sa.rec = d_rec;
+        sa.cbits = d_cbits;
       }
     }
     HIP_TRY(hipEventRecord(c->laid[fb], sst));  // the records and the stream layout: the walk may start
@@ -1842,7 +1920,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       c->trace_first.push_back(two_parts ? first : 0);
       c->trace_n++;
     }
-    c->walk_a_valid = sst != st;
+    // (two_rec: also when the second records set came with this batch's layout)
+    c->walk_a_valid = c->two_rec && !serial;
     StatsArgs sta{};
     if (c->pass == 1) {  // slot counts from the records, before the next batch's symbols rewrite them
       sta.rec = d_rec;

@@ -92,6 +92,23 @@ def test_schedule_variants_match_oracle(debug, monkeypatch):
         assert got == ref, (debug, s.name)
 
 
+@pytest.mark.parametrize("debug", ["dsets=lazy", "dsets=lazy,rec2_drop=1", "dsets=lazy,rec2_drop=0",
+                                   "dsets=eager,rec2_drop=0"])
+def test_lazy_decision_sets_match_oracle(debug, monkeypatch):
+    """Decision sets sized from the first batches (dsets=lazy, the default
+    for large batches), the second records set taken afterwards, and given
+    back when a set has to grow (rec2_drop=k: as if set k did not fit beside
+    it; the batch's own records set is kept).  A flat first batch makes the
+    later random ones grow both sets."""
+    monkeypatch.setenv("FFV1HIP_DEBUG", debug)
+    s = Stream("lazy420", 176, 144, "yuv420p10", 9, slices=4, coder=1, gop_size=3, source="random", depth=10)
+    frames = list(s.frames())
+    frames[:3] = [[np.full_like(p, 200) for p in f] for f in frames[:3]]
+    _, _, ref = oracle_encode(s, frames)
+    _, got = hip_encode(s, frames, batch=3)
+    assert got == ref
+
+
 @pytest.mark.parametrize("recsets", [2, 1])
 @pytest.mark.parametrize("stream", [s for s in PARITY_STREAMS if s.coder != 0 and s.gop_size != 1][:4],
                          ids=[s.name for s in PARITY_STREAMS if s.coder != 0 and s.gop_size != 1][:4])
