@@ -114,7 +114,7 @@ class CopyPool {
 // measurement: serial, walkdbg, walktrace, hostdbg; schedule (defaults are
 // the measured best): walk_prio, range_prio, dseg_prio, sym_grid, bits_grid,
 // dseg_grid, walk_split=0, copy_threads, dec_swap=0; test hooks: coder=chain,
-// dense=0, recsets=1, slice_cap, walk_part_a, force_multi, dsets=eager|lazy,
+// dense=0, recsets=1, slice_cap, walk_part_a, force_multi, dsets=eager|lazy, budget=q,
 // rec2_drop=set.  Unknown names
 // are an error at create time, so a misspelt hook never silently measures
 // the default.
@@ -141,7 +141,7 @@ static const char* const kKnobNames[] = {"serial",     "walkdbg",    "walktrace"
                                          "range_prio", "dseg_prio",  "sym_grid",  "bits_grid", "dseg_grid",
                                          "walk_split", "copy_threads", "dec_swap", "coder",    "dense", "walk_blocks",
                                          "recsets",    "slice_cap",  "walk_part_a", "force_multi", "bounds_shrink", "range_split", "rd_grid",
-                                         "dsets", "rec2_drop"};
+                                         "dsets", "rec2_drop", "budget"};
 
 static int parse_knobs(Knobs* k) {
   k->kv.clear();
@@ -1181,6 +1181,17 @@ static int ensure_decisions(ffv1hip_ctx* c, int fb, int64_t need, uint2** rec, u
   return grow_decisions(c, fb, want);
 }
 
+// A batch whose decision sets would be sized by decision_cap's guess (its
+// worst case is over 2^31 decisions) is sized from its content instead:
+// decision sets, the second records set and the slice byte budget
+// (dsets=eager|lazy overrides).
+static bool lazy_sizing(const ffv1hip_ctx* c) {
+  const int64_t nb = c->max_batch;
+  const int64_t worst = nb * c->frame_samples * c->wmax + nb * c->nslices * kStreamSlack;
+  const std::string ds = c->knobs.str("dsets");
+  return ds == "lazy" || (decision_cap(c, nb) < worst && ds != "eager");
+}
+
 static int alloc_device(ffv1hip_ctx* c) {
   HIP_TRY(hipSetDevice(c->device));
   const int nb = c->max_batch;
@@ -1304,9 +1315,6 @@ static int alloc_device(ffv1hip_ctx* c) {
     // room real content leaves (4:4:4 12-bit at 19 GOPs: ~3 decisions per
     // sample against the guess of 12, so both records sets fit beside them)
     const int64_t cap = decision_cap(c, nb);
-    const int64_t worst = int64_t(nb) * c->frame_samples * c->wmax + int64_t(nb) * c->nslices * kStreamSlack;
-    const std::string ds = c->knobs.str("dsets");
-    c->lazy_sets = ds == "lazy" || (cap < worst && ds != "eager");
     if (!c->lazy_sets)
       for (int k = 0; k < 2; k++)
         if (grow_decisions(c, k, cap) < 0) return -5;
@@ -1442,8 +1450,17 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
     c->frames_mode = p.ac && !p.colorspace && !p.transparency && p.version <= 3 && lds <= kWalkLdsMax &&
                      c->knobs.str("coder") != "chain";
     c->wmax = 2 * (p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample) + 1;
-    // the decision-stream coder writes a slice's digits (2 bytes each) where
-    // ffv1_sink then writes its bytes
+    // a large batch, sized from what its content needs (lazy_sizing): the
+    // byte budget starts at a quarter (what noise needs is over it; a slice
+    // over the budget is encoded again with one sized from what it needed)
+    c->lazy_sets = c->frames_mode && lazy_sizing(c);
+    if (c->lazy_sets && !c->knobs.has("slice_cap") && c->knobs.get("budget", 4) > 1) {
+      const int64_t q = c->knobs.get("budget", 4);
+      c->slice_cap = ((c->slice_cap - 4096) / q + 4096 + 255) & ~int64_t(255);
+      c->packet_stride = ((c->slice_cap + 16) * c->nslices + 255) & ~int64_t(255);
+    }
+    // the decision-stream coder writes a slice's digits (the values of low,
+    // 4 bytes each) where ffv1_sink then writes its bytes
     c->slice_stride = c->frames_mode ? slice_stride_frames(c->slice_cap) : c->slice_cap;
   }
   int rc = alloc_device(c);
@@ -2098,10 +2115,25 @@ static int grow_slice_budget(ffv1hip_ctx* c, int64_t needed) {
   c->slice_stride = c->frames_mode ? slice_stride_frames(cap) : cap;
   c->packet_stride = ((cap + 16) * c->nslices + 255) & ~int64_t(255);
   const size_t pk_bytes = size_t(c->packet_stride) * c->max_batch;
-  if (hipMalloc(&c->d_slice_out, size_t(c->slice_stride) * c->nslices * c->max_batch) != hipSuccess ||
-      hipMalloc(&c->d_packets, pk_bytes) != hipSuccess ||
-      (c->two_pk && hipMalloc(&c->d_packets2, pk_bytes) != hipSuccess))
-    return set_err(-12, "slice buffers for a %lld-byte budget", (long long)cap);
+  for (int attempt = 0;; attempt++) {
+    if (hipMalloc(&c->d_slice_out, size_t(c->slice_stride) * c->nslices * c->max_batch) == hipSuccess &&
+        hipMalloc(&c->d_packets, pk_bytes) == hipSuccess &&
+        (!c->two_pk || hipMalloc(&c->d_packets2, pk_bytes) == hipSuccess))
+      break;
+    (void)hipGetLastError();
+    for (uint8_t** q : {&c->d_slice_out, &c->d_packets, &c->d_packets2}) {
+      if (*q) HIP_TRY(hipFree(*q));
+      *q = nullptr;
+    }
+    if (attempt > 0 || !c->two_rec) return set_err(-12, "slice buffers for a %lld-byte budget", (long long)cap);
+    // the batches are rolled back (nothing in flight): the second records
+    // set makes room, and the context goes on with one
+    HIP_TRY(hipFree(c->d_rec2));
+    HIP_TRY(hipFree(c->d_cbits2));
+    c->d_rec2 = nullptr;
+    c->d_cbits2 = nullptr;
+    c->two_rec = false;
+  }
   return c->pipe.on ? alloc_compact(c) : 0;
 }
 
