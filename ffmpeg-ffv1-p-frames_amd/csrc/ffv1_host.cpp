@@ -141,7 +141,7 @@ static const char* const kKnobNames[] = {"serial",     "walkdbg",    "walktrace"
                                          "range_prio", "dseg_prio",  "sym_grid",  "bits_grid", "dseg_grid",
                                          "walk_split", "copy_threads", "dec_swap", "coder",    "dense", "walk_blocks",
                                          "recsets",    "slice_cap",  "walk_part_a", "force_multi", "bounds_shrink", "range_split", "rd_grid",
-                                         "dsets", "rec2_drop", "budget"};
+                                         "dsets", "rec2_drop", "budget", "pack"};
 
 static int parse_knobs(Knobs* k) {
   k->kv.clear();
@@ -191,6 +191,42 @@ void pool_copy2d(CopyPool& pool, uint8_t* dst, int64_t dp, const uint8_t* src, i
       for (int64_t r = a; r < b; r++) std::memcpy(dst + r * dp, src + r * sp, size_t(wb));
     }
   });
+}
+
+// Rows r0 .. r1-1 of w 16-bit samples (pitch sp bytes) packed three to a
+// 32-bit word (bits 0-9, 10-19, 20-29) into rows of pb bytes at dst; returns
+// the OR of the samples (>= 1024: they did not fit, the frame goes as is).
+static uint32_t pack10_rows(uint8_t* dst, int64_t pb, const uint8_t* src, int64_t sp, int w, int64_t r0, int64_t r1) {
+  uint32_t acc = 0;
+  const int n3 = w / 3, tail = w - 3 * n3;
+  for (int64_t r = r0; r < r1; r++) {
+    const uint16_t* const s = reinterpret_cast<const uint16_t*>(src + r * sp);
+    uint32_t* const d = reinterpret_cast<uint32_t*>(dst + r * pb);
+    uint32_t m = 0;
+    for (int j = 0; j < n3; j++) {
+      const uint32_t a = s[3 * j], b = s[3 * j + 1], c = s[3 * j + 2];
+      m |= a | b | c;
+      d[j] = a | (b << 10) | (c << 20);
+    }
+    if (tail) {
+      const uint32_t a = s[3 * n3], b = tail == 2 ? s[3 * n3 + 1] : 0u;
+      m |= a | b;
+      d[n3] = a | (b << 10);
+    }
+    acc |= m;
+  }
+  return acc;
+}
+
+static uint32_t pool_pack10(CopyPool& pool, uint8_t* dst, int64_t pb, const uint8_t* src, int64_t sp, int w,
+                            int64_t rows) {
+  if (rows <= 0) return 0;
+  if (int64_t(w) * 2 * rows < (int64_t(1) << 20) || pool.size() == 1) return pack10_rows(dst, pb, src, sp, w, 0, rows);
+  std::atomic<uint32_t> acc{0};
+  pool.run([&](int part, int np) {
+    acc.fetch_or(pack10_rows(dst, pb, src, sp, w, rows * part / np, rows * (part + 1) / np));
+  });
+  return acc.load();
 }
 
 // ---------------------------------------------------------------------------
@@ -592,6 +628,15 @@ struct ffv1hip_ctx {
     int* h_status = nullptr;  // [2][4]
     int* hd_status = nullptr;
     int64_t h_pk_cap[2]{};
+    // 10-bit samples in 16-bit words cross PCIe packed three to a 32-bit
+    // word (pack10_rows), into a packed area per frame set that
+    // ffv1_unpack10 expands into the frame slots; rawf: frames staged as is
+    bool pack10 = false;
+    uint8_t* d_packed[2]{};
+    int64_t packed_frame_bytes = 0;
+    int64_t poff[kMaxPlanes]{};
+    int pw[kMaxPlanes]{}, prow[kMaxPlanes]{};  // samples per row, packed bytes per row
+    std::vector<uint8_t> rawf[2];
     uint8_t* d_compact[2]{};  // the same, back to back in HBM (one D2H copy)
     int64_t d_compact_cap[2]{};
     // FFV1HIP_HOSTDBG=1 (measurement hook): where ffv1hip_encode's host time
@@ -2361,6 +2406,37 @@ static int pipe_open_parts(ffv1hip_ctx* c) {
       drop_second_set(c);
     }
   }
+  {  // 10-bit samples packed for PCIe (pack=0: as they are)
+    const ffv1hip_params& p = c->P;
+    P.pack10 = p.sample_bytes == 2 && p.packed_at_lsb && p.bits_per_raw_sample == 10 && !is_ya8(p) &&
+               c->knobs.get("pack", 0) != 0;
+    if (P.pack10) {
+      int64_t off[kMaxPlanes];
+      int pst[kMaxPlanes], rows[kMaxPlanes], np;
+      slot_layout(c, off, pst, rows, &np);
+      int64_t o = 0;
+      for (int k = 0; k < np; k++) {
+        P.poff[k] = o;
+        P.pw[k] = pst[k] / 2;
+        P.prow[k] = (P.pw[k] + 2) / 3 * 4;
+        o += int64_t(P.prow[k]) * rows[k];
+      }
+      P.packed_frame_bytes = (o + 255) & ~int64_t(255);
+      for (int k = 0; k < (P.overlap ? 2 : 1) && P.pack10; k++) {
+        if (hipMalloc(&P.d_packed[k], size_t(P.packed_frame_bytes) * c->max_batch) != hipSuccess) {
+          (void)hipGetLastError();
+          P.d_packed[k] = nullptr;
+          P.pack10 = false;  // (the frames go as they are)
+        }
+        P.rawf[k].assign(size_t(c->max_batch), 1);
+      }
+      if (!P.pack10)
+        for (uint8_t*& d : P.d_packed) {
+          if (d) (void)hipFree(d);
+          d = nullptr;
+        }
+    }
+  }
   for (int k = 0; k < 2; k++) {  // both packet sets' mapped sizes (the second may come into use)
     HIP_TRY(hipHostMalloc(&P.h_sizes[k], sizeof(int64_t) * size_t(c->max_batch), hipHostMallocMapped));
     HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&P.hd_sizes[k]), P.h_sizes[k], 0));
@@ -2408,6 +2484,8 @@ static void pipe_close(ffv1hip_ctx* c) {
     if (h) (void)hipHostFree(h);
   if (P.h_status) (void)hipHostFree(P.h_status);
   for (uint8_t* d : P.d_compact)
+    if (d) (void)hipFree(d);
+  for (uint8_t* d : P.d_packed)
     if (d) (void)hipFree(d);
   if (P.xfer) (void)hipStreamDestroy(P.xfer);
   if (P.d2h) (void)hipStreamDestroy(P.d2h);
@@ -2493,17 +2571,72 @@ static int stage_rows(ffv1hip_ctx* c, uint8_t* dst, const uint8_t* src, int64_t 
   return 0;
 }
 
-// One host frame into batch slot `slot` of frame set `set`.
+// stage_rows for 10-bit samples: rows of w samples packed into the pinned
+// slots (pb bytes a row) and sent to the packed area at dst; *acc: the OR
+// of the samples.
+static int stage_rows_packed(ffv1hip_ctx* c, uint8_t* dst, const uint8_t* src, int64_t sp, int w, int64_t pb,
+                             int64_t rows, uint32_t* acc) {
+  ffv1hip_ctx::HostPipe& P = c->pipe;
+  for (int64_t r = 0; r < rows;) {
+    if (P.fill + pb > P.slot_bytes) {
+      const int rc = stage_flush(c);
+      if (rc < 0) return rc;
+    }
+    double t0 = P.dbg ? wall_s() : 0;
+    if (P.fill == 0 && P.slot_busy[P.next]) {
+      HIP_TRY(hipEventSynchronize(P.slot_ev[P.next]));
+      P.slot_busy[P.next] = false;
+    }
+    const int64_t nr = std::min(rows - r, (P.slot_bytes - P.fill) / pb);
+    uint8_t* const h = P.h_slot[P.next] + P.fill;
+    double t1 = P.dbg ? wall_s() : 0;
+    *acc |= pool_pack10(*P.pool, h, pb, src + r * sp, sp, w, nr);
+    double t2 = P.dbg ? wall_s() : 0;
+    HIP_TRY(hipMemcpyAsync(dst + r * pb, h, size_t(nr * pb), hipMemcpyHostToDevice, P.xfer));
+    if (P.dbg) {
+      const double t3 = wall_s();
+      P.t_slot += t1 - t0;
+      P.t_copy += t2 - t1;
+      P.t_dma += t3 - t2;
+    }
+    P.fill += nr * pb;
+    r += nr;
+  }
+  return 0;
+}
+
+// One host frame into batch slot `slot` of frame set `set`: packed (10-bit
+// samples, none over 10 bits, not caller-pinned) or as it is.
 static int stage_frame(ffv1hip_ctx* c, int set, int64_t slot, const void* const* planes, const int* strides) {
+  ffv1hip_ctx::HostPipe& P = c->pipe;
   int64_t off[kMaxPlanes];
   int pst[kMaxPlanes], rows[kMaxPlanes], np;
   slot_layout(c, off, pst, rows, &np);
-  uint8_t* const base = (set ? c->d_frames2 : c->d_frames) + slot * c->frame_bytes;
-  for (int k = 0; k < np; k++) {
+  for (int k = 0; k < np; k++)
     if (!planes[k]) return set_err(-22, "null plane %d", k);
-    const int rc = stage_rows(c, base + off[k], static_cast<const uint8_t*>(planes[k]), strides[k], pst[k], rows[k]);
-    if (rc < 0) return rc;
+  uint8_t* const base = (set ? c->d_frames2 : c->d_frames) + slot * c->frame_bytes;
+  bool raw = true;
+  if (P.pack10 && P.d_packed[set]) {
+    bool pinned = false;
+    for (int k = 0; k < np; k++)
+      pinned = pinned || (rows[k] > 0 && host_registered(c, planes[k], int64_t(rows[k] - 1) * strides[k] + pst[k]));
+    if (!pinned) {
+      uint8_t* const pbase = P.d_packed[set] + slot * P.packed_frame_bytes;
+      uint32_t acc = 0;
+      for (int k = 0; k < np && acc < 1024u; k++) {
+        const int rc = stage_rows_packed(c, pbase + P.poff[k], static_cast<const uint8_t*>(planes[k]), strides[k],
+                                         P.pw[k], P.prow[k], rows[k], &acc);
+        if (rc < 0) return rc;
+      }
+      raw = acc >= 1024u;  // a sample over 10 bits: the frame goes as it is (the packed bytes unused)
+    }
+    P.rawf[set][size_t(slot)] = raw ? 1 : 0;
   }
+  if (raw)
+    for (int k = 0; k < np; k++) {
+      const int rc = stage_rows(c, base + off[k], static_cast<const uint8_t*>(planes[k]), strides[k], pst[k], rows[k]);
+      if (rc < 0) return rc;
+    }
   return 0;
 }
 
@@ -2514,7 +2647,37 @@ static int launch_staged(ffv1hip_ctx* c, int set, int n) {
   int64_t off[kMaxPlanes];
   int pst[kMaxPlanes], rows[kMaxPlanes], np;
   slot_layout(c, off, pst, rows, &np);
-  return run_batch(c, set ? c->d_frames2 : c->d_frames, c->frame_bytes, off, pst, n, c->pipe.xfer);
+  ffv1hip_ctx::HostPipe& P = c->pipe;
+  uint8_t* const frames = set ? c->d_frames2 : c->d_frames;
+  if (P.pack10 && P.d_packed[set]) {  // the packed frames into their slots, after their copies
+    for (int f0 = 0; f0 < n; f0 += kUnpackFrames) {
+      UnpackArgs ua{};
+      ua.packed = P.d_packed[set];
+      ua.frames = frames;
+      ua.packed_frame_bytes = P.packed_frame_bytes;
+      ua.frame_bytes = c->frame_bytes;
+      ua.np = np;
+      ua.f0 = f0;
+      bool any = false;
+      for (int k = 0; k < np; k++) {
+        ua.poff[k] = P.poff[k];
+        ua.off[k] = off[k];
+        ua.prow[k] = P.prow[k] / 4;
+        ua.width[k] = P.pw[k];
+        ua.rows[k] = rows[k];
+        ua.pst[k] = pst[k];
+      }
+      const int nf = std::min(kUnpackFrames, n - f0);
+      for (int i = 0; i < nf; i++) {
+        const bool r = P.rawf[set][size_t(f0 + i)] != 0;
+        ua.raw[i >> 5] |= uint32_t(r) << (i & 31);
+        any = any || !r;
+      }
+      if (any && launch_unpack10(ua, nf, P.xfer) < 0)
+        return set_err(-5, "unpack launch failed: %s", hipGetErrorString(hipGetLastError()));
+    }
+  }
+  return run_batch(c, frames, c->frame_bytes, off, pst, n, P.xfer);
 }
 
 // A settled batch's packets (n of them, packet set pk) into the pinned

@@ -443,6 +443,20 @@ int launch_assemble(const AssembleArgs& a, int nframes, void* stream);
 int launch_compact_packets(const uint8_t* packets, int64_t stride, const int64_t* sizes, int n, uint8_t* out,
                            void* stream);
 int launch_sizes_out(const int64_t* sizes, int n, int64_t* host_mapped, void* stream);
+// ffv1_unpack10: frames f0 .. f0+n-1 of a batch's packed 10-bit samples
+// (three to a word) into their 16-bit frame slots, n <= kUnpackFrames
+constexpr int kUnpackFrames = 1024;
+struct UnpackArgs {
+  const uint8_t* packed;
+  uint8_t* frames;
+  int64_t packed_frame_bytes, frame_bytes;
+  int64_t poff[kMaxPlanes], off[kMaxPlanes];  // a plane in a packed / 16-bit frame slot
+  int prow[kMaxPlanes];                       // words per packed row
+  int width[kMaxPlanes], rows[kMaxPlanes], pst[kMaxPlanes];
+  int np, f0;
+  uint32_t raw[kUnpackFrames / 32];  // frames staged as is
+};
+int launch_unpack10(const UnpackArgs& a, int nframes, void* stream);
 int launch_ints_out(const int* src, int n, int* host_mapped, void* stream);
 
 }  // namespace ffv1hip

@@ -2835,6 +2835,39 @@ int launch_ints_out(const int* src, int n, int* host_mapped, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// Host-frame path, 10-bit samples: the host packs three samples to a 32-bit
+// word (bits 0-9, 10-19, 20-29; a row's last word holds one to three), so a
+// frame crosses PCIe in 2/3 of its bytes; here they go back to 16-bit
+// samples in the frame slot, one block row per (frame, plane).  A frame the
+// host staged as is (a sample over 10 bits, or caller-pinned) is skipped.
+__global__ __launch_bounds__(256) void ffv1_unpack10(UnpackArgs a) {
+  const int f = (int)blockIdx.y / a.np, p = (int)blockIdx.y - f * a.np;
+  if ((a.raw[f >> 5] >> (f & 31)) & 1u) return;
+  const int wpr = a.prow[p], width = a.width[p];
+  const int nw = wpr * a.rows[p];
+  const uint32_t* const src =
+      reinterpret_cast<const uint32_t*>(a.packed + (int64_t)(a.f0 + f) * a.packed_frame_bytes + a.poff[p]);
+  uint8_t* const dst = a.frames + (int64_t)(a.f0 + f) * a.frame_bytes + a.off[p];
+  for (int i = (int)(blockIdx.x * blockDim.x + threadIdx.x); i < nw; i += (int)(gridDim.x * blockDim.x)) {
+    const int r = i / wpr, j = i - r * wpr, x = 3 * j;
+    const uint32_t w = src[i];
+    uint16_t* const row = reinterpret_cast<uint16_t*>(dst + (int64_t)r * a.pst[p]);
+    row[x] = (uint16_t)(w & 0x3FFu);
+    if (x + 1 < width) row[x + 1] = (uint16_t)((w >> 10) & 0x3FFu);
+    if (x + 2 < width) row[x + 2] = (uint16_t)((w >> 20) & 0x3FFu);
+  }
+}
+
+int launch_unpack10(const UnpackArgs& a, int nframes, void* stream) {
+  if (nframes <= 0) return 0;
+  if (nframes > kUnpackFrames || a.np < 1 || a.np > kMaxPlanes) return -1;
+  int maxw = 0;
+  for (int p = 0; p < a.np; p++) maxw = max(maxw, a.prow[p] * a.rows[p]);
+  dim3 grid((unsigned)max(1, min(512, (maxw + 255) / 256)), (unsigned)(nframes * a.np)), block(256);
+  hipLaunchKernelGGL(ffv1_unpack10, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_compact_packets(const uint8_t* packets, int64_t stride, const int64_t* sizes, int n, uint8_t* out,
                            void* stream) {
   if (n <= 0) return 0;

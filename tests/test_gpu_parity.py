@@ -109,6 +109,24 @@ def test_lazy_decision_sets_match_oracle(debug, monkeypatch):
     assert got == ref
 
 
+@pytest.mark.parametrize("pack", ["pack=1", "pack=0"])
+def test_packed_10bit_host_frames(pack, monkeypatch):
+    """10-bit host frames cross PCIe packed three samples to a word and are
+    unpacked in HBM (ffv1_unpack10); a frame with a sample over 10 bits (the
+    encoder codes the 16-bit value as it is) goes as it is, beside packed
+    ones in the same batch; odd widths leave one or two samples in a row's
+    last word.  The oracle's packets either way (pack=0: no packing)."""
+    monkeypatch.setenv("FFV1HIP_DEBUG", pack)
+    for s in [Stream("pk420", 190, 64, "yuv420p10", 7, slices=4, coder=1, gop_size=3, source="random", depth=10),
+              Stream("pk422", 95, 61, "yuv422p10", 5, slices=4, coder=1, gop_size=5, source="random", depth=10)]:
+        frames = [[p.copy() for p in f] for f in s.frames()]
+        frames[1][0][3, 5] = 1500    # luma over 10 bits
+        frames[4][2][0, 0] = 1024    # Cr, just over
+        _, _, ref = oracle_encode(s, frames)
+        _, got = hip_encode(s, frames, batch=3)
+        assert got == ref, s.name
+
+
 @pytest.mark.parametrize("recsets", [2, 1])
 @pytest.mark.parametrize("stream", [s for s in PARITY_STREAMS if s.coder != 0 and s.gop_size != 1][:4],
                          ids=[s.name for s in PARITY_STREAMS if s.coder != 0 and s.gop_size != 1][:4])
