@@ -1130,8 +1130,19 @@ static int64_t decision_cap(const ffv1hip_ctx* c, int64_t nb) {
 // HBM the context's buffers take for a batch of nb frames (the second walk
 // records set, allocated only with room to spare, and the host-frame path's
 // frame slots, allocated on its first use, not counted).
+// The slice byte budget a large batch can go down to (alloc_rec2): a
+// quarter, or 1/q with budget=q; else the budget as it is.
+static int64_t low_slice_cap(const ffv1hip_ctx* c) {
+  const int64_t q = c->knobs.get("budget", 4);
+  if (!c->lazy_sets || q <= 1 || c->knobs.has("slice_cap")) return c->slice_cap;
+  return std::min(c->slice_cap, ((c->slice_cap - 4096) / q + 4096 + 255) & ~int64_t(255));
+}
+
 static int64_t device_bytes(const ffv1hip_ctx* c, int64_t nb) {
-  int64_t b = nb * (c->slice_stride * c->nslices + c->packet_stride);
+  // (a large batch counted at the budget it can go down to)
+  const int64_t cap = low_slice_cap(c);
+  const int64_t stride = c->frames_mode ? slice_stride_frames(cap) : cap;
+  int64_t b = nb * (stride * c->nslices + (((cap + 16) * c->nslices + 255) & ~int64_t(255)));
   b += 2 * int64_t(c->pcount) * c->contexts * 32 * c->nslices;  // the P-frame carry
   if (c->frames_mode) {
     b += nb * (8 * c->frame_samples + 4 * int64_t(kChunkWords) * c->frame_chunks);  // walk records, chunk bits
@@ -1168,6 +1179,28 @@ static int alloc_rec2(ffv1hip_ctx* c) {
   const size_t d0 = size_t(c->dcap[0]), d1 = c->dcap[1] ? size_t(c->dcap[1]) : d0;
   const size_t unsized = c->dcap[1] ? 0 : d1 + d1 / 8;  // set 1, still to come
   const size_t margin = unsized + (d0 + d1) / 8 + (size_t(2) << 30);
+  // no room, in the first batch (its coder has not run): the slice byte
+  // budget goes down to a quarter and a slice over it encodes its batch
+  // again with a budget sized from what it needed (budget=q: down to 1/q,
+  // room or not)
+  if ((free_b <= rec_bytes + cb_bytes + margin || c->knobs.has("budget")) && c->nsub == 0) {
+    const int64_t cap = low_slice_cap(c);
+    if (cap < c->slice_cap) {
+      HIP_TRY(hipDeviceSynchronize());
+      for (uint8_t** b : {&c->d_slice_out, &c->d_packets, &c->d_packets2}) {
+        if (*b) HIP_TRY(hipFree(*b));
+        *b = nullptr;
+      }
+      c->slice_cap = cap;
+      c->slice_stride = slice_stride_frames(cap);
+      c->packet_stride = ((cap + 16) * c->nslices + 255) & ~int64_t(255);
+      const size_t pk_bytes = size_t(c->packet_stride) * nb;
+      HIP_TRY(hipMalloc(&c->d_slice_out, size_t(c->slice_stride) * c->nslices * nb));
+      HIP_TRY(hipMalloc(&c->d_packets, pk_bytes));
+      if (c->two_pk) HIP_TRY(hipMalloc(&c->d_packets2, pk_bytes));
+      HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+    }
+  }
   if (free_b > rec_bytes + cb_bytes + margin) {
     if (hipMalloc(&c->d_rec2, rec_bytes) == hipSuccess && hipMalloc(&c->d_cbits2, cb_bytes) == hipSuccess) {
       c->two_rec = true;
@@ -1179,9 +1212,9 @@ static int alloc_rec2(ffv1hip_ctx* c) {
   }
   if (c->knobs.has("hostdbg"))
     std::fprintf(stderr, "hostdbg: decision sets %.2f / %.2f GB, %.2f GB free, second records set (%.2f GB + "
-                         "margin %.2f GB): %s\n", double(c->dcap[0]) / 1e9, double(c->dcap[1]) / 1e9,
+                         "margin %.2f GB): %s; slice budget %lld bytes\n", double(c->dcap[0]) / 1e9, double(c->dcap[1]) / 1e9,
                  double(free_b) / 1e9, double(rec_bytes + cb_bytes) / 1e9, double(margin) / 1e9,
-                 c->two_rec ? "yes" : "no");
+                 c->two_rec ? "yes" : "no", (long long)c->slice_cap);
   return 0;
 }
 
@@ -1227,14 +1260,24 @@ static int ensure_decisions(ffv1hip_ctx* c, int fb, int64_t need, uint2** rec, u
 }
 
 // A batch whose decision sets would be sized by decision_cap's guess (its
-// worst case is over 2^31 decisions) is sized from its content instead:
-// decision sets, the second records set and the slice byte budget
-// (dsets=eager|lazy overrides).
+// worst case is over 2^31 decisions) and that does not fit with both records
+// sets that way is sized from its content instead: decision sets, the
+// second records set and the slice byte budget (dsets=eager|lazy
+// overrides).  (One that fits allocates everything at create: none of it
+// lands in the first batches' time.)
+static int64_t device_bytes(const ffv1hip_ctx* c, int64_t nb);
 static bool lazy_sizing(const ffv1hip_ctx* c) {
   const int64_t nb = c->max_batch;
   const int64_t worst = nb * c->frame_samples * c->wmax + nb * c->nslices * kStreamSlack;
   const std::string ds = c->knobs.str("dsets");
-  return ds == "lazy" || (decision_cap(c, nb) < worst && ds != "eager");
+  if (ds == "lazy") return true;
+  const int64_t cap = decision_cap(c, nb);
+  if (ds == "eager" || cap >= worst) return false;
+  size_t free_b = 0, total_b = 0;
+  if (hipSetDevice(c->device) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) return true;
+  const int64_t rec2 = nb * (8 * c->frame_samples + 4 * int64_t(kChunkWords) * c->frame_chunks);
+  const int64_t eager = device_bytes(c, nb) + rec2 + cap / 2 + (int64_t(5) << 30);  // alloc_rec2's old margin
+  return eager > int64_t(free_b);
 }
 
 static int alloc_device(ffv1hip_ctx* c) {
@@ -1292,9 +1335,23 @@ static int alloc_device(ffv1hip_ctx* c) {
   HIP_TRY(hipMemcpy(c->d_nops, c->nops.data(), c->nops.size() * sizeof(int), hipMemcpyHostToDevice));
   HIP_TRY(hipMalloc(&c->d_segs, sizeof(Segment) * (nb + 1)));
   HIP_TRY(hipMalloc(&c->d_keys, nb));
-  HIP_TRY(hipMalloc(&c->d_slice_out, size_t(c->slice_stride) * c->nslices * nb));
+  if (hipMalloc(&c->d_slice_out, size_t(c->slice_stride) * c->nslices * nb) != hipSuccess ||
+      hipMalloc(&c->d_packets, size_t(c->packet_stride) * nb) != hipSuccess) {
+    // a large batch: at the budget it can go down to (what device_bytes counted)
+    (void)hipGetLastError();
+    for (uint8_t** q : {&c->d_slice_out, &c->d_packets}) {
+      if (*q) HIP_TRY(hipFree(*q));
+      *q = nullptr;
+    }
+    const int64_t cap = low_slice_cap(c);
+    if (cap >= c->slice_cap) return set_err(-12, "slice buffers for a %lld-byte budget", (long long)c->slice_cap);
+    c->slice_cap = cap;
+    c->slice_stride = slice_stride_frames(cap);
+    c->packet_stride = ((cap + 16) * c->nslices + 255) & ~int64_t(255);
+    HIP_TRY(hipMalloc(&c->d_slice_out, size_t(c->slice_stride) * c->nslices * nb));
+    HIP_TRY(hipMalloc(&c->d_packets, size_t(c->packet_stride) * nb));
+  }
   HIP_TRY(hipMalloc(&c->d_slice_bytes, sizeof(int64_t) * c->nslices * nb));
-  HIP_TRY(hipMalloc(&c->d_packets, size_t(c->packet_stride) * nb));
   HIP_TRY(hipMalloc(&c->d_packet_size, sizeof(int64_t) * nb));
   const size_t state_bytes = size_t(c->pcount) * c->contexts * 32;
   for (uint8_t*& pb : c->d_persist) {
@@ -1495,15 +1552,8 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
     c->frames_mode = p.ac && !p.colorspace && !p.transparency && p.version <= 3 && lds <= kWalkLdsMax &&
                      c->knobs.str("coder") != "chain";
     c->wmax = 2 * (p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample) + 1;
-    // a large batch, sized from what its content needs (lazy_sizing): the
-    // byte budget starts at a quarter (what noise needs is over it; a slice
-    // over the budget is encoded again with one sized from what it needed)
+    // a large batch, sized from what its content needs (lazy_sizing)
     c->lazy_sets = c->frames_mode && lazy_sizing(c);
-    if (c->lazy_sets && !c->knobs.has("slice_cap") && c->knobs.get("budget", 4) > 1) {
-      const int64_t q = c->knobs.get("budget", 4);
-      c->slice_cap = ((c->slice_cap - 4096) / q + 4096 + 255) & ~int64_t(255);
-      c->packet_stride = ((c->slice_cap + 16) * c->nslices + 255) & ~int64_t(255);
-    }
     // the decision-stream coder writes a slice's digits (the values of low,
     // 4 bytes each) where ffv1_sink then writes its bytes
     c->slice_stride = c->frames_mode ? slice_stride_frames(c->slice_cap) : c->slice_cap;
@@ -1865,6 +1915,9 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
           return set_err(-12, "decision buffers for %lld decisions: %s", (long long)need, g_err);
         sa.rec = d_rec;
         sa.cbits = d_cbits;
+        ca.slice_out = c->d_slice_out;  // (alloc_rec2 may have lowered the budget)
+        ca.slice_cap = c->slice_cap;
+        ca.slice_stride = c->slice_stride;
       }
     }
     HIP_TRY(hipEventRecord(c->laid[fb], sst));  // the records and the stream layout: the walk may start

@@ -93,13 +93,15 @@ def test_schedule_variants_match_oracle(debug, monkeypatch):
 
 
 @pytest.mark.parametrize("debug", ["dsets=lazy", "dsets=lazy,rec2_drop=1", "dsets=lazy,rec2_drop=0",
-                                   "dsets=eager,rec2_drop=0"])
+                                   "dsets=eager,rec2_drop=0", "dsets=lazy,budget=4", "dsets=lazy,budget=8,rec2_drop=1"])
 def test_lazy_decision_sets_match_oracle(debug, monkeypatch):
     """Decision sets sized from the first batches (dsets=lazy, the default
     for large batches), the second records set taken afterwards, and given
     back when a set has to grow (rec2_drop=k: as if set k did not fit beside
-    it; the batch's own records set is kept).  A flat first batch makes the
-    later random ones grow both sets."""
+    it; the batch's own records set is kept); budget=q: the slice byte budget
+    lowered to 1/q in the first batch (what happens when the second records
+    set does not fit), the random batches then re-encoded with a larger one.
+    A flat first batch makes the later random ones grow both sets."""
     monkeypatch.setenv("FFV1HIP_DEBUG", debug)
     s = Stream("lazy420", 176, 144, "yuv420p10", 9, slices=4, coder=1, gop_size=3, source="random", depth=10)
     frames = list(s.frames())
