@@ -119,7 +119,9 @@ void ffv1hip_destroy(ffv1hip_ctx *ctx);
  * bytes for version < 2.  Returns the size or a negative error. */
 int ffv1hip_extradata(ffv1hip_ctx *ctx, uint8_t *buf, int cap);
 
-/* Upper bound of one packet produced by this context. */
+/* Upper bound of one packet produced by this context: the slice byte budget
+ * times the slices.  It grows after a budget re-encode, and a large batch
+ * that lowers its budget to make room in HBM (its first batch) lowers it. */
 int64_t ffv1hip_max_packet_size(const ffv1hip_ctx *ctx);
 
 /* AVCodec.encode2 over a batch (ffv1enc.c:1222 encode_frame, called once
