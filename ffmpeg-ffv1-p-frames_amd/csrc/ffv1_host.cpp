@@ -141,10 +141,21 @@ static const char* const kKnobNames[] = {"serial",     "walkdbg",    "walktrace"
                                          "range_prio", "dseg_prio",  "sym_grid",  "bits_grid", "dseg_grid",
                                          "walk_split", "copy_threads", "dec_swap", "coder",    "dense", "walk_blocks",
                                          "recsets",    "slice_cap",  "walk_part_a", "force_multi", "bounds_shrink", "range_split", "rd_grid",
-                                         "dsets", "rec2_drop", "budget", "pack"};
+                                         "dsets", "rec2_drop", "budget", "pack", "v4_cap0"};
+
+extern "C" char** environ;
 
 static int parse_knobs(Knobs* k) {
   k->kv.clear();
+  // the per-hook variables of earlier rounds (FFV1HIP_DENSE, FFV1HIP_CODER,
+  // ...) are no longer read: one set is an error, not a silent default
+  for (char** ev = environ; ev && *ev; ev++) {
+    const std::string v(*ev);
+    if (v.rfind("FFV1HIP_", 0) != 0) continue;
+    const std::string name = v.substr(0, v.find('='));
+    if (name != "FFV1HIP_DEBUG" && name != "FFV1HIP_LIB" && name != "FFV1HIP_ARCH")
+      return set_err(-22, "%s is not read: hooks go in FFV1HIP_DEBUG=name[=value],...", name.c_str());
+  }
   const char* e = std::getenv("FFV1HIP_DEBUG");
   if (!e) return 0;
   std::string all(e);
@@ -1849,6 +1860,9 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   ca.v4pcm = p.version > 3 && p.ac;
   ca.v4_cap0 = 16384 + int64_t(p.width) * p.height * 12;
   ca.v4_cap = ca.v4_cap0 / c->nslices;
+  // (v4_cap0=bytes, test hook: a smaller buffer for slice 0 alone, so that it
+  // re-codes as PCM too; the oracle's FFV1_ORACLE_V4_CAP0)
+  if (c->knobs.has("v4_cap0")) ca.v4_cap0 = c->knobs.get("v4_cap0", 0);
   ca.frames = d_frames;
   ca.frame_bytes = frame_bytes;
   for (int k = 0; k < kMaxPlanes; k++) {
@@ -3158,6 +3172,15 @@ int64_t ffv1hip_get_slice_states_device(ffv1hip_ctx* c, void* d_buf, int64_t cap
   hipStream_t const s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
   if (c->dep_valid) HIP_TRY(hipStreamWaitEvent(s, c->done_ev, 0));
   HIP_TRY(hipMemcpyAsync(d_buf, c->d_persist[c->pcur], size_t(n), hipMemcpyDeviceToDevice, s));
+  if (s != c->stream) {
+    // the context's next batches rewrite d_persist[pcur] (two batches on):
+    // they start after this read on the caller's stream
+    if (!c->xchg_ev) HIP_TRY(hipEventCreateWithFlags(&c->xchg_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(c->xchg_ev, s));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->xchg_ev, 0));
+    HIP_TRY(hipEventRecord(c->dep_ev, c->stream));
+    c->dep_valid = true;
+  }
   return n;
 }
 
@@ -3178,6 +3201,9 @@ int ffv1hip_set_slice_states_device(ffv1hip_ctx* c, const void* d_buf, int64_t s
   HIP_TRY(hipEventRecord(c->done_ev, c->stream));
   c->dep_valid = true;
   c->have_states = true;
+  // ... and so does the caller's stream: d_buf may be reused on it once the
+  // copy has read it (include/ffv1hip.h)
+  if (stream) HIP_TRY(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), c->done_ev, 0));
   return 0;
 }
 

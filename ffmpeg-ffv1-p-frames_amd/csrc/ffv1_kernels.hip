@@ -685,8 +685,10 @@ __device__ __forceinline__ void run_header_ops(const CodeArgs& a, Lane& L, SinkT
                                                int slice, bool live, const uint8_t* dtab,
                                                const uint8_t* ftab, int osb, int flush_at, int f,
                                                int q0 = 0, int q1 = kMaxOps, bool pcm = false) {
-  if (q0 == 0)
-    for (int i = 0; i < osb; i++) os[i] = 128;
+  // fresh op states (encode_slice_header's state[32] = 128, ffv1enc.c:1031);
+  // slice 0's PCM re-run (q0 past the key bit) keeps only the key bit's set 0
+  if (q0 == 0 || pcm)
+    for (int i = q0 == 0 ? 0 : 32; i < osb; i++) os[i] = 128;
   const int sel = key * a.nslices + slice;
   const int n = live ? min(a.nops[sel], q1) : 0;
   const Op* ops = a.ops + (int64_t)sel * kMaxOps;
@@ -2702,7 +2704,15 @@ int walk_block_waves(int nsegs, int nslices, int per_short, int short_multi, int
   const int nsingle = walk_items(nsegs, nslices, per_short, short_multi) - nfull;
   if (nfull > 4 * cus || nsingle > cus) return 1;
   const int w = nsingle > 0 ? 5 : 4;
-  return walk_block_lds_dev(rows, w) <= 160 * 1024 ? w : 1;
+  // the block's LDS against the device's (not the 160 KB of gfx950: a part
+  // with less falls back to one-wave blocks instead of failing the launch)
+  int dev = 0, lds = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return 1;
+  }
+  return walk_block_lds_dev(rows, w) <= lds ? w : 1;
 }
 
 int walk_items(int nsegs, int nslices, int per_short, int short_multi) {

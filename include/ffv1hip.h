@@ -244,11 +244,12 @@ int     ffv1hip_set_picture_number(ffv1hip_ctx *ctx, int64_t picture_number);
  * with no host staging).  get: once the last call's batch is settled (its
  * slice budget checked), a device-to-device copy into d_buf is queued on
  * `stream` (a hipStream_t; NULL: the context's own), ordered after the
- * batch; returns the byte count (or the size needed when d_buf is NULL).
+ * batch, and the context's later batches are ordered after that copy;
+ * returns the byte count (or the size needed when d_buf is NULL).
  * set: the context's next frames start from the states at d_buf, copied on
  * the context's stream once the work queued so far on `stream` is done;
- * the caller may reuse d_buf once `stream` passes a later event, the
- * context's next call sees the states. */
+ * work queued on `stream` after the call runs after the copy (d_buf may be
+ * rewritten there), and the context's next call sees the states. */
 int64_t ffv1hip_get_slice_states_device(ffv1hip_ctx *ctx, void *d_buf,
                                         int64_t cap, void *stream);
 int     ffv1hip_set_slice_states_device(ffv1hip_ctx *ctx, const void *d_buf,

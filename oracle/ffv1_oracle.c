@@ -805,6 +805,11 @@ ffv1o_enc *ffv1o_enc_new(const ffv1o_config *cfg)
          * touched as far as used */
         const int64_t pkt = 16384 + (int64_t)cfg->width * cfg->height * (cfg->version > 3 ? 12 : 140);
         s->cap = i == 0 ? pkt : pkt / e->nslices;
+        /* test hook: a smaller v4 buffer for slice 0 alone, so that it fails
+         * the 35 * w check too (the HIP encoder's FFV1HIP_DEBUG=v4_cap0) */
+        const char *hook = getenv("FFV1_ORACLE_V4_CAP0");
+        if (hook && cfg->version > 3 && i == 0)
+            s->cap = atoll(hook);
         s->buf = malloc(s->cap);
         for (int p = 0; p < e->plane_count; p++) {
             s->ps[p].rac = malloc((size_t)e->contexts * 32);

@@ -112,6 +112,20 @@ def test_unsupported_parameters_are_refused():
     assert e.value.code == -38
 
 
+@pytest.mark.parametrize("var,val,msg", [("FFV1HIP_DENSE", "0", "FFV1HIP_DENSE is not read"),
+                                          ("FFV1HIP_DEBUG", "walk_prio=1,no_such_hook", "unknown hook")])
+def test_hooks_misspelt_or_legacy_are_refused(var, val, msg, monkeypatch):
+    """Measurement hooks go through FFV1HIP_DEBUG=name[=value],... only: an
+    unknown name there, or one of the per-hook variables of earlier rounds,
+    fails create (before any GPU work) instead of silently measuring the
+    default."""
+    from ffv1hip import configure, HipEncoder, FFV1Error
+    monkeypatch.setenv(var, val)
+    with pytest.raises(FFV1Error) as e:
+        HipEncoder(configure(352, 288, "yuv420p", coder=1, slices=4), 0, 1)
+    assert e.value.code == -22 and msg in str(e.value)
+
+
 def test_decoder_contract_checks_before_the_gpu():
     """ffv1hip_dec_create refuses what the GPU decoder does not decode
     (-ENOSYS) and extradata the parameters would not produce

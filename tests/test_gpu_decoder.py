@@ -126,7 +126,55 @@ def test_hip_decoder_conceals_like_oracle(stream):
             np.testing.assert_array_equal(a, b, err_msg=f"frame {i}")
 
 
-def test_hip_encode_decode_4k_p10_roundtrip():
+def _swap_slices(packet: bytes, ec: bool, nslices: int, i: int, j: int) -> bytes:
+    """The packet with the coded slices at positions i and j exchanged, each
+    with its own trailer (size, and with ec its CRC, which stays valid)."""
+    trailer = 3 + (5 if ec else 0)
+    end, chunks = len(packet), []
+    for _ in range(nslices):
+        size = int.from_bytes(packet[end - trailer:end - trailer + 3], "big")
+        chunks.append(packet[end - trailer - size:end])
+        end -= size + trailer
+    chunks.reverse()
+    assert end == 0
+    chunks[i], chunks[j] = chunks[j], chunks[i]
+    return b"".join(chunks)
+
+
+def test_hip_decoder_header_naming_another_slice_diverges():
+    """The one documented divergence ("Known reference quirks"):
+    a slice header that parses but names another slice's rectangle.  Slices
+    1 and 2 of a keyframe exchanged (CRCs intact, no key bit in either):
+    the reference decoder decodes each slice into the rectangle its header
+    names with the states of the slice position (ffv1dec.c:282-359, 410-419),
+    which a keyframe has just reset, so the oracle decoder returns the input
+    picture exactly; the GPU decoder counts both headers as failed, leaves
+    the two rectangles undecoded and reports them damaged, and decodes every
+    other slice as the oracle does."""
+    from ffv1hip import HipDecoder
+    from helpers import slice_rect
+    s = Stream("swap", 192, 96, "yuv420p10", 1, slices=6, gop_size=1, source="random", depth=10)
+    frames = list(s.frames())
+    cfg, ex, pkts = oracle_encode(s, frames)
+    ns = cfg.num_h_slices * cfg.num_v_slices
+    bad = _swap_slices(pkts[0][0], True, ns, 1, 2)
+    assert bad != pkts[0][0] and len(bad) == len(pkts[0][0])
+    want, key = oracle.Decoder(cfg, ex).decode(bad)
+    assert key
+    for a, b in zip(want, frames[0]):  # the reference's behaviour: decoded into the named rectangles
+        np.testing.assert_array_equal(a, b)
+    hdec = HipDecoder(hip_params(s), ex, 0)
+    (got, k), = hdec.decode([bad])
+    assert k and hdec.damaged_slices == 2
+    hdec.close()
+    mask = np.zeros((s.height, s.width), bool)
+    for i in (1, 2):
+        x0, y0, x1, y1 = slice_rect(cfg, i)
+        mask[y0:y1, x0:x1] = True
+    # luma: equal outside the two rectangles, different inside (left undecoded)
+    np.testing.assert_array_equal(got[0][~mask], want[0][~mask])
+    assert (got[0][mask] != want[0][mask]).mean() > 0.9
+
     """BASELINE configs[2] at full size: HIP encoder -> HIP decoder is lossless."""
     from ffv1hip import HipDecoder, HipEncoder
     s = Stream("c3", 3840, 2160, "yuv420p10", 4, slices=64, gop_size=3, source="d2", depth=10)

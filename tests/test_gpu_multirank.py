@@ -165,3 +165,45 @@ def test_exchange_step_device_resident_states():
     for i in range(N):
         h.update(local[i][0])
     assert h.hexdigest() == _pin()["stream_md5"]
+
+
+def test_set_slice_states_device_orders_the_callers_stream():
+    """ffv1hip_set_slice_states_device copies d_buf on the context's stream;
+    the caller's stream is ordered after that copy (include/ffv1hip.h), so a
+    buffer rewritten on it right after the call (an RCCL receive into the
+    same tensor, a caching-allocator reuse) never reaches the context: the
+    continued stream equals one encoder's over the whole GOP.  And the
+    snapshot taken on a caller stream is not overwritten by the context's
+    later batches."""
+    import numpy as np
+    import torch
+    from ffv1hip import HipEncoder, configure, load_library, synth
+    params = configure(480, 270, "yuv420p10", slices=4, coder=1, gop_size=12)
+    frames = list(synth.videogen_frames(480, 270, 12, depth=10))
+    ref = HipEncoder(params, 0, 12)
+    want = ref.encode(frames)
+    ref.close()
+    a = HipEncoder(params, 0, 7)
+    a.encode(frames[:7])
+    n = a.state_bytes()
+    side = torch.cuda.Stream()
+    snap = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    with torch.cuda.stream(side):
+        a.get_slice_states_device(snap)
+        host_snap = snap.cpu().numpy()
+    a.encode(frames[:5])  # the context's next batches rewrite both carry buffers
+    a.encode(frames[:5])
+    torch.cuda.synchronize()
+    assert np.array_equal(host_snap, snap.cpu().numpy())
+    a.close()
+    b = HipEncoder(params, 0, 5)
+    buf = snap.clone()
+    L = load_library()
+    with torch.cuda.stream(side):
+        rc = L.ffv1hip_set_slice_states_device(b._h, buf.data_ptr(), n, side.cuda_stream)
+        assert rc == 0
+        buf.zero_()  # queued on the caller's stream right after the call
+    assert L.ffv1hip_set_picture_number(b._h, 7) == 0
+    got = b.encode(frames[7:12])
+    b.close()
+    assert got == want[7:12]

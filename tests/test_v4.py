@@ -210,3 +210,45 @@ def test_gpu_decoder_v4_pcm_slices(case):
     pkts = [enc.encode(f) for f in frames]
     p = configure(w, h, pix_fmt, slices=slices, level=4, coder=1, gop_size=3, experimental=True)
     gpu_decode_vs_oracle(p, cfg, enc.extradata(), pkts, frames)
+
+
+# Slice 0 owns the whole v4 packet and never fails the 35 * w check at real
+# sizes; a test hook lowers its buffer alone (oracle: FFV1_ORACLE_V4_CAP0,
+# HIP: FFV1HIP_DEBUG=v4_cap0) so that slice 0 re-codes as PCM: the re-code
+# restarts after the key bit with a fresh slice-header state (ffv1enc.c:1031,
+# 1157, 1207-1217).  (case, slice 0's buffer bytes)
+PCM0_CASES = [(("gbrp14", 376, 8, 4, False), 10250), (("yuv444p16", 340, 8, 4, True), 10000)]
+PCM0_IDS = [f"{c[0][0]}_{c[0][1]}x{c[0][2]}{'_mixed' if c[0][4] else ''}" for c in PCM0_CASES]
+
+
+@pytest.mark.parametrize("case,cap0", PCM0_CASES, ids=PCM0_IDS)
+def test_oracle_v4_pcm_slice0_roundtrip(case, cap0, monkeypatch):
+    monkeypatch.setenv("FFV1_ORACLE_V4_CAP0", str(cap0))
+    cfg, frames = _pcm_frames(*case, n=4)
+    enc = oracle.Encoder(cfg)
+    pkts, modes = [], []
+    for f in frames:
+        pkts.append(enc.encode(f))
+        modes.append(enc.last_slice_pcm())
+    assert modes[0][0] == 1 and modes[2][0] == 1
+    _lossless(cfg, enc.extradata(), pkts, frames)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,cap0", PCM0_CASES, ids=PCM0_IDS)
+def test_hip_v4_pcm_slice0_matches_oracle(case, cap0, monkeypatch):
+    """Slice 0 re-coded as PCM (its buffer lowered by the hooks): the HIP
+    packets equal the oracle's (parity unpinned)."""
+    from ffv1hip import HipEncoder, configure
+    monkeypatch.setenv("FFV1_ORACLE_V4_CAP0", str(cap0))
+    monkeypatch.setenv("FFV1HIP_DEBUG", f"v4_cap0={cap0}")
+    pix_fmt, w, h, slices, mixed = case
+    cfg, frames = _pcm_frames(*case, n=4)
+    enc = oracle.Encoder(cfg)
+    ref = [enc.encode(f) for f in frames]
+    p = configure(w, h, pix_fmt, slices=slices, level=4, coder=1, gop_size=3, experimental=True)
+    henc = HipEncoder(p, 0, 2)
+    got = henc.encode(frames)
+    henc.close()
+    for i, (g, r) in enumerate(zip(got, ref)):
+        assert g == r, f"frame {i}"
