@@ -278,6 +278,176 @@ __device__ inline void decode_row_u(RacDec& c, uint8_t* st8, const sconst_i32* s
   }
 }
 
+// The range-coded rows on the vector units: the same chain on every lane in
+// VGPRs (the compiler sees LDS-loaded, hence per-lane, values), so the CU's
+// chains code on their SIMDs' VALUs in parallel instead of queueing on the
+// CU's one scalar unit (six chains per CU: the scalar version spent ~100 CU
+// cycles per decision, 6.6 s for a 288-frame 4K batch).  A decision reads
+// its state from the row image (registers), looks its successor pair up in
+// the LDS table off the decision chain, and a row's image is written back by
+// lane 0 once per symbol.
+__device__ __forceinline__ uint32_t vreg(uint32_t v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ uint64_t vreg(uint64_t v) { return (uint64_t(vreg(uint32_t(v >> 32))) << 32) | vreg(uint32_t(v)); }
+__device__ __forceinline__ int64_t vreg(int64_t v) { return int64_t(vreg(uint64_t(v))); }
+
+// lane 0's coder (after the slice header) on every lane, in VGPRs
+__device__ __forceinline__ void vec_coder(RacDec& c) {
+  c.low = vreg(uni(c.low));
+  c.range = vreg(uni(c.range));
+  c.ptr = vreg(uni(c.ptr));
+  c.end = vreg(uni(c.end));
+  c.wi = vreg(uni(c.wi));
+  c.w0 = vreg(uni(c.w0));
+  c.w1 = vreg(uni(c.w1));
+}
+
+__device__ __forceinline__ int get_v(RacDec& c, uint32_t src, uint32_t& dst, int SH, const uint16_t* tt,
+                                     const uint64_t* w) {
+  const uint32_t s = (src >> SH) & 0xFFu;
+  const uint32_t pair = tt[s];  // to0 | to1 << 8, for the row image only
+  const uint32_t r1 = (c.range * s) >> 8;
+  const uint32_t rr = c.range - r1;
+  const int bit = c.low >= rr;
+  c.low -= bit ? rr : 0u;
+  c.range = bit ? r1 : rr;
+  const uint32_t ns = bit ? pair >> 8 : pair & 0xFFu;
+  dst = (dst & ~(0xFFu << SH)) | (ns << SH);
+  if (c.range < 0x100) rac_refill(c, w);
+  return bit;
+}
+
+template <int K>
+__device__ __forceinline__ int get_kv(RacDec& c, const uint32_t (&r)[8], uint32_t (&n)[8], const uint16_t* tt,
+                                      const uint64_t* w) {
+  return get_v(c, r[K >> 2], n[K >> 2], (K & 3) * 8, tt, w);
+}
+
+template <int K>
+__device__ __forceinline__ void unary_v(RacDec& c, const uint32_t (&r)[8], uint32_t (&n)[8], int& e,
+                                        const uint16_t* tt, const uint64_t* w) {
+  if constexpr (K <= 9) {
+    if (get_kv<K>(c, r, n, tt, w)) {
+      e = K;
+      unary_v<K + 1>(c, r, n, e, tt, w);
+    }
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void mant_v(RacDec& c, const uint32_t (&r)[8], uint32_t (&n)[8], int e, uint32_t& a,
+                                       const uint16_t* tt, const uint64_t* w) {
+  if constexpr (K >= 0) {
+    if (K < e) a = 2 * a + uint32_t(get_kv<22 + K>(c, r, n, tt, w));
+    mant_v<K - 1>(c, r, n, e, a, tt, w);
+  }
+}
+
+// get_symbol_inline (ffv1dec.c:44-66), signed, on the row at `row` (LDS)
+__device__ inline int symbol_v(RacDec& c, uint8_t* row, const uint16_t* tt, const uint64_t* w) {
+  const uint4* r4 = reinterpret_cast<const uint4*>(row);
+  const uint4 a0 = r4[0], a1 = r4[1];
+  const uint32_t r[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+  uint32_t n[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) n[i] = r[i];
+  int ret;
+  if (get_kv<0>(c, r, n, tt, w)) {
+    ret = 0;
+  } else {
+    int e = 0;
+    unary_v<1>(c, r, n, e, tt, w);
+    bool bad = false;
+    if (e == 9) {  // slot 10 for the rest of the run: its state from n after its first decision
+      uint32_t src = r[2];
+      while (get_v(c, src, n[2], 16, tt, w)) {
+        src = n[2];
+        if (++e > 31) {
+          bad = true;
+          break;
+        }
+      }
+    }
+    if (bad) {
+      ret = kInvalidData;
+    } else {
+      uint32_t a = 1, src = r[7];
+      for (int i = e - 1; i >= 9; i--) {  // slot 31
+        a = 2 * a + uint32_t(get_v(c, src, n[7], 24, tt, w));
+        src = n[7];
+      }
+      mant_v<8>(c, r, n, e, a, tt, w);
+      const int j = 11 + (e < 10 ? e : 10);  // the sign slot, row words 2..5
+      const int sh = (j & 3) * 8;
+      int sg;
+      switch (j >> 2) {
+        case 2: sg = get_v(c, r[2], n[2], sh, tt, w); break;
+        case 3: sg = get_v(c, r[3], n[3], sh, tt, w); break;
+        case 4: sg = get_v(c, r[4], n[4], sh, tt, w); break;
+        default: sg = get_v(c, r[5], n[5], sh, tt, w); break;
+      }
+      ret = sg ? int(0u - a) : int(a);
+    }
+  }
+  if (threadIdx.x == 0) {
+    uint4* const o4 = reinterpret_cast<uint4*>(row);
+    o4[0] = make_uint4(n[0], n[1], n[2], n[3]);
+    o4[1] = make_uint4(n[4], n[5], n[6], n[7]);
+  }
+  return ret;
+}
+
+// decode_line (ffv1dec.c:42-117), range coder, by the whole wave on
+// per-lane copies of the same values (see symbol_v); quant tables in LDS
+__device__ inline void decode_row_v(RacDec& c, uint8_t* st8, const uint16_t* tt, const uint64_t* pkw,
+                                    const int16_t* qt, bool model1, int16_t* cur, const int16_t* up, int w,
+                                    int bits) {
+  const int mask = int((1u << bits) - 1u);
+  int T = up[0];
+  const int T0 = T;
+  int L = T;
+  int LT = cur[0];
+  int RT = w > 1 ? up[1] : T;
+  for (int x = 0; x < w; x++) {
+    const int RTn = x + 2 < w ? up[x + 2] : (x + 1 < w ? RT : T);  // the next sample's, read a sample ahead
+    int ctx = qt[(L - LT) & 0xFF] + qt[256 + ((LT - T) & 0xFF)] + qt[512 + ((T - RT) & 0xFF)];
+    if (model1) {
+      const int LL = x >= 2 ? int(cur[x - 2]) : (x == 1 ? T0 : 0);
+      const int TT = cur[x];
+      ctx += qt[768 + ((LL - L) & 0xFF)] + qt[1024 + ((TT - T) & 0xFF)];
+    }
+    const int actx = ctx < 0 ? -ctx : ctx;
+    int diff = symbol_v(c, st8 + actx * 32, tt, pkw);
+    if (ctx < 0) diff = -diff;
+    const int pred = median3u(L, L + T - LT, T);
+    const int v = int(int16_t((pred + diff) & mask));
+    if (threadIdx.x == 0) cur[x] = int16_t(v);
+    LT = T;
+    T = RT;
+    RT = RTn;
+    L = v;
+  }
+}
+
+// decode_line's PCM mode on vector registers (see decode_row_pcm_u)
+__device__ inline void decode_row_pcm_v(RacDec& c, const uint64_t* pkw, int16_t* cur, int w, int bits) {
+  for (int x = 0; x < w; x++) {
+    int v = 0;
+    for (int i = 0; i < bits; i++) {
+      const uint32_t r1 = (c.range * 128u) >> 8;
+      const uint32_t rr = c.range - r1;
+      const int bit = c.low >= rr;
+      c.low -= bit ? rr : 0u;
+      c.range = bit ? r1 : rr;
+      if (c.range < 0x100) rac_refill(c, pkw);
+      v = 2 * v + bit;
+    }
+    if (threadIdx.x == 0) cur[x] = int16_t(v);
+  }
+}
+
 // decode_line's slice_coding_mode 1 (version 4 PCM, ffv1dec.c:111-120): every
 // sample's bits MSB first, each on a fresh state 128; uniform like
 // decode_row_u
@@ -478,7 +648,11 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
   uint16_t* const dtt = tt + 256;                              // [256] default table
   uint8_t* const hdr = reinterpret_cast<uint8_t*>(dtt + 256);  // [32] header states, [32] scratch
   int16_t* const qt = reinterpret_cast<int16_t*>(hdr + 64);    // [5][256]
-  int16_t* const ring = qt + 5 * 256;                          // [rgb ? 3 : 1][2][row_cap]
+  // [5][256] with context model 1, [3][256] otherwise (its LL / TT tables
+  // unused): 1 KB less per chain, so that six chains fit on a CU (a 24-GOP
+  // 4K batch, 1536 chains, then decodes in one round instead of two)
+  const int nq = a.context_model ? 5 : 3;
+  int16_t* const ring = qt + nq * 256;                         // [rgb ? 3 : 1][2][row_cap]
   __shared__ int bad;
   __shared__ int s_reset, s_pcm, s_by, s_ry;  // v4 slice header: reset, slice_coding_mode, RCT coefficients
   const uint64_t* pkw = reinterpret_cast<const uint64_t*>(a.pkts);
@@ -486,7 +660,7 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
     tt[i] = uint16_t(a.ftab[i] | (a.ftab[256 + i] << 8));
     dtt[i] = uint16_t(a.dtab[i] | (a.dtab[256 + i] << 8));
   }
-  for (int i = lane; i < 5 * 256; i += kDecThreads) qt[i] = a.qt[i];
+  for (int i = lane; i < nq * 256; i += kDecThreads) qt[i] = a.qt[i];
   const int bits = a.coded_bits;
   const bool model1 = a.context_model != 0;
   const int64_t words = a.state_bytes / 4;
@@ -606,7 +780,7 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
       br.cache = 0;
       br.nc = 0;
     }
-    if constexpr (!GOLOMB) uni_coder(c);  // lane 0's coder after the header, to every lane
+    if constexpr (!GOLOMB) vec_coder(c);  // lane 0's coder after the header, to every lane
     int run_index = 0;
     uint8_t* const obase = a.out + int64_t(f) * a.frame_bytes;
     const int64_t per = a.state_bytes / a.pcount;  // one plane context's states
@@ -646,9 +820,9 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
           const int16_t* up = ring + ((y + 1) & 1) * a.row_cap;
           if constexpr (!GOLOMB) {
             if (pcm)
-              decode_row_pcm_u(c, pkw, cur, w, bits);
+              decode_row_pcm_v(c, pkw, cur, w, bits);
             else
-              decode_row_u(c, pst, (const sconst_i32*)(a.stab), pkw, model1, cur, up, w, bits);
+              decode_row_v(c, pst, tt, pkw, qt, model1, cur, up, w, bits);
           } else if (lane == 0) {
             decode_row<GOLOMB>(c, br, pst, reinterpret_cast<uint64_t*>(pst), tt, pkw, qt, model1, cur, up, w, bits,
                                run_index);
@@ -684,9 +858,9 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
           const int16_t* up = ring + (2 * p + ((y + 1) & 1)) * a.row_cap;
           if constexpr (!GOLOMB) {
             if (pcm)
-              decode_row_pcm_u(c, pkw, cur, w, pbits);
+              decode_row_pcm_v(c, pkw, cur, w, pbits);
             else
-              decode_row_u(c, pst, (const sconst_i32*)(a.stab), pkw, model1, cur, up, w, bits);
+              decode_row_v(c, pst, tt, pkw, qt, model1, cur, up, w, bits);
           } else if (lane == 0) {
             decode_row<GOLOMB>(c, br, pst, reinterpret_cast<uint64_t*>(pst), tt, pkw, qt, model1, cur, up, w, bits,
                                run_index);
@@ -786,7 +960,8 @@ __global__ void __launch_bounds__(256) ffv1_conceal(DecodeArgs a) {
 
 int64_t decode_lds_bytes(const DecodeArgs& a, bool global_states) {
   const int64_t sb = global_states ? 0 : ((a.swap ? a.state_bytes / 2 : a.state_bytes) + 15) & ~int64_t(15);
-  return sb + 1024 + 64 + 5 * 256 * 2 + int64_t(a.rgb ? 2 * (3 + (a.transparency ? 1 : 0)) : 2) * a.row_cap * 2;
+  return sb + 1024 + 64 + (a.context_model ? 5 : 3) * 256 * 2 +
+         int64_t(a.rgb ? 2 * (3 + (a.transparency ? 1 : 0)) : 2) * a.row_cap * 2;
 }
 
 int launch_decode(const DecodeArgs& a, int nsegs, void* stream) {

@@ -141,7 +141,7 @@ static const char* const kKnobNames[] = {"serial",     "walkdbg",    "walktrace"
                                          "range_prio", "dseg_prio",  "sym_grid",  "bits_grid", "dseg_grid",
                                          "walk_split", "copy_threads", "dec_swap", "coder",    "dense", "walk_blocks",
                                          "recsets",    "slice_cap",  "walk_part_a", "force_multi", "bounds_shrink", "range_split", "rd_grid",
-                                         "dsets", "rec2_drop", "budget", "pack", "v4_cap0"};
+                                         "dsets", "rec2_drop", "budget", "pack", "v4_cap0", "readback"};
 
 extern "C" char** environ;
 
@@ -153,7 +153,7 @@ static int parse_knobs(Knobs* k) {
     const std::string v(*ev);
     if (v.rfind("FFV1HIP_", 0) != 0) continue;
     const std::string name = v.substr(0, v.find('='));
-    if (name != "FFV1HIP_DEBUG" && name != "FFV1HIP_LIB" && name != "FFV1HIP_ARCH")
+    if (name != "FFV1HIP_DEBUG" && name != "FFV1HIP_LIB" && name != "FFV1HIP_ARCH" && name != "FFV1HIP_SYNTH_LIB")
       return set_err(-22, "%s is not read: hooks go in FFV1HIP_DEBUG=name[=value],...", name.c_str());
   }
   const char* e = std::getenv("FFV1HIP_DEBUG");
@@ -480,6 +480,13 @@ struct ffv1hip_ctx {
   int64_t* d_dbase = nullptr;    // 3 x [batch frame][slice] first decision of each stream
   int64_t* d_dtotal = nullptr;   // [3] decisions of the batch (incl. alignment)
   int64_t* h_dtotal = nullptr;   // pinned readback of d_dtotal
+  // the totals as the layout kernels leave them, in mapped host memory, and
+  // the frames of the batch in each metadata set: the estimate that lets a
+  // batch launch without waiting for its own total (a guarded launch)
+  int64_t* h_tot_map = nullptr;
+  int64_t* hd_tot_map = nullptr;
+  int tri_n[3] = {0, 0, 0};
+  bool no_guard_once = false;    // the next run_batch sizes its set from the read-back total
   uint8_t* d_pre[2] = {nullptr, nullptr};    // [decision] state before the decision
   uint8_t* d_scratch = nullptr;               // where idle walk chains write their stage
   uint32_t* d_bounds = nullptr;               // debug build: the first out-of-bounds write's site (sticky)
@@ -1080,6 +1087,7 @@ static void free_device(ffv1hip_ctx* c) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_dtotal) (void)hipHostFree(c->h_dtotal);
+  if (c->h_tot_map) (void)hipHostFree(c->h_tot_map);
   for (hipEvent_t& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t& e : c->kev)
@@ -1384,6 +1392,9 @@ static int alloc_device(ffv1hip_ctx* c) {
     HIP_TRY(hipMalloc(&c->d_dbase, 3 * sizeof(int64_t) * size_t(nb) * c->nslices));
     HIP_TRY(hipMalloc(&c->d_dtotal, 3 * sizeof(int64_t)));
     HIP_TRY(hipHostMalloc(&c->h_dtotal, 3 * sizeof(int64_t), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(&c->h_tot_map, 3 * sizeof(int64_t), hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->hd_tot_map), c->h_tot_map, 0));
+    for (int k = 0; k < 3; k++) c->h_tot_map[k] = 0;
     for (hipEvent_t& e : c->coded3) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->walk_a, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->walk_go, hipEventDisableTiming));
@@ -1618,11 +1629,10 @@ int ffv1hip_set_pass(ffv1hip_ctx* c, int pass, const char* stats_in) {
   if (p.version < 2) return set_err(-22, "2-pass needs version >= 2 (ffv1hip_options.pass)");
   HIP_TRY(hipSetDevice(c->device));
   if (pass == 1) {
-    // the range coder's counts come from the decision stream (the
-    // frame-parallel mode); Golomb-Rice codes no range decisions and
-    // writes zero counts, as the reference does
-    if (p.ac && !c->frames_mode)
-      return set_err(-38, "pass-1 statistics need the frame-parallel range coder (YCbCr, context model 0)");
+    // the range coder's counts: from the decision stream in the
+    // frame-parallel mode, by the chained coder as it codes otherwise
+    // (context model 1, RGB, alpha, version 4); Golomb-Rice codes no range
+    // decisions and writes zero counts, as the reference does
     const size_t bytes = sizeof(unsigned long long) * (512 + size_t(64) * c->contexts);
     HIP_TRY(hipMalloc(&c->d_rcstat, bytes));
     HIP_TRY(hipMalloc(&c->d_rcstat_bak, bytes));
@@ -1910,12 +1920,33 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     sa.max_blocks = c->grid_sym;
     if (timed(0, sst, [&] { return launch_symbols(sa, sst); }) < 0)
       return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
+    // this batch's decisions, estimated from the earlier batches' totals
+    // (per frame, the largest of the other two metadata sets, + 1/8), before
+    // its layout overwrites its own set's
+    int64_t est = 0;
+    for (int k = 0; k < 3; k++)
+      if (k != t3 && c->tri_n[k] > 0) est = std::max(est, c->h_tot_map[k] / c->tri_n[k]);
+    est = est ? est * n + est * n / 8 + int64_t(n) * c->nslices * kStreamSlack : 0;
+    c->tri_n[t3] = n;
     if (timed(4, sst, [&] {
-          return launch_layout(d_dcount, n * c->nslices, d_dbase, c->d_dtotal + t3, d_segs, d_segtot, d_wmap, sst);
+          return launch_layout(d_dcount, n * c->nslices, d_dbase, c->d_dtotal + t3, d_segs, d_segtot, d_wmap,
+                               c->hd_tot_map + t3, sst);
         }) < 0)
       return set_err(-5, "layout launch failed: %s", hipGetErrorString(hipGetLastError()));
-    // decisions of this batch: the worst case fits without asking the device
+    // decisions of this batch: the worst case fits without asking the device;
+    // else, when the estimate fits the set as it is, the batch launches
+    // guarded (its kernels skip it if its total does not fit after all, and
+    // it is encoded again at settle, ds_over) without waiting for its
+    // layout: the host goes on staging the next batch meanwhile.  Pass 1
+    // (one count snapshot) and the readback=1 hook always read the total back.
     int64_t need = int64_t(n) * c->frame_samples * c->wmax + int64_t(n) * c->nslices * kStreamSlack;
+    bool guarded = false;
+    if (need > c->dcap[fb] && est > 0 && est <= c->dcap[fb] && c->pass != 1 && !c->no_guard_once &&
+        !c->knobs.has("readback")) {
+      guarded = true;
+      need = c->dcap[fb];
+    }
+    c->no_guard_once = false;
     if (need > c->dcap[fb]) {
       HIP_TRY(hipMemcpyAsync(c->h_dtotal + t3, c->d_dtotal + t3, sizeof(int64_t), hipMemcpyDeviceToHost, sst));
       HIP_TRY(hipStreamSynchronize(sst));
@@ -1936,8 +1967,14 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     }
     HIP_TRY(hipEventRecord(c->laid[fb], sst));  // the records and the stream layout: the walk may start
     if (sst != st) HIP_TRY(hipStreamWaitEvent(sst, c->pre_read[fb], 0));  // d_bits[fb]: range / dseg of batch k-2
-    HIP_TRY(hipMemsetAsync(c->d_bits[fb], 0, size_t((need + 31) / 32) * 4, sst));
-    DecisionStream ds{d_dcount, d_dbase, c->d_pre[fb], c->d_bits[fb]};
+    if (guarded) {
+      if (launch_zero_bits(c->d_bits[fb], c->d_dtotal + t3, c->dcap[fb], sst) < 0)
+        return set_err(-5, "zero launch failed: %s", hipGetErrorString(hipGetLastError()));
+    } else {
+      HIP_TRY(hipMemsetAsync(c->d_bits[fb], 0, size_t((need + 31) / 32) * 4, sst));
+    }
+    DecisionStream ds{d_dcount, d_dbase, c->d_pre[fb], c->d_bits[fb], guarded ? c->d_dtotal + t3 : nullptr,
+                      c->dcap[fb]};
     BitsArgs ba{};
     ba.cbits = sa.cbits;
     ba.frame_chunks = c->frame_chunks;
@@ -2154,6 +2191,10 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       if (timed(0, st, [&] { return launch_symbols(sa, st); }) < 0)
         return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
       ca.j = j;
+      if (c->pass == 1 && p.ac) {
+        ca.rc_stat = c->d_rcstat;
+        ca.rc_stat2 = c->d_rcstat + 512;
+      }
       if (timed(1, st, [&] { return p.ac ? launch_code(ca, st) : launch_code_golomb(ca, st); }) < 0)
         return set_err(-5, "code launch failed: %s", hipGetErrorString(hipGetLastError()));
     }
@@ -2292,7 +2333,7 @@ static int settle_batch(ffv1hip_ctx* c, int64_t b) {
       HIP_TRY(hipMemcpy(status, c->d_status + 4 * L.status_set, sizeof(status), hipMemcpyDeviceToHost));
     }
     pcm_fail = status[2] != 0;
-    if (!status[0]) break;
+    if (!status[0] && !status[3]) break;
     if (attempt >= 2 || !L.valid)
       return set_err(-28, "%d slices exceeded the slice byte budget", status[0]);
     if (!redo_next && b + 1 < c->nsub) {
@@ -2317,8 +2358,11 @@ static int settle_batch(ffv1hip_ctx* c, int64_t b) {
                         hipMemcpyDeviceToDevice));
     c->dep_valid = false;  // synchronised above
     c->nsub = b;
-    int rc = grow_slice_budget(c, status[1]);
+    int rc = status[0] ? grow_slice_budget(c, status[1]) : 0;
     if (rc < 0) return rc;
+    // a guarded launch whose decisions did not fit its set (status[3]): sized
+    // from its read-back total this time
+    if (status[3]) c->no_guard_once = true;
     rc = run_batch(c, R.frames, R.frame_bytes, R.plane_off, R.plane_stride, R.n, nullptr);
     if (rc < 0) return rc;
   }
@@ -2843,7 +2887,7 @@ int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides
         return;
       }
       P.t_settle += wall_s() - t0;
-      if (P.h_status[4 * sset]) {  // over the budget: settled at the join
+      if (P.h_status[4 * sset] || P.h_status[4 * sset + 3]) {  // over the budget or the set: settled at the join
         o.redo = true;
         return;
       }
@@ -3473,6 +3517,7 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
   la.rgb = p.colorspace;
   la.transparency = p.transparency;
   la.row_cap = d->row_cap;
+  la.context_model = p.context_model;
   constexpr int64_t kDecLds = 64 * 1024;
   d->global_states = decode_lds_bytes(la, false) > kDecLds;
   // dec_swap=0 (measurement hook): both plane groups in the LDS

@@ -148,7 +148,15 @@ struct DecisionStream {
   const int64_t* dbase;       // [frame][slice]
   uint8_t* pre;
   uint32_t* bits;
+  // A batch launched before its decision count is known on the host (the
+  // layout's total not read back): the kernels that touch pre / bits skip
+  // the batch when the total exceeds the set's capacity, ffv1_dfix flags it
+  // (status[3]) and the host encodes it again with a larger set.  total null:
+  // the set was sized from the read-back total.
+  const int64_t* total;
+  int64_t cap;
 };
+__device__ __forceinline__ bool ds_over(const DecisionStream& ds) { return ds.total && *ds.total > ds.cap; }
 
 // Debug build (build.py --check: -DFFV1HIP_BOUNDS, lib/libffv1hip_check.so):
 // the walk's, dseg's, dfix's and sink's writes are checked against the
@@ -263,6 +271,10 @@ struct CodeArgs {
   int range_pass;             // 0 whole streams, 1 the luma chains, 2 the chroma chains
   int dseg_part;              // ffv1_dseg: -1 every segment, 0 the luma chains', 1 the chroma chains'
   int range_blocks;           // set by launch_range_dseg
+  // pass 1 (ffv1_code): put_symbol_inline's counts (ffv1enc.c:190-199),
+  // rc_stat[256][2] by state, rc_stat2[contexts][32][2] by (context, slot)
+  unsigned long long* rc_stat;
+  unsigned long long* rc_stat2;
 };
 
 // Pass-1 statistics (ffv1enc.c:190-199): rc_stat[state][bit] from the
@@ -418,7 +430,8 @@ int launch_symbols(const SymbolArgs& a, void* stream);
 int launch_rct_params(const RctArgs& a, void* stream);
 int launch_code(const CodeArgs& a, void* stream);
 int launch_layout(const int* dcount, int nstreams, int64_t* dbase, int64_t* total, StreamSegs* segs,
-                  int* seg_totals, int* wmap, void* stream);
+                  int* seg_totals, int* wmap, int64_t* total_host, void* stream);
+int launch_zero_bits(uint32_t* bits, const int64_t* total, int64_t cap, void* stream);
 // items [first, first + count) of the batch's walk (count < 0: to the end)
 int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first = 0, int count = -1);
 // Items (waves) of a batch's walk: the longer plane group's chains first, one

@@ -758,6 +758,52 @@ __device__ __forceinline__ int64_t terminate(Lane& L, SinkT& S, bool state129, i
   return S.finish();
 }
 
+// Pass 1 (ffv1enc.c:190-199, 315-321): every decision of a plane symbol
+// counted by the state it is coded with and by (context, slot), from the
+// row's states before the symbol (each slot codes once per symbol but slots
+// 10 and 31, whose later decisions see the states their earlier ones left).
+// Plain global atomics: pass 1 is a statistics run, not the timed path.
+__device__ __forceinline__ uint32_t row_byte(const Lane& L, int k) {
+  const int d = k >> 2;
+  const uint32_t w = d == 0 ? L.r0 : d == 1 ? L.r1 : d == 2 ? L.r2 : d == 3 ? L.r3
+                   : d == 4 ? L.r4 : d == 5 ? L.r5 : d == 6 ? L.r6 : L.r7;
+  return (w >> ((k & 3) * 8)) & 0xFFu;
+}
+
+__device__ void count_symbol(const CodeArgs& a, const Lane& L, int v, int ctx, const uint8_t* tab) {
+  unsigned long long* const st2 = a.rc_stat2 + (int64_t)ctx * 64;
+  auto cnt = [&](int slot, int bit, uint32_t s) {
+    atomicAdd(a.rc_stat + s * 2 + bit, 1ull);
+    atomicAdd(st2 + slot * 2 + bit, 1ull);
+  };
+  if (v == 0) {
+    cnt(0, 1, row_byte(L, 0));
+    return;
+  }
+  const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
+  const int e = 31 - __builtin_clz(mag);
+  uint32_t s10 = row_byte(L, 10), s31 = row_byte(L, 31);
+  cnt(0, 0, row_byte(L, 0));
+  for (int i = 0; i < e; i++) {
+    const int slot = 1 + min(i, 9);
+    const uint32_t s = slot == 10 ? s10 : row_byte(L, slot);
+    cnt(slot, 1, s);
+    if (slot == 10) s10 = tab[256 | s10];
+  }
+  {
+    const int slot = 1 + min(e, 9);
+    cnt(slot, 0, slot == 10 ? s10 : row_byte(L, slot));
+  }
+  for (int i = e - 1; i >= 0; i--) {
+    const int slot = 22 + min(i, 9), bit = (mag >> i) & 1;
+    const uint32_t s = slot == 31 ? s31 : row_byte(L, slot);
+    cnt(slot, bit, s);
+    if (slot == 31) s31 = tab[(bit << 8) | s31];
+  }
+  const int sslot = 11 + min(e, 10);
+  cnt(sslot, v < 0, row_byte(L, sslot));
+}
+
 // One lane per (segment, slice) chain coding frame j of every segment, the
 // chain's states carried in `tables` from frame to frame.
 __host__ __device__ constexpr size_t code_lds_bytes(int lanes) {
@@ -823,6 +869,7 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
 
   const SliceGeom& g = a.geom[slice];
   const int64_t nsym = live ? g.nsym : 0;
+  const int contexts = (int)(a.state_bytes / (32 * a.pcount));  // rows per plane context (pass-1 counts)
   // v4: encode_line's check at every line start (ffv1enc.c:282-286): fewer
   // than 35 * w bytes left in the slice's buffer (the bytes written so far,
   // renorm_encoder's outstanding byte and 0xFF run not counted) fails the
@@ -868,6 +915,7 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
       PFb = r[1];
     }
     const int v = (int16_t)(sv & 0xFFFF);
+    if (a.rc_stat && act) count_symbol(a, L, v, row - row / contexts * contexts, ftab);
     const bool nz = act && v != 0;
     const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
     const int e = nz ? 31 - __builtin_clz(mag) : -1;
@@ -1167,6 +1215,10 @@ __device__ __forceinline__ void range_pass(const CodeArgs& a, int64_t c, int pas
 }
 
 __global__ __launch_bounds__(kRangeThreads) void ffv1_range(CodeArgs a) {
+  if (ds_over(a.ds)) {  // the batch is encoded again: flagged for the host (status[3])
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.status + 3, 1);
+    return;
+  }
   set_prio(a.range_prio);
   range_pass<2>(a, (int64_t)blockIdx.x * kRangeThreads + threadIdx.x, a.range_pass);
 }
@@ -1180,9 +1232,7 @@ constexpr int kDsegThreads = kWave;
 
 // Where a segment's digits go: a buffer resource over its stream's digit
 // area (the wave's 64 segments are one stream's) and the byte offset of the
-// lane's next digit.  Every decision issues the store; the lanes without a
-// shift give an offset past the resource, which the hardware drops (no
-// branch around the store), as it drops the stores of a stream running past
+// lane's next digit.  The hardware drops the stores of a stream running past
 // its slot (the join then reports the overflow).
 struct DigitOut {
   __amdgpu_buffer_rsrc_t rs;
@@ -1203,7 +1253,10 @@ __device__ __forceinline__ void put_dec(int& low, int& range, DigitOut& o, int s
   // the compiler rebuild the same VCC for the low select and cost three
   // more VALU per decision: 17 vs 14.)
   const bool sh = nr < 0x100;
-  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)low, o.rs, sh ? o.kb : (int)0x80000000, 0, 0);
+  // the store of the lanes that shift (an exec-masked store; issuing it for
+  // every lane with an out-of-range offset for the others loaded the
+  // address path with 64 lanes per decision: 19.23 -> 19.40 Gpix/s)
+  if (sh) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)low, o.rs, o.kb, 0, 0);
   o.kb += sh ? 4 : 0;
   low = sh ? (int)__builtin_amdgcn_perm(0u, (uint32_t)low, 0x0c0c000cu) : low;  // (low & 0xFF) << 8
   range = sh ? nr << 8 : nr;
@@ -1326,6 +1379,7 @@ __device__ __forceinline__ void dseg_body(const CodeArgs& a, int vb, int vgrid, 
 }
 
 __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
+  if (ds_over(a.ds)) return;
   set_prio(a.dseg_prio);
   dseg_body(a, blockIdx.x, gridDim.x, a.dseg_part);
 }
@@ -1337,6 +1391,7 @@ __global__ __launch_bounds__(kDsegThreads) void ffv1_dseg(CodeArgs a) {
 // other; on one stream, so no fifth hardware queue (an extra stream for the
 // same overlap serialised).
 __global__ __launch_bounds__(kRangeThreads) void ffv1_range_dseg(CodeArgs a) {
+  if (ds_over(a.ds)) return;
   if ((int)blockIdx.x < a.range_blocks) {
     set_prio(a.range_prio);
     range_pass<2>(a, (int64_t)blockIdx.x * kRangeThreads + threadIdx.x, 2);
@@ -1356,6 +1411,7 @@ __global__ __launch_bounds__(kRangeThreads) void ffv1_range_dseg(CodeArgs a) {
 constexpr int kFixThreads = kWave;
 __global__ __launch_bounds__(kFixThreads) void ffv1_dfix(CodeArgs a) {
   const int64_t st = (int64_t)blockIdx.x * kFixThreads + threadIdx.x;
+  if (ds_over(a.ds) || a.status[3]) return;  // skipped by the walk and the coder (ffv1_range flagged it)
   if (st >= (int64_t)a.nframes * a.nslices) return;
   const int f = (int)(st / a.nslices), slice = (int)(st % a.nslices);
   const HdrState h = a.hdr[a.keyflags[f] * a.nslices + slice];
@@ -1693,6 +1749,7 @@ template <int WAVES>
 __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t fixed[kT3Bytes + WAVES * kStageBytes];
   extern __shared__ __attribute__((aligned(16))) uint8_t tbl[];  // [wave][2][rows + 1 dummy row][32]
+  if (ds_over(a.ds)) return;  // the batch is encoded again (uniform: before the barrier)
   const int64_t half = a.state_bytes / 2;  // one plane group's [contexts][32] in the persisted states
   const int64_t thalf = (int64_t)a.rows * 32;  // ... and its table in LDS (dense rows: 365 x 32)
   const int tsz = (int)thalf + 32;
@@ -2015,7 +2072,7 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
 constexpr int kLayoutThreads = 128;  // 2 KB of LDS: it runs beside the walk, which holds the rest
 __global__ __launch_bounds__(kLayoutThreads) void ffv1_layout(const int* dcount, int nstreams, int64_t* dbase,
                                                               int64_t* total, StreamSegs* segs, int* seg_totals,
-                                                              int* wmap) {
+                                                              int* wmap, int64_t* total_host) {
   __shared__ int64_t part[kLayoutThreads];
   __shared__ int64_t spart[kLayoutThreads];  // segments << 32 | 64-segment groups
   const int t = threadIdx.x;
@@ -2068,6 +2125,7 @@ __global__ __launch_bounds__(kLayoutThreads) void ffv1_layout(const int* dcount,
   }
   if (t == kLayoutThreads - 1) {
     *total = part[t];
+    if (total_host) *total_host = part[t];  // mapped: the host's estimate for later batches
     seg_totals[0] = (int)(spart[t] >> 32);
     seg_totals[1] = (int)(spart[t] & 0xFFFFFFFF);
   }
@@ -2088,6 +2146,7 @@ __global__ __launch_bounds__(kBitsThreads) void ffv1_bits(BitsArgs a) {
   __shared__ int off[kBitsThreads];
   __shared__ int tot[kBitsThreads];
   __shared__ int wsum[kBitsWaves];
+  if (ds_over(a.ds)) return;  // (uniform: before any barrier)
   const int t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
   // stream sid = frame * nslices + slice, strided over a grid that may be
   // smaller than the streams (a bounded grid: room for the walk beside it)
@@ -2372,6 +2431,7 @@ constexpr int kStatsLdsCtx = 32;
 
 __global__ __launch_bounds__(kStatsThreads) void ffv1_stats_states(StatsArgs a) {
   __shared__ uint32_t h[512];
+  if (ds_over(a.ds)) return;
   for (int i = threadIdx.x; i < 512; i += kStatsThreads) h[i] = 0;
   __syncthreads();
   const int64_t st = (int64_t)blockIdx.y * a.nslices + blockIdx.x;
@@ -2766,9 +2826,25 @@ int launch_bits(const BitsArgs& a, void* stream) {
 }
 
 int launch_layout(const int* dcount, int nstreams, int64_t* dbase, int64_t* total, StreamSegs* segs,
-                  int* seg_totals, int* wmap, void* stream) {
+                  int* seg_totals, int* wmap, int64_t* total_host, void* stream) {
   hipLaunchKernelGGL(ffv1_layout, dim3(1), dim3(kLayoutThreads), 0, reinterpret_cast<hipStream_t>(stream), dcount,
-                     nstreams, dbase, total, segs, seg_totals, wmap);
+                     nstreams, dbase, total, segs, seg_totals, wmap, total_host);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// The decision bits of a guarded batch zeroed on the device, as far as its
+// total (the host does not know it): min(total, cap) decisions
+constexpr int kZeroThreads = 256;
+__global__ __launch_bounds__(kZeroThreads) void ffv1_zero_bits(uint32_t* bits, const int64_t* total, int64_t cap) {
+  const int64_t n = (min(*total, cap) + 31) / 32 / 4;  // uint4 words
+  uint4* const b4 = reinterpret_cast<uint4*>(bits);
+  for (int64_t i = (int64_t)blockIdx.x * kZeroThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kZeroThreads)
+    b4[i] = make_uint4(0, 0, 0, 0);
+}
+
+int launch_zero_bits(uint32_t* bits, const int64_t* total, int64_t cap, void* stream) {
+  hipLaunchKernelGGL(ffv1_zero_bits, dim3(512), dim3(kZeroThreads), 0, reinterpret_cast<hipStream_t>(stream), bits,
+                     total, cap);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -175,6 +175,8 @@ def test_hip_decoder_header_naming_another_slice_diverges():
     np.testing.assert_array_equal(got[0][~mask], want[0][~mask])
     assert (got[0][mask] != want[0][mask]).mean() > 0.9
 
+
+def test_hip_encode_decode_4k_p10_roundtrip():
     """BASELINE configs[2] at full size: HIP encoder -> HIP decoder is lossless."""
     from ffv1hip import HipDecoder, HipEncoder
     s = Stream("c3", 3840, 2160, "yuv420p10", 4, slices=64, gop_size=3, source="d2", depth=10)

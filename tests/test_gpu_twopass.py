@@ -21,10 +21,19 @@ TWO_PASS = [
            source="d2", depth=10),
     Stream("bgr0_chained", 96, 64, "bgr0", 4, slices=4, coder=1, gop_size=2, source="random"),
 ]
+# pass 1 on the chained coder beyond TWO_PASS: alpha (a third plane context)
+# and version 4 (RCT coefficients per slice); parity unpinned
+PASS1_EXTRA = [
+    Stream("yuva_chained", 128, 96, "yuva420p10", 3, slices=4, coder=1, gop_size=2, source="random", depth=10),
+    Stream("gbrp12_v4", 96, 64, "gbrp12", 3, slices=4, coder=1, gop_size=2, source="random", experimental=True),
+]
 
 
 def _kw(s):
-    return dict(slices=s.slices, coder=s.coder, context=s.context, gop_size=s.gop_size)
+    kw = dict(slices=s.slices, coder=s.coder, context=s.context, gop_size=s.gop_size)
+    if s.experimental:
+        kw.update(level=4, experimental=True)
+    return kw
 
 
 def _oracle_pass1(s, frames):
@@ -35,8 +44,12 @@ def _oracle_pass1(s, frames):
     return e.stats_out()
 
 
-@pytest.mark.parametrize("stream", TWO_PASS[:2], ids=[s.name for s in TWO_PASS[:2]])
+@pytest.mark.parametrize("stream", TWO_PASS + PASS1_EXTRA, ids=[s.name for s in TWO_PASS + PASS1_EXTRA])
 def test_pass1_statistics_match_oracle(stream):
+    """Frame-parallel (YCbCr, context model 0: from the decision stream and
+    the walk records) and chained (context model 1, RGB, alpha, version 4:
+    counted by ffv1_code as it codes) pass-1 statistics, equal to the
+    oracle's text."""
     from ffv1hip import HipEncoder, configure
     frames = list(stream.frames())
     enc = HipEncoder(configure(stream.width, stream.height, stream.pix_fmt, pass_=1, **_kw(stream)), 0, 3)
