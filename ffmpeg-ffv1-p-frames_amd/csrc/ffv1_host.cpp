@@ -141,7 +141,7 @@ static const char* const kKnobNames[] = {"serial",     "walkdbg",    "walktrace"
                                          "range_prio", "dseg_prio",  "sym_grid",  "bits_grid", "dseg_grid",
                                          "walk_split", "copy_threads", "dec_swap", "coder",    "dense", "walk_blocks",
                                          "recsets",    "slice_cap",  "walk_part_a", "force_multi", "bounds_shrink", "range_split", "rd_grid",
-                                         "dsets", "rec2_drop", "budget", "pack", "v4_cap0", "readback"};
+                                         "dsets", "rec2_drop", "budget", "pack", "v4_cap0", "readback", "xq", "fsets"};
 
 extern "C" char** environ;
 
@@ -624,9 +624,13 @@ struct ffv1hip_ctx {
   struct HostPipe {
     bool on = false;
     bool overlap = false;  // two frame sets and two packet sets: batch k+1 stages while batch k codes
+    // frame sets: 1, 2 (overlap) or 3 (ffv1hip_encode stages batch k+2
+    // while batch k finishes, collecting it only before k+2's launch)
+    int nsets = 1;
     std::unique_ptr<CopyPool> pool;
     std::unique_ptr<CopyPool> pool_out;  // the copy-out thread's: packets into the caller's buffer
     hipStream_t xfer = nullptr;
+    bool d2h_borrowed = false;  // d2h is one of the context's kernel streams
     hipStream_t d2h = nullptr;  // ffv1hip_encode: packets out beside the next batch's frames in
     static constexpr int kSlots = 6;
     int64_t slot_bytes = 0;
@@ -650,11 +654,11 @@ struct ffv1hip_ctx {
     // word (pack10_rows), into a packed area per frame set that
     // ffv1_unpack10 expands into the frame slots; rawf: frames staged as is
     bool pack10 = false;
-    uint8_t* d_packed[2]{};
+    uint8_t* d_packed[3]{};
     int64_t packed_frame_bytes = 0;
     int64_t poff[kMaxPlanes]{};
     int pw[kMaxPlanes]{}, prow[kMaxPlanes]{};  // samples per row, packed bytes per row
-    std::vector<uint8_t> rawf[2];
+    std::vector<uint8_t> rawf[3];
     uint8_t* d_compact[2]{};  // the same, back to back in HBM (one D2H copy)
     int64_t d_compact_cap[2]{};
     // FFV1HIP_HOSTDBG=1 (measurement hook): where ffv1hip_encode's host time
@@ -666,6 +670,7 @@ struct ffv1hip_ctx {
     double t_sizes = 0, t_compact = 0, t_dcopy = 0;  // inside the D2H (FFV1HIP_HOSTDBG)
   } pipe;
   uint8_t* d_frames2 = nullptr;
+  uint8_t* d_frames3 = nullptr;
   // encode2 with the pipe: the set being filled and the launched batches
   // whose packets are not handed out yet (batch id, pts)
   int q_set = 0;
@@ -2470,12 +2475,14 @@ static void pipe_release(ffv1hip_ctx* c);
 // The second frame / packet set of the overlapped host path, freed.
 static void drop_second_set(ffv1hip_ctx* c) {
   (void)hipGetLastError();
-  for (void** q : {(void**)&c->d_frames2, (void**)&c->d_packets2, (void**)&c->d_packet_size2}) {
+  for (void** q : {(void**)&c->d_frames2, (void**)&c->d_frames3, (void**)&c->d_packets2,
+                   (void**)&c->d_packet_size2}) {
     if (*q) (void)hipFree(*q);
     *q = nullptr;
   }
   c->two_pk = false;
   c->pipe.overlap = false;
+  c->pipe.nsets = 1;
 }
 
 static int pipe_open_parts(ffv1hip_ctx* c) {
@@ -2487,8 +2494,22 @@ static int pipe_open_parts(ffv1hip_ctx* c) {
     return set_err(-12, "the frame slots of a %d-frame batch (%.1f GB) do not fit in device memory", c->max_batch,
                    double(fset) / 1e9);
   }
-  HIP_TRY(hipStreamCreateWithFlags(&P.xfer, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&P.d2h, hipStreamNonBlocking));
+  {
+    // xq=0: both copy streams at the greatest priority (a queue pool of their
+    // own); xq=1: default priority (they share the 4 hardware queues with the
+    // kernel streams); xq=2: transfer stream prioritised, packets out on the side stream
+    const int xq = c->knobs.get("xq", 0);
+    int lo = 0, hi = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    const int pr = xq == 1 ? 0 : hi;
+    HIP_TRY(hipStreamCreateWithPriority(&P.xfer, hipStreamNonBlocking, pr));
+    if (xq == 2) {
+      P.d2h = c->bits_stream ? c->bits_stream : c->stream;
+      P.d2h_borrowed = true;
+    } else {
+      HIP_TRY(hipStreamCreateWithPriority(&P.d2h, hipStreamNonBlocking, pr));
+    }
+  }
   int nt = int(std::thread::hardware_concurrency());
   if (const char* e = std::getenv("OMP_NUM_THREADS"))  // the host's CPU share where it is set
     if (std::atoi(e) > 0) nt = std::min(nt, std::atoi(e));
@@ -2513,6 +2534,16 @@ static int pipe_open_parts(ffv1hip_ctx* c) {
         hipMalloc(&c->d_packet_size2, sizeof(int64_t) * c->max_batch) == hipSuccess) {
       c->two_pk = true;
       P.overlap = true;
+      P.nsets = 2;
+      // a third frame set with room to spare (fsets=2: two)
+      if (c->knobs.get("fsets", 3) >= 3 && free_b > 2 * fset + 3 * pk_bytes + (size_t(4) << 30)) {
+        if (hipMalloc(&c->d_frames3, fset) == hipSuccess) {
+          P.nsets = 3;
+        } else {
+          (void)hipGetLastError();
+          c->d_frames3 = nullptr;
+        }
+      }
     } else {
       drop_second_set(c);
     }
@@ -2520,7 +2551,7 @@ static int pipe_open_parts(ffv1hip_ctx* c) {
   {  // 10-bit samples packed for PCIe (pack=0: as they are)
     const ffv1hip_params& p = c->P;
     P.pack10 = p.sample_bytes == 2 && p.packed_at_lsb && p.bits_per_raw_sample == 10 && !is_ya8(p) &&
-               c->knobs.get("pack", 0) != 0;
+               c->knobs.get("pack", 1) != 0;
     if (P.pack10) {
       int64_t off[kMaxPlanes];
       int pst[kMaxPlanes], rows[kMaxPlanes], np;
@@ -2533,7 +2564,7 @@ static int pipe_open_parts(ffv1hip_ctx* c) {
         o += int64_t(P.prow[k]) * rows[k];
       }
       P.packed_frame_bytes = (o + 255) & ~int64_t(255);
-      for (int k = 0; k < (P.overlap ? 2 : 1) && P.pack10; k++) {
+      for (int k = 0; k < P.nsets && P.pack10; k++) {
         if (hipMalloc(&P.d_packed[k], size_t(P.packed_frame_bytes) * c->max_batch) != hipSuccess) {
           (void)hipGetLastError();
           P.d_packed[k] = nullptr;
@@ -2599,10 +2630,11 @@ static void pipe_close(ffv1hip_ctx* c) {
   for (uint8_t* d : P.d_packed)
     if (d) (void)hipFree(d);
   if (P.xfer) (void)hipStreamDestroy(P.xfer);
-  if (P.d2h) (void)hipStreamDestroy(P.d2h);
-  for (void* q : {(void*)c->d_frames2, (void*)c->d_packets2, (void*)c->d_packet_size2})
+  if (P.d2h && !P.d2h_borrowed) (void)hipStreamDestroy(P.d2h);
+  for (void* q : {(void*)c->d_frames2, (void*)c->d_frames3, (void*)c->d_packets2, (void*)c->d_packet_size2})
     if (q) (void)hipFree(q);
   c->d_frames2 = nullptr;
+  c->d_frames3 = nullptr;
   c->d_packets2 = nullptr;
   c->d_packet_size2 = nullptr;
 }
@@ -2718,6 +2750,10 @@ static int stage_rows_packed(ffv1hip_ctx* c, uint8_t* dst, const uint8_t* src, i
 
 // One host frame into batch slot `slot` of frame set `set`: packed (10-bit
 // samples, none over 10 bits, not caller-pinned) or as it is.
+static uint8_t* frame_set(const ffv1hip_ctx* c, int set) {
+  return set == 0 ? c->d_frames : set == 1 ? c->d_frames2 : c->d_frames3;
+}
+
 static int stage_frame(ffv1hip_ctx* c, int set, int64_t slot, const void* const* planes, const int* strides) {
   ffv1hip_ctx::HostPipe& P = c->pipe;
   int64_t off[kMaxPlanes];
@@ -2725,7 +2761,7 @@ static int stage_frame(ffv1hip_ctx* c, int set, int64_t slot, const void* const*
   slot_layout(c, off, pst, rows, &np);
   for (int k = 0; k < np; k++)
     if (!planes[k]) return set_err(-22, "null plane %d", k);
-  uint8_t* const base = (set ? c->d_frames2 : c->d_frames) + slot * c->frame_bytes;
+  uint8_t* const base = frame_set(c, set) + slot * c->frame_bytes;
   bool raw = true;
   if (P.pack10 && P.d_packed[set]) {
     bool pinned = false;
@@ -2759,7 +2795,7 @@ static int launch_staged(ffv1hip_ctx* c, int set, int n) {
   int pst[kMaxPlanes], rows[kMaxPlanes], np;
   slot_layout(c, off, pst, rows, &np);
   ffv1hip_ctx::HostPipe& P = c->pipe;
-  uint8_t* const frames = set ? c->d_frames2 : c->d_frames;
+  uint8_t* const frames = frame_set(c, set);
   if (P.pack10 && P.d_packed[set]) {  // the packed frames into their slots, after their copies
     for (int f0 = 0; f0 < n; f0 += kUnpackFrames) {
       UnpackArgs ua{};
@@ -2960,11 +2996,15 @@ int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides
   const int fstep = input_planes(c->P) == 4 ? FFV1HIP_PLANES_YUVA : FFV1HIP_PLANES;  // plane pointers per frame
   for (int j = 0, base = 0; base < n_frames; j++, base += c->max_batch) {
     const int n = std::min(c->max_batch, n_frames - base);
-    const int set = P.overlap ? (j & 1) : 0;
-    // batch j's frames and packets go where batch j - 2's were
-    if (P.overlap && (rc = retire(c->nsub - 2)) < 0) break;
+    const int set = j % P.nsets;
+    // batch j's packets go where batch j - 2's were, and with two frame sets
+    // its frames too: batch j - 2 is collected before they are staged; with
+    // three, before batch j launches (its frames and batch j - 1's stay in
+    // place for a budget re-encode)
+    if (P.nsets == 2 && (rc = retire(c->nsub - 2)) < 0) break;
     for (int i = 0; i < n && rc >= 0; i++)
       rc = stage_frame(c, set, i, planes + fstep * (base + i), strides + fstep * (base + i));
+    if (rc >= 0 && P.nsets == 3) rc = retire(c->nsub - 2);
     if (rc >= 0) rc = launch_staged(c, set, n);
     if (rc < 0) break;
     Out& o = ot[(c->nsub - 1) & 1];

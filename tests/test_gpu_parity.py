@@ -361,12 +361,16 @@ def test_encode2_pipelined_budget_reencode(batch, monkeypatch):
     assert [(p.data, p.key) for p in pkts] == ref
 
 
+@pytest.mark.parametrize("fsets", [None, "2"])
 @pytest.mark.parametrize("cap", [None, "512"])
-def test_host_encode_many_batches(cap, monkeypatch):
+def test_host_encode_many_batches(cap, fsets, monkeypatch):
     """ffv1hip_encode over several batches in one call (frames staged while
-    the previous batch codes), with and without the budget re-encode."""
-    if cap:
-        monkeypatch.setenv("FFV1HIP_DEBUG", f"slice_cap={cap}")
+    the previous batch codes), with and without the budget re-encode, with
+    three frame sets (the default: batch k+2 stages while batch k finishes)
+    and with two (fsets=2)."""
+    hooks = ([f"slice_cap={cap}"] if cap else []) + ([f"fsets={fsets}"] if fsets else [])
+    if hooks:
+        monkeypatch.setenv("FFV1HIP_DEBUG", ",".join(hooks))
     from ffv1hip import HipEncoder
     s = PARITY_STREAMS[1]
     frames = list(s.frames())

@@ -22,13 +22,6 @@ import os
 import sys
 import time
 
-# the host-frame path runs four streams of the context besides the caller's
-# (walk, symbols, coder, transfer, packets out: five): with the HIP
-# runtime's default of 4 hardware queues two of them share one and
-# serialise (encode2 batch 48: 2,823 vs 3,097 Mpix/s with 8); set before HIP
-# starts.  (A second transfer stream measured no faster: the H2D DMA moves
-# ~26 GB/s either way.)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import numpy as np
 
@@ -46,7 +39,8 @@ B = gops * GOP
 src = list(synth.videogen_frames(W, H, B, depth=10))
 L = load_library()
 res = {"config": "4K 3840x2160 yuv420p10le, coder=1, slices=64, keyint=12", "clip_frames": B,
-       "copy_threads": os.environ.get("OMP_NUM_THREADS")}
+       "copy_threads": os.environ.get("OMP_NUM_THREADS"),
+       "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "4 (runtime default)"), "hooks": os.environ.get("FFV1HIP_DEBUG")}
 # the pool: every frame's planes back to back in one buffer (an application's frame pool)
 fbytes = sum(p.nbytes for p in src[0])
 pool = np.empty(fbytes * B, np.uint8)
