@@ -34,37 +34,42 @@ __constant__ uint8_t kLog2Run[41] = {  // ff_log2_run (bitstream.c:40-46)
 struct RacDec {
   uint32_t low, range;
   int64_t ptr, end;  // byte offsets into the packet buffer
-  int64_t wi;        // index of the 8-byte word w0 holds
-  uint64_t w0, w1;   // the word holding ptr and the one after it (in flight)
+  uint64_t win;      // the bytes from ptr to the end of its 8-byte word, the one at ptr lowest
+  uint64_t nxt;      // the word after it; bytes at or past end read as 0 in both
 };
+
+// word k of the packet buffer with the bytes at or past `end` zeroed (no
+// load at all past it)
+__device__ inline uint64_t rac_word(const uint64_t* w, int64_t k, int64_t end) {
+  const int64_t b = k * 8;
+  if (b >= end) return 0;
+  const uint64_t v = w[k];
+  return end - b >= 8 ? v : v & ((uint64_t(1) << ((end - b) * 8)) - 1u);
+}
 
 __device__ inline void rac_init(RacDec& c, const uint8_t* pk, int64_t start, int64_t end) {
   // ff_init_range_decoder + the first two bytes (rangecoder.c:53-61)
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(pk);
   c.range = 0xFF00;
   c.low = (uint32_t(pk[start]) << 8) | pk[start + 1];
   c.ptr = start + 2;
   c.end = end;
-  const uint64_t* w = reinterpret_cast<const uint64_t*>(pk);
-  c.wi = c.ptr >> 3;
-  c.w0 = w[c.wi];
-  c.w1 = w[c.wi + 1];
+  c.win = rac_word(w, c.ptr >> 3, end) >> ((c.ptr & 7) * 8);
+  c.nxt = rac_word(w, (c.ptr >> 3) + 1, end);
 }
 
-// refill (rangecoder.h:104-115): ptr advances one byte at a time, so the
-// next word is always w1; the word after it is loaded a word ahead.
+// refill (rangecoder.h:104-115): the byte at ptr is the window's lowest (0
+// past the end); at a word boundary the next word moves in and the one after
+// it is loaded, eight refills ahead of its use
 __device__ inline void rac_refill(RacDec& c, const uint64_t* w) {
   c.range <<= 8;
-  c.low <<= 8;
-  if (c.ptr < c.end) {
-    const int64_t wi = c.ptr >> 3;
-    if (wi != c.wi) {
-      c.w0 = c.w1;
-      c.w1 = w[wi + 1];
-      c.wi = wi;
-    }
-    c.low += uint32_t(c.w0 >> ((c.ptr & 7) * 8)) & 0xFF;
-  }
+  c.low = (c.low << 8) | uint32_t(c.win & 0xFFu);
+  c.win >>= 8;
   c.ptr++;
+  if (__builtin_amdgcn_ballot_w64((c.ptr & 7) == 0)) {  // (the active lanes agree)
+    c.win = c.nxt;
+    c.nxt = rac_word(w, (c.ptr >> 3) + 1, c.end);
+  }
 }
 
 // get_rac (rangecoder.h:117-147), branch-free: the transition pair of the
@@ -73,7 +78,7 @@ __device__ inline void rac_refill(RacDec& c, const uint64_t* w) {
 __device__ inline int rac_get(RacDec& c, uint8_t* st, const uint16_t* tt, const uint64_t* w) {
   const uint32_t s = *st;
   const uint32_t pair = tt[s];
-  const uint32_t r1 = (c.range * s) >> 8;
+  const uint32_t r1 = __umul24(c.range, s) >> 8;
   const uint32_t rr = c.range - r1;
   const int bit = c.low >= rr;
   c.low -= bit ? rr : 0u;
@@ -98,185 +103,14 @@ __device__ inline int rac_symbol(RacDec& c, uint8_t* st, int is_signed, const ui
   return int(a);
 }
 
-// The range-coded rows run on the scalar unit: every lane of the wave runs
-// the same chain on the same values, each LDS or packet load is made uniform
-// with readfirstlane, so the compiler keeps the coder state, the context
-// row and the sample taps in SGPRs and codes a decision in SALU instructions
-// with scalar branches (a lane-0-only chain pays a VALU issue slot and an
-// exec-mask branch for every step).  Stores come from lane 0.
+// readfirstlane: lane 0's value as a wave-uniform one
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ int uni(int v) { return int(__builtin_amdgcn_readfirstlane(uint32_t(v))); }
 __device__ __forceinline__ int64_t uni(int64_t v) {
   return int64_t((uint64_t(uni(uint32_t(uint64_t(v) >> 32))) << 32) | uni(uint32_t(v)));
 }
 __device__ __forceinline__ uint64_t uni(uint64_t v) { return (uint64_t(uni(uint32_t(v >> 32))) << 32) | uni(uint32_t(v)); }
 
-__device__ __forceinline__ void uni_coder(RacDec& c) {
-  c.low = uni(c.low);
-  c.range = uni(c.range);
-  c.ptr = uni(c.ptr);
-  c.end = uni(c.end);
-  c.wi = uni(c.wi);
-  c.w0 = uni(c.w0);
-  c.w1 = uni(c.w1);
-}
-
-__device__ __forceinline__ void refill_u(RacDec& c, const uint64_t* w) {
-  c.range <<= 8;
-  c.low <<= 8;
-  if (c.ptr < c.end) {
-    const int64_t wi = c.ptr >> 3;
-    if (wi != c.wi) {
-      c.w0 = c.w1;
-      c.w1 = uni(w[wi + 1]);
-      c.wi = wi;
-    }
-    c.low += uint32_t(c.w0 >> ((c.ptr & 7) * 8)) & 0xFF;
-  }
-  c.ptr++;
-}
-
-// Read-only tables through the scalar cache (constant address space,
-// uniform index): transition pairs and quant tables (DecodeArgs::stab)
-typedef const int32_t __attribute__((address_space(4))) sconst_i32;
-
-// get_rac (rangecoder.h:117-147) on state byte SH of row word `src`; the
-// successor state goes into `dst` (the row's new image), so the next
-// decision, on another slot, does not wait for this one's table lookup
-__device__ __forceinline__ int get_u(RacDec& c, uint32_t src, uint32_t& dst, int SH, const sconst_i32* sk,
-                                     const uint64_t* w) {
-  const uint32_t s = (src >> SH) & 0xFFu;
-  const uint32_t pair = uint32_t(sk[s]);
-  const uint32_t r1 = (c.range * s) >> 8;
-  const uint32_t rr = c.range - r1;
-  const int bit = c.low >= rr;
-  if (bit) {
-    c.low -= rr;
-    c.range = r1;
-  } else {
-    c.range = rr;
-  }
-  const uint32_t ns = bit ? pair >> 8 : pair & 0xFFu;
-  dst = (dst & ~(0xFFu << SH)) | (ns << SH);
-  if (c.range < 0x100) refill_u(c, w);
-  return bit;
-}
-
-template <int K>
-__device__ __forceinline__ int get_ku(RacDec& c, const uint32_t (&r)[8], uint32_t (&n)[8], const sconst_i32* sk,
-                                      const uint64_t* w) {
-  return get_u(c, r[K >> 2], n[K >> 2], (K & 3) * 8, sk, w);
-}
-
-// the exponent's unary run on slots K..9 (e = K-1 on entry)
-template <int K>
-__device__ __forceinline__ void unary_u(RacDec& c, const uint32_t (&r)[8], uint32_t (&n)[8], int& e,
-                                        const sconst_i32* sk, const uint64_t* w) {
-  if constexpr (K <= 9) {
-    if (get_ku<K>(c, r, n, sk, w)) {
-      e = K;
-      unary_u<K + 1>(c, r, n, e, sk, w);
-    }
-  }
-}
-
-// mantissa bits i = K .. 0 on slots 22 + i (those below e)
-template <int K>
-__device__ __forceinline__ void mant_u(RacDec& c, const uint32_t (&r)[8], uint32_t (&n)[8], int e, uint32_t& a,
-                                       const sconst_i32* sk, const uint64_t* w) {
-  if constexpr (K >= 0) {
-    if (K < e) a = 2 * a + uint32_t(get_ku<22 + K>(c, r, n, sk, w));
-    mant_u<K - 1>(c, r, n, e, a, sk, w);
-  }
-}
-
-// get_symbol_inline (ffv1dec.c:44-66), signed, on the row at `row` (32-byte
-// aligned; LDS or a global table): the row's 32 states read once into
-// registers; every slot but 10 and 31 codes at most one decision, so a
-// decision reads its state from the row as read and writes its successor
-// into the new image n, written back at the end
-__device__ inline int symbol_u(RacDec& c, uint8_t* row, const sconst_i32* sk, const uint64_t* w) {
-  uint32_t* const r1w = reinterpret_cast<uint32_t*>(row);
-  uint32_t r[8], n[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) n[i] = r[i] = uni(r1w[i]);
-  if (get_ku<0>(c, r, n, sk, w)) {
-    if (threadIdx.x == 0) r1w[0] = n[0];  // only slot 0 moved
-    return 0;
-  }
-  int e = 0, ret;
-  unary_u<1>(c, r, n, e, sk, w);
-  bool bad = false;
-  if (e == 9) {  // slot 10 for the rest of the run: its state from n after its first decision
-    uint32_t src = r[2];
-    while (get_u(c, src, n[2], 16, sk, w)) {
-      src = n[2];
-      if (++e > 31) {
-        bad = true;
-        break;
-      }
-    }
-  }
-  if (bad) {
-    ret = kInvalidData;
-  } else {
-    uint32_t a = 1, src = r[7];
-    for (int i = e - 1; i >= 9; i--) {  // slot 31
-      a = 2 * a + uint32_t(get_u(c, src, n[7], 24, sk, w));
-      src = n[7];
-    }
-    mant_u<8>(c, r, n, e, a, sk, w);
-    const int j = 11 + (e < 10 ? e : 10);  // the sign slot, row words 2..5
-    const int sh = (j & 3) * 8;
-    int sg;
-    switch (j >> 2) {
-      case 2: sg = get_u(c, r[2], n[2], sh, sk, w); break;
-      case 3: sg = get_u(c, r[3], n[3], sh, sk, w); break;
-      case 4: sg = get_u(c, r[4], n[4], sh, sk, w); break;
-      default: sg = get_u(c, r[5], n[5], sh, sk, w); break;
-    }
-    ret = sg ? int(0u - a) : int(a);
-  }
-  if (threadIdx.x == 0) {
-    uint4* const r4 = reinterpret_cast<uint4*>(row);
-    r4[0] = make_uint4(n[0], n[1], n[2], n[3]);
-    r4[1] = make_uint4(n[4], n[5], n[6], n[7]);
-  }
-  return ret;
-}
-
 __device__ inline int median3u(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
-
-// decode_line (ffv1dec.c:42-117), range coder, by the whole wave on uniform
-// values: one row into `cur` (which holds row y-2 until each sample is
-// written; `up` is row y-1), the reference's zeroed-ring neighbourhood
-__device__ inline void decode_row_u(RacDec& c, uint8_t* st8, const sconst_i32* sk, const uint64_t* pkw,
-                                    bool model1, int16_t* cur, const int16_t* up, int w, int bits) {
-  const sconst_i32* const q = sk + 256;  // quant tables [5][256]
-  const int mask = int((1u << bits) - 1u);
-  int T = uni(int(up[0]));
-  const int T0 = T;
-  int L = T;
-  int LT = uni(int(cur[0]));
-  for (int x = 0; x < w; x++) {
-    const int RT = x + 1 < w ? uni(int(up[x + 1])) : T;
-    int ctx = q[(L - LT) & 0xFF] + q[256 + ((LT - T) & 0xFF)] + q[512 + ((T - RT) & 0xFF)];
-    if (model1) {
-      const int LL = x >= 2 ? uni(int(cur[x - 2])) : (x == 1 ? T0 : 0);
-      const int TT = uni(int(cur[x]));
-      ctx += q[768 + ((LL - L) & 0xFF)] + q[1024 + ((TT - T) & 0xFF)];
-    }
-    const int actx = ctx < 0 ? -ctx : ctx;
-    int diff = symbol_u(c, st8 + actx * 32, sk, pkw);
-    if (ctx < 0) diff = -diff;
-    const int pred = median3u(L, L + T - LT, T);
-    const int v = int(int16_t((pred + diff) & mask));
-    if (threadIdx.x == 0) cur[x] = int16_t(v);
-    LT = T;
-    T = RT;
-    L = v;
-  }
-}
 
 // The range-coded rows on the vector units: the same chain on every lane in
 // VGPRs (the compiler sees LDS-loaded, hence per-lane, values), so the CU's
@@ -299,103 +133,142 @@ __device__ __forceinline__ void vec_coder(RacDec& c) {
   c.range = vreg(uni(c.range));
   c.ptr = vreg(uni(c.ptr));
   c.end = vreg(uni(c.end));
-  c.wi = vreg(uni(c.wi));
-  c.w0 = vreg(uni(c.w0));
-  c.w1 = vreg(uni(c.w1));
+  c.win = vreg(uni(c.win));
+  c.nxt = vreg(uni(c.nxt));
 }
 
 __device__ __forceinline__ int get_v(RacDec& c, uint32_t src, uint32_t& dst, int SH, const uint16_t* tt,
                                      const uint64_t* w) {
   const uint32_t s = (src >> SH) & 0xFFu;
   const uint32_t pair = tt[s];  // to0 | to1 << 8, for the row image only
-  const uint32_t r1 = (c.range * s) >> 8;
+  const uint32_t r1 = __umul24(c.range, s) >> 8;
   const uint32_t rr = c.range - r1;
-  const int bit = c.low >= rr;
+  // every lane holds the same coder: the compare's lane mask is the bit, so
+  // the branches on it are scalar (no exec-mask save and restore)
+  const bool bit = __builtin_amdgcn_ballot_w64(c.low >= rr) != 0;
   c.low -= bit ? rr : 0u;
   c.range = bit ? r1 : rr;
-  const uint32_t ns = bit ? pair >> 8 : pair & 0xFFu;
-  dst = (dst & ~(0xFFu << SH)) | (ns << SH);
-  if (c.range < 0x100) rac_refill(c, w);
+  // the successor into byte SH / 8 of the image: one byte permute (pair's
+  // byte 1 on a 1, byte 0 on a 0; the image's other bytes as they are)
+  const uint32_t keep = 0x03020100u & ~(0xFFu << SH);
+  dst = __builtin_amdgcn_perm(pair, dst, keep | ((bit ? 5u : 4u) << SH));
+  if (__builtin_amdgcn_ballot_w64(c.range < 0x100u)) rac_refill(c, w);
+  return bit;
+}
+// (Reading the pairs of the likely next decisions one decision ahead
+// measured slower: 3.37 -> 3.66 s for a 12-frame 4K GOP; the waits for the
+// in-order LDS counter then cover the prefetches too.)
+
+// get_rac on state s, the decision alone: symbol_v updates the row's states
+// once per symbol, one slot per lane
+__device__ __forceinline__ bool dec_s(RacDec& c, uint32_t s, const uint64_t* w) {
+  const uint32_t r1 = __umul24(c.range, s) >> 8;
+  const uint32_t rr = c.range - r1;
+  const bool bit = __builtin_amdgcn_ballot_w64(c.low >= rr) != 0;
+  c.low -= bit ? rr : 0u;
+  c.range = bit ? r1 : rr;
+  if (__builtin_amdgcn_ballot_w64(c.range < 0x100u)) rac_refill(c, w);
   return bit;
 }
 
 template <int K>
-__device__ __forceinline__ int get_kv(RacDec& c, const uint32_t (&r)[8], uint32_t (&n)[8], const uint16_t* tt,
-                                      const uint64_t* w) {
-  return get_v(c, r[K >> 2], n[K >> 2], (K & 3) * 8, tt, w);
+__device__ __forceinline__ bool dec_k(RacDec& c, const uint32_t (&r)[8], const uint64_t* w) {
+  return dec_s(c, (r[K >> 2] >> ((K & 3) * 8)) & 0xFFu, w);
 }
 
+// the exponent's unary run on slots K..9 (e = K-1 on entry)
 template <int K>
-__device__ __forceinline__ void unary_v(RacDec& c, const uint32_t (&r)[8], uint32_t (&n)[8], int& e,
-                                        const uint16_t* tt, const uint64_t* w) {
+__device__ __forceinline__ void unary_v(RacDec& c, const uint32_t (&r)[8], int& e, const uint64_t* w) {
   if constexpr (K <= 9) {
-    if (get_kv<K>(c, r, n, tt, w)) {
+    if (dec_k<K>(c, r, w)) {
       e = K;
-      unary_v<K + 1>(c, r, n, e, tt, w);
+      unary_v<K + 1>(c, r, e, w);
     }
   }
 }
 
+// mantissa bits i = K .. 0 on slots 22 + i (those below e)
 template <int K>
-__device__ __forceinline__ void mant_v(RacDec& c, const uint32_t (&r)[8], uint32_t (&n)[8], int e, uint32_t& a,
-                                       const uint16_t* tt, const uint64_t* w) {
+__device__ __forceinline__ void mant_v(RacDec& c, const uint32_t (&r)[8], int e, uint32_t& a, const uint64_t* w) {
   if constexpr (K >= 0) {
-    if (K < e) a = 2 * a + uint32_t(get_kv<22 + K>(c, r, n, tt, w));
-    mant_v<K - 1>(c, r, n, e, a, tt, w);
+    if (K < e) a = 2 * a + uint32_t(dec_k<22 + K>(c, r, w));
+    mant_v<K - 1>(c, r, e, a, w);
   }
 }
 
-// get_symbol_inline (ffv1dec.c:44-66), signed, on the row at `row` (LDS)
+// get_symbol_inline (ffv1dec.c:44-66), signed, on the row at `row`.  The
+// decisions read their states from the row as read (every slot but 10 and 31
+// codes at most one decision of a symbol); then each lane k < 32 (and its
+// twin k + 32) moves slot k's state on by the slot's decision, if it had
+// one, with the successor pair it looked up when the symbol started, and
+// writes it back: no table lookup and no wait on the decision chain.  Slots
+// 10 and 31, which repeat past e = 9, go through get_v in the row image n.
 __device__ inline int symbol_v(RacDec& c, uint8_t* row, const uint16_t* tt, const uint64_t* w) {
+  const int k = threadIdx.x & 31;
   const uint4* r4 = reinterpret_cast<const uint4*>(row);
   const uint4 a0 = r4[0], a1 = r4[1];
+  const uint32_t sk = row[k];     // this lane's slot state
+  const uint32_t pk = tt[sk];     // and its successor pair, beside the decisions
   const uint32_t r[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-  uint32_t n[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) n[i] = r[i];
+  uint32_t n2 = r[2], n7 = r[7];  // slots 10 and 31 after their runs
   int ret;
-  if (get_kv<0>(c, r, n, tt, w)) {
+  // what the symbol coded: zero flag zf; else the exponent e (> 31: invalid,
+  // slots 1..10 only), the magnitude and the sign
+  bool zf, neg = false;
+  int e = 0;
+  uint32_t a = 1;
+  zf = dec_k<0>(c, r, w);
+  if (zf) {
     ret = 0;
   } else {
-    int e = 0;
-    unary_v<1>(c, r, n, e, tt, w);
-    bool bad = false;
+    unary_v<1>(c, r, e, w);
     if (e == 9) {  // slot 10 for the rest of the run: its state from n after its first decision
       uint32_t src = r[2];
-      while (get_v(c, src, n[2], 16, tt, w)) {
-        src = n[2];
-        if (++e > 31) {
-          bad = true;
-          break;
-        }
+      while (get_v(c, src, n2, 16, tt, w)) {
+        src = n2;
+        if (++e > 31) break;
       }
     }
-    if (bad) {
+    if (e > 31) {
       ret = kInvalidData;
     } else {
-      uint32_t a = 1, src = r[7];
+      uint32_t src = r[7];
       for (int i = e - 1; i >= 9; i--) {  // slot 31
-        a = 2 * a + uint32_t(get_v(c, src, n[7], 24, tt, w));
-        src = n[7];
+        a = 2 * a + uint32_t(get_v(c, src, n7, 24, tt, w));
+        src = n7;
       }
-      mant_v<8>(c, r, n, e, a, tt, w);
+      mant_v<8>(c, r, e, a, w);
       const int j = 11 + (e < 10 ? e : 10);  // the sign slot, row words 2..5
-      const int sh = (j & 3) * 8;
-      int sg;
-      switch (j >> 2) {
-        case 2: sg = get_v(c, r[2], n[2], sh, tt, w); break;
-        case 3: sg = get_v(c, r[3], n[3], sh, tt, w); break;
-        case 4: sg = get_v(c, r[4], n[4], sh, tt, w); break;
-        default: sg = get_v(c, r[5], n[5], sh, tt, w); break;
-      }
-      ret = sg ? int(0u - a) : int(a);
+      const int q = j >> 2;
+      const uint32_t wd = q == 2 ? r[2] : q == 3 ? r[3] : q == 4 ? r[4] : r[5];
+      neg = dec_s(c, (wd >> ((j & 3) * 8)) & 0xFFu, w);
+      ret = neg ? int(0u - a) : int(a);
     }
   }
-  if (threadIdx.x == 0) {
-    uint4* const o4 = reinterpret_cast<uint4*>(row);
-    o4[0] = make_uint4(n[0], n[1], n[2], n[3]);
-    o4[1] = make_uint4(n[4], n[5], n[6], n[7]);
+  // lane k: slot k's decision (put_symbol_inline's slot order, ffv1enc.c:185-231)
+  const bool ok = e <= 31;
+  const int em = e < 9 ? e : 9;
+  bool t, b;
+  if (k == 0) {
+    t = true;
+    b = zf;
+  } else if (zf) {
+    t = b = false;
+  } else if (k <= 9) {
+    t = k <= e + 1;
+    b = k <= e;
+  } else if (k >= 11 && k <= 21) {
+    t = ok && k == 11 + (e < 10 ? e : 10);
+    b = neg;
+  } else if (k >= 22 && k <= 30) {
+    t = ok && k - 22 < em;
+    b = ((a >> (k - 22)) & 1u) != 0;
+  } else {
+    t = b = false;  // 10, 31: from n2 / n7
   }
+  uint32_t ns = t ? (b ? (pk >> 8) & 0xFFu : pk & 0xFFu) : sk;
+  ns = k == 10 ? (n2 >> 16) & 0xFFu : (k == 31 ? n7 >> 24 : ns);
+  row[k] = uint8_t(ns);
   return ret;
 }
 
@@ -431,40 +304,18 @@ __device__ inline void decode_row_v(RacDec& c, uint8_t* st8, const uint16_t* tt,
   }
 }
 
-// decode_line's PCM mode on vector registers (see decode_row_pcm_u)
+// decode_line's slice_coding_mode 1 (version 4 PCM, ffv1dec.c:111-120): every
+// sample's bits MSB first, each on a fresh state 128, on vector registers
 __device__ inline void decode_row_pcm_v(RacDec& c, const uint64_t* pkw, int16_t* cur, int w, int bits) {
   for (int x = 0; x < w; x++) {
     int v = 0;
     for (int i = 0; i < bits; i++) {
-      const uint32_t r1 = (c.range * 128u) >> 8;
+      const uint32_t r1 = c.range >> 1;  // range * 128 >> 8
       const uint32_t rr = c.range - r1;
-      const int bit = c.low >= rr;
+      const int bit = __builtin_amdgcn_ballot_w64(c.low >= rr) != 0;
       c.low -= bit ? rr : 0u;
       c.range = bit ? r1 : rr;
-      if (c.range < 0x100) rac_refill(c, pkw);
-      v = 2 * v + bit;
-    }
-    if (threadIdx.x == 0) cur[x] = int16_t(v);
-  }
-}
-
-// decode_line's slice_coding_mode 1 (version 4 PCM, ffv1dec.c:111-120): every
-// sample's bits MSB first, each on a fresh state 128; uniform like
-// decode_row_u
-__device__ inline void decode_row_pcm_u(RacDec& c, const uint64_t* pkw, int16_t* cur, int w, int bits) {
-  for (int x = 0; x < w; x++) {
-    int v = 0;
-    for (int i = 0; i < bits; i++) {
-      const uint32_t r1 = (c.range * 128u) >> 8;
-      const uint32_t rr = c.range - r1;
-      const int bit = c.low >= rr;
-      if (bit) {
-        c.low -= rr;
-        c.range = r1;
-      } else {
-        c.range = rr;
-      }
-      if (c.range < 0x100) refill_u(c, pkw);
+      if (__builtin_amdgcn_ballot_w64(c.range < 0x100u)) rac_refill(c, pkw);
       v = 2 * v + bit;
     }
     if (threadIdx.x == 0) cur[x] = int16_t(v);
