@@ -111,11 +111,12 @@ class CopyPool {
 // created (so each context sees the value set at its creation, and nothing is
 // cached in function statics):
 //   FFV1HIP_DEBUG="name[=value],name[=value],..."
-// measurement: serial, walkdbg, walktrace, hostdbg; schedule (defaults are
-// the measured best): walk_prio, range_prio, dseg_prio, sym_grid, bits_grid,
-// dseg_grid, walk_split=0, copy_threads, dec_swap=0; test hooks: coder=chain,
-// dense=0, recsets=1, slice_cap, walk_part_a, force_multi, dsets=eager|lazy, budget=q,
-// rec2_drop=set.  Unknown names
+// measurement: serial, walkdbg, walktrace, hostdbg, copy_threads; test hooks
+// (each forces a path the product takes on its own only in some configs or
+// under memory pressure): coder=chain, dense=0, walk_blocks=0, recsets=1,
+// range_split=0, slice_cap, walk_part_a, force_multi, bounds_shrink,
+// dsets=eager|lazy, budget=q, rec2_drop=set, pack=0, fsets=2, v4_cap0,
+// readback.  Unknown names
 // are an error at create time, so a misspelt hook never silently measures
 // the default.
 struct Knobs {
@@ -137,11 +138,11 @@ struct Knobs {
   }
 };
 
-static const char* const kKnobNames[] = {"serial",     "walkdbg",    "walktrace", "hostdbg",   "walk_prio",
-                                         "range_prio", "dseg_prio",  "sym_grid",  "bits_grid", "dseg_grid",
-                                         "walk_split", "copy_threads", "dec_swap", "coder",    "dense", "walk_blocks",
-                                         "recsets",    "slice_cap",  "walk_part_a", "force_multi", "bounds_shrink", "range_split", "rd_grid",
-                                         "dsets", "rec2_drop", "budget", "pack", "v4_cap0", "readback", "xq", "fsets"};
+static const char* const kKnobNames[] = {"serial",      "walkdbg",     "walktrace", "hostdbg",       "copy_threads",
+                                         "coder",       "dense",       "walk_blocks", "recsets",     "slice_cap",
+                                         "walk_part_a", "force_multi", "bounds_shrink", "range_split", "dsets",
+                                         "rec2_drop",   "budget",      "pack",        "v4_cap0",     "readback",
+                                         "fsets"};
 
 extern "C" char** environ;
 
@@ -541,10 +542,10 @@ struct ffv1hip_ctx {
   // grid caps of the kernels that run beside the states walk (their blocks
   // stride over the work): a grid of one block per item fills every SIMD's
   // wave slots and registers, and walk waves launched meanwhile wait for CU
-  // room until those blocks retire (FFV1HIP_SYM_GRID / _BITS_GRID / _DSEG_GRID)
+  // room until those blocks retire (values measured best in earlier rounds)
   int grid_sym = 4096, grid_bits = 2048, grid_dseg = 4096;
   int cus = 256;      // compute units of the device (a walk wave per SIMD: 4 per CU)
-  int prio_dseg = 0;  // FFV1HIP_DSEG_PRIO (walk / range: per batch, run_batch)
+  int prio_dseg = 0;  // dseg's wave priority (walk / range: per batch, run_batch)
   SliceGeom* d_geom = nullptr;
   int* d_slot_frames = nullptr;  // [j][slot]
   int* d_status = nullptr;       // [set][4]: [0] slices over budget, [1] most bytes one needed
@@ -583,7 +584,7 @@ struct ffv1hip_ctx {
     std::vector<int> keys;
   } hist[2];
   hipEvent_t hist_done[2] = {nullptr, nullptr};  // batch slot k's last kernel
-  // FFV1HIP_WALKTRACE=1 (measurement hook): every walk wave's start and end
+  // FFV1HIP_DEBUG=walktrace (measurement hook): every walk wave's start and end
   // (s_memrealtime, 100 MHz) for up to kTraceBatches batches, kept on the
   // device and summarised at ffv1hip_destroy: dispatch spread and duration
   // of each launch part
@@ -630,7 +631,6 @@ struct ffv1hip_ctx {
     std::unique_ptr<CopyPool> pool;
     std::unique_ptr<CopyPool> pool_out;  // the copy-out thread's: packets into the caller's buffer
     hipStream_t xfer = nullptr;
-    bool d2h_borrowed = false;  // d2h is one of the context's kernel streams
     hipStream_t d2h = nullptr;  // ffv1hip_encode: packets out beside the next batch's frames in
     static constexpr int kSlots = 6;
     int64_t slot_bytes = 0;
@@ -661,13 +661,13 @@ struct ffv1hip_ctx {
     std::vector<uint8_t> rawf[3];
     uint8_t* d_compact[2]{};  // the same, back to back in HBM (one D2H copy)
     int64_t d_compact_cap[2]{};
-    // FFV1HIP_HOSTDBG=1 (measurement hook): where ffv1hip_encode's host time
+    // FFV1HIP_DEBUG=hostdbg (measurement hook): where ffv1hip_encode's host time
     // goes, seconds: waiting for a staging slot, copying into slots, issuing
     // their DMA, waiting for the copy-out thread, settling a batch, and in
     // the copy-out: packets over PCIe, into the caller's buffer
     bool dbg = false;
     double t_slot = 0, t_copy = 0, t_dma = 0, t_join = 0, t_settle = 0, t_d2h = 0, t_out = 0;
-    double t_sizes = 0, t_compact = 0, t_dcopy = 0;  // inside the D2H (FFV1HIP_HOSTDBG)
+    double t_sizes = 0, t_compact = 0, t_dcopy = 0;  // inside the D2H (hostdbg)
   } pipe;
   uint8_t* d_frames2 = nullptr;
   uint8_t* d_frames3 = nullptr;
@@ -1019,7 +1019,7 @@ static int upload_hdr(ffv1hip_ctx* c) {
 
 static void pipe_close(ffv1hip_ctx* c);
 
-// FFV1HIP_WALKTRACE: per traced batch and launch part, when its waves
+// walktrace: per traced batch and launch part, when its waves
 // started (spread from the batch's first), how long they ran, when the
 // last ended (ms).
 static void dump_walk_trace(ffv1hip_ctx* c) {
@@ -1328,10 +1328,6 @@ static int alloc_device(ffv1hip_ctx* c) {
                      (long long)fit);
     }
   }
-  c->grid_sym = c->knobs.get("sym_grid", c->grid_sym);
-  c->grid_bits = c->knobs.get("bits_grid", c->grid_bits);
-  c->grid_dseg = std::max(1, c->knobs.get("dseg_grid", c->grid_dseg));
-  c->prio_dseg = c->knobs.get("dseg_prio", c->prio_dseg);
   HIP_TRY(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   for (hipEvent_t& e : c->hist_done) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -2043,8 +2039,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       range_first = c->d_qt_walk && !chroma_long &&
                     walk_items(nsegs, c->nslices, wa.per_short, wa.short_multi) <= resident;
     }
-    wa.prio = c->knobs.get("walk_prio", range_first ? 0 : 2);
-    const int range_prio = c->knobs.get("range_prio", range_first ? 3 : 0);
+    wa.prio = range_first ? 0 : 2;
+    const int range_prio = range_first ? 3 : 0;
     wa.init = c->d_init;
     wa.rows = c->walk_rows;
     wa.dense = c->d_qt_walk != nullptr;
@@ -2068,12 +2064,11 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       wa.dbg = d_dbg;
     }
     // split schedule: the first part is what the CUs hold at once
-    // (the walk_split=0 hook: one launch); one timed region either way
-    const bool split_env = c->knobs.get("walk_split", 1) != 0;
+    // (one launch measured slower, round 4); one timed region either way
     const int nitems = walk_items(nsegs, c->nslices, wa.per_short, wa.short_multi);
     // walk_part_a (test hook): the first part's waves
     const bool pa = c->knobs.has("walk_part_a");
-    const int first = sst != st && split_env ? (pa ? c->knobs.get("walk_part_a", 0) : walk_resident(wa)) : 0;
+    const int first = sst != st ? (pa ? c->knobs.get("walk_part_a", 0) : walk_resident(wa)) : 0;
     // ... and only when the second part leaves room on the CUs beside it
     // (at most 80 % of the resident slots: c5's 100 % ran slower in round 2)
     const bool two_parts = wa.block_waves == 1 && first > 0 && first < nitems &&
@@ -2162,7 +2157,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     if (rsplit) {
       ca.range_pass = 2;
       CodeArgs cf = ca;  // the fused launch's dseg grid (rd_grid hook)
-      cf.dseg_blocks = std::max(1, std::min(ca.dseg_blocks, c->knobs.get("rd_grid", ca.dseg_blocks)));
+      cf.dseg_blocks = std::max(1, ca.dseg_blocks);
       if (timed(7, cst, [&] { return launch_range_dseg(cf, cst); }) < 0)
         return set_err(-5, "range / dseg launch failed: %s", hipGetErrorString(hipGetLastError()));
       ca.dseg_part = 1;
@@ -2495,20 +2490,14 @@ static int pipe_open_parts(ffv1hip_ctx* c) {
                    double(fset) / 1e9);
   }
   {
-    // xq=0: both copy streams at the greatest priority (a queue pool of their
-    // own); xq=1: default priority (they share the 4 hardware queues with the
-    // kernel streams); xq=2: transfer stream prioritised, packets out on the side stream
-    const int xq = c->knobs.get("xq", 0);
+    // both copy streams at the greatest priority: a queue pool of their own,
+    // so that the host path fits the runtime's default 4 hardware queues
+    // (at default priority the packets-out stream shared the walk stream's
+    // queue: encode2 batch 240 7,132 -> 8,383 Mpix/s, gpurun_out/r5l)
     int lo = 0, hi = 0;
     HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    const int pr = xq == 1 ? 0 : hi;
-    HIP_TRY(hipStreamCreateWithPriority(&P.xfer, hipStreamNonBlocking, pr));
-    if (xq == 2) {
-      P.d2h = c->bits_stream ? c->bits_stream : c->stream;
-      P.d2h_borrowed = true;
-    } else {
-      HIP_TRY(hipStreamCreateWithPriority(&P.d2h, hipStreamNonBlocking, pr));
-    }
+    HIP_TRY(hipStreamCreateWithPriority(&P.xfer, hipStreamNonBlocking, hi));
+    HIP_TRY(hipStreamCreateWithPriority(&P.d2h, hipStreamNonBlocking, hi));
   }
   int nt = int(std::thread::hardware_concurrency());
   if (const char* e = std::getenv("OMP_NUM_THREADS"))  // the host's CPU share where it is set
@@ -2630,7 +2619,7 @@ static void pipe_close(ffv1hip_ctx* c) {
   for (uint8_t* d : P.d_packed)
     if (d) (void)hipFree(d);
   if (P.xfer) (void)hipStreamDestroy(P.xfer);
-  if (P.d2h && !P.d2h_borrowed) (void)hipStreamDestroy(P.d2h);
+  if (P.d2h) (void)hipStreamDestroy(P.d2h);
   for (void* q : {(void*)c->d_frames2, (void*)c->d_frames3, (void*)c->d_packets2, (void*)c->d_packet_size2})
     if (q) (void)hipFree(q);
   c->d_frames2 = nullptr;
@@ -3560,9 +3549,7 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
   la.context_model = p.context_model;
   constexpr int64_t kDecLds = 64 * 1024;
   d->global_states = decode_lds_bytes(la, false) > kDecLds;
-  // dec_swap=0 (measurement hook): both plane groups in the LDS
-  d->swap = !d->global_states && p.ac && !p.colorspace && p.chroma_planes && !p.transparency &&
-            d->knobs.get("dec_swap", 1) != 0;
+  d->swap = !d->global_states && p.ac && !p.colorspace && p.chroma_planes && !p.transparency;
   if (decode_lds_bytes(la, true) > kDecLds) {
     delete d;
     return fail(set_err(-38, "GPU decoder: slice too wide for the LDS row buffer"));

@@ -113,7 +113,7 @@ def test_unsupported_parameters_are_refused():
 
 
 @pytest.mark.parametrize("var,val,msg", [("FFV1HIP_DENSE", "0", "FFV1HIP_DENSE is not read"),
-                                          ("FFV1HIP_DEBUG", "walk_prio=1,no_such_hook", "unknown hook")])
+                                          ("FFV1HIP_DEBUG", "serial,no_such_hook", "unknown hook")])
 def test_hooks_misspelt_or_legacy_are_refused(var, val, msg, monkeypatch):
     """Measurement hooks go through FFV1HIP_DEBUG=name[=value],... only: an
     unknown name there, or one of the per-hook variables of earlier rounds,
