@@ -77,47 +77,29 @@ __device__ __forceinline__ uint64_t decision_bits(int v) {
   return unary | mant | ((uint64_t)(v < 0) << (2 * e + 2));
 }
 
-// 16 bits -> the even bits of a word
-__device__ __forceinline__ uint32_t spread16(uint32_t x) {
-  x &= 0xFFFFu;
-  x = (x | (x << 8)) & 0x00FF00FFu;
-  x = (x | (x << 4)) & 0x0F0F0F0Fu;
-  x = (x | (x << 2)) & 0x33333333u;
-  x = (x | (x << 1)) & 0x55555555u;
-  return x;
-}
-
-// Per-slot codes of one symbol with e <= 9, two bits per slot (slots 0..15
-// in the first word, 16..31 in the second): 0/1 the slot's decision bit,
-// 2 no decision.  Slot 0 zero flag, 1..e+1 unary, 11+e sign, 22..21+e
-// mantissa (put_symbol_inline, ffv1enc.c:185-231).
-__device__ __forceinline__ void slot_codes(int v, uint32_t& c0, uint32_t& c1) {
+// Per-slot decisions of one symbol (put_symbol_inline, ffv1enc.c:185-231):
+// slot 0 zero flag, 1..e+1 unary, 11+e sign, 22..21+e mantissa, as two slot
+// masks, one bit per slot: bm the decision bit, nd "no decision" (the walk's
+// code for lane k: nd ? 2 : bit; both set: several decisions, code 3, at
+// e = 10, 11).  The walk reads bit k of each, so nothing is spread to 2-bit
+// codes (that took ~48 VALU per record).
+__device__ __forceinline__ void slot_masks(int v, uint32_t& bm, uint32_t& nd) {
   const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
   const int e = v ? 31 - __builtin_clz(mag) : -1;
+  const uint32_t neg = (uint32_t)(v < 0);
   if (e >= 10) {
-    // e = 10, 11: slots 1..9 a one each, slot 10 the ones of i = 9..e-1 and
-    // the terminating zero (code 3), sign in slot 21, mantissa bits 0..8 in
-    // slots 22..30, bits 9..e-1 in slot 31 (one: its bit; two: code 3)
-    const uint32_t pres = 0x7FFu & ~1u;  // slots 1..10
+    // slots 1..9 a one each, slot 10 several (3), sign in 21, mantissa bits
+    // 0..8 in 22..30, bits 9..e-1 in 31 (one at e = 10, several at 11)
     const uint32_t lo9 = mag & 0x1FFu;
-    uint32_t cc0 = spread16(pres & 0x3FEu) | (spread16(~pres & 0xFFFFu) << 1);  // 1s in 1..9, none elsewhere but 10
-    cc0 = (cc0 & ~(3u << 20)) | (3u << 20);                                       // slot 10: several
-    cc0 &= ~3u;                                                                   // slot 0: 0 (nonzero)
-    uint32_t hi = (uint32_t)(v < 0) << 5 | (lo9 << 6);  // slot 21 (bit 5 of the high half), 22..30
-    uint32_t pr = (1u << 5) | (0x1FFu << 6);
-    uint32_t cc1 = spread16(hi) | (spread16(~pr & 0xFFFFu) << 1);
-    const uint32_t c31 = e == 10 ? ((mag >> 9) & 1u) : 3u;
-    cc1 = (cc1 & ~(3u << 30)) | (c31 << 30);
-    c0 = cc0;
-    c1 = cc1;
+    const uint32_t t = 0x3FFu | (1u << 21) | (0x1FFu << 22) | (e == 10 ? 1u << 31 : 0u);  // (slot 10: several)
+    bm = 0x3FEu | (1u << 10) | (neg << 21) | (lo9 << 22) | (e == 10 ? ((mag >> 9) & 1u) << 31 : 1u << 31);
+    nd = ~t;
     return;
   }
   const uint32_t lo = v ? (1u << e) - 1u : 0u;  // e ones
-  const uint32_t tm = v ? (1u | (((2u << e) - 1u) << 1) | (1u << (11 + e)) | (lo << 22)) : 1u;
-  const uint32_t bm = v ? ((lo << 1) | ((uint32_t)(v < 0) << (11 + e)) | ((mag & lo) << 22)) : 1u;
-  const uint32_t nt = ~tm;
-  c0 = spread16(bm) | (spread16(nt) << 1);
-  c1 = spread16(bm >> 16) | (spread16(nt >> 16) << 1);
+  const uint32_t t = v ? (1u | (((2u << e) - 1u) << 1) | (1u << (11 + e)) | (lo << 22)) : 1u;
+  bm = v ? ((lo << 1) | (neg << (11 + e)) | ((mag & lo) << 22)) : 1u;
+  nd = ~t;
 }
 
 // Inclusive wave scan in DPP moves (no LDS round trips): within rows of 16
@@ -1603,8 +1585,7 @@ __device__ __forceinline__ int walk_long(int st, const uint8_t* ftab, int v, int
 
 // per-lane constants of the step
 struct WalkLane {
-  int csh, hsh;       // code shift; D or D+2e
-  uint32_t mlo;       // all ones for slots 0..15 (codes in the record's y word)
+  int k, hsh;         // the lane's slot; D or D+2e
   int kk;             // k + this half's table base
   int dummy;          // stage byte of untouched slots
   int msh, mwd, mbase;  // slots 10 / 31: where the record keeps the composed row (code 3)
@@ -1622,16 +1603,17 @@ struct StepIn {
 template <bool MULTI = false>
 __device__ __forceinline__ StepIn derive(const uint4& r, const WalkLane& W, int kc) {
   StepIn d;
-  const uint32_t sel = (r.y & W.mlo) | (r.z & ~W.mlo);  // bitwise: a select of members would go to scratch
-  d.code = __builtin_amdgcn_ubfe(sel, W.csh, 2);
+  const uint32_t bit = __builtin_amdgcn_ubfe(r.y, W.k, 1);
+  const int nd = __builtin_amdgcn_sbfe((int)r.z, W.k, 1);  // all ones: no decision (several, with the bit)
   const int pos = (int)__builtin_amdgcn_ubfe(r.w, W.hsh, 12) + kc;
   if constexpr (MULTI) {
+    d.code = nd ? (bit ? 3u : 2u) : bit;
     d.pos = d.code == 2u ? W.dummy : pos;
   } else {
-    // codes 0..2 only: bit 1 of the code, sign-extended, is the "no
-    // decision" mask, and a bitwise insert takes the dummy byte (no compare,
-    // so no VCC write and the wait states a select of it would need)
-    const int nd = __builtin_amdgcn_sbfe((int)sel, W.csh + 1, 1);
+    // codes 0..2 only (no bit where there is no decision): code = nd & 2 |
+    // bit, and a bitwise insert takes the dummy byte (no compare, so no VCC
+    // write and the wait states a select of it would need)
+    d.code = ((uint32_t)nd & 2u) | bit;
     d.pos = (nd & W.dummy) | (~nd & pos);
   }
   d.addr = (int)(r.x & 0xFFFFu) + W.kk;
@@ -1718,13 +1700,13 @@ int64_t walk_block_lds_dev(int rows, int waves) {
 }
 
 // The 8-byte record in HBM (ffv1_symbols) as the walk's step reads it from
-// LDS: the slot codes (y, z) follow from the residual in x (slot_codes), so
-// they are derived here once per chunk instead of being stored and read back
-// (16 -> 8 bytes per sample).
+// LDS: the slot masks (y = bits, z = no decision) follow from the residual
+// in x (slot_masks), so they are derived here once per chunk instead of
+// being stored and read back (16 -> 8 bytes per sample).
 __device__ __forceinline__ uint4 expand_rec(const uint2& r) {
-  uint32_t c0, c1;
-  slot_codes((int)(int16_t)(r.x >> 16), c0, c1);
-  return make_uint4(r.x, c0, c1, r.y);
+  uint32_t bm, nd;
+  slot_masks((int)(int16_t)(r.x >> 16), bm, nd);
+  return make_uint4(r.x, bm, nd, r.y);
 }
 
 // (Expanding the next chunk's records inside the step loop, in the shadow of
@@ -1827,8 +1809,7 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
   const uint4 v128 = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
 
   WalkLane W;
-  W.csh = (2 * k) & 31;
-  W.mlo = k < 16 ? ~0u : 0u;
+  W.k = k;
   const bool isU = k <= 10;                // zero flag / exponent slots: decision D + k
   W.hsh = isU ? 0 : 16;                    // else from D + 2e: sign +2, mantissa 22+i: +1-i
   const int kslot = isU ? k : (k <= 21 ? 2 : 23 - k);
@@ -1837,7 +1818,7 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
   W.msh = k == 31 ? 28 : 12;
   W.mwd = k == 31 ? 2 : 3;
   W.mbase = k == 31 ? 4 : 0;
-  const uint4 nullrec = make_uint4((uint32_t)thalf, 0xAAAAAAAAu, 0xAAAAAAAAu, 0u);  // dummy row, no decisions
+  const uint4 nullrec = make_uint4((uint32_t)thalf, 0u, ~0u, 0u);  // dummy row, no decisions
 
   // The stage of chunk c goes out at the start of chunk c+1, before its
   // loads are issued: vmcnt counts in issue order, so waiting for chunk
