@@ -39,6 +39,7 @@ namespace ffv1hip {
 namespace {
 
 constexpr int kWave = 64;
+constexpr int kBufDword3 = 0x00020000;  // gfx9-family raw buffer (32-bit data format)
 
 __device__ __forceinline__ int median3(int a, int b, int c) {
   return max(min(a, b), min(max(a, b), c));
@@ -185,14 +186,22 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   const int sh = a.packed_at_lsb ? 0 : a.msb_shift;
   const uint8_t* const fr = a.frames + (int64_t)f * a.frame_bytes;
   const int2 co = RGB && a.rct ? a.rct[(int64_t)f * a.nslices + slice] : make_int2(1, 1);
+  // YCbCr planes through a buffer resource: a sample's address is one 24-bit
+  // multiply-add on 32-bit offsets, not 64-bit arithmetic (a plane is < 2 GB)
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, 0x7FFFFFFF, kBufDword3);
   auto load = [&](int x, int y) -> int {
     if constexpr (SB == 4) {
       return rct_sample<4>(a, fr, p, px + x, py + y, co);
     } else {
       if constexpr (SB == 2 && RGB) return rct_sample<2>(a, fr, p, px + x, py + y, co);
-      const uint8_t* r = base + (int64_t)(py + y) * stride;
-      if constexpr (SB == 1) return r[(px + x) * step];
-      else return (int16_t)(reinterpret_cast<const uint16_t*>(r)[px + x] >> sh);
+      if constexpr (SB == 1) {
+        const uint32_t off = __umul24((uint32_t)(py + y), (uint32_t)stride) + (uint32_t)((px + x) * step);
+        return __builtin_amdgcn_raw_buffer_load_b8(prs, off, 0, 0);
+      } else {
+        const uint32_t off = __umul24((uint32_t)(py + y), (uint32_t)stride) + (uint32_t)(px + x) * 2u;
+        return (int16_t)(__builtin_amdgcn_raw_buffer_load_b16(prs, off, 0, 0) >> sh);
+      }
     }
   };
 
@@ -1220,8 +1229,6 @@ struct DigitOut {
   __amdgpu_buffer_rsrc_t rs;
   int kb;
 };
-constexpr int kBufDword3 = 0x00020000;  // gfx9-family raw buffer (32-bit data format)
-
 
 // put_rac + renorm_encoder's shift (rangecoder.h:52-102): the value of low
 // before a shift is stored as the lane's next digit.
