@@ -143,16 +143,18 @@ __device__ __forceinline__ int get_v(RacDec& c, uint32_t src, uint32_t& dst, int
   const uint32_t pair = tt[s];  // to0 | to1 << 8, for the row image only
   const uint32_t r1 = __umul24(c.range, s) >> 8;
   const uint32_t rr = c.range - r1;
-  // every lane holds the same coder: the compare's lane mask is the bit, so
-  // the branches on it are scalar (no exec-mask save and restore)
-  const bool bit = __builtin_amdgcn_ballot_w64(c.low >= rr) != 0;
-  c.low -= bit ? rr : 0u;
-  c.range = bit ? r1 : rr;
+  // every lane holds the same coder: the selects take the compare's lane
+  // mask as it is, and its ballot is the bit, so the branches on it are
+  // scalar (no exec-mask save and restore)
+  const bool lb = c.low >= rr;
+  c.low -= lb ? rr : 0u;
+  c.range = lb ? r1 : rr;
+  const bool bit = __builtin_amdgcn_ballot_w64(lb) != 0;
   // the successor into byte SH / 8 of the image: one byte permute (pair's
   // byte 1 on a 1, byte 0 on a 0; the image's other bytes as they are)
   const uint32_t keep = 0x03020100u & ~(0xFFu << SH);
   dst = __builtin_amdgcn_perm(pair, dst, keep | ((bit ? 5u : 4u) << SH));
-  if (__builtin_amdgcn_ballot_w64(c.range < 0x100u)) rac_refill(c, w);
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(c.range < 0x100u) != 0, 0)) rac_refill(c, w);
   return bit;
 }
 // (Reading the pairs of the likely next decisions one decision ahead
@@ -164,11 +166,12 @@ __device__ __forceinline__ int get_v(RacDec& c, uint32_t src, uint32_t& dst, int
 __device__ __forceinline__ bool dec_s(RacDec& c, uint32_t s, const uint64_t* w) {
   const uint32_t r1 = __umul24(c.range, s) >> 8;
   const uint32_t rr = c.range - r1;
-  const bool bit = __builtin_amdgcn_ballot_w64(c.low >= rr) != 0;
-  c.low -= bit ? rr : 0u;
-  c.range = bit ? r1 : rr;
-  if (__builtin_amdgcn_ballot_w64(c.range < 0x100u)) rac_refill(c, w);
-  return bit;
+  const bool lb = c.low >= rr;  // (see get_v)
+  c.low -= lb ? rr : 0u;
+  c.range = lb ? r1 : rr;
+  // a refill is the rare case: the common path falls through
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(c.range < 0x100u) != 0, 0)) rac_refill(c, w);
+  return __builtin_amdgcn_ballot_w64(lb) != 0;
 }
 
 template <int K>
@@ -187,13 +190,23 @@ __device__ __forceinline__ void unary_v(RacDec& c, const uint32_t (&r)[8], int& 
   }
 }
 
-// mantissa bits i = K .. 0 on slots 22 + i (those below e)
-template <int K>
+// mantissa bits i = min(e, 9) - 1 .. 0 on slots 22 + i: one jump into the
+// run by the bit count (a compare and branch per bit before)
 __device__ __forceinline__ void mant_v(RacDec& c, const uint32_t (&r)[8], int e, uint32_t& a, const uint64_t* w) {
-  if constexpr (K >= 0) {
-    if (K < e) a = 2 * a + uint32_t(dec_k<22 + K>(c, r, w));
-    mant_v<K - 1>(c, r, e, a, w);
+#define FFV1_MANT(I) a = 2 * a + uint32_t(dec_k<22 + (I)>(c, r, w))
+  switch (e < 9 ? e : 9) {
+    case 9: FFV1_MANT(8); [[fallthrough]];
+    case 8: FFV1_MANT(7); [[fallthrough]];
+    case 7: FFV1_MANT(6); [[fallthrough]];
+    case 6: FFV1_MANT(5); [[fallthrough]];
+    case 5: FFV1_MANT(4); [[fallthrough]];
+    case 4: FFV1_MANT(3); [[fallthrough]];
+    case 3: FFV1_MANT(2); [[fallthrough]];
+    case 2: FFV1_MANT(1); [[fallthrough]];
+    case 1: FFV1_MANT(0); [[fallthrough]];
+    default: break;
   }
+#undef FFV1_MANT
 }
 
 // get_symbol_inline (ffv1dec.c:44-66), signed, on the row at `row`.  The
@@ -237,7 +250,7 @@ __device__ inline int symbol_v(RacDec& c, uint8_t* row, const uint16_t* tt, cons
         a = 2 * a + uint32_t(get_v(c, src, n7, 24, tt, w));
         src = n7;
       }
-      mant_v<8>(c, r, e, a, w);
+      mant_v(c, r, e, a, w);
       const int j = 11 + (e < 10 ? e : 10);  // the sign slot, row words 2..5
       const int q = j >> 2;
       const uint32_t wd = q == 2 ? r[2] : q == 3 ? r[3] : q == 4 ? r[4] : r[5];
@@ -296,7 +309,7 @@ __device__ inline void decode_row_v(RacDec& c, uint8_t* st8, const uint16_t* tt,
     if (ctx < 0) diff = -diff;
     const int pred = median3u(L, L + T - LT, T);
     const int v = int(int16_t((pred + diff) & mask));
-    if (threadIdx.x == 0) cur[x] = int16_t(v);
+    cur[x] = int16_t(v);  // every lane the same value to the same address: no exec mask to set up
     LT = T;
     T = RT;
     RT = RTn;
@@ -318,7 +331,7 @@ __device__ inline void decode_row_pcm_v(RacDec& c, const uint64_t* pkw, int16_t*
       if (__builtin_amdgcn_ballot_w64(c.range < 0x100u)) rac_refill(c, pkw);
       v = 2 * v + bit;
     }
-    if (threadIdx.x == 0) cur[x] = int16_t(v);
+    cur[x] = int16_t(v);
   }
 }
 
