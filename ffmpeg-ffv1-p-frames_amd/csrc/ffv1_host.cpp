@@ -114,7 +114,7 @@ class CopyPool {
 // measurement: serial, walkdbg, walktrace, hostdbg, copy_threads; test hooks
 // (each forces a path the product takes on its own only in some configs or
 // under memory pressure): coder=chain, dense=0, walk_blocks=0, recsets=1,
-// range_split=0, slice_cap, walk_part_a, force_multi, bounds_shrink,
+// slice_cap, walk_part_a, force_multi, bounds_shrink,
 // dsets=eager|lazy, budget=q, rec2_drop=set, pack=0, fsets=2, v4_cap0,
 // readback.  Unknown names
 // are an error at create time, so a misspelt hook never silently measures
@@ -140,7 +140,7 @@ struct Knobs {
 
 static const char* const kKnobNames[] = {"serial",      "walkdbg",     "walktrace", "hostdbg",       "copy_threads",
                                          "coder",       "dense",       "walk_blocks", "recsets",     "slice_cap",
-                                         "walk_part_a", "force_multi", "bounds_shrink", "range_split", "dsets",
+                                         "walk_part_a", "force_multi", "bounds_shrink", "dsets",
                                          "rec2_drop",   "budget",      "pack",        "v4_cap0",     "readback",
                                          "fsets"};
 
@@ -2144,24 +2144,24 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     HIP_TRY(hipMemsetAsync(ca.status, 0, sizeof(int) * 4, cst));
     // range alone (the serial chain), every segment from its checkpoint,
     // the segments joined, then the bytes.  Split at the luma / chroma
-    // boundary (the range_split=0 hook: not), the luma segments' dseg runs
-    // beside the chroma chains' range pass in one launch, so the coder
-    // stream is range(luma) + max(range(chroma), dseg(luma)) + dseg(chroma)
-    // instead of range + dseg.  (Timing: the fused launch counts as dseg.)
+    // boundary, the luma segments' dseg runs beside the chroma chains' range
+    // pass in one launch, so the coder stream is range(luma) +
+    // max(range(chroma), dseg(luma)) + dseg(chroma) instead of range + dseg
+    // (the unsplit pass measured slower, round 4; its hook is gone).
+    // (Timing: the fused launch counts as dseg.)
     ca.rstate = c->d_rstate;
-    const bool rsplit = c->knobs.get("range_split", 1) != 0;
-    ca.range_pass = rsplit ? 1 : 0;
+    ca.range_pass = 1;
     ca.dseg_part = -1;
     if (timed(1, cst, [&] { return launch_range(ca, cst); }) < 0)
       return set_err(-5, "range launch failed: %s", hipGetErrorString(hipGetLastError()));
-    if (rsplit) {
-      ca.range_pass = 2;
-      CodeArgs cf = ca;  // the fused launch's dseg grid (rd_grid hook)
+    ca.range_pass = 2;
+    {
+      CodeArgs cf = ca;  // the fused launch's dseg grid
       cf.dseg_blocks = std::max(1, ca.dseg_blocks);
       if (timed(7, cst, [&] { return launch_range_dseg(cf, cst); }) < 0)
         return set_err(-5, "range / dseg launch failed: %s", hipGetErrorString(hipGetLastError()));
-      ca.dseg_part = 1;
     }
+    ca.dseg_part = 1;
     if (timed(7, cst, [&] { return launch_dseg(ca, cst); }) < 0)
       return set_err(-5, "dseg launch failed: %s", hipGetErrorString(hipGetLastError()));
     HIP_TRY(hipEventRecord(c->pre_read[fb], cst));

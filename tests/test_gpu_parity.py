@@ -75,11 +75,10 @@ def test_chained_coder_matches_oracle(stream, monkeypatch):
     assert got == ref
 
 
-@pytest.mark.parametrize("debug", ["range_split=0", "walk_blocks=0", "serial", "range_split=0,serial"])
+@pytest.mark.parametrize("debug", ["walk_blocks=0", "serial", "walk_blocks=0,serial"])
 def test_schedule_variants_match_oracle(debug, monkeypatch):
-    """The coder's range pass whole or split at the luma / chroma boundary
-    (ffv1_range_dseg), the walk in 5-wave or one-wave blocks, overlapped or
-    one kernel at a time: the same bytes, at a batch (two GOPs of 4:2:0
+    """The walk in 5-wave or one-wave blocks, overlapped or one kernel at a
+    time: the same bytes, at a batch (two GOPs of 4:2:0
     10-bit and a 4:4:4 stream, whose chroma chains are the long ones) that
     puts every chain in one round."""
     monkeypatch.setenv("FFV1HIP_DEBUG", debug)
