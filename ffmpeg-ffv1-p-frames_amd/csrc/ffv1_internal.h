@@ -115,10 +115,12 @@ struct RctArgs {
 //      start of its chunk; bit 31: same row as the previous sample of the
 //      chunk; bit 30: same row as the sample two back in the chunk; bits
 //      12..14 / 28..29: the composed rows of slots 10 / 31 at e = 10, 11
-// The walk expands a chunk's records in LDS to uint4 {x, y, z, w}, y and z
-// two bits per slot (slots 0..15, 16..31): 0/1 the slot's decision bit, 2
-// no decision, 3 several decisions (slot 10 at e >= 10, slot 31 at e >= 11);
-// e <= 11 only, the chunks with a larger exponent take walk_long.
+// The walk expands a chunk's records in LDS to uint4 {x, y, z, w}: in a
+// chunk of symbols with e <= 9, y and z are slot masks (one bit per slot:
+// y the decision bit, z "no decision"); in a chunk with e = 10, 11 symbols,
+// two bits per slot (y slots 0..15, z 16..31): 0/1 the slot's decision bit,
+// 2 no decision, 3 several decisions (slot 10 at e >= 10, slot 31 at e >=
+// 11); the chunks with a larger exponent take walk_long.
 constexpr uint32_t kRecSame = 0x80000000u;
 constexpr uint32_t kRecSame2 = 0x40000000u;
 

@@ -103,6 +103,55 @@ __device__ __forceinline__ void slot_masks(int v, uint32_t& bm, uint32_t& nd) {
   nd = ~t;
 }
 
+// The same per-slot decisions as 2-bit codes, two bits per slot (c0 slots
+// 0..15, c1 16..31): 0/1 the decision bit, 2 none, 3 several (slot 10 at e
+// >= 10, slot 31 at e = 11).  The walk expands the chunks with e = 10, 11
+// symbols this way: one field extract gives a lane its code there, where the
+// two masks need a combination of three (measured with codes in every
+// chunk: c4, where such chunks are common, 7.95 -> 8.33 Gpix/s, c3 19.02 ->
+// 18.87; so the plain chunks keep the masks, cheaper to expand).
+__device__ __forceinline__ uint32_t spread16(uint32_t x) {
+  x &= 0xFFFFu;
+  x = (x | (x << 8)) & 0x00FF00FFu;
+  x = (x | (x << 4)) & 0x0F0F0F0Fu;
+  x = (x | (x << 2)) & 0x33333333u;
+  x = (x | (x << 1)) & 0x55555555u;
+  return x;
+}
+
+// Per-slot codes of one symbol with e <= 9, two bits per slot (slots 0..15
+// in the first word, 16..31 in the second): 0/1 the slot's decision bit,
+// 2 no decision.  Slot 0 zero flag, 1..e+1 unary, 11+e sign, 22..21+e
+// mantissa (put_symbol_inline, ffv1enc.c:185-231).
+__device__ __forceinline__ void slot_codes(int v, uint32_t& c0, uint32_t& c1) {
+  const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
+  const int e = v ? 31 - __builtin_clz(mag) : -1;
+  if (e >= 10) {
+    // e = 10, 11: slots 1..9 a one each, slot 10 the ones of i = 9..e-1 and
+    // the terminating zero (code 3), sign in slot 21, mantissa bits 0..8 in
+    // slots 22..30, bits 9..e-1 in slot 31 (one: its bit; two: code 3)
+    const uint32_t pres = 0x7FFu & ~1u;  // slots 1..10
+    const uint32_t lo9 = mag & 0x1FFu;
+    uint32_t cc0 = spread16(pres & 0x3FEu) | (spread16(~pres & 0xFFFFu) << 1);  // 1s in 1..9, none elsewhere but 10
+    cc0 = (cc0 & ~(3u << 20)) | (3u << 20);                                       // slot 10: several
+    cc0 &= ~3u;                                                                   // slot 0: 0 (nonzero)
+    uint32_t hi = (uint32_t)(v < 0) << 5 | (lo9 << 6);  // slot 21 (bit 5 of the high half), 22..30
+    uint32_t pr = (1u << 5) | (0x1FFu << 6);
+    uint32_t cc1 = spread16(hi) | (spread16(~pr & 0xFFFFu) << 1);
+    const uint32_t c31 = e == 10 ? ((mag >> 9) & 1u) : 3u;
+    cc1 = (cc1 & ~(3u << 30)) | (c31 << 30);
+    c0 = cc0;
+    c1 = cc1;
+    return;
+  }
+  const uint32_t lo = v ? (1u << e) - 1u : 0u;  // e ones
+  const uint32_t tm = v ? (1u | (((2u << e) - 1u) << 1) | (1u << (11 + e)) | (lo << 22)) : 1u;
+  const uint32_t bm = v ? ((lo << 1) | ((uint32_t)(v < 0) << (11 + e)) | ((mag & lo) << 22)) : 1u;
+  const uint32_t nt = ~tm;
+  c0 = spread16(bm) | (spread16(nt) << 1);
+  c1 = spread16(bm >> 16) | (spread16(nt >> 16) << 1);
+}
+
 // Inclusive wave scan in DPP moves (no LDS round trips): within rows of 16
 // by row_shr 1, 2, 4, 8, then the row totals by row_bcast 15 / 31.
 __device__ __forceinline__ int wave_incl_scan(int x, int /*lane*/) {
@@ -1596,6 +1645,8 @@ struct WalkLane {
   int kk;             // k + this half's table base
   int dummy;          // stage byte of untouched slots
   int msh, mwd, mbase;  // slots 10 / 31: where the record keeps the composed row (code 3)
+  int csh;            // multi chunks: the lane's 2-bit code field in its code word
+  uint32_t mlo;       // ... all ones: the code word is y (slots 0..15), else z
 };
 
 // A symbol as lane k of its chain sees it.
@@ -1610,13 +1661,14 @@ struct StepIn {
 template <bool MULTI = false>
 __device__ __forceinline__ StepIn derive(const uint4& r, const WalkLane& W, int kc) {
   StepIn d;
-  const uint32_t bit = __builtin_amdgcn_ubfe(r.y, W.k, 1);
-  const int nd = __builtin_amdgcn_sbfe((int)r.z, W.k, 1);  // all ones: no decision (several, with the bit)
   const int pos = (int)__builtin_amdgcn_ubfe(r.w, W.hsh, 12) + kc;
-  if constexpr (MULTI) {
-    d.code = nd ? (bit ? 3u : 2u) : bit;
+  if constexpr (MULTI) {  // records of 2-bit codes (expand_codes)
+    const uint32_t sel = (r.y & W.mlo) | (r.z & ~W.mlo);  // bitwise: a select of members would go to scratch
+    d.code = __builtin_amdgcn_ubfe(sel, W.csh, 2);
     d.pos = d.code == 2u ? W.dummy : pos;
-  } else {
+  } else {  // records of slot masks (expand_rec)
+    const uint32_t bit = __builtin_amdgcn_ubfe(r.y, W.k, 1);
+    const int nd = __builtin_amdgcn_sbfe((int)r.z, W.k, 1);  // all ones: no decision
     // codes 0..2 only (no bit where there is no decision): code = nd & 2 |
     // bit, and a bitwise insert takes the dummy byte (no compare, so no VCC
     // write and the wait states a select of it would need)
@@ -1714,6 +1766,12 @@ __device__ __forceinline__ uint4 expand_rec(const uint2& r) {
   uint32_t bm, nd;
   slot_masks((int)(int16_t)(r.x >> 16), bm, nd);
   return make_uint4(r.x, bm, nd, r.y);
+}
+// ... and in a chunk with e = 10, 11 symbols as 2-bit codes (slot_codes)
+__device__ __forceinline__ uint4 expand_codes(const uint2& r) {
+  uint32_t c0, c1;
+  slot_codes((int)(int16_t)(r.x >> 16), c0, c1);
+  return make_uint4(r.x, c0, c1, r.y);
 }
 
 // (Expanding the next chunk's records inside the step loop, in the shadow of
@@ -1825,7 +1883,10 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
   W.msh = k == 31 ? 28 : 12;
   W.mwd = k == 31 ? 2 : 3;
   W.mbase = k == 31 ? 4 : 0;
+  W.csh = (2 * k) & 31;
+  W.mlo = k < 16 ? ~0u : 0u;
   const uint4 nullrec = make_uint4((uint32_t)thalf, 0u, ~0u, 0u);  // dummy row, no decisions
+  const uint4 nullcodes = make_uint4((uint32_t)thalf, 0xAAAAAAAAu, 0xAAAAAAAAu, 0u);  // ... as codes (2: none)
 
   // The stage of chunk c goes out at the start of chunk c+1, before its
   // loads are issued: vmcnt counts in issue order, so waiting for chunk
@@ -1926,9 +1987,15 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
                              (uint64_t)(__builtin_amdgcn_readlane(mlo, 0) | __builtin_amdgcn_readlane(mlo, 32));
         const bool mul = msk != 0 || a.force_multi;
         const int64_t pos0 = gbase + run;  // decision index of the chunk's first decision
-        myrecs[k] = pick(k < cnt, expand_rec(cx.m0), nullrec);
-        myrecs[k + 32] = pick(k + 32 < cnt, expand_rec(cx.m1), nullrec);
-        if (k < kRecSlots - kChunk) myrecs[kChunk + k] = nullrec;
+        if (!mul) {
+          myrecs[k] = pick(k < cnt, expand_rec(cx.m0), nullrec);
+          myrecs[k + 32] = pick(k + 32 < cnt, expand_rec(cx.m1), nullrec);
+          if (k < kRecSlots - kChunk) myrecs[kChunk + k] = nullrec;
+        } else {  // (uniform) the multi step's codes
+          myrecs[k] = pick(k < cnt, expand_codes(cx.m0), nullcodes);
+          myrecs[k + 32] = pick(k + 32 < cnt, expand_codes(cx.m1), nullcodes);
+          if (k < kRecSlots - kChunk) myrecs[kChunk + k] = nullcodes;
+        }
         __builtin_amdgcn_wave_barrier();
 
         if (lng) {  // e >= 12 somewhere: one symbol at a time, recorded straight to HBM
