@@ -116,7 +116,7 @@ class CopyPool {
 // under memory pressure): coder=chain, dense=0, walk_blocks=0, recsets=1,
 // slice_cap, walk_part_a, force_multi, bounds_shrink,
 // dsets=eager|lazy, budget=q, rec2_drop=set, pack=0, fsets=2, v4_cap0,
-// readback.  Unknown names
+// readback, guard_skip.  Unknown names
 // are an error at create time, so a misspelt hook never silently measures
 // the default.
 struct Knobs {
@@ -142,21 +142,25 @@ static const char* const kKnobNames[] = {"serial",      "walkdbg",     "walktrac
                                          "coder",       "dense",       "walk_blocks", "recsets",     "slice_cap",
                                          "walk_part_a", "force_multi", "bounds_shrink", "dsets",
                                          "rec2_drop",   "budget",      "pack",        "v4_cap0",     "readback",
-                                         "fsets"};
+                                         "fsets",       "guard_skip"};
 
-extern "C" char** environ;
+// The per-hook environment variables of earlier rounds.  They are no longer
+// read, so one that is set is an error (a measurement that silently ran the
+// default); every other FFV1HIP_* name (FFV1HIP_LIB, FFV1HIP_TWOPASS_LIB, ...)
+// belongs to someone else and is left alone.
+static const char* const kLegacyVars[] = {
+    "FFV1HIP_BITS",          "FFV1HIP_BITS_INLINE", "FFV1HIP_CODEDBG",    "FFV1HIP_CODER",     "FFV1HIP_CODE_WAVE_PRIO",
+    "FFV1HIP_COPYOUT_SYNC",  "FFV1HIP_COPY_THREADS", "FFV1HIP_DEC_SWAP",  "FFV1HIP_DENSE",     "FFV1HIP_FORCE_MULTI",
+    "FFV1HIP_HOSTDBG",       "FFV1HIP_LANES",       "FFV1HIP_PARTIAL",    "FFV1HIP_RANGE_FAT", "FFV1HIP_RANGE_PRIO",
+    "FFV1HIP_RECSETS",       "FFV1HIP_RESERVE_CUS", "FFV1HIP_SERIAL",     "FFV1HIP_SLICE_CAP", "FFV1HIP_SPLIT_MAX",
+    "FFV1HIP_SYM_DELAY_US",  "FFV1HIP_WALKDBG",     "FFV1HIP_WALKTRACE",  "FFV1HIP_WALK_FAT",  "FFV1HIP_WALK_LDS_PAD",
+    "FFV1HIP_WALK_LONG_BOOST", "FFV1HIP_WALK_PART_A", "FFV1HIP_WALK_PRIO", "FFV1HIP_WALK_SPLIT"};
 
 static int parse_knobs(Knobs* k) {
   k->kv.clear();
-  // the per-hook variables of earlier rounds (FFV1HIP_DENSE, FFV1HIP_CODER,
-  // ...) are no longer read: one set is an error, not a silent default
-  for (char** ev = environ; ev && *ev; ev++) {
-    const std::string v(*ev);
-    if (v.rfind("FFV1HIP_", 0) != 0) continue;
-    const std::string name = v.substr(0, v.find('='));
-    if (name != "FFV1HIP_DEBUG" && name != "FFV1HIP_LIB" && name != "FFV1HIP_ARCH" && name != "FFV1HIP_SYNTH_LIB")
-      return set_err(-22, "%s is not read: hooks go in FFV1HIP_DEBUG=name[=value],...", name.c_str());
-  }
+  for (const char* name : kLegacyVars)
+    if (std::getenv(name))
+      return set_err(-22, "%s is not read: hooks go in FFV1HIP_DEBUG=name[=value],...", name);
   const char* e = std::getenv("FFV1HIP_DEBUG");
   if (!e) return 0;
   std::string all(e);
@@ -488,6 +492,8 @@ struct ffv1hip_ctx {
   int64_t* hd_tot_map = nullptr;
   int tri_n[3] = {0, 0, 0};
   bool no_guard_once = false;    // the next run_batch sizes its set from the read-back total
+  int64_t guard_skips = 0;       // batches the guard_skip hook launched to be skipped (ffv1hip_debug_counter)
+  int64_t guard_reruns = 0;      // guarded batches encoded again at settle (status[3])
   uint8_t* d_pre[2] = {nullptr, nullptr};    // [decision] state before the decision
   uint8_t* d_scratch = nullptr;               // where idle walk chains write their stage
   uint32_t* d_bounds = nullptr;               // debug build: the first out-of-bounds write's site (sticky)
@@ -545,6 +551,7 @@ struct ffv1hip_ctx {
   // room until those blocks retire (values measured best in earlier rounds)
   int grid_sym = 4096, grid_bits = 2048, grid_dseg = 4096;
   int cus = 256;      // compute units of the device (a walk wave per SIMD: 4 per CU)
+  int lds_block = 0;  // LDS one workgroup may take (the walk's 4/5-wave blocks are held to it)
   int prio_dseg = 0;  // dseg's wave priority (walk / range: per batch, run_batch)
   SliceGeom* d_geom = nullptr;
   int* d_slot_frames = nullptr;  // [j][slot]
@@ -695,6 +702,14 @@ extern "C" {
 
 const char* ffv1hip_last_error(void) { return g_err; }
 int ffv1hip_abi_version(void) { return FFV1HIP_ABI_VERSION; }
+
+int64_t ffv1hip_debug_counter(const ffv1hip_ctx* c, const char* name) {
+  if (!c || !name) return -1;
+  if (!std::strcmp(name, "guard_skips")) return c->guard_skips;
+  if (!std::strcmp(name, "guard_reruns")) return c->guard_reruns;
+  return -1;
+}
+
 int ffv1hip_debug_checks(void) { return kBoundsCheck ? 1 : 0; }
 
 int ffv1hip_configure(ffv1hip_params* out, const ffv1hip_options* o) {
@@ -1329,6 +1344,7 @@ static int alloc_device(ffv1hip_ctx* c) {
     }
   }
   HIP_TRY(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
+  HIP_TRY(hipDeviceGetAttribute(&c->lds_block, hipDeviceAttributeMaxSharedMemoryPerBlock, c->device));
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   for (hipEvent_t& e : c->hist_done) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_TRY(hipMalloc(&c->d_qt, sizeof(c->qt)));
@@ -1372,7 +1388,9 @@ static int alloc_device(ffv1hip_ctx* c) {
     HIP_TRY(hipMalloc(&c->d_packets, size_t(c->packet_stride) * nb));
   }
   HIP_TRY(hipMalloc(&c->d_slice_bytes, sizeof(int64_t) * c->nslices * nb));
+  HIP_TRY(hipMemset(c->d_slice_bytes, 0, sizeof(int64_t) * c->nslices * nb));
   HIP_TRY(hipMalloc(&c->d_packet_size, sizeof(int64_t) * nb));
+  HIP_TRY(hipMemset(c->d_packet_size, 0, sizeof(int64_t) * nb));
   const size_t state_bytes = size_t(c->pcount) * c->contexts * 32;
   for (uint8_t*& pb : c->d_persist) {
     HIP_TRY(hipMalloc(&pb, state_bytes * c->nslices));
@@ -1942,10 +1960,15 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     // (one count snapshot) and the readback=1 hook always read the total back.
     int64_t need = int64_t(n) * c->frame_samples * c->wmax + int64_t(n) * c->nslices * kStreamSlack;
     bool guarded = false;
-    if (need > c->dcap[fb] && est > 0 && est <= c->dcap[fb] && c->pass != 1 && !c->no_guard_once &&
-        !c->knobs.has("readback")) {
+    // (the guard_skip test hook: every batch launches guarded with a set its
+    // decisions never fit, so that its kernels skip it and it takes the
+    // recovery path: status[3], settle, the read-back re-run)
+    const bool force_skip = c->knobs.has("guard_skip") && c->pass != 1 && !c->no_guard_once;
+    if (force_skip ||
+        (need > c->dcap[fb] && est > 0 && est <= c->dcap[fb] && c->pass != 1 && !c->no_guard_once &&
+         !c->knobs.has("readback"))) {
       guarded = true;
-      need = c->dcap[fb];
+      need = std::min(need, c->dcap[fb]);
     }
     c->no_guard_once = false;
     if (need > c->dcap[fb]) {
@@ -1975,7 +1998,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       HIP_TRY(hipMemsetAsync(c->d_bits[fb], 0, size_t((need + 31) / 32) * 4, sst));
     }
     DecisionStream ds{d_dcount, d_dbase, c->d_pre[fb], c->d_bits[fb], guarded ? c->d_dtotal + t3 : nullptr,
-                      c->dcap[fb]};
+                      force_skip ? int64_t(-1) : c->dcap[fb]};
+    if (force_skip) c->guard_skips++;
     BitsArgs ba{};
     ba.cbits = sa.cbits;
     ba.frame_chunks = c->frame_chunks;
@@ -2034,8 +2058,11 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       wa.short_multi = walk_split_short(nsegs, c->nslices, wa.per_short, 4 * c->cus, resident);
       // (the walk_blocks=0 hook, and the split-launch test hook, keep one-wave blocks)
       wa.block_waves = c->knobs.get("walk_blocks", 1) && !c->knobs.has("walk_part_a")
-                           ? walk_block_waves(nsegs, c->nslices, wa.per_short, wa.short_multi, wa.rows, c->cus)
+                           ? walk_block_waves(nsegs, c->nslices, wa.per_short, wa.short_multi, wa.rows, c->cus, c->lds_block)
                            : 1;
+      if (c->knobs.has("hostdbg"))
+        std::fprintf(stderr, "hostdbg: walk of %d segments: %d-wave blocks (%d B of LDS per block allowed)\n", nsegs,
+                     wa.block_waves, c->lds_block);
       range_first = c->d_qt_walk && !chroma_long &&
                     walk_items(nsegs, c->nslices, wa.per_short, wa.short_multi) <= resident;
     }
@@ -2202,6 +2229,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   c->last_nsegs = c->frames_mode ? n : nsegs;
 
   AssembleArgs b{};
+  b.skip = c->frames_mode ? ca.status + 3 : nullptr;
   b.slice_out = c->d_slice_out;
   b.slice_cap = c->slice_cap;
   b.slice_stride = c->slice_stride;
@@ -2218,7 +2246,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
   if (c->pipe.on) {  // the host-frame path then collects the batch with one D2H copy and no GPU work
     ffv1hip_ctx::HostPipe& P = c->pipe;
     if (launch_sizes_out(c->psize(L.pk), n, P.hd_sizes[L.pk], cst) < 0 ||
-        launch_compact_packets(c->pkts(L.pk), c->packet_stride, c->psize(L.pk), n, P.d_compact[L.pk], cst) < 0 ||
+        launch_compact_packets(c->pkts(L.pk), c->packet_stride, c->psize(L.pk), n, P.d_compact[L.pk], b.skip, cst) < 0 ||
         launch_ints_out(ca.status, 4, P.hd_status + 4 * sset, cst) < 0)
       return set_err(-5, "collect launch failed: %s", hipGetErrorString(hipGetLastError()));
   }
@@ -2316,7 +2344,12 @@ static int settle_batch(ffv1hip_ctx* c, int64_t b) {
   bool redo_next = false;
   bool pcm_fail = false;
   ffv1hip_ctx::LastBatch next;
-  for (int attempt = 0;; attempt++) {
+  // re-runs: a slice over the byte budget (status[0]) grows the budget, at
+  // most twice; a guarded batch whose decisions did not fit its set
+  // (status[3], the kernels skipped it) runs once more with its total read
+  // back, which cannot be skipped again, so it gets its own count
+  int budget_runs = 0, set_runs = 0;
+  for (;;) {
     const ffv1hip_ctx::LastBatch& L = c->hist[b & 1];
     HIP_TRY(hipEventSynchronize(c->hist_done[b & 1]));
     if (kBoundsCheck && c->d_bounds) {
@@ -2334,8 +2367,18 @@ static int settle_batch(ffv1hip_ctx* c, int64_t b) {
     }
     pcm_fail = status[2] != 0;
     if (!status[0] && !status[3]) break;
-    if (attempt >= 2 || !L.valid)
+    if (!L.valid || (status[0] && budget_runs >= 2) || (status[3] && set_runs >= 1)) {
+      if (status[3])
+        return set_err(-28, "batch %lld: its decisions did not fit the decision set of a guarded launch, "
+                            "even when encoded again with the total read back", (long long)b);
       return set_err(-28, "%d slices exceeded the slice byte budget", status[0]);
+    }
+    if (status[3]) {
+      set_runs++;
+      c->guard_reruns++;
+    } else {
+      budget_runs++;
+    }
     if (!redo_next && b + 1 < c->nsub) {
       // pass 1 keeps one count snapshot, from before the last batch
       if (c->pass == 1) return set_err(-28, "pass 1: a slice of batch %lld went over the byte budget after a "
@@ -2521,6 +2564,7 @@ static int pipe_open_parts(ffv1hip_ctx* c) {
     if (free_b > fset + 3 * pk_bytes + (size_t(2) << 30) && hipMalloc(&c->d_frames2, fset) == hipSuccess &&
         hipMalloc(&c->d_packets2, pk_bytes) == hipSuccess &&
         hipMalloc(&c->d_packet_size2, sizeof(int64_t) * c->max_batch) == hipSuccess) {
+      HIP_TRY(hipMemset(c->d_packet_size2, 0, sizeof(int64_t) * c->max_batch));
       c->two_pk = true;
       P.overlap = true;
       P.nsets = 2;

@@ -368,6 +368,7 @@ struct BitsArgs {
 };
 
 struct AssembleArgs {
+  const int* skip;             // frame-parallel mode: status[3], set when the batch was skipped (ds_over); or null
   const uint8_t* slice_out;
   int64_t slice_cap;
   int64_t slice_stride;
@@ -442,7 +443,7 @@ int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first = 0, int c
 // (4:2:0 luma vs Cb + Cr, 4:4:4 Cb + Cr vs luma: 2).
 int walk_items(int nsegs, int nslices, int per_short, int short_multi);
 int walk_split_short(int nsegs, int nslices, int per_short, int simds, int resident);
-int walk_block_waves(int nsegs, int nslices, int per_short, int short_multi, int rows, int cus);
+int walk_block_waves(int nsegs, int nslices, int per_short, int short_multi, int rows, int cus, int lds_block);
 int walk_per_short(const SliceGeom& g);
 int walk_resident(const WalkArgs& a);  // (uses a.rows)
 int launch_range(const CodeArgs& a, void* stream);
@@ -456,7 +457,7 @@ constexpr int64_t kWalkLdsMax = 64 * 1024;  // states walk: one plane group's ta
 int launch_code_golomb(const CodeArgs& a, void* stream);
 int launch_assemble(const AssembleArgs& a, int nframes, void* stream);
 int launch_compact_packets(const uint8_t* packets, int64_t stride, const int64_t* sizes, int n, uint8_t* out,
-                           void* stream);
+                           const int* skip, void* stream);
 int launch_sizes_out(const int64_t* sizes, int n, int64_t* host_mapped, void* stream);
 // ffv1_unpack10: frames f0 .. f0+n-1 of a batch's packed 10-bit samples
 // (three to a word) into their 16-bit frame slots, n <= kUnpackFrames

@@ -1506,6 +1506,7 @@ __global__ __launch_bounds__(kFixThreads) void ffv1_dfix(CodeArgs a) {
 // i, which sits at bytes 4i .. 4i+3).
 constexpr int kSinkThreads = kWave;
 __global__ __launch_bounds__(kSinkThreads) void ffv1_sink(CodeArgs a) {
+  if (ds_over(a.ds) || a.status[3]) return;  // a skipped batch (ffv1_range flagged it): no digits to turn into bytes
   const int64_t st = blockIdx.x;
   const int lane = threadIdx.x;
   uint8_t* const out = a.slice_out + st * a.slice_stride;
@@ -2571,6 +2572,7 @@ __global__ __launch_bounds__(kAsmThreads) void ffv1_assemble_packets(AssembleArg
   __shared__ uint32_t pw[40];
   __shared__ int64_t part[kAsmThreads];
   __shared__ uint32_t crc_part[kAsmThreads];
+  if (a.skip && *a.skip) return;  // a skipped batch (status[3]): its slices were never coded
   const int t = threadIdx.x;
   const int s = blockIdx.x, f = blockIdx.y;
   const int64_t* sb = a.slice_bytes + (int64_t)f * a.nslices;
@@ -2813,21 +2815,16 @@ int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first, int count
 // one round with every full-length wave alone on a SIMD (at most 4 per CU
 // of them, at most one one-segment wave per CU) and the block's LDS fits a
 // CU; else 1 (waves placed by the dispatcher, several rounds).
-int walk_block_waves(int nsegs, int nslices, int per_short, int short_multi, int rows, int cus) {
+int walk_block_waves(int nsegs, int nslices, int per_short, int short_multi, int rows, int cus, int lds_block) {
   const int npairs = (nslices + 1) / 2;
   const int nfull = npairs * (nsegs + short_multi);
   const int nsingle = walk_items(nsegs, nslices, per_short, short_multi) - nfull;
   if (nfull > 4 * cus || nsingle > cus) return 1;
   const int w = nsingle > 0 ? 5 : 4;
-  // the block's LDS against the device's (not the 160 KB of gfx950: a part
-  // with less falls back to one-wave blocks instead of failing the launch)
-  int dev = 0, lds = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess) {
-    (void)hipGetLastError();
-    return 1;
-  }
-  return walk_block_lds_dev(rows, w) <= lds ? w : 1;
+  // the block's LDS against what one workgroup may take on this device
+  // (queried once at create; a part with less falls back to one-wave blocks
+  // instead of failing the launch)
+  return walk_block_lds_dev(rows, w) <= lds_block ? w : 1;
 }
 
 int walk_items(int nsegs, int nslices, int per_short, int short_multi) {
@@ -2932,8 +2929,10 @@ namespace {
 // from its aligned slot, byte stores to the unaligned place).
 constexpr int kCompactThreads = 256;
 __global__ __launch_bounds__(kCompactThreads) void ffv1_compact_packets(const uint8_t* packets, int64_t stride,
-                                                                         const int64_t* sizes, int n, uint8_t* out) {
+                                                                         const int64_t* sizes, int n, uint8_t* out,
+                                                                         const int* skip) {
   __shared__ int64_t part[kCompactThreads];
+  if (skip && *skip) return;  // a skipped batch: no packets (the host encodes it again)
   const int i = blockIdx.x;
   int64_t s = 0;
   for (int k = threadIdx.x; k < i; k += kCompactThreads) s += sizes[k];
@@ -3010,10 +3009,10 @@ int launch_unpack10(const UnpackArgs& a, int nframes, void* stream) {
 }
 
 int launch_compact_packets(const uint8_t* packets, int64_t stride, const int64_t* sizes, int n, uint8_t* out,
-                           void* stream) {
+                           const int* skip, void* stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(ffv1_compact_packets, dim3(n), dim3(kCompactThreads), 0, reinterpret_cast<hipStream_t>(stream),
-                     packets, stride, sizes, n, out);
+                     packets, stride, sizes, n, out, skip);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -77,7 +77,7 @@ EXPORTED_SYMBOLS = (
     "ffv1hip_dec_create", "ffv1hip_dec_destroy", "ffv1hip_decode", "ffv1hip_dec_reset",
     "ffv1hip_set_picture_number", "ffv1hip_encode2", "ffv1hip_encode2_delay", "ffv1hip_encode2_last_packet",
     "ffv1hip_dec_damaged_slices",
-    "ffv1hip_set_pass", "ffv1hip_stats_out",
+    "ffv1hip_set_pass", "ffv1hip_stats_out", "ffv1hip_debug_counter",
 )
 
 
@@ -167,6 +167,8 @@ def load_library():
     L.ffv1hip_dec_damaged_slices.argtypes = [vp]
     L.ffv1hip_dec_damaged_slices.restype = ctypes.c_int
     L.ffv1hip_abi_version.argtypes = []
+    L.ffv1hip_debug_counter.argtypes = [vp, ctypes.c_char_p]
+    L.ffv1hip_debug_counter.restype = ctypes.c_int64
     L.ffv1hip_abi_version.restype = ctypes.c_int
     L.ffv1hip_get_slice_states_device.argtypes = [vp, vp, i64, vp]
     L.ffv1hip_get_slice_states_device.restype = i64
@@ -444,6 +446,10 @@ class HipEncoder:
         if rc < 0:
             raise FFV1Error(rc, "ffv1hip_last_kernel_stats")
         return st.as_dict()
+
+    def debug_counter(self, name: str) -> int:
+        """A test counter of the context (ffv1hip_debug_counter): guard_skips, guard_reruns."""
+        return int(load_library().ffv1hip_debug_counter(self._h, name.encode()))
 
     def slice_states(self) -> bytes:
         L = load_library()

@@ -336,6 +336,12 @@ int ffv1hip_abi_version(void);
  * call whose batch wrote outside a buffer fails with -EFAULT naming the
  * kernel; 0 for the release build. */
 int ffv1hip_debug_checks(void);
+/* Test counters of a context (no reference counterpart): "guard_skips", the
+ * batches the FFV1HIP_DEBUG=guard_skip hook launched so that their kernels
+ * skip them, and "guard_reruns", the guarded batches encoded again at settle
+ * because their decisions did not fit the decision set (status[3]); -1 for
+ * an unknown name. */
+int64_t ffv1hip_debug_counter(const ffv1hip_ctx *ctx, const char *name);
 
 #ifdef __cplusplus
 }

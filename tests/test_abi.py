@@ -126,6 +126,20 @@ def test_hooks_misspelt_or_legacy_are_refused(var, val, msg, monkeypatch):
     assert e.value.code == -22 and msg in str(e.value)
 
 
+def test_other_ffv1hip_variables_are_not_hooks(monkeypatch):
+    """Only the legacy per-hook names are refused: FFV1HIP_TWOPASS_LIB (the
+    sanitizer run's), FFV1HIP_LIB and the like belong to other tools, and a
+    process carrying them still creates its encoder (here, without a GPU, it
+    gets as far as the device check)."""
+    from ffv1hip import configure, HipEncoder, FFV1Error
+    monkeypatch.setenv("FFV1HIP_TWOPASS_LIB", "/nonexistent/libffv1twopass.so")
+    monkeypatch.setenv("FFV1HIP_SOMETHING_ELSE", "1")
+    try:
+        HipEncoder(configure(352, 288, "yuv420p", coder=1, slices=4), 0, 1).close()
+    except FFV1Error as e:
+        assert "is not read" not in str(e) and "unknown hook" not in str(e)
+
+
 def test_decoder_contract_checks_before_the_gpu():
     """ffv1hip_dec_create refuses what the GPU decoder does not decode
     (-ENOSYS) and extradata the parameters would not produce

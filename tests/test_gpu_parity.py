@@ -497,6 +497,59 @@ def test_device_path_never_truncates(sync, monkeypatch):
     assert got == [p for p, _ in ref[4:]]
 
 
+@pytest.mark.parametrize("path", ["encode", "encode_fsets2", "encode_batches", "device_fetch", "encode2"])
+def test_guarded_launch_recovery_matches_oracle(path, monkeypatch):
+    """The recovery path of a guarded launch: a batch launched
+    before its decision count is read back, whose decisions then do not fit
+    its decision set, is skipped by every kernel (ds_over), flagged by
+    ffv1_range (status[3]) and encoded again at settle with the total read
+    back.  The guard_skip hook forces it on every batch (including the next
+    batch's re-run that a rolled-back batch drags along); the packets of every
+    host path equal the oracle's and the re-runs are counted."""
+    from ffv1hip import AVCodecContext, FFV1Encoder, HipEncoder
+    monkeypatch.setenv("FFV1HIP_DEBUG", "guard_skip" + (",fsets=2" if path == "encode_fsets2" else ""))
+    s = PARITY_STREAMS[1]  # 480x270 10-bit, 4 slices, gop 4
+    frames = list(s.frames())
+    _, ex_ref, ref = oracle_encode(s, frames)
+    params = hip_params(s)
+    if path == "encode2":
+        avctx = AVCodecContext(s.width, s.height, s.pix_fmt, gop_size=s.gop_size, slices=s.slices, coder=s.coder)
+        enc2 = FFV1Encoder(batch=3)
+        assert enc2.init(avctx) == 0
+        pkts = [enc2.encode2(f, pts=i) for i, f in enumerate(frames)]
+        pkts = [p for p in pkts if p is not None]
+        while (p := enc2.encode2(None)) is not None:
+            pkts.append(p)
+        skips, reruns = enc2._enc.debug_counter("guard_skips"), enc2._enc.debug_counter("guard_reruns")
+        enc2.close()
+        got = [(p.data, p.key) for p in pkts]
+    else:
+        enc = HipEncoder(params, 0, 3)
+        if path in ("encode", "encode_fsets2"):
+            got = enc.encode(frames)
+        elif path == "encode_batches":
+            got = []
+            for i in range(0, len(frames), 3):
+                got += enc.encode(frames[i:i + 3])
+        else:
+            import torch
+            got = []
+            for i in range(0, len(frames), 3):
+                part = frames[i:i + 3]
+                d = _device_batch(params, part)
+                enc.encode_device(d[0].data_ptr(), d[1], d[2], d[3], len(part))
+                got += enc.fetch(len(part))
+                torch.cuda.synchronize()
+        skips, reruns = enc.debug_counter("guard_skips"), enc.debug_counter("guard_reruns")
+        enc.close()
+    assert got == ref
+    # every batch's first launch was skipped; each skipped run is either run
+    # again at its settle (counted) or replaced by the re-run that a rolled-back
+    # earlier batch drags along (which may be skipped in turn)
+    assert skips >= (len(frames) + 2) // 3, (skips, reruns)
+    assert 1 <= reruns <= skips, (skips, reruns)
+
+
 FULL_SIZE = {
     # BASELINE configs[3]: 4K yuv444p16 at 12 bit (u16 >> 4), videogen content
     "c4_4k_444p12": Stream("c4", 3840, 2160, "yuv444p16", 3, slices=64, gop_size=12,
