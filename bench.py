@@ -82,22 +82,37 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_frames(n_total, data, keep):
-    """The frames i < n_total of the clip with keep(i) (the others skipped)."""
+def clip_frames(n_total, data, keep):
+    """The frames i < n_total of the clip with keep(i), one at a time; the
+    others are skipped (D1: the objects move, nothing is drawn; D2: the
+    frame's noise is still drawn, the RNG stream being shared)."""
     from ffv1hip import synth
     if data == "d1":
-        gen = synth.videogen_frames(W, H, n_total, depth=DEPTH, chroma444=C444, keep=keep)
-    else:
-        gen = synth.d2_frames(W, H, n_total, depth=DEPTH, chroma444=C444, keep=keep)
-    return [f for f in gen]
+        return synth.videogen_frames(W, H, n_total, depth=DEPTH, chroma444=C444, keep=keep)
+    return synth.d2_frames(W, H, n_total, depth=DEPTH, chroma444=C444, keep=keep)
 
 
-def pack_batch(frames, frame_bytes):
-    buf = np.zeros((len(frames), frame_bytes), np.uint8)
-    for i, f in enumerate(frames):
-        flat = np.concatenate([p.reshape(-1).view(np.uint8) for p in f])
-        buf[i, :flat.size] = flat
-    return buf
+def pack_clip(gen, n, frame_bytes):
+    """This rank's n frames packed as they are generated into one host batch
+    [frame][frame_bytes] (what goes to HBM), and the frames as plane views
+    into it: a rank holds one batch of host memory, never a frame list beside it."""
+    buf = np.zeros((n, frame_bytes), np.uint8)
+    frames = []
+    for i, f in enumerate(gen):
+        off, views = 0, []
+        for p in f:
+            nb = p.size * p.itemsize
+            buf[i, off:off + nb] = p.reshape(-1).view(np.uint8)
+            views.append(buf[i, off:off + nb].view(p.dtype).reshape(p.shape))
+            off += nb
+        frames.append(views)
+    assert len(frames) == n
+    return buf, frames
+
+
+def make_frames(n_total, data, keep):
+    """The kept frames of the clip as a list (tools and tests)."""
+    return [f for f in clip_frames(n_total, data, keep)]
 
 
 def cpu_threads():
@@ -173,9 +188,10 @@ def cpu_baseline(frames, threads):
     }
 
 
-def load_traffic(frames_per_step, kernel):
+def load_traffic(frames_per_step, kernel, data="d1"):
     """HBM bytes per launch of `kernel` from the committed PMC profile of the
-    same configuration and batch (profiles/pmc_traffic*.json), else None."""
+    same configuration, batch and clip (profiles/pmc_traffic*.json; a file
+    without a "data" key was profiled on the D1 clip), else None."""
     import glob
     import re
 
@@ -188,7 +204,8 @@ def load_traffic(frames_per_step, kernel):
             d = json.load(open(path))
         except Exception:
             continue
-        if d.get("frames_per_launch") == frames_per_step and d.get("config") == f"{W}x{H} {PIX_FMT}":
+        if (d.get("frames_per_launch") == frames_per_step and d.get("config") == f"{W}x{H} {PIX_FMT}"
+                and d.get("data", "d1") == data):
             k = d.get("kernels", {}).get(kernel)
             if k:
                 return k.get("hbm_bytes")
@@ -303,11 +320,9 @@ def main():
     # one clip of world x gops GOPs; this rank's are GOPs rank, rank+world, ...
     my_gops = [rank + world * j for j in range(args.gops)]
     t0 = time.perf_counter()
-    frames = make_frames(world * B, args.data, keep=lambda i: (i // GOP) % world == rank)
-    assert len(frames) == B
-    host = pack_batch(frames, frame_bytes)
+    host, frames = pack_clip(clip_frames(world * B, args.data, keep=lambda i: (i // GOP) % world == rank),
+                             B, frame_bytes)
     d_frames = torch.from_numpy(host).to(f"cuda:{local_rank}")
-    del host
     torch.cuda.synchronize()
     log(f"[rank {rank}] {B} frames (GOPs {my_gops[0]}, {my_gops[0] + world}, ...) generated and "
         f"resident in HBM in {time.perf_counter() - t0:.1f}s")
@@ -473,7 +488,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
-                "traffic": load_traffic(B, KERNEL[dom]),
+                "traffic": load_traffic(B, KERNEL[dom], args.data),
                 "algorithmic_bytes_per_launch": int(algo_per_launch),
                 "avg_launch_ms": round(ms_per_launch, 3),
             },

@@ -34,15 +34,14 @@ def test_full_gop_matches_oracle_digest(config, data, gop):
     golden = bench.load_bench_golden(config if data == "d1" else f"{config}_d2")
     assert golden and len(golden["gops"]) > gop
     G = bench.GOP
-    frames = bench.make_frames((gop + 1) * G, data, keep=lambda i: i // G == gop)
-    assert len(frames) == G
     params = bench.hip_configure()
     shapes = params.plane_shapes()
     plane_bytes = [h * w * params.sample_bytes for h, w in shapes]
     frame_bytes = (sum(plane_bytes) + 255) // 256 * 256
     offs = [0, plane_bytes[0], plane_bytes[0] + plane_bytes[1]]
     strides = [shapes[k][1] * params.sample_bytes for k in range(3)]
-    d_frames = torch.from_numpy(bench.pack_batch(frames, frame_bytes)).to("cuda:0")
+    host, _ = bench.pack_clip(bench.clip_frames((gop + 1) * G, data, keep=lambda i: i // G == gop), G, frame_bytes)
+    d_frames = torch.from_numpy(host).to("cuda:0")
     torch.cuda.synchronize()
     enc = HipEncoder(params, 0, G)
     try:

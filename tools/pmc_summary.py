@@ -31,7 +31,7 @@ def per_kernel(path, counter):
     return {k: statistics.mean(v) for k, v in vals.items()}
 
 
-def main(tag, frames_per_launch, config, out_name="pmc_traffic_rNN.json"):
+def main(tag, frames_per_launch, config, out_name="pmc_traffic_rNN.json", data="d1"):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
@@ -57,7 +57,7 @@ def main(tag, frames_per_launch, config, out_name="pmc_traffic_rNN.json"):
         v["launches_per_step"] = n
         v["hbm_bytes_per_step"] = v["hbm_bytes"] * n
     out = {
-        "tag": tag, "config": config, "frames_per_launch": frames_per_launch,
+        "tag": tag, "config": config, "data": data, "frames_per_launch": frames_per_launch,
         "note": "per-launch means over the profiled bench run; FETCH_SIZE doubled (gfx950), WRITE_SIZE as is",
         "kernels": kernels,
         "rocprof_avg_ms": stats,
@@ -72,4 +72,5 @@ def main(tag, frames_per_launch, config, out_name="pmc_traffic_rNN.json"):
 if __name__ == "__main__":
     main(sys.argv[1] if len(sys.argv) > 1 else "r01", int(sys.argv[2]) if len(sys.argv) > 2 else 252,
          sys.argv[3] if len(sys.argv) > 3 else "3840x2160 yuv420p10",
-         sys.argv[4] if len(sys.argv) > 4 else "pmc_traffic_rNN.json")
+         sys.argv[4] if len(sys.argv) > 4 else "pmc_traffic_rNN.json",
+         sys.argv[5] if len(sys.argv) > 5 else "d1")
