@@ -573,6 +573,24 @@ __global__ void __launch_bounds__(kDecThreads) ffv1_decode_slices(DecodeArgs a) 
           ok &= rac_symbol(c, hdr, 0, dtt, pkw) == a.chroma_v_shift;
           ok &= rac_get(c, hdr, dtt, pkw) == a.transparency;
           for (int t = 0; t < 5 && ok; t++) ok &= skip_quant_table(c, hdr + 32, dtt, pkw);
+        } else if (key && a.version == 2) {
+          // read_header's v2 branch (ffv1dec.c:801-868): the slice count,
+          // each slice's rectangle in grid units and every plane's quant set,
+          // one state array; a stream naming another layout than the grid's
+          // is refused (distinct symbols name distinct rectangles here)
+          for (int i = 0; i < 32; i++) hdr[i] = 128;
+          const int n = a.num_h * a.num_v;
+          ok &= rac_symbol(c, hdr, 0, dtt, pkw) == n;
+          for (int j = 0; j < n && ok; j++) {
+            const int jx = j % a.num_h, jy = j / a.num_h;
+            const int x0 = int(int64_t(a.width) * jx / a.num_h), x1 = int(int64_t(a.width) * (jx + 1) / a.num_h);
+            const int y0 = int(int64_t(a.height) * jy / a.num_v), y1 = int(int64_t(a.height) * (jy + 1) / a.num_v);
+            ok &= rac_symbol(c, hdr, 0, dtt, pkw) == int(int64_t(x0 + 1) * a.num_h / a.width);
+            ok &= rac_symbol(c, hdr, 0, dtt, pkw) == int(int64_t(y0 + 1) * a.num_v / a.height);
+            ok &= rac_symbol(c, hdr, 0, dtt, pkw) == int(int64_t(x1 - x0 + 1) * a.num_h / a.width) - 1;
+            ok &= rac_symbol(c, hdr, 0, dtt, pkw) == int(int64_t(y1 - y0 + 1) * a.num_v / a.height) - 1;
+            for (int i = 0; i < a.pcount && ok; i++) ok &= rac_symbol(c, hdr, 0, dtt, pkw) == a.context_model;
+          }
         }
       }
       if (a.version > 2) {

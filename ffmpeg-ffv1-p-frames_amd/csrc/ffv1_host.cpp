@@ -757,7 +757,9 @@ int ffv1hip_configure(ffv1hip_params* out, const ffv1hip_options* o) {
   p.ec = o->slicecrc < 0 ? (version >= 3) : o->slicecrc;
   if ((version == 2 || version > 3) && !o->experimental)
     return set_err(FFV1HIP_AVERROR_INVALIDDATA, "version %d is experimental in the reference", version);
-  if (version == 2) return set_err(-38, "version 2 (in-band slice layout) is not supported");
+  // version 2's extradata has no ec field (ffv1enc.c:593-598): its slice
+  // CRCs would be unreadable by the reference decoder
+  if (version == 2 && p.ec) return set_err(-38, "version 2 with slice CRCs (no ec field in its extradata)");
   // coder (ffv1enc.c:708-718)
   int ac = 0;
   if (o->coder != -1) ac = o->coder > 0 ? 2 : 0;
@@ -926,6 +928,19 @@ static void build_ops(ffv1hip_ctx* c) {
             for (i = 1; i < 128; i++)
               if (c->qt[t][i] != c->qt[t][i - 1]) { L.sym(kSetQ0 + t, 0, i - last - 1, false); last = i; }
             L.sym(kSetQ0 + t, 0, i - last - 1, false);
+          }
+        } else if (key && p.version == 2) {  // write_header (ffv1enc.c:523-541): the grid in band
+          const int nh = p.num_h_slices, nv = p.num_v_slices;
+          L.sym(kSetHdr, 0, c->nslices, false);
+          for (int j = 0; j < c->nslices; j++) {
+            const int jx = j % nh, jy = j / nh;
+            const int x0 = int(int64_t(p.width) * jx / nh), x1 = int(int64_t(p.width) * (jx + 1) / nh);
+            const int y0 = int(int64_t(p.height) * jy / nv), y1 = int(int64_t(p.height) * (jy + 1) / nv);
+            L.sym(kSetHdr, 0, int(int64_t(x0 + 1) * nh / p.width), false);
+            L.sym(kSetHdr, 0, int(int64_t(y0 + 1) * nv / p.height), false);
+            L.sym(kSetHdr, 0, int(int64_t(x1 - x0 + 1) * nh / p.width) - 1, false);
+            L.sym(kSetHdr, 0, int(int64_t(y1 - y0 + 1) * nv / p.height) - 1, false);
+            for (int k = 0; k < c->pcount; k++) L.sym(kSetHdr, 0, p.context_model, false);
           }
         }
       }
@@ -1491,9 +1506,14 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
                                                                     : p.sample_bytes == 2 && p.packed_at_lsb &&
                                                                           p.bits_per_raw_sample <= 14 && !p.transparency)
                                          : false;
-  if (p.version == 2 || p.version > 4 || p.num_h_slices * p.num_v_slices > 256 ||
+  if (p.version > 4 || p.num_h_slices * p.num_v_slices > 256 || (p.version == 2 && p.ec) ||
       p.bits_per_raw_sample < 8 || p.bits_per_raw_sample > 16 || p.width <= 0 || p.height <= 0 || !fmt_ok)
     return fail(set_err(-38, "unsupported parameter set"));
+  // version 2's keyframe header (2 + slices x (4 + planes) symbols) within
+  // slice 0's header program: the reference grid (<= 64 slices) fits
+  if (p.version == 2 && 2 + p.num_h_slices * p.num_v_slices * (6 + (p.transparency != 0)) > kMaxOps)
+    return fail(set_err(-38, "version 2 with %d slices: its keyframe header exceeds %d header symbols",
+                        p.num_h_slices * p.num_v_slices, kMaxOps));
   if (p.num_h_slices > p.width || p.num_v_slices > p.height)
     return fail(set_err(-22, "more slices than rows/columns"));
   ffv1hip_ctx* c = new ffv1hip_ctx();
@@ -3505,7 +3525,7 @@ ffv1hip_dec* ffv1hip_dec_create(const ffv1hip_params* params, const uint8_t* ext
   };
   if (!params) return fail(set_err(-22, "invalid arguments"));
   const ffv1hip_params& p = *params;
-  if (p.version == 2 || p.version > 4 || p.num_h_slices * p.num_v_slices > 256 || p.bits_per_raw_sample < 8 ||
+  if ((p.version == 2 && p.ec) || p.version > 4 || p.num_h_slices * p.num_v_slices > 256 || p.bits_per_raw_sample < 8 ||
       p.bits_per_raw_sample > 16 || p.width <= 0 || p.height <= 0 || p.num_h_slices <= 0 || p.num_v_slices <= 0 ||
       (p.version < 2 && p.num_h_slices * p.num_v_slices != 1) || p.context_model < 0 || p.context_model > 1 ||
       p.colorspace < 0 || p.colorspace > 1 || p.ac < 0 || p.ac > 2)

@@ -2400,14 +2400,18 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
   }
 
   // range-coded prefix: key bit / header / slice header, then (v3) a 0 on
-  // state 129 and ff_rac_terminate (ffv1enc.c:1173-1183)
+  // state 129 and ff_rac_terminate (ffv1enc.c:1173-1183); below version 3
+  // only the slice at the origin has one (v2's other slices start with their
+  // Golomb bits: they code no decision, and their sink takes no byte)
+  const bool prefix = a.version > 2 || slice == 0;
   Lane L;
   lane_init(L, ring + lane * kRingStride);
   uint8_t* const out = a.slice_out + ((int64_t)(live ? f : 0) * a.nslices + slice) * a.slice_stride;
-  Sink S = make_sink(out, live ? a.slice_cap : 0);  // idle lanes write nothing
+  Sink S = make_sink(out, live && prefix ? a.slice_cap : 0);  // idle lanes write nothing
   run_header_ops(a, L, S, opsets + lane * kOpsetBytes, key, slice, live, tabs, tabs + 512, kOpsetBytes,
                  kHeaderFlushAt, live ? f : 0);
-  const int64_t ac_bytes = terminate(L, S, a.version > 2, kRing);
+  const int64_t acb = terminate(L, S, a.version > 2, kRing);
+  const int64_t ac_bytes = prefix ? acb : 0;
   if (!live) return;
 
   BitSink b{0ull, 0, ac_bytes, out, a.slice_cap};

@@ -63,8 +63,9 @@ typedef struct ffv1hip_params {
     int packed_at_lsb;        /* u16 samples LSB-aligned (yuv*p9/p10, gbrp) */
     int sample_bytes;         /* 1 or 2 bytes per stored sample; 4: bgr0,
                                  one packed B,G,R,X plane                   */
-    int version;              /* 0, 1, 3 or 4 (experimental: per-slice RCT
-                                 coefficients in the slice header)          */
+    int version;              /* 0, 1, 3, or 2 / 4 (experimental: the slice
+                                 layout in the keyframe header / per-slice
+                                 RCT coefficients in the slice header)      */
     int ac;                   /* 0 Golomb-Rice, 1 range default, 2 range custom */
     int ec;                   /* slice CRC-32 trailers                      */
     int context_model;        /* 0: 666 contexts, 1: 7563                   */
@@ -291,13 +292,14 @@ int ffv1hip_last_kernel_stats(ffv1hip_ctx *ctx, ffv1hip_kernel_stats *out);
 
 /* Decoder: the AVCodec callbacks of ff_ffv1_decoder (ffv1dec.c decode_init
  * :1007, decode_frame :896-1030, decode_end) for the streams this library
- * encodes: versions 0, 1, 3 and 4 (per-slice RCT coefficients, PCM slices),
+ * encodes: versions 0, 1, 2 (the slice layout in the keyframe header), 3 and
+ * 4 (per-slice RCT coefficients, PCM slices),
  * range coder (default or custom table) or Golomb-Rice, context model 0 or
  * 1, YCbCr or RGB, with alpha (YUVA, YA8, RGB32).  ffv1hip_dec_create takes
  * the stream's parameters and its extradata, which must be the one those
  * parameters produce (what read_extradata, ffv1dec.c:509-631, would parse;
  * none below version 2, whose in-band keyframe header must agree with the
- * parameters); otherwise FFV1HIP_AVERROR_INVALIDDATA.  Unsupported
+ * parameters, as must version 2's in-band slice layout); otherwise FFV1HIP_AVERROR_INVALIDDATA.  Unsupported
  * parameters give -ENOSYS. */
 typedef struct ffv1hip_dec ffv1hip_dec;
 ffv1hip_dec *ffv1hip_dec_create(const ffv1hip_params *params,

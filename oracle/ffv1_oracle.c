@@ -615,11 +615,13 @@ int ffv1o_configure3(ffv1o_config *cfg, int width, int height,
     int ec = slicecrc;
     if (ec < 0)
         ec = version >= 3;
-    /* versions 2 and 4 need -strict experimental (:703-706); version 2's
-     * in-band slice layout (write_header, :523-541) is not restated */
+    /* versions 2 and 4 need -strict experimental (:703-706).  Version 2's
+     * extradata has no ec field (write_extradata, ffv1enc.c:593-598), so
+     * its packets with slice CRCs are unreadable by the reference decoder:
+     * refused here */
     if ((version == 2 || version > 3) && !experimental)
         return AVERR_INVALIDDATA;
-    if (version == 2)
+    if (version == 2 && ec)
         return AVERR_ENOSYS;
 
     /* coder, ffv1enc.c:708-718 (coder -1 keeps the private default 0) */
@@ -1175,6 +1177,27 @@ static void put_v01_header(const ffv1o_enc *e, rc_enc *c)
     put_quant_tables(c, (int16_t(*)[256])e->qt);
 }
 
+/* write_header for v2 keyframes (ffv1enc.c:523-541): the slice layout
+ * in-band, one state array for all of it; every plane's quant set index is
+ * the context model (plane_count 2, 3 with alpha, ffv1enc.c:720, 890-891) */
+static void put_v2_header(const ffv1o_enc *e, rc_enc *c)
+{
+    const ffv1o_config *cfg = &e->cfg;
+    uint8_t st[32];
+    memset(st, 128, 32);
+    const int nh = cfg->num_h_slices, nv = cfg->num_v_slices, n = nh * nv;
+    rc_put_symbol(c, st, n, 0);
+    for (int i = 0; i < n; i++) {
+        const slice_ctx *s = &e->sl[i];
+        rc_put_symbol(c, st, (int)((int64_t)(s->x0 + 1) * nh / cfg->width), 0);
+        rc_put_symbol(c, st, (int)((int64_t)(s->y0 + 1) * nv / cfg->height), 0);
+        rc_put_symbol(c, st, (int)((int64_t)(s->w + 1) * nh / cfg->width) - 1, 0);
+        rc_put_symbol(c, st, (int)((int64_t)(s->h + 1) * nv / cfg->height) - 1, 0);
+        for (int j = 0; j < 2 + (cfg->transparency != 0); j++)
+            rc_put_symbol(c, st, cfg->context_model, 0);
+    }
+}
+
 /* encode_slice_header (ffv1enc.c:1031-1062) */
 static void clear_slice_states(ffv1o_enc *e, slice_ctx *s);
 
@@ -1620,6 +1643,8 @@ static int enc_slice(ffv1o_enc *e, int i, int key, const uint8_t *const planes[4
         rc_put(&c, &ks, key);
         if (key && cfg->version < 2)
             put_v01_header(e, &c);
+        else if (key && cfg->version == 2)
+            put_v2_header(e, &c);
         c.t = &e->frame_tab;
     }
     /* v4 picks the slice's RCT coefficients; a range-coded v4 slice that
@@ -1874,6 +1899,7 @@ typedef struct dslice {
     int pcm, rct_by, rct_ry; /* v4 slice header (ffv1dec.c:344-356); else 0, 1, 1 */
     plane_state ps[3];
     int damaged; /* slice_damaged: set by a CRC / header / end mismatch, cleared by read_header */
+    int qi;      /* v2: the slice's quant set from the keyframe header */
 } dslice;
 
 struct ffv1o_dec {
@@ -2246,6 +2272,37 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
             d->contexts = get_quant_tables(&c0, d->qt);
             if (d->contexts < 0)
                 return -1;
+        } else if (d->version == 2) { /* read_header v2, ffv1dec.c:801-868 */
+            uint8_t st[32];
+            memset(st, 128, 32);
+            /* the reference takes any count up to the grid's; an encoder
+             * writes the whole grid (ffv1enc.c:1008), and so must a packet
+             * here */
+            if (rc_get_symbol(&c0, st, 0) != d->nslices)
+                return -1;
+            const int64_t W = d->cfg.width, H = d->cfg.height;
+            for (int j = 0; j < d->nslices; j++) {
+                dslice *s = &d->sl[j];
+                int64_t sx = rc_get_symbol(&c0, st, 0) * W, sy = rc_get_symbol(&c0, st, 0) * H;
+                int64_t sw = (rc_get_symbol(&c0, st, 0) + 1) * W + sx;
+                int64_t sh = (rc_get_symbol(&c0, st, 0) + 1) * H + sy;
+                sx /= d->num_h;
+                sy /= d->num_v;
+                sw = sw / d->num_h - sx;
+                sh = sh / d->num_v - sy;
+                if ((uint32_t)sw > W || (uint32_t)sh > H || (uint32_t)sx + (uint64_t)(uint32_t)sw > (uint64_t)W ||
+                    (uint32_t)sy + (uint64_t)(uint32_t)sh > (uint64_t)H)
+                    return -1;
+                s->x0 = (int)sx; s->y0 = (int)sy; s->w = (int)sw; s->h = (int)sh;
+                /* each plane names its set; the slices here code every plane
+                 * with one set, so they must agree (ours always do) */
+                for (int k = 0; k < d->plane_count; k++) {
+                    unsigned idx = (unsigned)rc_get_symbol(&c0, st, 0);
+                    if (idx > 1 || !d->ctx_count[idx] || (k && (int)idx != s->qi))
+                        return -1;
+                    s->qi = (int)idx;
+                }
+            }
         }
         d->key_ok = 1;
     } else if (!d->key_ok) {
@@ -2308,6 +2365,11 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
          * (ffv1.h:161-176): context model 1's in-band v0/v1 tables */
         int model1 = d->qt[3][127] != 0;
         int contexts = d->contexts;
+        if (d->version == 2) { /* the keyframe header's set (ffv1dec.c:845-858) */
+            qt = (const int16_t(*)[256])d->qsets[s->qi];
+            model1 = s->qi;
+            contexts = d->ctx_count[s->qi];
+        }
         d->sl[i].damaged |= crc_bad[i];
         if (d->version > 2) { /* decode_slice_header, ffv1dec.c:282-359 */
             uint8_t st[32];
@@ -2359,7 +2421,7 @@ int ffv1o_dec_frame(ffv1o_dec *d, const uint8_t *pkt, int64_t size,
         }
         if (key || reset) /* ffv1dec.c:414-415 */
             for (int pp = 0; pp < d->plane_count; pp++) {
-                if (d->version > 2 && d->init_states[model1])
+                if (d->version > 1 && d->init_states[model1]) /* ffv1.c:181-190 */
                     memcpy(s->ps[pp].rac, d->init_states[model1], (size_t)contexts * 32);
                 else
                     memset(s->ps[pp].rac, 128, (size_t)contexts * 32);

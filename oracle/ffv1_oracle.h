@@ -44,7 +44,7 @@ typedef struct ffv1o_config {
     int bits_per_raw_sample;  /* 8..16                                         */
     int packed_at_lsb;        /* 1: u16 samples hold the value in the LSBs     */
     int sample_bytes;         /* 1 (8-bit formats) or 2                        */
-    int version;              /* 0, 1, 3 or 4 (experimental)                   */
+    int version;              /* 0, 1, 3, or 2 / 4 (experimental)             */
     int ac;                   /* 0 Golomb-Rice, 1 range default, 2 range custom */
     int ec;                   /* slice CRCs                                    */
     int context_model;        /* 0 (666 contexts) or 1 (7563)                  */
