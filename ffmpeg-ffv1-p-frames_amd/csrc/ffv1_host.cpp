@@ -142,7 +142,7 @@ static const char* const kKnobNames[] = {"serial",      "walkdbg",     "walktrac
                                          "coder",       "dense",       "walk_blocks", "recsets",     "slice_cap",
                                          "walk_part_a", "force_multi", "bounds_shrink", "dsets",
                                          "rec2_drop",   "budget",      "pack",        "v4_cap0",     "readback",
-                                         "fsets",       "guard_skip"};
+                                         "fsets",       "guard_skip",  "walk_prio",   "range_prio"};
 
 // The per-hook environment variables of earlier rounds.  They are no longer
 // read, so one that is set is an error (a measurement that silently ran the
@@ -2086,8 +2086,8 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       range_first = c->d_qt_walk && !chroma_long &&
                     walk_items(nsegs, c->nslices, wa.per_short, wa.short_multi) <= resident;
     }
-    wa.prio = range_first ? 0 : 2;
-    const int range_prio = range_first ? 3 : 0;
+    wa.prio = c->knobs.get("walk_prio", range_first ? 0 : 2);
+    const int range_prio = c->knobs.get("range_prio", range_first ? 3 : 0);
     wa.init = c->d_init;
     wa.rows = c->walk_rows;
     wa.dense = c->d_qt_walk != nullptr;
@@ -2970,8 +2970,8 @@ int ffv1hip_encode(ffv1hip_ctx* c, const void* const* planes, const int* strides
     hipEvent_t const ev = c->hist_done[b & 1];
     o.th = std::thread([&o, &P, c, ev, pk, sset]() {
       const double t0 = wall_s();
-      if (hipEventSynchronize(ev) != hipSuccess) {
-        o.rc = set_err(-5, "batch wait failed");
+      if (const hipError_t e = hipEventSynchronize(ev); e != hipSuccess) {
+        o.rc = set_err(-5, "batch wait failed: %s", hipGetErrorString(e));
         o.err = g_err;
         return;
       }

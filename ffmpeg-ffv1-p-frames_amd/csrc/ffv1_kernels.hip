@@ -1907,8 +1907,9 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
     stage4[0] = t;
   };
 
-  // wave priority (FFV1HIP_WALK_PRIO, default 0: with the walk in one round
-  // the coder's range pass is the longer chain and runs above it)
+  // wave priority (run_batch's choice: 0 with the walk in one round, where
+  // the coder's range pass is the longer chain and runs above it; the
+  // walk_prio hook overrides)
   set_prio(a.prio);
   uint64_t t_loop = 0, n_steps = 0;
   const uint64_t t_all = a.dbg || a.trace ? __builtin_amdgcn_s_memtime() : 0;
@@ -2075,10 +2076,11 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
           t_loop += __builtin_amdgcn_s_memtime() - t0;
           n_steps += kChunk;
         }
-        pdst = live ? a.ds.pre + (pos0 & ~(int64_t)15) : a.scratch;
-        if constexpr (kBoundsCheck) {
-          if (live && !in_chain(pos0 & ~(int64_t)15, kCopyBlocks * 32 * 16, kBndWalkStage)) pdst = a.scratch;
-        }
+        // one select (a pointer assigned before the bounds check and again
+        // inside it once compiled to a register the check had reused)
+        bool sok = live;
+        if constexpr (kBoundsCheck) sok = sok && in_chain(pos0 & ~(int64_t)15, kCopyBlocks * 32 * 16, kBndWalkStage);
+        pdst = sok ? a.ds.pre + (pos0 & ~(int64_t)15) : a.scratch;
         plast = (align + total) >> 4;
         __builtin_amdgcn_wave_barrier();
         run += total;
