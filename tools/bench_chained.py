@@ -15,7 +15,7 @@ other.  Per case:
 Cases: BASELINE configs[0] (CIF yuv420p Golomb, intra), Golomb at 1080p
 (24 slices, intra), context model 1 at the c3 shape (4K yuv420p10, 64 slices,
 g=12), and bgr0 at 1080p (24 slices, g=12, the reversible colour transform).
-Usage: python tools/bench_chained.py [out.json] [steps]
+Usage: python tools/bench_chained.py [out.json] [steps] [case,case,...]
 """
 import hashlib
 import json
@@ -38,6 +38,10 @@ CASES = [
     ("golomb_1080p_intra_s24", 1920, 1080, "yuv420p", 24, 0, 0, 1, 240, "d1"),
     ("ctx1_4k_p10_s64_g12", 3840, 2160, "yuv420p10", 64, 1, 1, 12, 240, "d1"),
     ("bgr0_1080p_s24_g12", 1920, 1080, "bgr0", 24, 1, 0, 12, 240, "d1"),
+    # the same P-frame streams with more GOPs per call: a chain per (GOP,
+    # slice) lane, so the lanes (and waves) grow with the batch
+    ("ctx1_4k_p10_s64_g12_b960", 3840, 2160, "yuv420p10", 64, 1, 1, 12, 960, "d1"),
+    ("bgr0_1080p_s24_g12_b2400", 1920, 1080, "bgr0", 24, 1, 0, 12, 2400, "d1"),
 ]
 
 
@@ -54,9 +58,12 @@ def main():
     from ffv1hip import HipEncoder, configure
     out_json = sys.argv[1] if len(sys.argv) > 1 else None
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    only = set(sys.argv[3].split(",")) if len(sys.argv) > 3 else None
     threads = bench.cpu_threads()
     res = {"cases": [], "cpu_threads": threads, "steps": steps}
     for name, W, H, pf, slices, coder, context, gop, B, data in CASES:
+        if only and name not in only:
+            continue
         t0 = time.perf_counter()
         frames = frames_of(W, H, pf, B)
         params = configure(W, H, pf, slices=slices, coder=coder, context=context, gop_size=gop)
