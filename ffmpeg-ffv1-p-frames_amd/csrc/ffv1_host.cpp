@@ -142,7 +142,7 @@ static const char* const kKnobNames[] = {"serial",      "walkdbg",     "walktrac
                                          "coder",       "dense",       "walk_blocks", "recsets",     "slice_cap",
                                          "walk_part_a", "force_multi", "bounds_shrink", "dsets",
                                          "rec2_drop",   "budget",      "pack",        "v4_cap0",     "readback",
-                                         "fsets",       "guard_skip",  "walk_prio",   "range_prio"};
+                                         "fsets",       "guard_skip",  "walk_prio",   "range_prio",  "compact"};
 
 // The per-hook environment variables of earlier rounds.  They are no longer
 // read, so one that is set is an error (a measurement that silently ran the
@@ -458,6 +458,7 @@ struct ffv1hip_ctx {
   uint8_t* d_frames = nullptr;
   int16_t* d_qt = nullptr;
   int walk_rows = 0;             // frames mode: context rows per plane group in the walk's LDS
+  int walk_rowb = 32;            // ... and bytes per row (kCompactRowBytes at 8 bits)
   int16_t* d_qt_walk = nullptr;  // dense rows (kDenseRows): quant tables with weights 1, 9, 81
   uint8_t* d_tabs = nullptr;
   Op* d_ops = nullptr;
@@ -1606,7 +1607,12 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
     // numbering, a test hook)
     const bool dense = p.context_model == 0 && p.bits_per_raw_sample > 8 && c->knobs.get("dense", 1) != 0;
     c->walk_rows = dense ? kDenseRows : c->contexts;
-    const int64_t lds = walk_lds_bytes(c->walk_rows);
+    // 8 bits, context model 0: rows of the 24 slots a symbol can use there
+    // (compact=0: 32-byte rows, a test hook)
+    c->walk_rowb = !dense && p.context_model == 0 && p.bits_per_raw_sample <= 8 && c->knobs.get("compact", 1) != 0
+                       ? kCompactRowBytes
+                       : 32;
+    const int64_t lds = walk_lds_bytes(c->walk_rows, c->walk_rowb);
     // RGB interleaves the three planes' rows (encode_rgb_frame): chained
     // alpha (a third plane context) and v4 (per-frame slice header values):
     // the chained coders
@@ -1957,6 +1963,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     if (sst == st) HIP_TRY(hipStreamWaitEvent(st, c->bitsed[fb ^ 1], 0));
     sa.frame_chunks = c->frame_chunks;
     sa.max_blocks = c->grid_sym;
+    sa.rowb = c->walk_rowb;
     if (timed(0, sst, [&] { return launch_symbols(sa, sst); }) < 0)
       return set_err(-5, "symbols launch failed: %s", hipGetErrorString(hipGetLastError()));
     // this batch's decisions, estimated from the earlier batches' totals
@@ -2073,12 +2080,14 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       const SliceGeom& g0 = c->geom[0];
       const bool chroma_long = 2 * int64_t(g0.pw[1]) * g0.ph[1] > int64_t(g0.pw[0]) * g0.ph[0];
       wa.rows = c->walk_rows;
+      wa.rowb = c->walk_rowb;
       wa.per_short = walk_per_short(g0);
       const int resident = walk_resident(wa);
       wa.short_multi = walk_split_short(nsegs, c->nslices, wa.per_short, 4 * c->cus, resident);
       // (the walk_blocks=0 hook, and the split-launch test hook, keep one-wave blocks)
       wa.block_waves = c->knobs.get("walk_blocks", 1) && !c->knobs.has("walk_part_a")
-                           ? walk_block_waves(nsegs, c->nslices, wa.per_short, wa.short_multi, wa.rows, c->cus, c->lds_block)
+                           ? walk_block_waves(nsegs, c->nslices, wa.per_short, wa.short_multi, wa.rows, wa.rowb, c->cus,
+                                              c->lds_block)
                            : 1;
       if (c->knobs.has("hostdbg"))
         std::fprintf(stderr, "hostdbg: walk of %d segments: %d-wave blocks (%d B of LDS per block allowed)\n", nsegs,
@@ -2146,6 +2155,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       sta.rc_stat = c->d_rcstat;
       sta.rc_stat2 = c->d_rcstat + 512;
       sta.dense = c->d_qt_walk != nullptr;
+      sta.rowb = c->walk_rowb;
       if (launch_stats(sta, false, st) < 0) return set_err(-5, "stats launch failed");
     }
     if (walkdbg) {

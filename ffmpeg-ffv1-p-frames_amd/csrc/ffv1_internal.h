@@ -92,6 +92,7 @@ struct SymbolArgs {
   const int2* rct;            // v4: [batch frame][slice] {by, ry} RCT coefficients, else null (1, 1)
   int max_blocks;             // grid cap (0: one block per item); the blocks stride over the items
   int nz;                     // set by launch_symbols: plane parts per (slice, slot)
+  int rowb = 32;              // with rec: the walk's bytes per row (a record's row address = row x rowb)
 };
 
 // v4's choose_rct_params (ffv1enc.c:1064-1144) for every (frame, slice) of
@@ -290,6 +291,7 @@ struct StatsArgs {
   unsigned long long* rc_stat;   // [256][2]
   unsigned long long* rc_stat2;  // [contexts][32][2]
   int dense;                     // the records address dense rows (dense_ctx)
+  int rowb = 32;                 // the records' row address = row x rowb
 };
 int launch_stats(const StatsArgs& a, bool states, void* stream);
 
@@ -327,6 +329,7 @@ struct WalkArgs {
   int rows;                   // context rows of a plane group's table in LDS (kDenseRows when dense)
   int dense;                  // records address dense rows (dense_row), the state tables keep contexts
   Bounds bnd;                 // debug build: the extents of the writes
+  int rowb = 32;              // bytes per row in LDS: 32, or kCompactRowBytes at 8 bits (context model 0)
 };
 
 constexpr int kTraceWords = 8;
@@ -340,6 +343,17 @@ constexpr int kTraceWords = 8;
 // walk waves fit on a CU instead of three.  Persisted / initial states keep
 // the context numbering.
 constexpr int kDenseRows = 365;
+
+// At 8 bits a residual is folded to [-128, 127], so e <= 7 and
+// put_symbol_inline (ffv1enc.c:185-231) uses only slots 0-8 (zero flag and
+// exponent), 11-18 (sign) and 22-28 (mantissa): 24 of a row's 32.  The walk's
+// LDS rows then hold those 24 (walk_slot_pos), a plane group's table is
+// 666 x 24 bytes instead of 666 x 32, and four walk waves fit on a CU instead
+// of three.  The records carry the row's byte offset (row x row bytes).
+constexpr int kCompactRowBytes = 24;
+__host__ __device__ constexpr int walk_slot_pos(int k) {  // compact position of slot k, -1: unused at 8 bits
+  return k <= 8 ? k : (k >= 11 && k <= 18) ? k - 2 : (k >= 22 && k <= 28) ? k - 5 : -1;
+}
 __host__ __device__ inline int dense_ctx(int row) {  // row -> its context
   const int q0 = (row + 4) % 9 - 4;
   const int r1 = (row - q0) / 9;
@@ -443,7 +457,8 @@ int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first = 0, int c
 // (4:2:0 luma vs Cb + Cr, 4:4:4 Cb + Cr vs luma: 2).
 int walk_items(int nsegs, int nslices, int per_short, int short_multi);
 int walk_split_short(int nsegs, int nslices, int per_short, int simds, int resident);
-int walk_block_waves(int nsegs, int nslices, int per_short, int short_multi, int rows, int cus, int lds_block);
+int walk_block_waves(int nsegs, int nslices, int per_short, int short_multi, int rows, int rowb, int cus,
+                     int lds_block);
 int walk_per_short(const SliceGeom& g);
 int walk_resident(const WalkArgs& a);  // (uses a.rows)
 int launch_range(const CodeArgs& a, void* stream);
@@ -452,7 +467,7 @@ int launch_range_dseg(const CodeArgs& a, void* stream);
 int launch_dfix(const CodeArgs& a, void* stream);
 int launch_sink(const CodeArgs& a, void* stream);
 int launch_bits(const BitsArgs& a, void* stream);
-int64_t walk_lds_bytes(int rows);  // one walk wave's LDS for tables of `rows` context rows
+int64_t walk_lds_bytes(int rows, int rowb);  // one walk wave's LDS for tables of `rows` context rows of `rowb` bytes
 constexpr int64_t kWalkLdsMax = 64 * 1024;  // states walk: one plane group's table + T9 + staging in LDS
 int launch_code_golomb(const CodeArgs& a, void* stream);
 int launch_assemble(const AssembleArgs& a, int nframes, void* stream);

@@ -319,7 +319,7 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
     if (rec) {
       // the walk record: row inside the plane group, slot codes, the decision
       // offset inside the chunk (wave prefix sum), same-row flag
-      const int raddr = ctx * 32;
+      const int raddr = (int)__umul24((uint32_t)ctx, (uint32_t)a.rowb);  // ctx >= 0 here
       const int incl = wave_incl_scan(nd, lane);
       const int d0 = incl - nd;
       const unsigned mag = diff < 0 ? 0u - (unsigned)diff : (unsigned)diff;
@@ -1597,7 +1597,7 @@ constexpr int kLdsPre = kLdsRecs + 2 * kRecSlots * 16;        // wave 0: [2][kPr
 constexpr int kStageBytes = 2 * kRecSlots * 16 + 2 * kPreHalf;  // one wave's records and recorded states
 constexpr int kLdsFixed = kLdsN + kT3Bytes + kStageBytes;     // a one-wave block
 
-int64_t walk_lds_bytes_dev(int rows);
+int64_t walk_lds_bytes_dev(int rows, int rowb);
 
 // Any exponent, one symbol: lane k < 32 of a half applies all decisions of
 // slot k in order (slot 10 takes e-8 exponent decisions beyond e = 9, slot
@@ -1643,7 +1643,9 @@ __device__ __forceinline__ int walk_long(int st, const uint8_t* ftab, int v, int
 // per-lane constants of the step
 struct WalkLane {
   int k, hsh;         // the lane's slot; D or D+2e
-  int kk;             // k + this half's table base
+  int kt;             // the slot's byte in a row (k; compact rows: walk_slot_pos, an unused slot the dummy row's byte k)
+  uint32_t amask;     // 0xFFFF, 0 for an unused slot of compact rows (its byte is not in the symbol's row)
+  int kk;             // kt + this half's table base
   int dummy;          // stage byte of untouched slots
   int msh, mwd, mbase;  // slots 10 / 31: where the record keeps the composed row (code 3)
   int csh;            // multi chunks: the lane's 2-bit code field in its code word
@@ -1676,7 +1678,7 @@ __device__ __forceinline__ StepIn derive(const uint4& r, const WalkLane& W, int 
     d.code = ((uint32_t)nd & 2u) | bit;
     d.pos = (nd & W.dummy) | (~nd & pos);
   }
-  d.addr = (int)(r.x & 0xFFFFu) + W.kk;
+  d.addr = (int)(r.x & W.amask) + W.kk;
   d.same = (int)r.w < 0;  // kRecSame
   d.same2 = r.w >= kRecSame2;  // bit 31 or 30: one compare, no mask (same wins in walk_step)
   return d;
@@ -1753,10 +1755,10 @@ __device__ __forceinline__ void walk_multi_fill(uint8_t* fixed, const uint4* myr
   }
 }
 
-int64_t walk_lds_bytes_dev(int rows) { return kLdsFixed + 2 * ((int64_t)rows * 32 + 32); }
+int64_t walk_lds_bytes_dev(int rows, int rowb) { return kLdsFixed + 2 * ((int64_t)rows * rowb + 32); }
 // a block of `waves` walk waves: one N table, each wave its stage and two tables
-int64_t walk_block_lds_dev(int rows, int waves) {
-  return kT3Bytes + (int64_t)waves * (kStageBytes + 2 * ((int64_t)rows * 32 + 32));
+int64_t walk_block_lds_dev(int rows, int waves, int rowb) {
+  return kT3Bytes + (int64_t)waves * (kStageBytes + 2 * ((int64_t)rows * rowb + 32));
 }
 
 // The 8-byte record in HBM (ffv1_symbols) as the walk's step reads it from
@@ -1793,13 +1795,15 @@ __device__ __forceinline__ uint4 pick(bool c, uint4 a, uint4 b) {
 // workgroup's waves go to them in turn), and wave 4 a one-segment item,
 // which shares wave 0's SIMD as the younger wave (the arbiter favours the
 // older): a wave of full length never shares its SIMD with another walk wave.
-template <int WAVES>
+// ROWB: bytes per LDS row, 32 or kCompactRowBytes (8 bits: the 24 slots
+// put_symbol_inline can use there)
+template <int WAVES, int ROWB = 32>
 __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t fixed[kT3Bytes + WAVES * kStageBytes];
   extern __shared__ __attribute__((aligned(16))) uint8_t tbl[];  // [wave][2][rows + 1 dummy row][32]
   if (ds_over(a.ds)) return;  // the batch is encoded again (uniform: before the barrier)
   const int64_t half = a.state_bytes / 2;  // one plane group's [contexts][32] in the persisted states
-  const int64_t thalf = (int64_t)a.rows * 32;  // ... and its table in LDS (dense rows: 365 x 32)
+  const int64_t thalf = (int64_t)a.rows * ROWB;  // ... and its table in LDS (dense rows: 365 x 32; 8 bits: 666 x 24)
   const int tsz = (int)thalf + 32;
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = WAVES > 1 ? (int)(threadIdx.x >> 6) : 0;
@@ -1879,7 +1883,15 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
   const bool isU = k <= 10;                // zero flag / exponent slots: decision D + k
   W.hsh = isU ? 0 : 16;                    // else from D + 2e: sign +2, mantissa 22+i: +1-i
   const int kslot = isU ? k : (k <= 21 ? 2 : 23 - k);
-  W.kk = (2 * wv + h) * tsz + k;
+  if constexpr (ROWB == 32) {
+    W.kt = k;
+    W.amask = 0xFFFFu;
+  } else {
+    const int pk = walk_slot_pos(k);
+    W.kt = pk >= 0 ? pk : (int)thalf + k;
+    W.amask = pk >= 0 ? 0xFFFFu : 0u;
+  }
+  W.kk = (2 * wv + h) * tsz + W.kt;
   W.dummy = wo + h * kPreHalf + kPreData + k;
   W.msh = k == 31 ? 28 : 12;
   W.mwd = k == 31 ? 2 : 3;
@@ -1921,13 +1933,18 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
   const uint4* const src = seg.load_states && live
                                ? reinterpret_cast<const uint4*>(a.persist_in + (int64_t)sl * a.state_bytes + goff)
                                : reinterpret_cast<const uint4*>(a.init);
-  {
+  if constexpr (ROWB == 32) {
     uint4* const t4 = reinterpret_cast<uint4*>(mytbl);
     for (int64_t i = k; i < t16; i += 32) {  // table block i: row i / 2 (dense: its context's)
       const int64_t si = a.dense ? (int64_t)dense_ctx((int)(i >> 1)) * 2 + (i & 1) : i;
       t4[i] = src ? src[si] : v128;
     }
     if (k < 2) t4[t16 + k] = v128;  // dummy row
+  } else {  // compact rows (not dense): lane k moves slot k of every row
+    const uint8_t* const sb = reinterpret_cast<const uint8_t*>(src);
+    if (W.amask)
+      for (int r = 0; r < a.rows; r++) mytbl[r * ROWB + W.kt] = src ? sb[r * 32 + k] : (uint8_t)128;
+    mytbl[thalf + k] = 128;  // dummy row
   }
   __builtin_amdgcn_wave_barrier();  // (a wave's LDS operations run in order)
   for (int j = 0; j < seg.nframes; j++) {
@@ -2007,14 +2024,14 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
           // on its predecessor's row takes the state from the register), so a
           // symbol waits on its transition lookups only
           uint4 r = myrecs[0];
-          int st = mytbl[(int)(r.x & 0xFFFFu) + k];
+          int st = mytbl[(int)(r.x & W.amask) + W.kt];
           for (int t = 0; t < cmax; t++) {
             const uint4 rn = myrecs[t + 1];
-            const int stn = mytbl[(int)(rn.x & 0xFFFFu) + k];
+            const int stn = mytbl[(int)(rn.x & W.amask) + W.kt];
             if (t < cnt && lok) {
               st = walk_long(st, fixed + kLdsN, (int)(int16_t)(r.x >> 16), k,
                              a.ds.pre + pos0 + (int)(r.w & 0xFFFu));
-              mytbl[(int)(r.x & 0xFFFFu) + k] = (uint8_t)st;
+              mytbl[(int)(r.x & W.amask) + W.kt] = (uint8_t)st;
             }
             st = (int)rn.w < 0 ? st : stn;
             r = rn;
@@ -2046,7 +2063,7 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
         if (!mul) {
           static_for<0, kChunk>([&](auto tc) {
             constexpr int T = decltype(tc)::value;
-            walk_step(fixed, tbl, d0, (int)(rn.x & 0xFFFFu) + W.kk, e1, e2, l0, l1, addr_prev, st);
+            walk_step(fixed, tbl, d0, (int)(rn.x & W.amask) + W.kk, e1, e2, l0, l1, addr_prev, st);
             const uint4 r3 = myrecs[T + 3];  // three ahead
             __builtin_amdgcn_sched_barrier(0);  // keeps the read here, not sunk to its use a step later
             d0 = d1;
@@ -2057,7 +2074,7 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
           StepIn m0 = derive_m(myrecs[0], W, kc), m1 = derive_m(myrecs[1], W, kc);
           static_for<0, kChunk>([&](auto tc) {
             constexpr int T = decltype(tc)::value;
-            walk_step(fixed, tbl, m0, (int)(rn.x & 0xFFFFu) + W.kk, e1, e2, l0, l1, addr_prev, st);
+            walk_step(fixed, tbl, m0, (int)(rn.x & W.amask) + W.kk, e1, e2, l0, l1, addr_prev, st);
             const uint4 r3 = myrecs[T + 3];
             __builtin_amdgcn_sched_barrier(0);
             m0 = m1;
@@ -2096,7 +2113,12 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
                 a.bnd.persist_bytes, kBndWalkStates)) {
     uint4* dst = reinterpret_cast<uint4*>(a.persist_out + (int64_t)sl * a.state_bytes + goff);
     const uint4* t4 = reinterpret_cast<const uint4*>(mytbl);
-    if (!a.dense) {
+    if constexpr (ROWB != 32) {  // compact rows: an unused slot keeps its state (it never codes)
+      uint8_t* const db = reinterpret_cast<uint8_t*>(dst);
+      const uint8_t* const sb = reinterpret_cast<const uint8_t*>(src);
+      for (int r = 0; r < a.rows; r++)
+        db[r * 32 + k] = W.amask ? mytbl[r * ROWB + W.kt] : (src ? sb[r * 32 + k] : (uint8_t)128);
+    } else if (!a.dense) {
       for (int64_t i = k; i < n16; i += 32) dst[i] = t4[i];
     } else {  // contexts that cannot occur keep the states the segment started from
       for (int64_t i = k; i < n16; i += 32) {
@@ -2523,7 +2545,7 @@ __global__ __launch_bounds__(kStatsThreads) void ffv1_stats_slots(StatsArgs a) {
   const uint2* r = a.rec + (int64_t)f * a.frame_samples + g.sym_off + g.plane_sym_off[p];
   for (int64_t i = threadIdx.x; i < n; i += kStatsThreads) {
     const uint2 v = r[i];
-    const int row = (int)(v.x & 0xFFFFu) >> 5;
+    const int row = (int)(v.x & 0xFFFFu) / a.rowb;
     const int ctx = a.dense ? dense_ctx(row) : row;
     const int diff = (int16_t)(v.x >> 16);
     const bool lds = ctx < kStatsLdsCtx;
@@ -2787,16 +2809,19 @@ int launch_dfix(const CodeArgs& a, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int64_t walk_lds_bytes(int rows) { return walk_lds_bytes_dev(rows); }
+int64_t walk_lds_bytes(int rows, int rowb) { return walk_lds_bytes_dev(rows, rowb); }
 
 int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first, int count) {
-  if (walk_lds_bytes_dev(a.rows) > kWalkLdsMax || a.rows * 32 > 0xFFFF) return -1;
+  if ((a.rowb != 32 && (a.rowb != kCompactRowBytes || a.dense)) || walk_lds_bytes_dev(a.rows, a.rowb) > kWalkLdsMax ||
+      a.rows * a.rowb > 0xFFFF)
+    return -1;
   WalkArgs b = a;
   if (b.per_short < 1) b.per_short = 1;
   b.nsegs = nsegs;
   b.short_multi = std::max(0, std::min(b.short_multi, (nsegs + b.per_short - 1) / b.per_short));
   b.nitems = walk_items(nsegs, a.nslices, b.per_short, b.short_multi);
-  const size_t tables = (size_t)(2 * ((int64_t)a.rows * 32 + 32));  // one wave's; the fixed part is static
+  const size_t tables = (size_t)(2 * ((int64_t)a.rows * a.rowb + 32));  // one wave's; the fixed part is static
+  const bool compact = a.rowb == kCompactRowBytes;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (a.block_waves > 1) {  // one round: a block per CU (walk_block_waves)
     const int npairs = (a.nslices + 1) / 2;
@@ -2805,15 +2830,18 @@ int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first, int count
     const int blocks = std::max((nfull + 3) / 4, nsingle);
     b.item0 = 0;
     if (a.block_waves == 5)
-      hipLaunchKernelGGL(ffv1_walk<5>, dim3((unsigned)blocks), dim3(kWalkThreads * 5), 5 * tables, st, b);
+      hipLaunchKernelGGL((compact ? ffv1_walk<5, kCompactRowBytes> : ffv1_walk<5>), dim3((unsigned)blocks),
+                         dim3(kWalkThreads * 5), 5 * tables, st, b);
     else
-      hipLaunchKernelGGL(ffv1_walk<4>, dim3((unsigned)blocks), dim3(kWalkThreads * 4), 4 * tables, st, b);
+      hipLaunchKernelGGL((compact ? ffv1_walk<4, kCompactRowBytes> : ffv1_walk<4>), dim3((unsigned)blocks),
+                         dim3(kWalkThreads * 4), 4 * tables, st, b);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
   if (count < 0) count = b.nitems - first;
   if (first < 0 || count <= 0 || first + count > b.nitems) return count == 0 ? 0 : -1;
   b.item0 = first;
-  hipLaunchKernelGGL(ffv1_walk<1>, dim3((unsigned)count), dim3(kWalkThreads), tables, st, b);
+  hipLaunchKernelGGL((compact ? ffv1_walk<1, kCompactRowBytes> : ffv1_walk<1>), dim3((unsigned)count), dim3(kWalkThreads),
+                     tables, st, b);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2821,7 +2849,8 @@ int launch_walk(const WalkArgs& a, int nsegs, void* stream, int first, int count
 // one round with every full-length wave alone on a SIMD (at most 4 per CU
 // of them, at most one one-segment wave per CU) and the block's LDS fits a
 // CU; else 1 (waves placed by the dispatcher, several rounds).
-int walk_block_waves(int nsegs, int nslices, int per_short, int short_multi, int rows, int cus, int lds_block) {
+int walk_block_waves(int nsegs, int nslices, int per_short, int short_multi, int rows, int rowb, int cus,
+                     int lds_block) {
   const int npairs = (nslices + 1) / 2;
   const int nfull = npairs * (nsegs + short_multi);
   const int nsingle = walk_items(nsegs, nslices, per_short, short_multi) - nfull;
@@ -2830,7 +2859,7 @@ int walk_block_waves(int nsegs, int nslices, int per_short, int short_multi, int
   // the block's LDS against what one workgroup may take on this device
   // (queried once at create; a part with less falls back to one-wave blocks
   // instead of failing the launch)
-  return walk_block_lds_dev(rows, w) <= lds_block ? w : 1;
+  return walk_block_lds_dev(rows, w, rowb) <= lds_block ? w : 1;
 }
 
 int walk_items(int nsegs, int nslices, int per_short, int short_multi) {
@@ -2866,7 +2895,7 @@ int walk_per_short(const SliceGeom& g) {
 
 // Walk waves one CU holds at once (LDS-bound), for launch splitting.
 int walk_resident(const WalkArgs& a) {
-  const size_t dyn = (size_t)(2 * ((int64_t)a.rows * 32 + 32));
+  const size_t dyn = (size_t)(2 * ((int64_t)a.rows * a.rowb + 32));
   int per_cu = 0, dev = 0, cus = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ffv1_walk<1>, kWalkThreads, dyn) != hipSuccess ||
       hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {

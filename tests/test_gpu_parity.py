@@ -91,6 +91,24 @@ def test_schedule_variants_match_oracle(debug, monkeypatch):
         assert got == ref, (debug, s.name)
 
 
+@pytest.mark.parametrize("debug", ["", "compact=0", "compact=0,walk_blocks=0"])
+def test_compact_rows_at_8_bits_match_oracle(debug, monkeypatch):
+    """8-bit context model 0 in the frame-parallel path: the walk's LDS rows
+    hold the 24 slots a symbol can use at 8 bits (e <= 7), an unused slot's
+    byte in the dummy row (the default), or all 32 (compact=0, a test hook):
+    the oracle's bytes either way, on video, noise (every exponent and sign
+    slot) and 4:4:4 / gray."""
+    monkeypatch.setenv("FFV1HIP_DEBUG", debug)
+    for s in [Stream("c8_420", 352, 288, "yuv420p", 8, slices=4, coder=1, gop_size=4),
+              Stream("c8_noise", 176, 144, "yuv420p", 6, slices=4, coder=1, gop_size=3, source="random"),
+              Stream("c8_444", 176, 144, "yuv444p", 5, slices=6, coder=-2, gop_size=5, chroma444=True),
+              Stream("c8_gray", 128, 96, "gray", 4, slices=4, coder=1, gop_size=2, source="random")]:
+        frames = list(s.frames())
+        _, _, ref = oracle_encode(s, frames)
+        _, got = hip_encode(s, frames, batch=len(frames))
+        assert got == ref, (debug, s.name)
+
+
 @pytest.mark.parametrize("debug", ["dsets=lazy", "dsets=lazy,rec2_drop=1", "dsets=lazy,rec2_drop=0",
                                    "dsets=eager,rec2_drop=0", "dsets=lazy,budget=4", "dsets=lazy,budget=8,rec2_drop=1"])
 def test_lazy_decision_sets_match_oracle(debug, monkeypatch):
