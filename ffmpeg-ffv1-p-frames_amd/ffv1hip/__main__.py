@@ -2,7 +2,7 @@
 
     python -m ffv1hip encode -s 352x288 -pix_fmt yuv420p [-slices 4] [-level 3]
                              [-coder 1] [-context 0] [-g 12] [-slicecrc 1]
-                             [-batch 12] in.yuv out.avi
+                             [-strict experimental] [-batch 12] in.yuv out.avi
     python -m ffv1hip decode in.avi out.yuv
     python -m ffv1hip info in.avi
 
@@ -24,6 +24,13 @@ import sys
 import numpy as np
 
 from . import AVCodecContext, FFV1Encoder, HipDecoder, configure
+from .encoder import FF_COMPLIANCE_EXPERIMENTAL
+
+
+def _strict(v: str) -> int:
+    """ffmpeg's -strict: a number or one of its names (options_table.h)."""
+    names = {"very": 2, "strict": 1, "normal": 0, "unofficial": -1, "experimental": -2}
+    return names[v] if v in names else int(v)
 from .avi import read_avi, write_avi
 
 
@@ -52,7 +59,8 @@ def _read_frames(path, params):
 def encode(a) -> int:
     w, h = (int(v) for v in a.s.lower().split("x"))
     avctx = AVCodecContext(w, h, a.pix_fmt, gop_size=a.g, slices=a.slices, level=a.level,
-                           coder=a.coder, context=a.context, slicecrc=a.slicecrc)
+                           coder=a.coder, context=a.context, slicecrc=a.slicecrc,
+                           strict_std_compliance=_strict(a.strict))
     enc = FFV1Encoder(batch=a.batch)
     enc.init(avctx)
     params = enc.params
@@ -77,7 +85,8 @@ def decode(a) -> int:
     if fourcc != b"FFV1":
         raise SystemExit(f"{a.input}: not an FFV1 stream ({fourcc!r})")
     params = configure(w, h, a.pix_fmt, slices=a.slices, coder=a.coder, context=a.context,
-                       gop_size=a.g, level=a.level)
+                       gop_size=a.g, level=a.level, slicecrc=a.slicecrc,
+                       experimental=_strict(a.strict) <= FF_COMPLIANCE_EXPERIMENTAL)
     dec = HipDecoder(params, extradata, 0)
     with open(a.output, "wb") as f:
         for i in range(0, len(packets), a.batch):
@@ -110,6 +119,7 @@ def main(argv=None) -> int:
         p.add_argument("-context", type=int, default=0)
         p.add_argument("-g", type=int, default=12)
         p.add_argument("-slicecrc", type=int, default=-1)
+        p.add_argument("-strict", default="normal", help="-strict experimental: levels 2 and 4")
         p.add_argument("-batch", type=int, default=12, help="frames per GPU call")
         p.add_argument("input")
         p.add_argument("output")

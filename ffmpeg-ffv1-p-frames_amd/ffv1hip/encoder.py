@@ -197,7 +197,7 @@ def configure(width: int, height: int, pix_fmt: str, slices: int = 0, level: int
               allow_large_grid: bool = False, pass_: int = 0, experimental: bool = False) -> Params:
     """encode_init's option -> bitstream-parameter derivation (ffv1enc.c:669-1029);
     pass_ 1 / 2 are AV_CODEC_FLAG_PASS1 / PASS2; experimental is -strict
-    experimental (version 4 at level 4, ffv1enc.c:703-706)."""
+    experimental (versions 2 and 4 at levels 2 and 4, ffv1enc.c:703-706)."""
     L = load_library()
     o = Options(width, height, pix_fmt.encode(), slices, level, coder, context, gop_size,
                 bits_per_raw_sample, slicecrc, int(allow_large_grid), pass_, int(experimental))
@@ -488,6 +488,7 @@ class AVCodecContext:
     slicecrc: int = -1
     extradata: bytes = b""
     allow_large_grid: bool = False
+    strict_std_compliance: int = 0   # FF_COMPLIANCE_EXPERIMENTAL (-2) admits versions 2 and 4
     flags: int = 0                   # AV_CODEC_FLAG_PASS1 / PASS2
     stats_in: Optional[str] = None   # pass 2: what pass 1 left in stats_out
     stats_out: str = ""              # pass 1: written at the flush (ffv1enc.c:1236-1277)
@@ -496,6 +497,7 @@ class AVCodecContext:
 
 
 AV_CODEC_FLAG_PASS1 = 1 << 9   # avcodec.h
+FF_COMPLIANCE_EXPERIMENTAL = -2  # avcodec.h: -strict experimental (ffv1enc.c:703-706)
 AV_CODEC_FLAG_PASS2 = 1 << 10
 
 
@@ -544,7 +546,8 @@ class FFV1Encoder:
         self.params = configure(avctx.width, avctx.height, avctx.pix_fmt, avctx.slices,
                                 avctx.level, avctx.coder, avctx.context, avctx.gop_size,
                                 avctx.bits_per_raw_sample, avctx.slicecrc,
-                                avctx.allow_large_grid, pass_)
+                                avctx.allow_large_grid, pass_,
+                                avctx.strict_std_compliance <= FF_COMPLIANCE_EXPERIMENTAL)
         self._enc = HipEncoder(self.params, self.device, self.batch)
         self._pass = pass_
         if pass_ == 1 or (pass_ == 2 and avctx.stats_in is not None):

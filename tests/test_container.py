@@ -76,3 +76,39 @@ def test_cli_encode_writes_the_fate_file(tmp_path, name):
         assert main(["decode", "-pix_fmt", pin["pix_fmt"], "-slices", str(opts.get("slices", 0)),
                      "-level", str(opts["level"]), str(out), str(back)]) == 0
         assert back.read_bytes() == raw.read_bytes()
+
+
+def test_cli_strict_names():
+    from ffv1hip.__main__ import _strict
+    assert _strict("experimental") == -2 and _strict("normal") == 0 and _strict("-2") == -2
+
+
+@pytest.mark.gpu
+def test_cli_level2_strict_experimental_roundtrip(tmp_path):
+    """`-level 2 -strict experimental` (ffv1enc.c:703-706) through the CLI:
+    the AVI's packets equal the oracle's version-2 packets, and the GPU
+    decoder gives the raw frames back; without -strict the level is refused."""
+    from ffv1hip.__main__ import main
+    from ffv1hip.avi import read_avi
+    from ffv1hip.encoder import FFV1Error
+    from helpers import Stream
+    s = Stream("cli_v2", 96, 64, "yuv420p", 5, level=2, slices=4, coder=1, gop_size=3, source="random",
+               experimental=True, seed=31)
+    frames = list(s.frames())
+    raw = tmp_path / "in.raw"
+    _write_raw(raw, frames)
+    out = tmp_path / "out.avi"
+    argv = ["encode", "-s", "96x64", "-pix_fmt", "yuv420p", "-g", "3", "-slices", "4", "-level", "2",
+            "-coder", "1", "-batch", "2"]
+    with pytest.raises(FFV1Error):
+        main(argv + [str(raw), str(out)])
+    assert main(argv + ["-strict", "experimental", str(raw), str(out)]) == 0
+    _, _, _, ex, pk = read_avi(out.read_bytes())
+    cfg = oracle.configure(96, 64, "yuv420p", slices=4, level=2, coder=1, gop_size=3, experimental=True)
+    enc = oracle.Encoder(cfg)
+    assert ex == enc.extradata()
+    assert [p for p, _ in pk] == [enc.encode(f)[0] for f in frames]
+    back = tmp_path / "back.raw"
+    assert main(["decode", "-pix_fmt", "yuv420p", "-slices", "4", "-level", "2", "-coder", "1", "-g", "3",
+                 "-strict", "experimental", str(out), str(back)]) == 0
+    assert back.read_bytes() == raw.read_bytes()
