@@ -1892,7 +1892,10 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
     W.amask = pk >= 0 ? 0xFFFFu : 0u;
   }
   W.kk = (2 * wv + h) * tsz + W.kt;
-  W.dummy = wo + h * kPreHalf + kPreData + k;
+  // one dummy byte per half for the slots without a decision: a shared
+  // address, where 32 lanes' distinct bytes made the stage write a 4-way
+  // conflict on 8 dwords
+  W.dummy = wo + h * kPreHalf + kPreData;
   W.msh = k == 31 ? 28 : 12;
   W.mwd = k == 31 ? 2 : 3;
   W.mbase = k == 31 ? 4 : 0;
