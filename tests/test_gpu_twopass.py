@@ -20,6 +20,8 @@ TWO_PASS = [
     Stream("ctx1_chained", 160, 120, "yuv420p10", 4, slices=4, coder=1, context=1, gop_size=2,
            source="d2", depth=10),
     Stream("bgr0_chained", 96, 64, "bgr0", 4, slices=4, coder=1, gop_size=2, source="random"),
+    # version 2: the initial states in its extradata, read back at keyframes
+    Stream("p8_v2", 176, 144, "yuv420p", 4, level=2, slices=4, coder=1, gop_size=2, experimental=True),
 ]
 # pass 1 on the chained coder beyond TWO_PASS: alpha (a third plane context)
 # and version 4 (RCT coefficients per slice); parity unpinned
@@ -32,7 +34,7 @@ PASS1_EXTRA = [
 def _kw(s):
     kw = dict(slices=s.slices, coder=s.coder, context=s.context, gop_size=s.gop_size)
     if s.experimental:
-        kw.update(level=4, experimental=True)
+        kw.update(level=s.level if s.level >= 0 else 4, experimental=True)
     return kw
 
 
