@@ -450,6 +450,7 @@ struct ffv1hip_ctx {
   int max_slots = 0;          // segments (= frame slots) per call
   bool frames_mode = false;   // states walk + decision-stream coder (range coder, LDS-sized tables)
   int wmax = 0;               // most decisions one symbol can take (2 * coded bits + 1)
+  int cwords = kChunkWords;   // frames mode: words per walk chunk (chunk_words(wmax))
   int64_t frame_samples = 0;  // symbols of one frame (each slice padded to 4)
   int64_t frame_chunks = 0;   // 64-sample walk chunks of one frame
   int max_ops = 0;
@@ -478,7 +479,7 @@ struct ffv1hip_ctx {
   uint32_t* d_sym = nullptr;     // [slot][frame_samples]; frames mode: walk records (uint2), set 0 of [batch frame][frame_samples]
   // frames mode, two buffer sets: the walk of batch k+1 runs while batch k codes
   uint8_t* d_keys2 = nullptr;    // 3 x [batch frame] keyflags
-  uint32_t* d_cbits = nullptr;   // 2 x [batch frame][frame_chunks][kChunkWords] packed decision bits
+  uint32_t* d_cbits = nullptr;   // 2 x [batch frame][frame_chunks][cwords] packed decision bits
   // the per-batch stream metadata has three sets (index tri): the symbols of
   // batch k rewrite set k % 3 while the coder of batch k-1 may still read its
   // set and the walk of batch k-1 run
@@ -1200,7 +1201,7 @@ static int64_t device_bytes(const ffv1hip_ctx* c, int64_t nb) {
   int64_t b = nb * (stride * c->nslices + (((cap + 16) * c->nslices + 255) & ~int64_t(255)));
   b += 2 * int64_t(c->pcount) * c->contexts * 32 * c->nslices;  // the P-frame carry
   if (c->frames_mode) {
-    b += nb * (8 * c->frame_samples + 4 * int64_t(kChunkWords) * c->frame_chunks);  // walk records, chunk bits
+    b += nb * (8 * c->frame_samples + 4 * int64_t(c->cwords) * c->frame_chunks);  // walk records, chunk bits
     const int64_t dcap = decision_cap(c, nb);
     b += 2 * (dcap + dcap / 8);                                                      // two decision sets
     int64_t segs = 0, groups = 0;
@@ -1228,7 +1229,7 @@ static int alloc_rec2(ffv1hip_ctx* c) {
   c->rec2_pending = false;
   const int nb = c->max_batch;
   const size_t rec_bytes = sizeof(uint2) * size_t(c->frame_samples) * nb;
-  const size_t cb_bytes = sizeof(uint32_t) * kChunkWords * size_t(c->frame_chunks) * nb;
+  const size_t cb_bytes = sizeof(uint32_t) * c->cwords * size_t(c->frame_chunks) * nb;
   size_t free_b = 0, total_b = 0;
   HIP_TRY(hipMemGetInfo(&free_b, &total_b));
   const size_t d0 = size_t(c->dcap[0]), d1 = c->dcap[1] ? size_t(c->dcap[1]) : d0;
@@ -1330,7 +1331,7 @@ static bool lazy_sizing(const ffv1hip_ctx* c) {
   if (ds == "eager" || cap >= worst) return false;
   size_t free_b = 0, total_b = 0;
   if (hipSetDevice(c->device) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) return true;
-  const int64_t rec2 = nb * (8 * c->frame_samples + 4 * int64_t(kChunkWords) * c->frame_chunks);
+  const int64_t rec2 = nb * (8 * c->frame_samples + 4 * int64_t(c->cwords) * c->frame_chunks);
   const int64_t eager = device_bytes(c, nb) + rec2 + cap / 2 + (int64_t(5) << 30);  // alloc_rec2's old margin
   return eager > int64_t(free_b);
 }
@@ -1422,7 +1423,7 @@ static int alloc_device(ffv1hip_ctx* c) {
     // after this batch's walk on the same stream, and wait for its bits)
     HIP_TRY(hipMalloc(&c->d_sym, sizeof(uint2) * size_t(c->frame_samples) * nb));
     HIP_TRY(hipMalloc(&c->d_keys2, 3 * size_t(nb)));
-    HIP_TRY(hipMalloc(&c->d_cbits, sizeof(uint32_t) * kChunkWords * size_t(c->frame_chunks) * nb));
+    HIP_TRY(hipMalloc(&c->d_cbits, sizeof(uint32_t) * c->cwords * size_t(c->frame_chunks) * nb));
     HIP_TRY(hipMalloc(&c->d_dcount, 3 * sizeof(int) * 3 * size_t(nb) * c->nslices));
     HIP_TRY(hipMalloc(&c->d_dbase, 3 * sizeof(int64_t) * size_t(nb) * c->nslices));
     HIP_TRY(hipMalloc(&c->d_dtotal, 3 * sizeof(int64_t)));
@@ -1619,6 +1620,7 @@ ffv1hip_ctx* ffv1hip_create(const ffv1hip_params* params, int device, int max_ba
     c->frames_mode = p.ac && !p.colorspace && !p.transparency && p.version <= 3 && lds <= kWalkLdsMax &&
                      c->knobs.str("coder") != "chain";
     c->wmax = 2 * (p.bits_per_raw_sample <= 8 ? 8 : p.bits_per_raw_sample) + 1;
+    c->cwords = chunk_words(c->wmax);
     // a large batch, sized from what its content needs (lazy_sizing)
     c->lazy_sets = c->frames_mode && lazy_sizing(c);
     // the decision-stream coder writes a slice's digits (the values of low,
@@ -1959,6 +1961,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     HIP_TRY(hipMemsetAsync(d_dcount, 0, sizeof(int) * 3 * size_t(n) * c->nslices, sst));
     sa.rec = d_rec;
     sa.cbits = d_cbits;
+    sa.cwords = c->cwords;
     // one set: the previous batch's bits kernel (its own stream) has read the chunk bits
     if (sst == st) HIP_TRY(hipStreamWaitEvent(st, c->bitsed[fb ^ 1], 0));
     sa.frame_chunks = c->frame_chunks;
@@ -2011,6 +2014,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
           return set_err(-12, "decision buffers for %lld decisions: %s", (long long)need, g_err);
         sa.rec = d_rec;
         sa.cbits = d_cbits;
+        sa.cwords = c->cwords;
         ca.slice_out = c->d_slice_out;  // (alloc_rec2 may have lowered the budget)
         ca.slice_cap = c->slice_cap;
         ca.slice_stride = c->slice_stride;
@@ -2029,6 +2033,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     if (force_skip) c->guard_skips++;
     BitsArgs ba{};
     ba.cbits = sa.cbits;
+    ba.cwords = c->cwords;
     ba.frame_chunks = c->frame_chunks;
     ba.geom = c->d_geom;
     ba.nslices = c->nslices;
@@ -2047,6 +2052,7 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     WalkArgs wa{};
     wa.rec = d_rec;
     wa.cbits = d_cbits;
+    wa.cwords = c->cwords;
     wa.frame_chunks = c->frame_chunks;
     wa.frame_samples = c->frame_samples;
     wa.geom = c->d_geom;

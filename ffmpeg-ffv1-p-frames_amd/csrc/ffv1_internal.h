@@ -60,8 +60,12 @@ struct SliceGeom {
 // Per walk chunk (64 consecutive samples of a plane), written by ffv1_symbols:
 // word 0 = the chunk's decisions | kChunkLong / kChunkMulti flags, words
 // 1.. = the decision bits in coding order (bit d in word 1 + d / 32), then a
-// zero word; words 68, 69 = which of the 64 symbols have e = 10 or 11.
-constexpr int kChunkWords = 70;  // header, 66 bit words + a zero word, the 64-bit multi-symbol mask
+// zero word; the last two words = which of the 64 symbols have e = 10 or 11.
+// A chunk takes chunk_words(wmax) words, wmax the most decisions one symbol
+// can take (2 x coded bits + 1): 46 at 10 bits, 54 at 12, 70 at 16.
+constexpr int kChunkWords = 70;  // the largest: header, 66 bit words + a zero word, the 64-bit multi-symbol mask
+__host__ __device__ constexpr int chunk_words(int wmax) { return 2 * wmax + 4; }
+static_assert(chunk_words(33) == kChunkWords, "16 bits: the largest chunk");
 constexpr uint32_t kChunkLong = 0x80000000u;   // a symbol with e >= 12 (|diff| >= 4096)
 constexpr uint32_t kChunkMulti = 0x40000000u;  // a symbol with e = 10 or 11 (slot 10 / 31 repeat)
 constexpr uint32_t kChunkFlags = kChunkLong | kChunkMulti;
@@ -86,13 +90,14 @@ struct SymbolArgs {
   int64_t frame_samples;
   int* dcount;                // optional [slot][slice][3]: range-coder decisions per plane
   uint2* rec;                 // optional, instead of sym: [slot][frame_samples] walk records
-  uint32_t* cbits;            // with rec: [slot][frame_chunks][kChunkWords]
+  uint32_t* cbits;            // with rec: [slot][frame_chunks][cwords]
   int64_t frame_chunks;
   int p_lo, p_hi;             // planes of this launch (p_hi 0: all); with rec, outputs by batch frame
   const int2* rct;            // v4: [batch frame][slice] {by, ry} RCT coefficients, else null (1, 1)
   int max_blocks;             // grid cap (0: one block per item); the blocks stride over the items
   int nz;                     // set by launch_symbols: plane parts per (slice, slot)
   int rowb = 32;              // with rec: the walk's bytes per row (a record's row address = row x rowb)
+  int cwords = kChunkWords;   // with rec: words per chunk (chunk_words)
 };
 
 // v4's choose_rct_params (ffv1enc.c:1064-1144) for every (frame, slice) of
@@ -303,7 +308,7 @@ int launch_stats(const StatsArgs& a, bool states, void* stream);
 // (frame, slice) streams then runs in parallel (launch_dcode).
 struct WalkArgs {
   const uint2* rec;           // [batch frame][frame_samples] walk records
-  const uint32_t* cbits;      // [batch frame][frame_chunks][kChunkWords]
+  const uint32_t* cbits;      // [batch frame][frame_chunks][cwords]
   int64_t frame_chunks;
   int64_t frame_samples;
   const SliceGeom* geom;
@@ -330,6 +335,7 @@ struct WalkArgs {
   int dense;                  // records address dense rows (dense_row), the state tables keep contexts
   Bounds bnd;                 // debug build: the extents of the writes
   int rowb = 32;              // bytes per row in LDS: 32, or kCompactRowBytes at 8 bits (context model 0)
+  int cwords = kChunkWords;   // words per chunk (chunk_words)
 };
 
 constexpr int kTraceWords = 8;
@@ -373,12 +379,13 @@ __host__ __device__ inline int dense_row(int ctx) {  // context -> its row, -1 w
 // Kernel 2b: the decision bits, from the chunks' packed words to their place
 // in the decision stream (one block per (frame, slice) stream).
 struct BitsArgs {
-  const uint32_t* cbits;      // [batch frame][frame_chunks][kChunkWords]
+  const uint32_t* cbits;      // [batch frame][frame_chunks][cwords]
   int64_t frame_chunks;
   const SliceGeom* geom;
   int nslices, nframes;
   DecisionStream ds;
   int max_blocks;             // grid cap (0: one block per stream); the blocks stride over the streams
+  int cwords = kChunkWords;   // words per chunk (chunk_words)
 };
 
 struct AssembleArgs {

@@ -204,7 +204,7 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   // beside it (~13 KB per CU is left by three walk waves)
   const int16_t* __restrict__ const qt = a.qt;
   __shared__ int red[kSymThreads / kWave];
-  __shared__ uint32_t cstage[kSymThreads / kWave][kChunkWords];  // a wave's chunk bits
+  __shared__ uint32_t cstage[kSymThreads / kWave][kChunkWords];  // a wave's chunk bits (the largest chunk)
   // a plane of a slice is split into kSymSplit runs of whole 256-sample steps;
   // work item vb = ((plane part) * nslots + slot) * nslices + slice, strided
   // over a grid that may be smaller than the items (launch_symbols: a bounded
@@ -262,7 +262,8 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
   uint2* const rec = a.rec ? a.rec + (int64_t)fs * a.frame_samples + g.sym_off + g.plane_sym_off[p] : nullptr;
   // the plane's chunk headers (read once: a reload inside the loop would
   // wait for the record stores)
-  uint32_t* const cbase = rec ? a.cbits + ((int64_t)fs * a.frame_chunks + g.chunk_off[p]) * kChunkWords : nullptr;
+  const int cw = a.cwords;
+  uint32_t* const cbase = rec ? a.cbits + ((int64_t)fs * a.frame_chunks + g.chunk_off[p]) * cw : nullptr;
   // the lane's sample, stepped along the plane without a division per step
   int cy = (int)((b0 + threadIdx.x) / pw), cx = (int)((b0 + threadIdx.x) - (int64_t)cy * pw);
   // whole waves per step: a wave's 64 consecutive samples are one walk chunk
@@ -336,7 +337,7 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
       uint32_t* const cs = cstage[wv];
       if (base + wv * kWave < n) {
         cs[lane] = 0u;
-        if (lane < kChunkWords - kWave) cs[kWave + lane] = 0u;
+        if (lane < cw - kWave) cs[kWave + lane] = 0u;
         if (valid) {
           const uint64_t x = decision_bits(diff) << (d0 & 31);
           atomicOr(&cs[1 + (d0 >> 5)], (uint32_t)x);
@@ -346,18 +347,17 @@ __global__ __launch_bounds__(kSymThreads) void ffv1_symbols(SymbolArgs a) {
         const bool lng = __ballot(valid && (diff >= 4096 || diff <= -4096)) != 0;
         const uint64_t mm = __ballot(valid && (diff >= 1024 || diff <= -1024) && diff < 4096 && diff > -4096);
         if (lane == 0) cs[0] = (uint32_t)total | (lng ? kChunkLong : 0u) | (mm ? kChunkMulti : 0u);
-        if (lane < 2) cs[kChunkWords - 2 + lane] = (uint32_t)(mm >> (32 * lane));
+        if (lane < 2) cs[cw - 2 + lane] = (uint32_t)(mm >> (32 * lane));
         // out: the header, the words the decisions fill and the two after
         // them (ffv1_bits reads a chunk's words up to the one its last
         // decision lands in at its stream offset, which may be one more),
         // and the mask words; the rest of the 70 stay unwritten (zero words:
         // ~3 of every 4 written before, 10 GB a c3 step)
-        uint32_t* const dst = cbase + ((base + wv * kWave) / kWave) * kChunkWords;
-        const int last = min(kChunkWords - 3, (total >> 5) + 2);
-        if (lane <= last) dst[lane] = cs[lane];
-        if (kWave + lane <= last || kWave + lane >= kChunkWords - 2) {
-          if (lane < kChunkWords - kWave) dst[kWave + lane] = cs[kWave + lane];
-        }
+        uint32_t* const dst = cbase + ((base + wv * kWave) / kWave) * cw;
+        const int last = min(cw - 3, (total >> 5) + 2);
+        if (lane < cw && (lane <= last || lane >= cw - 2)) dst[lane] = cs[lane];
+        const int w2 = kWave + lane;
+        if (w2 < cw && (w2 <= last || w2 >= cw - 2)) dst[w2] = cs[w2];
       }
     } else if (valid) {
       out[RGB ? ((int64_t)y * a.nplanes + p) * pw + x : idx] = ((uint32_t)(row0 + ctx) << 16) | (uint16_t)diff;
@@ -1965,7 +1965,7 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
     for (int pl = p0; pl < p1; pl++) {
       const int64_t nsym = live ? (pl < 2 ? g.plane_sym_off[pl + 1] : g.nsym) - g.plane_sym_off[pl] : 0;
       const uint2* rp = a.rec + (int64_t)f * a.frame_samples + g.sym_off + g.plane_sym_off[pl];
-      const uint32_t* cp = a.cbits + ((int64_t)f * a.frame_chunks + g.chunk_off[pl]) * kChunkWords;
+      const uint32_t* cp = a.cbits + ((int64_t)f * a.frame_chunks + g.chunk_off[pl]) * a.cwords;
       const int nch = (int)((nsym + kChunk - 1) / kChunk);
       const int nchunks = max(__builtin_amdgcn_readlane(nch, 0), __builtin_amdgcn_readlane(nch, 32));
       // a chunk's inputs: 2 records per lane and the chunk header
@@ -1981,10 +1981,10 @@ __global__ __launch_bounds__(kWalkThreads * WAVES) void ffv1_walk(WalkArgs a) {
         const int64_t b = (int64_t)c * kChunk;
         x.m0 = rp[b + k < nsym ? b + k : 0];
         x.m1 = rp[b + 32 + k < nsym ? b + 32 + k : 0];
-        const uint32_t* const ch = cp + (int64_t)(c < nch ? c : 0) * kChunkWords;
+        const uint32_t* const ch = cp + (int64_t)(c < nch ? c : 0) * a.cwords;
         x.hd = ch[0];
-        x.mlo = ch[kChunkWords - 2];
-        x.mhi = ch[kChunkWords - 1];
+        x.mlo = ch[a.cwords - 2];
+        x.mhi = ch[a.cwords - 1];
         return x;
       };
       In nx = load(0);
@@ -2238,16 +2238,16 @@ __global__ __launch_bounds__(kBitsThreads) void ffv1_bits(BitsArgs a) {
   const SliceGeom& g = a.geom[s];
   const int* dc = a.ds.dcount + sid * 3;
   const int64_t base = a.ds.dbase[sid];
-  const uint32_t* const fc = a.cbits + (int64_t)f * a.frame_chunks * kChunkWords;
+  const uint32_t* const fc = a.cbits + (int64_t)f * a.frame_chunks * a.cwords;
   int run = 0;  // stream-relative decision index of the next chunk
   for (int p = 0; p < 3; p++) {
     if (p == 1) run = (int)chroma_start(dc[0]);
     const int64_t nsym = (p < 2 ? g.plane_sym_off[p + 1] : g.nsym) - g.plane_sym_off[p];
     const int nch = (int)((nsym + kChunk - 1) / kChunk);
-    const uint32_t* const pc = fc + g.chunk_off[p] * kChunkWords;
+    const uint32_t* const pc = fc + g.chunk_off[p] * a.cwords;
     for (int c0 = 0; c0 < nch; c0 += kBitsThreads) {
       const int c = c0 + t;
-      const int n = c < nch ? (int)(pc[(int64_t)c * kChunkWords] & ~kChunkFlags) : 0;
+      const int n = c < nch ? (int)(pc[(int64_t)c * a.cwords] & ~kChunkFlags) : 0;
       const int x = wave_incl_scan(n, lane);
       if (lane == kWave - 1) wsum[wv] = x;
       __syncthreads();
@@ -2297,7 +2297,7 @@ __global__ __launch_bounds__(kBitsThreads) void ffv1_bits(BitsArgs a) {
           constexpr int K = decltype(kc)::value;
           const bool ok = i + K < i1;
           const int ii = ok ? i + K : i;
-          const uint32_t* const q = pc + (int64_t)(c0 + ii) * kChunkWords;
+          const uint32_t* const q = pc + (int64_t)(c0 + ii) * a.cwords;
           P[K] = base + __builtin_amdgcn_readfirstlane(off[ii]);
           T[K] = ok ? __builtin_amdgcn_readfirstlane(tot[ii]) : 0;
           NW[K] = ((int)(P[K] & 31) + T[K] + 31) >> 5;
@@ -2311,7 +2311,7 @@ __global__ __launch_bounds__(kBitsThreads) void ffv1_bits(BitsArgs a) {
             uint32_t lastw = 0u;
             word(i + K, lane, P[K], T[K], H[K], L[K], last, lastw);
             if (NW[K] > kWave) {  // long chunks (e >= 15 symbols): words 64..66
-              const uint32_t* const q = pc + (int64_t)(c0 + i + K) * kChunkWords;
+              const uint32_t* const q = pc + (int64_t)(c0 + i + K) * a.cwords;
               const int m = kWave + lane;
               const uint32_t hi = m < NW[K] ? q[1 + m] : 0u;
               const uint32_t lo = m < NW[K] ? q[m] : 0u;
