@@ -48,7 +48,7 @@ CONFIGS = {
                metric="Mpixels/s encoded (bit-exact) 1080p yuv420p FFV1 intra",
                workload="1080p 1920x1080 yuv420p, coder=1 (range, custom table), slices=24, intra-only"),
     "c4": dict(W=3840, H=2160, PIX_FMT="yuv444p16", SLICES=64, GOP=12, BPR=12, DEPTH=16, C444=True,
-               GRID=False, GOPS=20, PIN=None,  # 20: the most with two records sets (walk-bound, 8.5 Gpix/s); 21 (one set): 6.4
+               GRID=False, GOPS=21, PIN=None,  # 21: 1024 walk waves in 4-wave blocks, both records sets (8.59 vs 8.21 Gpix/s at 20); 22: one set, 6.55
                metric="Mpixels/s encoded (lossless) 4K yuv444p12 FFV1 P-frames",
                workload="4K 3840x2160 yuv444p16le + bits_per_raw_sample=12, coder=1, slices=64, keyint=12 P-frames"),
     "c5": dict(W=7680, H=4320, PIX_FMT="yuv420p10", SLICES=256, GOP=12, BPR=0, DEPTH=10, C444=False,
