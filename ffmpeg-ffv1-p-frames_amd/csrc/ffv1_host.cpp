@@ -143,7 +143,7 @@ static const char* const kKnobNames[] = {"serial",      "walkdbg",     "walktrac
                                          "walk_part_a", "force_multi", "bounds_shrink", "dsets",
                                          "rec2_drop",   "budget",      "pack",        "v4_cap0",     "readback",
                                          "fsets",       "guard_skip",  "walk_prio",   "range_prio",  "compact",
-                                         "sym_skip"};
+                                         "sym_skip",    "code_cpw"};
 
 // The per-hook environment variables of earlier rounds.  They are no longer
 // read, so one that is set is an error (a measurement that silently ran the
@@ -453,6 +453,7 @@ struct ffv1hip_ctx {
   int wmax = 0;               // most decisions one symbol can take (2 * coded bits + 1)
   int cwords = kChunkWords;   // frames mode: words per walk chunk (chunk_words(wmax))
   int64_t batches_run = 0;    // frames-mode batches started (the sym_skip measurement hook)
+  int64_t table_dummy = 0;    // chained mode: the first of ffv1_code's dummy tables
   int64_t frame_samples = 0;  // symbols of one frame (each slice padded to 4)
   int64_t frame_chunks = 0;   // 64-sample walk chunks of one frame
   int max_ops = 0;
@@ -1485,7 +1486,8 @@ static int alloc_device(ffv1hip_ctx* c) {
     if (!c->lazy_sets && alloc_rec2(c) < 0) return -5;
   } else {
     const size_t chains = (size_t(c->max_slots) * c->nslices + 63) & ~size_t(63);
-    HIP_TRY(hipMalloc(&c->d_tables, state_bytes * chains));
+    HIP_TRY(hipMalloc(&c->d_tables, state_bytes * (chains + 64)));  // + ffv1_code's 64 dummy tables
+    c->table_dummy = int64_t(chains);
     HIP_TRY(hipMalloc(&c->d_sym, sizeof(uint32_t) * size_t(c->frame_samples) * c->max_slots));
   }
   HIP_TRY(hipMalloc(&c->d_geom, sizeof(SliceGeom) * c->nslices));
@@ -2255,6 +2257,19 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
       ra.nframes = n;
       ra.rct = c->d_rct;
       if (launch_rct_params(ra, st) < 0) return set_err(-5, "rct launch failed");
+    }
+    // ffv1_code's chains per wave: the batch's chains spread over two waves
+    // per CU (a symbol costs a wave its chains' largest exponent, and few
+    // chains at 64 per wave leave the SIMDs idle).  Measured (one box each,
+    // tools/bench_chained.py): bgr0 1080p 480 chains 95 -> 132 Mpix/s (1 per
+    // wave); ctx1 4K 1280 chains 445 (64) / 453 (2) / 479 (3); 5120 chains
+    // 1,731 (64) / 1,732 (16) / 1,772 (10), but 1,587 at 7 (732 waves:
+    // three per CU lose).  The code_cpw hook overrides (64: the round-5 form).
+    ca.table_dummy = c->table_dummy;
+    {
+      const int64_t chains = int64_t(nsegs) * c->nslices, waves = int64_t(2) * std::max(1, c->cus);
+      ca.cpw = (int)std::min<int64_t>(64, std::max<int64_t>(1, (chains + waves - 1) / waves));
+      ca.cpw = std::min(64, std::max(1, c->knobs.get("code_cpw", ca.cpw)));
     }
     for (int j = 0; j < maxlen; j++) {
       sa.frame_of_slot = c->d_slot_frames + size_t(j) * nsegs;

@@ -283,6 +283,11 @@ struct CodeArgs {
   // rc_stat[256][2] by state, rc_stat2[contexts][32][2] by (context, slot)
   unsigned long long* rc_stat;
   unsigned long long* rc_stat2;
+  // ffv1_code: chains per wave (lanes 0 .. cpw-1; launch_code spreads a batch
+  // of few chains over more waves), and the first of the 64 dummy tables the
+  // other lanes write their rows to
+  int cpw = 64;
+  int64_t table_dummy = 0;
 };
 
 // Pass-1 statistics (ffv1enc.c:190-199): rc_stat[state][bit] from the

@@ -861,15 +861,20 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
   const uint8_t* ftab = tabs + 512;  // frame table
 
   const int lane = threadIdx.x;
-  const int64_t chain = (int64_t)blockIdx.x * kCodeThreads + lane;  // tables exist for the padded grid
+  // a.cpw chains per wave, on lanes 0 .. cpw-1 (a symbol costs the wave its
+  // chains' largest exponent, and a batch of few chains leaves SIMDs idle);
+  // the other lanes run idle on a dummy table, so their row stores touch no
+  // chain's.  Tables exist for the chains padded to 64.
+  const bool mine = lane < a.cpw;
+  const int64_t chain = (int64_t)blockIdx.x * a.cpw + (mine ? lane : 0);
   const int seg_i = (int)(chain / a.nslices);
   const int slice = (int)(chain % a.nslices);
-  bool live = seg_i < a.nsegs;
+  bool live = mine && seg_i < a.nsegs;
   Segment seg{0, 0, 0, 0};
   if (live) seg = a.segs[seg_i];
   live = live && a.j < seg.nframes;
   const int f = seg.first_frame + a.j;
-  uint8_t* const table = a.tables + chain * a.state_bytes;
+  uint8_t* const table = a.tables + (mine ? chain : a.table_dummy + (blockIdx.x & 63)) * a.state_bytes;
   const int key = live ? a.keyflags[f] : 0;
 
   // context states: continue, or reset at a keyframe (ff_ffv1_clear_slice_state)
@@ -2777,7 +2782,8 @@ int launch_symbols(const SymbolArgs& a, void* stream) {
 
 int launch_code(const CodeArgs& a, void* stream) {
   const int64_t chains = (int64_t)a.nsegs * a.nslices;
-  dim3 grid((unsigned)((chains + kCodeThreads - 1) / kCodeThreads)), block(kCodeThreads);
+  if (a.cpw < 1 || a.cpw > kCodeThreads) return -1;
+  dim3 grid((unsigned)((chains + a.cpw - 1) / a.cpw)), block(kCodeThreads);
   hipLaunchKernelGGL(ffv1_code, grid, block, code_lds_bytes(kCodeThreads), reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
