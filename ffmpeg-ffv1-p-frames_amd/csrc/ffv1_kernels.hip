@@ -2410,9 +2410,11 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code_golomb(CodeArgs a) {
   for (int i = threadIdx.x; i < 1024; i += kCodeThreads) tabs[i] = a.tabs[i];
   __syncthreads();
   const int lane = threadIdx.x;
-  const int64_t chain = (int64_t)blockIdx.x * kCodeThreads + lane;
+  // a.cpw chains per wave, as ffv1_code (the other lanes idle: they leave
+  // after the prefix and never touch a table)
+  const int64_t chain = (int64_t)blockIdx.x * a.cpw + (lane < a.cpw ? lane : 0);
   const int seg_i = (int)(chain / a.nslices), slice = (int)(chain % a.nslices);
-  bool live = seg_i < a.nsegs;
+  bool live = lane < a.cpw && seg_i < a.nsegs;
   Segment seg{0, 0, 0, 0};
   if (live) seg = a.segs[seg_i];
   live = live && a.j < seg.nframes;
@@ -2962,7 +2964,8 @@ int launch_sink(const CodeArgs& a, void* stream) {
 
 int launch_code_golomb(const CodeArgs& a, void* stream) {
   const int64_t chains = (int64_t)a.nsegs * a.nslices;
-  dim3 grid((unsigned)((chains + kCodeThreads - 1) / kCodeThreads)), block(kCodeThreads);
+  if (a.cpw < 1 || a.cpw > kCodeThreads) return -1;
+  dim3 grid((unsigned)((chains + a.cpw - 1) / a.cpw)), block(kCodeThreads);
   hipLaunchKernelGGL(ffv1_code_golomb, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
