@@ -75,6 +75,24 @@ def test_chained_coder_matches_oracle(stream, monkeypatch):
     assert got == ref
 
 
+@pytest.mark.parametrize("cpw", [1, 3, 64])
+def test_chained_chains_per_wave_match_oracle(cpw, monkeypatch):
+    """ffv1_code / ffv1_code_golomb with cpw chains per wave (the code_cpw
+    hook; by default launch_code spreads few chains over more waves, 64 is
+    the one-chain-per-lane form): the idle lanes, which run on dummy tables
+    in the range coder, leave every chain's bytes as the oracle's, with the
+    P-frame states carried across encode calls in the chains' tables."""
+    monkeypatch.setenv("FFV1HIP_DEBUG", f"coder=chain,code_cpw={cpw}")
+    for s in [Stream("cpw_ctx1", 176, 144, "yuv420p10", 8, slices=6, coder=1, context=1, gop_size=4, depth=10),
+              Stream("cpw_rgb", 128, 96, "bgr0", 6, slices=4, level=3, gop_size=3, source="random"),
+              Stream("cpw_golomb", 176, 144, "yuv420p", 6, slices=6, level=3, coder=0, gop_size=3,
+                     source="random")]:
+        frames = list(s.frames())
+        _, _, ref = oracle_encode(s, frames)
+        _, got = hip_encode(s, frames, batch=4)
+        assert got == ref, (cpw, s.name)
+
+
 @pytest.mark.parametrize("debug", ["walk_blocks=0", "serial", "walk_blocks=0,serial"])
 def test_schedule_variants_match_oracle(debug, monkeypatch):
     """The walk in 5-wave or one-wave blocks, overlapped or one kernel at a
