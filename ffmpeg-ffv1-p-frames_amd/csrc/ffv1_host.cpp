@@ -111,12 +111,12 @@ class CopyPool {
 // created (so each context sees the value set at its creation, and nothing is
 // cached in function statics):
 //   FFV1HIP_DEBUG="name[=value],name[=value],..."
-// measurement: serial, walkdbg, walktrace, hostdbg, copy_threads; test hooks
-// (each forces a path the product takes on its own only in some configs or
-// under memory pressure): coder=chain, dense=0, walk_blocks=0, recsets=1,
-// slice_cap, walk_part_a, force_multi, bounds_shrink,
-// dsets=eager|lazy, budget=q, rec2_drop=set, pack=0, fsets=2, v4_cap0,
-// readback, guard_skip.  Unknown names
+// measurement: serial, walkdbg, walktrace, hostdbg, copy_threads, walk_prio,
+// range_prio, sym_skip; test hooks (each forces a path the product takes on
+// its own only in some configs or under memory pressure): coder=chain,
+// dense=0, walk_blocks=0, recsets=1, slice_cap, walk_part_a, force_multi,
+// bounds_shrink, dsets=eager|lazy, budget=q, rec2_drop=set, pack=0, fsets=2,
+// v4_cap0, readback, guard_skip, compact=0, code_cpw=n.  Unknown names
 // are an error at create time, so a misspelt hook never silently measures
 // the default.
 struct Knobs {
@@ -1963,8 +1963,9 @@ static int run_batch(ffv1hip_ctx* c, const uint8_t* d_frames, int64_t frame_byte
     sa.nslots = n;
     sa.dcount = d_dcount;  // accumulated by the symbols blocks of each plane
     // sym_skip=k (measurement hook, valid only when every batch codes the
-    // same frames from a keyframe, as bench.py's): from batch k on, the
-    // records, chunk bits and counts of the batch three back are reused
+    // same frames from a keyframe, as bench.py's): from batch max(k, 6) on,
+    // no symbols pass; the batch reuses the records and chunk bits of the
+    // batch two back (set fb) and the counts of the batch three back (t3)
     const bool sym_skip = c->knobs.has("sym_skip") && c->batches_run >= std::max(6, c->knobs.get("sym_skip", 6));
     c->batches_run++;
     if (!sym_skip) HIP_TRY(hipMemsetAsync(d_dcount, 0, sizeof(int) * 3 * size_t(n) * c->nslices, sst));
