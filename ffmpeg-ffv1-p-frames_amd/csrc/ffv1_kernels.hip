@@ -803,10 +803,14 @@ __device__ __forceinline__ int64_t terminate(Lane& L, SinkT& S, bool state129, i
 // row's states before the symbol (each slot codes once per symbol but slots
 // 10 and 31, whose later decisions see the states their earlier ones left).
 // Plain global atomics: pass 1 is a statistics run, not the timed path.
+// (mask selects, as SignSlot: a ternary chain over the members with a run-time
+// k became an indexed load, which put the whole Lane in scratch memory for
+// every decision of the kernel, pass 1 or not)
 __device__ __forceinline__ uint32_t row_byte(const Lane& L, int k) {
   const int d = k >> 2;
-  const uint32_t w = d == 0 ? L.r0 : d == 1 ? L.r1 : d == 2 ? L.r2 : d == 3 ? L.r3
-                   : d == 4 ? L.r4 : d == 5 ? L.r5 : d == 6 ? L.r6 : L.r7;
+  auto m = [&](int i) { return 0u - (uint32_t)(d == i); };
+  const uint32_t w = (L.r0 & m(0)) | (L.r1 & m(1)) | (L.r2 & m(2)) | (L.r3 & m(3)) | (L.r4 & m(4)) |
+                     (L.r5 & m(5)) | (L.r6 & m(6)) | (L.r7 & m(7));
   return (w >> ((k & 3) * 8)) & 0xFFu;
 }
 
@@ -1375,7 +1379,12 @@ __device__ __forceinline__ void dseg_body(const CodeArgs& a, int vb, int vgrid, 
         if (i + 512 < n) static_for<0, 4>([&](auto jc) { nbg[decltype(jc)::value] = B4[(i >> 7) + 4 + decltype(jc)::value]; });
       }
       if (i + 128 < n) fetch((i >> 7) + 1, nxt);
-      const uint4 b4 = q == 0 ? bg[0] : q == 1 ? bg[1] : q == 2 ? bg[2] : bg[3];
+      // this block's bits are bg[0]; the group's others move up (a select
+      // on q, wave-uniform as it is, became an indexed load from scratch)
+      const uint4 b4 = bg[0];
+      bg[0] = bg[1];
+      bg[1] = bg[2];
+      bg[2] = bg[3];
       const uint32_t cbw[4] = {b4.x, b4.y, b4.z, b4.w};
       static_for<0, 4>([&](auto sc) {
         constexpr int S = decltype(sc)::value;
