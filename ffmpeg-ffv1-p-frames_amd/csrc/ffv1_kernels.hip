@@ -968,7 +968,8 @@ __global__ __launch_bounds__(kCodeThreads) void ffv1_code(CodeArgs a) {
     const bool nz = act && v != 0;
     const unsigned mag = v < 0 ? 0u - (unsigned)v : (unsigned)v;
     const int e = nz ? 31 - __builtin_clz(mag) : -1;
-    const int emax = wave_max5(e + 1) - 1;
+    // (one chain per wave: lane 0's own exponent, the idle lanes' being -1)
+    const int emax = (a.cpw == 1 ? __builtin_amdgcn_readfirstlane(e + 1) : wave_max5(e + 1)) - 1;
     switch (emax) {
       case -1: code_symbol<-1>(L, act, nz, v, mag, e, ftab); break;
       case 0: code_symbol<0>(L, act, nz, v, mag, e, ftab); break;
